@@ -1,0 +1,409 @@
+"""Generate golden vectors by executing the REFERENCE's own code on CPU.
+
+Run in the build container only (needs /root/reference, never on the GPU box):
+
+    python tests/golden/gen_golden.py
+
+What runs: the reference's own ``src/models.py`` (``MLP``, ``LinkPredictor``)
+and the functions ``kl_loss``, ``neighbor_samplers``, ``train_minibatch``,
+``train`` extracted (with ``ast``) from ``src/main.py``.  Their source text is
+read from /root/reference at generation time and compiled here; nothing of it
+is copied into the repo (the checked-in ``__pycache__`` .pyc is never loaded).
+
+What is injected (the reference's third-party imports are not installed):
+  * ``torch_geometric.nn`` names imported at models.py:3 -> inert placeholders
+    (the distillation path never constructs them);
+  * ``random_walk`` (torch_cluster) -> oracle.llp_oracle.random_walk on the
+    reference's (row, col) with coalesced=False semantics;
+  * ``negative_sampling`` (PyG) -> oracle.llp_oracle.negative_sampling_dense;
+  * the string constant "cuda" (main.py:50,191) -> "cpu" (SURVEY Q7).
+Every random tensor the reference draws (DataLoader permutations, randint,
+walks, negatives) is recorded so a test can replay it into the HIP engine.
+
+Output: ``tests/golden/*.npz`` (data only: inputs and expected outputs).
+"""
+from __future__ import annotations
+
+import argparse
+import ast
+import itertools
+import os
+import random
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from oracle import llp_oracle as O  # noqa: E402
+
+REF = "/root/reference/src"
+
+
+def _compile_file(path):
+    with open(path) as f:
+        return f.read()
+
+
+def load_reference_models():
+    """Exec src/models.py with an inert torch_geometric.nn (models.py:3)."""
+    pyg = types.ModuleType("torch_geometric")
+    pyg_nn = types.ModuleType("torch_geometric.nn")
+    for n in ("GCNConv", "SAGEConv", "GATConv", "APPNP"):
+        setattr(pyg_nn, n, type(n, (), {}))
+    pyg.nn = pyg_nn
+    saved = {k: sys.modules.get(k) for k in ("torch_geometric", "torch_geometric.nn")}
+    sys.modules["torch_geometric"] = pyg
+    sys.modules["torch_geometric.nn"] = pyg_nn
+    try:
+        mod = types.ModuleType("ref_models")
+        code = compile(_compile_file(os.path.join(REF, "models.py")), os.path.join(REF, "models.py"), "exec")
+        exec(code, mod.__dict__)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return mod
+
+
+class _CudaToCpu(ast.NodeTransformer):
+    def visit_Constant(self, node):
+        if node.value == "cuda":
+            return ast.copy_location(ast.Constant("cpu"), node)
+        return node
+
+
+class Recorder:
+    def __init__(self):
+        self.log = []
+
+    def add(self, kind, value):
+        self.log.append((kind, value.detach().clone() if torch.is_tensor(value) else value))
+
+
+def load_reference_main(rec: Recorder, rw_seed: int, neg_seed: int):
+    """Extract kl_loss/cosine_loss/neighbor_samplers/train_minibatch/train from
+    src/main.py (skipping the module-level main() call at main.py:515)."""
+    src = _compile_file(os.path.join(REF, "main.py"))
+    tree = ast.parse(src)
+    keep = {"cosine_loss", "kl_loss", "neighbor_samplers", "train_minibatch", "train"}
+    body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in keep]
+    mod_ast = _CudaToCpu().visit(ast.Module(body=body, type_ignores=[]))
+    ast.fix_missing_locations(mod_ast)
+
+    rw_counter = itertools.count()
+
+    def random_walk(row, col, start, walk_length, coalesced=True, p=1, q=1):
+        num_nodes = int(max(int(row.max()), int(col.max()), int(start.max()))) + 1
+        rowptr, colv = O.build_rowptr(row.numpy(), col.numpy(), num_nodes, coalesced=coalesced)
+        out = torch.from_numpy(O.random_walk(rowptr, colv, start.numpy(), walk_length, rw_seed, next(rw_counter)))
+        rec.add("random_walk", out)
+        return out
+
+    neg_rng = random.Random(neg_seed)
+
+    def negative_sampling(edge_index, num_nodes=None, num_neg_samples=None, method="sparse"):
+        assert method == "dense"
+        out = O.negative_sampling_dense(edge_index, num_nodes, num_neg_samples, rng=neg_rng)
+        rec.add("negative_sampling", out)
+        return out
+
+    class TorchProxy(types.ModuleType):
+        def __getattr__(self, name):
+            return getattr(torch, name)
+
+    tproxy = TorchProxy("torch")
+
+    def randint(*a, **k):
+        out = torch.randint(*a, **k)
+        rec.add("randint", out)
+        return out
+
+    tproxy.randint = randint
+
+    class RecDataLoader:
+        def __init__(self, *a, **k):
+            self.dl = torch.utils.data.DataLoader(*a, **k)
+
+        def __iter__(self):
+            for b in self.dl:
+                rec.add("perm", b)
+                yield b
+
+    class NNProxy(types.ModuleType):
+        def __getattr__(self, name):
+            return getattr(nn, name)
+
+    nproxy = NNProxy("nn")
+
+    class RecMarginRankingLoss(nn.MarginRankingLoss):
+        def forward(self, a, b, y):
+            out = super().forward(a, b, y)
+            rec.add("llp_r", out)
+            return out
+
+    class RecBCELoss(nn.BCELoss):
+        def forward(self, a, b):
+            out = super().forward(a, b)
+            rec.add("bce", out)
+            return out
+
+    nproxy.MarginRankingLoss = RecMarginRankingLoss
+    nproxy.BCELoss = RecBCELoss
+
+    ns = dict(torch=tproxy, nn=nproxy, F=F, np=np, itertools=itertools, DataLoader=RecDataLoader,
+              random_walk=random_walk, negative_sampling=negative_sampling,
+              cosine_similarity=F.cosine_similarity)
+    exec(compile(mod_ast, os.path.join(REF, "main.py"), "exec"), ns)
+    raw_kl = ns["kl_loss"]
+
+    def kl_loss(s, t, T):
+        out = raw_kl(s, t, T)
+        rec.add("llp_d", out)
+        return out
+
+    ns["kl_loss"] = kl_loss
+    return ns
+
+
+class RecAdam(torch.optim.Adam):
+    def __init__(self, params, rec, **kw):
+        super().__init__(params, **kw)
+        self.rec = rec
+
+    def step(self, closure=None):
+        grads = [p.grad.detach().clone() for g in self.param_groups for p in g["params"]]
+        self.rec.add("grads", grads)
+        return super().step(closure)
+
+
+def synth_graph(N, n_undirected, seed, interleave=True):
+    """Random simple-ish graph with a few duplicate pairs, written
+    OGB-style (u,v),(v,u) interleaved (Q1) when ``interleave``."""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randint(0, N, (n_undirected,), generator=g)
+    v = torch.randint(0, N, (n_undirected,), generator=g)
+    keep = u != v
+    u, v = u[keep], v[keep]
+    # duplicate ~5% of the pairs (multi-edges)
+    nd = max(1, u.numel() // 20)
+    u = torch.cat([u, u[:nd]]); v = torch.cat([v, v[:nd]])
+    pairs = torch.stack([u, v], 1)                       # (E_und, 2)
+    if interleave:
+        ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t().contiguous()
+    else:
+        ei = torch.cat([pairs, pairs.flip(1)], 0).t().contiguous()
+    return pairs, ei
+
+
+def flat_log(rec: Recorder):
+    return list(rec.log)
+
+
+def run_minibatch_case(name, ref_models, N, F_, H, L, E_und, lbs, args_over, seed, nepochs=1):
+    rec = Recorder()
+    ns = load_reference_main(rec, rw_seed=seed + 11, neg_seed=seed + 12)
+    torch.manual_seed(seed)
+    pairs, ei = synth_graph(N, E_und, seed)
+    x = torch.randn(N, F_) * 0.5
+    t_h = torch.randn(N, 256) * 0.3
+    data = types.SimpleNamespace(x=x, adj_t=ei, edge_index=ei)
+    split_edge = {"train": {"edge": pairs}}
+    args = argparse.Namespace(
+        transductive="transductive", node_batch_size=None, link_batch_size=lbs, datasets="collab",
+        rw_step=3, hops=3, ns_rate=3, ps_method="nb", hidden_channels=H, num_layers=L, dropout=0.0,
+        margin=0.05, LLP_D=1.0, LLP_R=1.0, True_label=0.1, KD_RM=0.0, KD_LM=0.0, predictor="mlp", lr=0.01)
+    for k, v in args_over.items():
+        setattr(args, k, v)
+    args.node_batch_size = int(N / (pairs.size(0) / args.link_batch_size))          # main.py:335
+    model = ref_models.MLP(args.num_layers, F_, H, H, args.dropout)
+    predictor = ref_models.LinkPredictor(args.predictor, H, H, 1, args.num_layers, args.dropout)
+    tpred = ref_models.LinkPredictor(args.predictor, 256, 256, 1, 2, args.dropout)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    init_stu = {k: v.clone() for k, v in model.state_dict().items()}
+    init_pred = {k: v.clone() for k, v in predictor.state_dict().items()}
+    opt = RecAdam(list(model.parameters()) + list(predictor.parameters()), rec, lr=args.lr)
+    losses = []
+    for ep in range(nepochs):
+        losses.append(ns["train_minibatch"](model, predictor, t_h, tpred, data, split_edge, opt, args, "cpu"))
+    out = dict(N=N, F=F_, H=H, L=L, x=x.numpy(), t_h=t_h.numpy(), edge_index=ei.numpy(), train_pairs=pairs.numpy(),
+               epoch_losses=np.array(losses, np.float64))
+    out.update({f"args/{k}": np.array(v) for k, v in vars(args).items()})
+    for k, v in init_stu.items():
+        out[f"init/stu/{k}"] = v.numpy()
+    for k, v in init_pred.items():
+        out[f"init/pred/{k}"] = v.numpy()
+    for k, v in tpred.state_dict().items():
+        out[f"tpred/{k}"] = v.numpy()
+    for k, v in model.state_dict().items():
+        out[f"final/stu/{k}"] = v.numpy()
+    for k, v in predictor.state_dict().items():
+        out[f"final/pred/{k}"] = v.numpy()
+    _dump_log(out, rec, kind_order="minibatch", args=args)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "steps:", out["nsteps"], "epoch losses:", losses)
+
+
+def _dump_log(out, rec, kind_order, args):
+    """Split the recorder log into per-step records."""
+    log = rec.log
+    step = -1
+    perms = []
+    cur = None
+    steps = []
+    for kind, v in log:
+        if kind == "perm":
+            perms.append(v)
+            continue
+        if kind in ("randint", "negative_sampling", "random_walk") and (cur is None or "grads" in cur):
+            cur = {"walks": [], "randint": []}
+            steps.append(cur)
+        if kind == "random_walk":
+            cur["walks"].append(v)
+        elif kind == "randint":
+            cur["randint"].append(v)
+        elif kind == "negative_sampling":
+            cur["neg_edge"] = v
+        elif kind in ("llp_d", "llp_r", "bce"):
+            cur[kind] = v
+        elif kind == "grads":
+            cur["grads"] = v
+    out["nsteps"] = np.array(len(steps))
+    out["perms_raw_count"] = np.array(len(perms))
+    for i, p in enumerate(perms):
+        out[f"perm/{i}"] = p.numpy()
+    for s, st in enumerate(steps):
+        for i, w in enumerate(st["walks"]):
+            out[f"step{s}/walk{i}"] = w.numpy()
+        for i, r in enumerate(st["randint"]):
+            out[f"step{s}/randint{i}"] = r.numpy()
+        if "neg_edge" in st:
+            out[f"step{s}/neg_edge"] = st["neg_edge"].numpy()
+        for k in ("llp_d", "llp_r", "bce"):
+            if k in st:
+                out[f"step{s}/{k}"] = st[k].numpy()
+        for i, g in enumerate(st["grads"]):
+            out[f"step{s}/grad{i}"] = g.numpy()
+
+
+def run_fullbatch_case(name, ref_models, N, F_, E_und, lbs, args_over, seed, transductive="transductive"):
+    rec = Recorder()
+    ns = load_reference_main(rec, rw_seed=seed + 21, neg_seed=seed + 22)
+    torch.manual_seed(seed)
+    pairs, ei = synth_graph(N, E_und, seed, interleave=False)
+    H = 256                                                 # main.py:185 needs H == t_h width
+    x = (torch.rand(N, F_) < 0.1).float()
+    t_h = torch.randn(N, 256) * 0.3
+    args = argparse.Namespace(
+        transductive=transductive, node_batch_size=None, link_batch_size=lbs, datasets="cora",
+        rw_step=3, hops=2, ns_rate=1, ps_method="nb", hidden_channels=H, num_layers=2, dropout=0.0,
+        margin=0.1, LLP_D=0.5, LLP_R=1.0, True_label=0.1, KD_RM=0.3, KD_LM=0.2, predictor="mlp", lr=0.01)
+    for k, v in args_over.items():
+        setattr(args, k, v)
+    if transductive == "transductive":
+        data = types.SimpleNamespace(x=x, adj_t=ei)
+        split_edge = {"train": {"edge": pairs}}
+        args.node_batch_size = int(N / (pairs.size(0) / args.link_batch_size))
+    else:
+        data = types.SimpleNamespace(x=x, edge_index=ei)
+        split_edge = None
+        args.node_batch_size = int(N / (ei.size(1) / args.link_batch_size))       # main.py:348
+    model = ref_models.MLP(args.num_layers, F_, H, H, args.dropout)
+    predictor = ref_models.LinkPredictor(args.predictor, H, H, 1, args.num_layers, args.dropout)
+    tpred = ref_models.LinkPredictor(args.predictor, 256, 256, 1, 2, args.dropout)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    init_stu = {k: v.clone() for k, v in model.state_dict().items()}
+    init_pred = {k: v.clone() for k, v in predictor.state_dict().items()}
+    opt = RecAdam(list(model.parameters()) + list(predictor.parameters()), rec, lr=args.lr)
+    loss = ns["train"](model, predictor, t_h, tpred, data, split_edge, opt, args, "cpu")
+    out = dict(N=N, F=F_, H=H, L=args.num_layers, x=x.numpy(), t_h=t_h.numpy(), edge_index=ei.numpy(),
+               train_pairs=pairs.numpy(), epoch_losses=np.array([loss], np.float64))
+    out.update({f"args/{k}": np.array(v) for k, v in vars(args).items()})
+    for k, v in init_stu.items():
+        out[f"init/stu/{k}"] = v.numpy()
+    for k, v in init_pred.items():
+        out[f"init/pred/{k}"] = v.numpy()
+    for k, v in tpred.state_dict().items():
+        out[f"tpred/{k}"] = v.numpy()
+    for k, v in model.state_dict().items():
+        out[f"final/stu/{k}"] = v.numpy()
+    for k, v in predictor.state_dict().items():
+        out[f"final/pred/{k}"] = v.numpy()
+    _dump_log(out, rec, kind_order="fullbatch", args=args)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "steps:", out["nsteps"], "epoch loss:", loss)
+
+
+def run_kl_rank_case(name, seed):
+    """kl_loss (main.py:27-31) on fixed inputs, incl. T != 1."""
+    rec = Recorder()
+    ns = load_reference_main(rec, 0, 0)
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for i, (B, C, T) in enumerate([(5, 12, 1.0), (7, 36, 1.0), (3, 8, 2.0)]):
+        s = torch.rand(B, C, generator=g)
+        t = torch.rand(B, C, generator=g)
+        out[f"case{i}/s"] = s.numpy(); out[f"case{i}/t"] = t.numpy(); out[f"case{i}/T"] = np.array(T)
+        out[f"case{i}/kl"] = ns["kl_loss"](s, t, T).numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def run_model_case(name, ref_models, seed):
+    """Reference MLP / LinkPredictor forward+backward on fixed inputs."""
+    torch.manual_seed(seed)
+    out = {}
+    mlp = ref_models.MLP(3, 24, 40, 40, 0.0)
+    x = torch.randn(33, 24, requires_grad=True)
+    y = mlp(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    out.update({f"mlp/{k}": v.detach().numpy() for k, v in mlp.state_dict().items()})
+    out.update({"mlp/x": x.detach().numpy(), "mlp/y": y.detach().numpy(), "mlp/gy": gy.numpy(),
+                "mlp/gx": x.grad.numpy()})
+    for k, p in mlp.named_parameters():
+        out[f"mlp/grad/{k}"] = p.grad.numpy()
+    for kind in ("mlp", "inner"):
+        lp = ref_models.LinkPredictor(kind, 40, 40, 1, 3, 0.0)
+        xi = torch.randn(29, 40, requires_grad=True)
+        xj = torch.randn(29, 40, requires_grad=True)
+        o = lp(xi, xj)
+        go = torch.randn_like(o)
+        o.backward(go)
+        out.update({f"lp_{kind}/{k}": v.detach().numpy() for k, v in lp.state_dict().items()})
+        out.update({f"lp_{kind}/xi": xi.detach().numpy(), f"lp_{kind}/xj": xj.detach().numpy(),
+                    f"lp_{kind}/out": o.detach().numpy(), f"lp_{kind}/gout": go.numpy(),
+                    f"lp_{kind}/gxi": xi.grad.numpy(), f"lp_{kind}/gxj": xj.grad.numpy()})
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def main():
+    ref_models = load_reference_models()
+    run_kl_rank_case("kl_loss", 1)
+    run_model_case("models_fwd_bwd", ref_models, 2)
+    # collab-style minibatch path (main.py:52-144), C = 3*3*(1+3) = 36 like the
+    # collab script, 3 link batches per epoch incl. a partial one, 2 epochs.
+    run_minibatch_case("minibatch_collab_small", ref_models, N=257, F_=16, H=32, L=3, E_und=300, lbs=128,
+                       args_over={}, seed=3, nepochs=2)
+    # ps_method='rw', ns_rate=1, hops=2, rw_step=2 (C = 8), LLP_R only weight
+    run_minibatch_case("minibatch_rw_small", ref_models, N=97, F_=8, H=24, L=2, E_und=150, lbs=64,
+                       args_over=dict(ps_method="rw", rw_step=2, hops=2, ns_rate=1, LLP_D=0.0, LLP_R=2.0,
+                                      True_label=1.0, margin=0.1), seed=4)
+    # full-batch path (main.py:147-236) with dense negative sampling + KD terms
+    run_fullbatch_case("fullbatch_cora_small", ref_models, N=120, F_=40, E_und=260, lbs=96, args_over={},
+                       seed=5)
+    run_fullbatch_case("fullbatch_production_small", ref_models, N=90, F_=30, E_und=180, lbs=1024,
+                       args_over=dict(KD_RM=0.0, KD_LM=0.0, LLP_D=1.0, LLP_R=0.5, hops=1, ns_rate=4),
+                       seed=6, transductive="production")
+
+
+if __name__ == "__main__":
+    main()

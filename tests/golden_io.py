@@ -1,0 +1,104 @@
+"""Load the golden fixtures written by tests/golden/gen_golden.py into replayable
+per-step records (inputs injected into the engine / oracle, expected outputs)."""
+from __future__ import annotations
+
+import os
+import types
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def _args(z):
+    a = types.SimpleNamespace()
+    for k in z.files:
+        if k.startswith("args/"):
+            v = z[k]
+            v = v.item() if v.ndim == 0 else v
+            if isinstance(v, np.str_):
+                v = str(v)
+            setattr(a, k[5:], v)
+    return a
+
+
+def _params(z, prefix, names):
+    return [torch.from_numpy(z[f"{prefix}/{n}"].copy()) for n in names]
+
+
+def stu_names(L):
+    return [f"layers.{i}.{w}" for i in range(L) for w in ("weight", "bias")]
+
+
+def pred_names(L):
+    return [f"lins.{i}.{w}" for i in range(L) for w in ("weight", "bias")]
+
+
+def load_case(name):
+    z = load(name)
+    a = _args(z)
+    L = int(z["L"])
+    Lp = L  # LinkPredictor(..., args.num_layers, ...) (main.py:353-354)
+    case = types.SimpleNamespace(
+        name=name, args=a, N=int(z["N"]), F=int(z["F"]), H=int(z["H"]), L=L,
+        x=torch.from_numpy(z["x"].copy()), t_h=torch.from_numpy(z["t_h"].copy()),
+        edge_index=torch.from_numpy(z["edge_index"].copy()),
+        train_pairs=torch.from_numpy(z["train_pairs"].copy()),
+        epoch_losses=z["epoch_losses"],
+        stu0=_params(z, "init/stu", stu_names(L)), pred0=_params(z, "init/pred", pred_names(Lp)),
+        tpred=_params(z, "tpred", pred_names(2)),
+        stu_final=_params(z, "final/stu", stu_names(L)), pred_final=_params(z, "final/pred", pred_names(Lp)),
+        steps=[])
+    nsteps = int(z["nsteps"])
+    minibatch = name.startswith("minibatch")
+    full = not minibatch
+    if a.transductive == "transductive":
+        pos_train_edge = case.train_pairs
+    else:
+        pos_train_edge = case.edge_index.t()
+    case.pos_train_edge = pos_train_edge
+    for s in range(nsteps):
+        st = types.SimpleNamespace()
+        st.link_perm = torch.from_numpy(z[f"perm/{2 * s}"].copy())
+        st.node_perm = torch.from_numpy(z[f"perm/{2 * s + 1}"].copy())
+        st.edge = pos_train_edge[st.link_perm].t()
+        walks = []
+        w = 0
+        while f"step{s}/walk{w}" in z.files:
+            walks.append(torch.from_numpy(z[f"step{s}/walk{w}"].copy()))
+            w += 1
+        ri = []
+        r = 0
+        while f"step{s}/randint{r}" in z.files:
+            ri.append(torch.from_numpy(z[f"step{s}/randint{r}"].copy()))
+            r += 1
+        if minibatch:
+            st.neg_edge = ri[0]                       # main.py:84
+            neg_batch = ri[1] if len(ri) > 1 else None
+        else:
+            st.neg_edge = torch.from_numpy(z[f"step{s}/neg_edge"].copy())   # main.py:206
+            neg_batch = ri[0] if ri else None
+        if walks:
+            pos = walks[0]
+            for wk in walks[1:]:
+                pos = torch.cat([pos, wk[:, 1:]], 1)   # main.py:45
+            st.samples = torch.cat([pos, neg_batch], 1)  # main.py:94,183
+        else:
+            st.samples = None
+        for k in ("llp_d", "llp_r", "bce"):
+            key = f"step{s}/{k}"
+            setattr(st, k, float(z[key]) if key in z.files else None)
+        ng = len(case.stu0) + len(case.pred0)
+        st.grads = [torch.from_numpy(z[f"step{s}/grad{i}"].copy()) for i in range(ng)]
+        case.steps.append(st)
+    case.full = full
+    return case
+
+
+MINIBATCH_CASES = ["minibatch_collab_small", "minibatch_rw_small"]
+FULLBATCH_CASES = ["fullbatch_cora_small", "fullbatch_production_small"]
