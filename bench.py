@@ -1,0 +1,227 @@
+#!/usr/bin/env python
+"""Headline benchmark: ogbl-collab LLP relational distillation (train_minibatch,
+src/main.py:52-144) at the collab script's configuration
+(scripts/LLP_transductive.sh:8: --hidden_channels=1024 --num_layers=3 --hops=3
+--rw_step=3 --ns_rate=3 --ps_method=nb --LLP_D=1 --LLP_R=0 --True_label=1
+--margin=0.01 --lr=0.001 --dropout=0 --minibatch; link_batch_size 65,536,
+node_batch_size 13,110) on synthetic collab-shape data.
+
+One step = one link batch: device sampling, student MLP + LinkPredictor
+forward/backward, frozen teacher predictor, fused LLP_D/LLP_R/BCE, clip, Adam.
+Metric: positive training edges per second (the reference's
+num_examples = edge.size(1), src/main.py:140), whole job.
+
+Multi-GPU (torchrun): the global batch stays 65,536 edges / 13,110 anchors
+(reference semantics) and is sharded across ranks; one RCCL all-reduce of the
+gradients per step (strong scaling).
+
+  python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "linkless-link-prediction_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "distillation edges/sec + Hits@20, ogbl-collab LLP at 1/2/4/8 MI355X"
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def collab_args():
+    return types.SimpleNamespace(hidden_channels=1024, num_layers=3, hops=3, rw_step=3, ns_rate=3, ps_method="nb",
+                                 LLP_D=1.0, LLP_R=0.0, True_label=1.0, KD_RM=0.0, KD_LM=0.0, margin=0.01, lr=0.001,
+                                 dropout=0.0, predictor="mlp", link_batch_size=64 * 1024, datasets="collab",
+                                 transductive="transductive", minibatch=True)
+
+
+def step_flops(B, C, P, F, H, L):
+    """Algorithmic FLOP of one distillation step."""
+    rows_mlp = B * (C + 1) + 4 * P
+    rows_pred = B * C + 2 * P
+    fwd_mlp = 2 * rows_mlp * (F * H + (L - 1) * H * H)
+    fwd_pred = 2 * rows_pred * ((L - 1) * H * H + H)
+    fwd_t = 2 * B * C * (256 * 256 + 256)
+    return 3 * (fwd_mlp + fwd_pred) - 2 * rows_mlp * F * H + fwd_t
+
+
+def cpu_baseline(data, a, t_h, init_params, B_full, P_full, sample_P=8192, steps=3):
+    """The CPU oracle (torch-CPU restatement of train_minibatch) on a bounded
+    sample of the same workload: one link batch of sample_P edges and the
+    proportional anchor batch, same H/L/C.  Edges/s scales linearly with the
+    batch, so the per-edge rate is comparable."""
+    from oracle import llp_oracle as O
+    B = max(1, int(B_full * sample_P / P_full))
+    P = sample_P
+    C = a.rw_step * a.hops * (1 + a.ns_rate)
+    x = data.x
+    stu = [p.clone().requires_grad_() for p in init_params[0]]
+    prd = [p.clone().requires_grad_() for p in init_params[1]]
+    tp = init_params[2]
+    adam = O.AdamState(stu + prd, lr=a.lr)
+    rowptr, colv = None, None
+    import llp_engine
+    rowptr, colv = llp_engine.build_sampler_csr(data.edge_index[0].numpy(), data.edge_index[1].numpy(), data.N)
+    rng = np.random.default_rng(1)
+    nthreads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        anchors = rng.permutation(data.N)[:B]
+        pos, neg = O.neighbor_samplers(rowptr, colv, anchors, data.N, a.rw_step, a.ps_method, a.ns_rate, a.hops,
+                                       seed=5, stream_base=16 * s)
+        samples = torch.from_numpy(np.concatenate([pos, neg], 1))
+        link = rng.integers(0, data.train_pairs.shape[0], P)
+        edge = data.train_pairs[link].t()
+        negE = torch.from_numpy(O.randint_edges(data.N, P, seed=5, stream=16 * s + 15))
+        r = O.distill_losses_minibatch(x, t_h, samples, edge, negE, stu[0::2], stu[1::2], prd[0::2], prd[1::2],
+                                       tp[0::2], tp[1::2], a)
+        new, _, _ = O.distill_step(stu, prd, adam, r["loss"])
+        stu = [p.requires_grad_() for p in new[:len(stu)]]
+        prd = [p.requires_grad_() for p in new[len(stu):]]
+    dt = time.perf_counter() - t0
+    assert C > 0
+    return dict(value=P * steps / dt, unit="edges/s", cores=nthreads, kind="port",
+                sample=f"{steps} oracle train_minibatch steps of {P} edges / {B} anchors at the collab shape "
+                       f"(H=1024, L=3, C={C}); {dt:.1f} s on {nthreads} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-edges", type=int, default=8192)
+    ap.add_argument("--scale", type=float, default=1.0, help="dataset scale (1.0 = ogbl-collab shape)")
+    ap.add_argument("--profile-kernels", action="store_true", help="exit right after the timed region")
+    opt = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import llp_data
+    import llp_engine
+    import models
+
+    a = collab_args()
+    data = llp_data.synthetic_collab(seed=0, scale=opt.scale, with_eval=False)
+    N, F, H, L = data.N, data.F, a.hidden_channels, a.num_layers
+    E_train = data.train_pairs.shape[0]
+    P_full = a.link_batch_size
+    B_full = int(N / (E_train / P_full))                    # src/main.py:335
+    C = a.rw_step * a.hops * (1 + a.ns_rate)
+
+    torch.manual_seed(1)
+    model = models.MLP(L, F, H, H, a.dropout)
+    pred = models.LinkPredictor("mlp", H, H, 1, L, a.dropout)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, a.dropout)
+    t_h = torch.randn(N, 256) * 0.3
+    init = ([p.detach().clone() for p in model.parameters()], [p.detach().clone() for p in pred.parameters()],
+            [p.detach().clone() for p in tpred.parameters()])
+    model, pred, tpred = model.to(dev), pred.to(dev), tpred.to(dev)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    optim = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
+    eng = llp_engine.DistillEngine(model, pred, tpred, data.x.to(dev), t_h.to(dev), data.edge_index[0].numpy(),
+                                   data.edge_index[1].numpy(), N, a, optim, dtype=opt.dtype, seed=123)
+    pairs = data.train_pairs.to(torch.int32).to(dev).contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    link_perm = torch.randperm(E_train, generator=g, device=dev).to(torch.int32)
+    node_perm = torch.randperm(N, generator=g, device=dev).to(torch.int32)
+    n_full = min(E_train // P_full, N // B_full)
+    # this rank's shard of every global batch
+    b0, b1 = rank * B_full // world, (rank + 1) * B_full // world
+    p0, p1 = rank * P_full // world, (rank + 1) * P_full // world
+
+    kern_ev = []
+
+    def one_step(s, timed):
+        j = s % n_full
+        anchors = node_perm[j * B_full + b0: j * B_full + b1]
+        links = link_perm[j * P_full + p0: j * P_full + p1]
+        eng.step_minibatch(anchors, links, pairs, b_offset=b0, p_offset=p0, B_total=B_full, P_total=P_full,
+                           kernel_events=kern_ev if timed else None)
+
+    for s in range(opt.warmup):
+        one_step(s, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.begin_epoch()
+    t0 = time.perf_counter()
+    for s in range(opt.steps):
+        one_step(opt.warmup + s, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if opt.profile_kernels:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    loss = eng.end_epoch(opt.steps * P_full)
+
+    # dominant kernel: student layer-2 forward GEMM (rows_mlp x 1024 x 1024, bf16 MFMA)
+    rows_mlp = (b1 - b0) * (C + 1) + 4 * (p1 - p0)
+    kt = [s.elapsed_time(e) for s, e in kern_ev]
+    k_ms = float(np.mean(kt)) if kt else float("nan")
+    k_flop = 2.0 * rows_mlp * H * H
+    peak = PEAK_BF16_TFLOPS if opt.dtype == "bf16" else PEAK_F32_TFLOPS
+    achieved = k_flop / (k_ms * 1e-3) / 1e12
+    flop_step = step_flops(B_full, C, P_full, F, H, L)
+
+    res = None
+    if rank == 0:
+        value = P_full * opt.steps / dt
+        res = {
+            "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": opt.steps,
+            "warmup": opt.warmup, "ms_per_step": dt / opt.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": opt.dtype,
+            "data": "synthetic (ogbl-collab shape: planted-partition graph, OGB-interleaved edges, random-init "
+                    "weights, random teacher embeddings)",
+            "config": {"workload": "ogbl-collab transductive LLP distillation (train_minibatch)", "N": N, "F": F,
+                       "hidden": H, "num_layers": L, "anchors_per_step": B_full, "contexts_per_anchor": C,
+                       "edges_per_step": P_full, "global_batch": P_full, "parallelism": f"dp{world}",
+                       "step_tflop": flop_step / 1e12, "mfma_util_step": flop_step / (dt / opt.steps) / 1e12 / peak
+                       / world},
+            "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<bf16> student layer-2 forward "
+                         f"({rows_mlp}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None, "kernel_ms": k_ms},
+            "loss": loss,
+        }
+        if world == 1 and not opt.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(data, a, t_h, init, B_full, P_full, sample_P=opt.cpu_sample_edges)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

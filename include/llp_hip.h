@@ -1,0 +1,252 @@
+/* libllp_hip.so — C ABI of the MI355X (gfx950) LLP distillation hot path.
+ *
+ * Every entry point takes caller-owned DEVICE pointers (row-major, contiguous
+ * unless a leading dimension says otherwise), plain sizes, and the HIP stream
+ * to launch on as `void* stream` (a hipStream_t; NULL = legacy stream).  No
+ * entry point allocates, frees or synchronises, so every call can be captured
+ * into a hipGraph.  Return 0 on success, else an LLP_E_* / hipError_t code;
+ * llp_last_error() gives a thread-local message.
+ *
+ * The reference (snap-research/linkless-link-prediction) is pure Python; it
+ * has no C ABI of its own.  Each entry point names the reference operation it
+ * replaces (file:line, paths relative to the reference root).
+ */
+#ifndef LLP_HIP_H_
+#define LLP_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LLP_OK 0
+#define LLP_E_ARG 10001
+#define LLP_E_WORKSPACE 10002
+
+enum llp_dtype { LLP_F32 = 0, LLP_BF16 = 1 };
+
+enum llp_act {
+  LLP_ACT_NONE = 0,      /* y = alpha*acc + bias                          */
+  LLP_ACT_RELU = 1,      /* y = max(alpha*acc + bias, 0)                  */
+  LLP_ACT_RELU_BWD = 2   /* y = (alpha*acc + bias) * (aux > 0): the ReLU
+                            backward fused into a dgrad GEMM's epilogue    */
+};
+
+/* A GEMM operand: logical row r (0 <= r < rows) is
+ *   ptr[(idx ? idx[r] : r) * ld + k]                       (plain / gathered)
+ *   ptr[(idx ? idx[r] : r) * ld + k] * ptr2[(idx2 ? idx2[r] : r) * ld2 + k]
+ *                                                          (Hadamard, ptr2 != NULL)
+ * Element type is the GEMM's dtype.  This is how the build avoids
+ * materialising x[this_target] (src/main.py:95-96) and x_i*x_j
+ * (src/models.py:140). */
+typedef struct llp_operand {
+  const void* ptr;
+  const int32_t* idx;
+  const void* ptr2;
+  const int32_t* idx2;
+  int64_t ld;
+  int64_t ld2;
+} llp_operand;
+
+int llp_version(void);
+const char* llp_last_error(void);
+/* 1 if the HIP runtime sees a device (never required to load the library). */
+int llp_device_count(void);
+
+/* ---------------------------------------------------------------- GEMM (MFMA)
+ * C[m,n] = epi(alpha * sum_k A[m,k] * B[n,k]),  m<M, n<N, k<K.
+ * Replaces nn.Linear forward (src/models.py:48,143,146) with B = weight [N,K],
+ * and the data-gradient dX = dY . W with B = W^T.  dtype LLP_F32 runs the exact
+ * f32 MFMA (v_mfma_f32_16x16x4_f32); LLP_BF16 runs v_mfma_f32_16x16x32_bf16
+ * with f32 accumulation.  c_dtype / aux_dtype select the output / aux element
+ * type.  bias (f32[N]) may be NULL. */
+/* Optional inverted dropout after the activation (F.dropout / nn.Dropout after
+ * ReLU, src/models.py:52-53,144-145): element (m, n) is kept iff
+ * u >= p with u = uniform draw #(m*N + n) of Philox stream
+ * 16*(*step_ctr) + stream_offset; kept values are scaled by 1/(1-p).
+ * The backward needs no mask: LLP_ACT_RELU_BWD against the stored dropped
+ * activation with alpha = 1/(1-p) is exact. */
+typedef struct llp_dropout {
+  float p;
+  uint64_t seed;
+  const int64_t* step_ctr;
+  int64_t stream_offset;
+} llp_dropout;
+
+int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K,
+                const llp_operand* A, const llp_operand* B,
+                void* C, int64_t ldc, int c_dtype,
+                const float* bias, int act, const void* aux, int64_t ld_aux, int aux_dtype,
+                float alpha, const llp_dropout* dropout, void* stream);
+
+/* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
+ * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then
+ * reduced in a fixed order: deterministic.  C is f32 with leading dim ldc.
+ * Replaces autograd's weight-gradient of nn.Linear (src/main.py:132). */
+int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q);
+int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q,
+                const llp_operand* A, const llp_operand* B,
+                float* C, int64_t ldc, int accumulate,
+                void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Column sums: out[n] (+)= sum_m Y[m,n] (bias gradient).  Deterministic. */
+int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N);
+int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
+               void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- link-predictor head
+ * logit[r] = dot(Z[r,:], w) + b; prob[r] = sigmoid(logit[r]) (either may be NULL).
+ * The last Linear(H,1) + torch.sigmoid of LinkPredictor (src/models.py:146,150),
+ * or the whole 'inner' predictor (src/models.py:147-148) with w = NULL (sum). */
+int llp_head_fwd(int dtype, int64_t R, int64_t H, const void* Z, int64_t ldz,
+                 const void* Z2, int64_t ldz2, const int32_t* iz, const int32_t* iz2,
+                 const float* w, const float* b, float* logit, float* prob, void* stream);
+
+/* Backward of the head: dZ[r,n] = alpha * dlogit[r] * w[n] * (Z[r,n] > 0)  (ReLU (+dropout: alpha = 1/(1-p)) of the
+ * layer below fused; relu_mask=0 disables the mask), dw[n] (+)= sum_r dlogit[r]*Z[r,n],
+ * db (+)= sum_r dlogit[r].  dw/db reductions are deterministic slabs. */
+int64_t llp_head_bwd_workspace_bytes(int64_t R, int64_t H);
+int llp_head_bwd(int dtype, int64_t R, int64_t H, const float* dlogit, const void* Z, int64_t ldz,
+                 const float* w, int relu_mask, float alpha, void* dZ, int64_t lddz, float* dw, float* db,
+                 int accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- fused LLP loss
+ * One wavefront per anchor b (src/main.py:98-130):
+ *   s = sigmoid(s_logit[b,:]) (Q4), t = t_prob[b,:];
+ *   LLP_D = sum_b KL(softmax(t/T) || softmax(s/T)) * T^2 / B          (main.py:27-31)
+ *   LLP_R = mean over b and pairs i<j of max(0, -y_ij (s_i - s_j) + margin),
+ *           y = +1 if t_i > t_j + margin, -1 if t_i < t_j - margin, else 0 (main.py:109-122)
+ *   BCE   = mean_r BCE(sigmoid(out_logit[r]), r < n_pos)                (main.py:125-127)
+ *   loss  = w_label*BCE + w_d*LLP_D + w_r*LLP_R                         (main.py:129-130)
+ * dlogit_ctx[b,c] / dlogit_lab[r] receive d(loss_scale*loss)/d(logit).
+ * Normalisers are explicit (B_total, n_lab_total) so a rank holding a shard
+ * computes its share of the global mean (multi-GPU).  terms_out (f32[4]) =
+ * {loss, bce, llp_d, llp_r} partial sums of this call, written (accumulate=0)
+ * or added (accumulate=1) deterministically. */
+int64_t llp_llp_loss_workspace_bytes(int64_t B, int64_t n_lab);
+int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob,
+                 int64_t n_lab, int64_t n_pos, const float* out_logit,
+                 double B_total, double n_lab_total, float margin, float T,
+                 float w_label, float w_d, float w_r, float loss_scale,
+                 float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- Hadamard backward
+ * Backward of x_i * x_j (src/models.py:140) for the minibatch row layout of
+ * src/main.py:95-105 (h rows: B anchor blocks of (1 + C) rows, then 2L src
+ * rows, then 2L dst rows; predictor rows: B*C context pairs then 2L label
+ * pairs).  Deterministic: every dh row is written exactly once.
+ *   dh[anchor b]      = sum_c dZ[b*C+c] * h[ctx(b,c)]
+ *   dh[ctx(b,c)]      = dZ[b*C+c] * h[anchor b]
+ *   dh[src i]         = dZ[B*C+i] * h[dst i],  dh[dst i] = dZ[B*C+i] * h[src i] */
+int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t H,
+                            const void* dZ, const float* drow, const void* h, void* dh, void* stream);
+
+/* Generic scatter form (full-batch train(), src/main.py:173-214, where rows of
+ * h repeat): dh[ia[r]] += dZ[r]*h2[ib[r]],  dh[ib[r]] += dZ[r]*h1[ia[r]]
+ * with f32 atomics into dh (f32).  For both forms drow != NULL replaces dZ by
+ * the row-broadcast dZ[r, :] = drow[r] (the 'inner' predictor, src/models.py:147-148). */
+int llp_hadamard_bwd_scatter(int dtype, int64_t R, int64_t H, const void* dZ, const float* drow,
+                             const int32_t* ia, const int32_t* ib, const void* h, float* dh, void* stream);
+
+/* ---------------------------------------------------------------- samplers
+ * Context sampler, src/main.py:33-50 + torch_cluster random_walk (p=q=1,
+ * coalesced=False semantics: rowptr = degree-count prefix sum of `row`,
+ * neighbours = col[rowptr[n]:rowptr[n+1]] in the given order).
+ * samples[b, 0] = start[b]; then the walks (ps_method 0 = 'rw': one walk of
+ * rw_step*hops steps; 1 = 'nb': rw_step walks of `hops` steps, start column
+ * dropped after the first); then rw_step*hops*ns_rate uniform negatives.
+ * Philox stream of walk i = stream_base + i, negatives stream_base + rw_step,
+ * with stream_base = 16*(*step_ctr) + stream_offset (device counter: graph-safe).
+ * Draw indices use the GLOBAL anchor position b + b_offset, so a rank holding
+ * anchors [b_offset, b_offset + B) draws what a single GPU would. */
+int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
+                        const int32_t* start, int64_t B, int64_t b_offset, int ps_method, int rw_step,
+                        int hops, int ns_rate, uint64_t seed, const int64_t* step_ctr,
+                        int64_t stream_offset, int32_t* samples, void* stream);
+
+/* torch.randint(0, N, [2, n_total]) (src/main.py:84,209) restricted to columns
+ * [offset, offset + n): out[0..n) = row 0, out[n..2n) = row 1.  Philox stream
+ * 16*(*step_ctr) + stream_offset, draw #(row*n_total + column). */
+int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
+                      const int64_t* step_ctr, int64_t stream_offset, int32_t* out, void* stream);
+
+/* Per-step index build for the minibatch layout (src/main.py:78,86-95):
+ * pos edges = pairs[perm[*step_ctr*P_stride + i]] (i < P), neg edges = neg[2,P];
+ * target (node id per h row) = [samples.flatten(), src(2P), dst(2P)]. */
+int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
+                      const int32_t* perm, const int64_t* step_ctr, int64_t perm_stride,
+                      int64_t P, const int32_t* neg, int32_t* target, void* stream);
+
+/* Teacher / predictor pair indices from samples: ia[b*C+c] = samples[b,0],
+ * ib[b*C+c] = samples[b,1+c]  (src/main.py:104,106). */
+int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* samples,
+                                int32_t* ia, int32_t* ib, void* stream);
+
+/* ---------------------------------------------------------------- SAGE aggregate
+ * out[i] = scale_i * sum_{e in [rowptr[i], rowptr[i+1])} w_e * x[col[e]]
+ *   mode 0 (forward mean):   scale_i = 1/max(deg_i,1), w_e = 1
+ *   mode 1 (backward of mean over the transposed CSR): scale_i = 1,
+ *          w_e = inv_deg[col[e]]
+ * PyG MessagePassing(aggr='mean') as used by SAGEConv / SAGEConv_updated
+ * (src/models.py:113, src/sageconv_updated.py:71-72), duplicates counted (Q2). */
+int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
+                      const void* x, int64_t ldx, const float* inv_deg, int mode,
+                      void* out, int64_t ldo, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------- optimiser tail
+ * Multi-tensor clip_grad_norm_(group, max_norm) per group (Q9) + Adam
+ * (torch.optim.Adam defaults, src/main.py:134-138,400-402).  Descriptor tables
+ * live in device memory (static per engine): see llp_tensor_desc. */
+typedef struct llp_tensor_desc {
+  float* param;        /* f32 master weights                                     */
+  float* grad;         /* f32 gradient                                           */
+  float* exp_avg;
+  float* exp_avg_sq;
+  void* shadow;        /* optional copy of param (same shape), or NULL           */
+  void* shadow_t;      /* optional transposed copy [cols][rows], or NULL         */
+  int64_t numel;
+  int64_t rows;        /* for the transposed copy                                */
+  int64_t cols;
+  int32_t group;       /* clip group id (0..7)                                   */
+  int32_t shadow_dtype;/* element type of shadow / shadow_t: LLP_F32 or LLP_BF16 */
+} llp_tensor_desc;
+
+/* sumsq[g] = sum of grad^2 over tensors of group g (n_groups <= 8). */
+int64_t llp_grad_sumsq_workspace_bytes(int n_tensors, int64_t max_numel);
+int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
+                   float* sumsq, void* workspace, int64_t workspace_bytes, void* stream);
+/* clip coef per group = min(1, max_norm/(sqrt(sumsq)+1e-6)) applied to the
+ * grads in place (as clip_grad_norm_ does); Adam step number *step (device,
+ * incremented by this call); refreshes the shadows.  sumsq NULL = no clip. */
+int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
+                  float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
+                  void* stream);
+/* Refresh bf16 shadows from masters (after loading weights). */
+int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream);
+
+/* ---------------------------------------------------------------- small utilities */
+int llp_convert(int src_dtype, int dst_dtype, int64_t n, const void* src, void* dst, void* stream);
+/* Sum loss terms into a running total (device), so an epoch needs one host sync. */
+int llp_accumulate(int64_t n, const float* src, float weight, double* dst, void* stream);
+int llp_increment(int64_t* ctr, void* stream);
+/* hipMemsetAsync(p, 0, bytes) on the stream. */
+int llp_zero(void* p, int64_t bytes, void* stream);
+
+/* Elementwise pieces of the module-level autograd ops (models.py):
+ * out = alpha * gy * (y > 0)   (y NULL: no mask)  — ReLU/dropout backward (src/models.py:52-53)
+ * dst[c, r] = src[r, c]                           — weight transpose for data-gradients
+ * out = a * b                                     — x_i * x_j backward (src/models.py:140)
+ * out[r, :] = z[r, :] * s[r]                      — 'inner' predictor backward
+ * out = gprob * prob * (1 - prob)                 — torch.sigmoid backward (src/models.py:150) */
+int llp_relu_bwd(int dtype, int64_t n, const void* gy, const void* y, float alpha, void* out, void* stream);
+int llp_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* dst, void* stream);
+int llp_mul(int dtype, int64_t n, const void* a, const void* b, void* out, void* stream);
+int llp_row_scale(int dtype, int64_t rows, int64_t cols, const void* z, const float* s, void* out, void* stream);
+int llp_sigmoid_bwd(int64_t n, const float* gprob, const float* prob, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLP_HIP_H_ */

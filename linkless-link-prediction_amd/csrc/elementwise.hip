@@ -1,0 +1,298 @@
+// Bandwidth-bound pieces of the step: Hadamard backward, clip_grad_norm_ + Adam
+// (multi-tensor, fused with the bf16 weight-shadow refresh), small utilities.
+#include "llp_common.h"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, int64_t i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+__device__ __forceinline__ void stf(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void stf(bf16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
+
+// ---------------------------------------------------------------- Hadamard backward
+// blockIdx.x < B: anchor b (its anchor row + C context rows);
+// else: a chunk of 64 label pairs.  Threads own columns.
+// drow != NULL: dZ[r, :] = drow[r] (the 'inner' predictor, whose logit is sum(x_i*x_j)).
+template <typename T>
+__device__ __forceinline__ float dz_at(const T* dZ, const float* drow, int64_t r, int64_t H, int64_t n) {
+  return drow ? drow[r] : ldf<T>(dZ + r * H, n);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void hadamard_bwd_blocks_kernel(int64_t B, int64_t C, int64_t L2, int64_t H,
+                                                                   const T* __restrict__ dZ,
+                                                                   const float* __restrict__ drow,
+                                                                   const T* __restrict__ h, T* __restrict__ dh) {
+  const int64_t C1 = C + 1;
+  if ((int64_t)blockIdx.x < B) {
+    const int64_t b = blockIdx.x;
+    const T* ha = h + (b * C1) * H;
+    for (int64_t n = threadIdx.x; n < H; n += blockDim.x) {
+      const float a = ldf<T>(ha, n);
+      float acc = 0.f;
+      for (int64_t c = 0; c < C; ++c) {
+        const float d = dz_at<T>(dZ, drow, b * C + c, H, n);
+        acc += d * ldf<T>(h + (b * C1 + 1 + c) * H, n);
+        stf(dh + (b * C1 + 1 + c) * H, n, d * a);
+      }
+      stf(dh + (b * C1) * H, n, acc);
+    }
+  } else {
+    const int64_t i0 = ((int64_t)blockIdx.x - B) * 64;
+    const int64_t i1 = min(L2, i0 + 64);
+    const int64_t base = B * C1;
+    for (int64_t i = i0; i < i1; ++i) {
+      const T* hs = h + (base + i) * H;
+      const T* hd = h + (base + L2 + i) * H;
+      for (int64_t n = threadIdx.x; n < H; n += blockDim.x) {
+        const float dv = dz_at<T>(dZ, drow, B * C + i, H, n);
+        stf(dh + (base + i) * H, n, dv * ldf<T>(hd, n));
+        stf(dh + (base + L2 + i) * H, n, dv * ldf<T>(hs, n));
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void hadamard_bwd_scatter_kernel(int64_t R, int64_t H, const T* __restrict__ dZ,
+                                                                    const float* __restrict__ drow,
+                                                                    const int32_t* __restrict__ ia,
+                                                                    const int32_t* __restrict__ ib,
+                                                                    const T* __restrict__ h, float* __restrict__ dh) {
+  const int64_t r = blockIdx.x;
+  if (r >= R) return;
+  const int64_t a = ia[r], bb = ib[r];
+  for (int64_t n = threadIdx.x; n < H; n += blockDim.x) {
+    const float d = dz_at<T>(dZ, drow, r, H, n);
+    atomicAdd(dh + a * H + n, d * ldf<T>(h + bb * H, n));
+    atomicAdd(dh + bb * H + n, d * ldf<T>(h + a * H, n));
+  }
+}
+
+// ---------------------------------------------------------------- optimiser
+constexpr int OPT_CHUNK = 4096;  // elements per block
+
+__device__ __forceinline__ void put_elem(void* base, int64_t i, float v, int dt) {
+  if (dt == LLP_BF16)
+    reinterpret_cast<bf16_t*>(base)[i] = f2bf(v);
+  else
+    reinterpret_cast<float*>(base)[i] = v;
+}
+__device__ __forceinline__ void put_shadows(const llp_tensor_desc& d, int64_t e, float v) {
+  if (d.shadow) put_elem(d.shadow, e, v, d.shadow_dtype);
+  if (d.shadow_t) {
+    const int64_t r = e / d.cols, c = e % d.cols;
+    put_elem(d.shadow_t, c * d.rows + r, v, d.shadow_dtype);
+  }
+}
+
+__global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* __restrict__ descs, int64_t max_chunks,
+                                                         float* __restrict__ partial) {
+  __shared__ float red[4];
+  const llp_tensor_desc d = descs[blockIdx.y];
+  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
+  float acc = 0.f;
+  if (e0 < d.numel) {
+    const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      const float g = d.grad[e];
+      acc += g * g;
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors, int64_t max_chunks,
+                                    const float* __restrict__ partial, int n_groups, float* __restrict__ sumsq) {
+  // one thread per group; fixed order -> deterministic
+  const int gidx = threadIdx.x;
+  if (gidx >= n_groups) return;
+  double s = 0.0;
+  for (int t = 0; t < n_tensors; ++t) {
+    if (descs[t].group != gidx) continue;
+    const int64_t nch = (descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK;
+    // per-tensor norm first, as torch.norm(stack([norm(g) for g])) does
+    double ts = 0.0;
+    for (int64_t c = 0; c < nch; ++c) ts += (double)partial[t * max_chunks + c];
+    s += ts;
+  }
+  sumsq[gidx] = (float)s;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __restrict__ descs,
+                                                   const float* __restrict__ sumsq, float max_norm, float lr,
+                                                   float beta1, float beta2, float eps,
+                                                   const int64_t* __restrict__ step) {
+  const llp_tensor_desc d = descs[blockIdx.y];
+  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
+  if (e0 >= d.numel) return;
+  const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
+  float coef = 1.f;
+  if (sumsq) {
+    const float total = sqrtf(sumsq[d.group]);
+    coef = fminf(max_norm / (total + 1e-6f), 1.f);   // clip_grad_norm_ (clamped coef)
+  }
+  const double t = (double)(*step + 1);
+  const float bc1 = (float)(1.0 - pow((double)beta1, t));
+  const float bc2s = (float)sqrt(1.0 - pow((double)beta2, t));
+  const float step_size = lr / bc1;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const float g = d.grad[e] * coef;
+    if (coef != 1.f) d.grad[e] = g;   // clip_grad_norm_ scales the .grad in place
+    const float m = beta1 * d.exp_avg[e] + (1.f - beta1) * g;
+    const float v = beta2 * d.exp_avg_sq[e] + (1.f - beta2) * g * g;
+    d.exp_avg[e] = m;
+    d.exp_avg_sq[e] = v;
+    const float denom = sqrtf(v) / bc2s + eps;
+    const float pnew = d.param[e] - step_size * (m / denom);
+    d.param[e] = pnew;
+    put_shadows(d, e, pnew);
+  }
+}
+
+__global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __restrict__ descs) {
+  const llp_tensor_desc d = descs[blockIdx.y];
+  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
+  if (e0 >= d.numel) return;
+  const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) put_shadows(d, e, d.param[e]);
+}
+
+__global__ void increment_kernel(int64_t* ctr) { *ctr += 1; }
+
+__global__ void convert_kernel(int src_bf16, int dst_bf16, int64_t n, const void* __restrict__ src,
+                               void* __restrict__ dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = src_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(src)[i]) : reinterpret_cast<const float*>(src)[i];
+    if (dst_bf16)
+      reinterpret_cast<bf16_t*>(dst)[i] = f2bf(v);
+    else
+      reinterpret_cast<float*>(dst)[i] = v;
+  }
+}
+
+__global__ void accumulate_kernel(int64_t n, const float* __restrict__ src, float weight, double* __restrict__ dst) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) dst[i] += (double)src[i] * (double)weight;
+}
+
+int64_t max_chunks_of(int64_t max_numel) { return (max_numel + OPT_CHUNK - 1) / OPT_CHUNK; }
+
+}  // namespace
+
+extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t H, const void* dZ,
+                                       const float* drow, const void* h, void* dh, void* stream) {
+  LLP_CHECK_ARG((dZ || drow) && h && dh, "llp_hadamard_bwd_blocks: null pointer");
+  const int64_t nblk = B + (L2 + 63) / 64;
+  if (nblk == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(hadamard_bwd_blocks_kernel<bf16_t>, dim3((unsigned)nblk), dim3(256), 0, s, B, C, L2, H,
+                       (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh);
+  else
+    hipLaunchKernelGGL(hadamard_bwd_blocks_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, B, C, L2, H,
+                       (const float*)dZ, drow, (const float*)h, (float*)dh);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_hadamard_bwd_scatter(int dtype, int64_t R, int64_t H, const void* dZ, const float* drow,
+                                        const int32_t* ia, const int32_t* ib, const void* h, float* dh, void* stream) {
+  LLP_CHECK_ARG((dZ || drow) && ia && ib && h && dh, "llp_hadamard_bwd_scatter: null pointer");
+  if (R == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(hadamard_bwd_scatter_kernel<bf16_t>, dim3((unsigned)R), dim3(256), 0, s, R, H,
+                       (const bf16_t*)dZ, drow, ia, ib, (const bf16_t*)h, dh);
+  else
+    hipLaunchKernelGGL(hadamard_bwd_scatter_kernel<float>, dim3((unsigned)R), dim3(256), 0, s, R, H, (const float*)dZ,
+                       drow, ia, ib, (const float*)h, dh);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+// The descriptor table is in device memory; the caller passes max_numel (the
+// largest numel in the table) so the grid is sized without reading it back.
+extern "C" int64_t llp_grad_sumsq_workspace_bytes(int n_tensors, int64_t max_numel) {
+  return (int64_t)n_tensors * max_chunks_of(max_numel) * (int64_t)sizeof(float);
+}
+
+extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
+                              float* sumsq, void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(descs && sumsq && workspace, "llp_grad_sumsq: null pointer");
+  LLP_CHECK_ARG(n_groups >= 1 && n_groups <= 8, "llp_grad_sumsq: n_groups in [1,8]");
+  LLP_CHECK_ARG(workspace_bytes >= llp_grad_sumsq_workspace_bytes(n_tensors, max_numel),
+                "llp_grad_sumsq: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t mc = max_chunks_of(max_numel);
+  // blocks past a tensor's numel exit immediately; x extent bounded by kMaxNumel
+  hipLaunchKernelGGL(grad_sumsq_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, mc,
+                     (float*)workspace);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(grad_sumsq_finalize, dim3(1), dim3(64), 0, s, descs, n_tensors, mc, (const float*)workspace,
+                     n_groups, sumsq);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
+                             float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
+                             void* stream) {
+  LLP_CHECK_ARG(descs && step, "llp_adam_step: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t mc = max_chunks_of(max_numel);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, sumsq, max_norm, lr,
+                     beta1, beta2, eps, (const int64_t*)step);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(increment_kernel, dim3(1), dim3(1), 0, s, step);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream) {
+  LLP_CHECK_ARG(descs, "llp_refresh_shadows: null pointer");
+  const int64_t mc = max_chunks_of(max_numel);
+  hipLaunchKernelGGL(shadow_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream, descs);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_convert(int src_dtype, int dst_dtype, int64_t n, const void* src, void* dst, void* stream) {
+  LLP_CHECK_ARG(src && dst, "llp_convert: null pointer");
+  if (n == 0) return LLP_OK;
+  unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(convert_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, src_dtype == LLP_BF16,
+                     dst_dtype == LLP_BF16, n, src, dst);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_accumulate(int64_t n, const float* src, float weight, double* dst, void* stream) {
+  LLP_CHECK_ARG(src && dst, "llp_accumulate: null pointer");
+  hipLaunchKernelGGL(accumulate_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, src, weight,
+                     dst);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_zero(void* p, int64_t bytes, void* stream) {
+  LLP_CHECK_ARG(p || bytes == 0, "llp_zero: null pointer");
+  if (bytes == 0) return LLP_OK;
+  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
+  if (e != hipSuccess) return llp::set_error((int)e, "llp_zero: %s", hipGetErrorString(e));
+  return LLP_OK;
+}
+
+extern "C" int llp_increment(int64_t* ctr, void* stream) {
+  LLP_CHECK_ARG(ctr, "llp_increment: null pointer");
+  hipLaunchKernelGGL(increment_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, ctr);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}

@@ -1,0 +1,595 @@
+// MFMA GEMMs for the LLP distillation step (gfx950).
+//
+//   llp_gemm_nt : C[m,n] = epi(alpha * sum_k A[m,k] B[n,k])   forward / data-grad
+//   llp_gemm_tn : C[p,q] = sum_m A[m,p] B[m,q]                weight-grad (split-m slabs)
+//
+// Operands are llp_operand rows: plain, gathered (idx) or Hadamard of two
+// gathered rows — the row gather x[this_target] (src/main.py:95-96) and the
+// predictor input x_i*x_j (src/models.py:140) happen while staging, never in HBM.
+//
+// Tiles: 128x128 per 256-thread workgroup (4 waves, 2x2, 64x64 per wave),
+// BK = 128 bytes of K per row (64 bf16 / 32 f32), register-staged double
+// buffering into one LDS array, XOR-swizzled 16-B chunks.
+//   bf16: v_mfma_f32_16x16x32_bf16, fragments by ds_read_b128 (NT) or
+//         ds_read_b64_tr_b16 transposed reads (TN).
+//   f32 : v_mfma_f32_16x16x4_f32 (exact f32 fma chain), fragments by
+//         ds_read_b128 with a k-permutation shared by both operands (NT) or
+//         ds_read_b32 (TN).
+#include "llp_common.h"
+
+namespace {
+
+constexpr int BM = 128;
+constexpr int BN = 128;
+constexpr int NTHREADS = 256;
+
+struct Op {
+  const char* ptr;
+  const int32_t* idx;
+  const char* ptr2;
+  const int32_t* idx2;
+  int64_t ld;   // elements
+  int64_t ld2;
+};
+
+struct NTParams {
+  Op A, B;
+  int64_t M, N, K;
+  void* C;
+  int64_t ldc;
+  int c_bf16;
+  const float* bias;
+  int act;
+  const void* aux;
+  int64_t ld_aux;
+  int aux_bf16;
+  float alpha;
+  float drop_p;          // 0 = no dropout
+  uint32_t drop_thresh;  // keep iff (x >> 8) >= drop_thresh  (u >= p, u = (x>>8) 2^-24)
+  float drop_scale;      // 1 / (1 - p)
+  uint64_t drop_seed;
+  const int64_t* drop_ctr;
+  int64_t drop_stream;
+};
+
+struct TNParams {
+  Op A, B;
+  int64_t M, P, Q;
+  int64_t mchunk;
+  int64_t splits;
+  float* ws;  // [splits][P][Q]
+};
+
+template <typename T>
+struct Traits;
+template <>
+struct Traits<float> {
+  static constexpr int ELEMS = 4;
+};
+template <>
+struct Traits<bf16_t> {
+  static constexpr int ELEMS = 8;
+};
+
+__device__ __forceinline__ float ld_elem(const float* p) { return *p; }
+__device__ __forceinline__ float ld_elem(const bf16_t* p) { return bf2f(*p); }
+
+__device__ __forceinline__ uint4 mul_chunk(uint4 a, uint4 b, float*) {
+  uint4 r;
+  r.x = __float_as_uint(__uint_as_float(a.x) * __uint_as_float(b.x));
+  r.y = __float_as_uint(__uint_as_float(a.y) * __uint_as_float(b.y));
+  r.z = __float_as_uint(__uint_as_float(a.z) * __uint_as_float(b.z));
+  r.w = __float_as_uint(__uint_as_float(a.w) * __uint_as_float(b.w));
+  return r;
+}
+__device__ __forceinline__ uint32_t mul_bf2(uint32_t a, uint32_t b) {
+  const float a0 = __uint_as_float(a << 16), a1 = __uint_as_float(a & 0xFFFF0000u);
+  const float b0 = __uint_as_float(b << 16), b1 = __uint_as_float(b & 0xFFFF0000u);
+  return (uint32_t)f2bf(a0 * b0) | ((uint32_t)f2bf(a1 * b1) << 16);
+}
+__device__ __forceinline__ uint4 mul_chunk(uint4 a, uint4 b, bf16_t*) {
+  return make_uint4(mul_bf2(a.x, b.x), mul_bf2(a.y, b.y), mul_bf2(a.z, b.z), mul_bf2(a.w, b.w));
+}
+
+// Load ELEMS consecutive elements [k0, k0+ELEMS) of a resolved row (p0 [, p1]).
+// Elements at k >= K read as 0.  `valid` = row in range.
+template <typename T, bool VEC>
+__device__ __forceinline__ uint4 load_chunk(const T* p0, const T* p1, int64_t k0, int64_t K, bool valid) {
+  constexpr int E = Traits<T>::ELEMS;
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (!valid) return r;
+  if (VEC) {
+    if (k0 < K) {
+      r = *reinterpret_cast<const uint4*>(p0 + k0);
+      if (p1) r = mul_chunk(r, *reinterpret_cast<const uint4*>(p1 + k0), (T*)nullptr);
+    }
+  } else {
+    T v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      T x = T(0);
+      if (k0 + e < K) {
+        x = p0[k0 + e];
+        if (p1) {
+          if constexpr (sizeof(T) == 4) {
+            x = x * p1[k0 + e];
+          } else {
+            x = f2bf(bf2f(x) * bf2f(p1[k0 + e]));
+          }
+        }
+      }
+      v[e] = x;
+    }
+    r = *reinterpret_cast<uint4*>(v);
+  }
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ const T* row_ptr(const Op& op, int64_t r) {
+  const int64_t pr = op.idx ? (int64_t)op.idx[r] : r;
+  return reinterpret_cast<const T*>(op.ptr) + pr * op.ld;
+}
+template <typename T>
+__device__ __forceinline__ const T* row_ptr2(const Op& op, int64_t r) {
+  if (!op.ptr2) return nullptr;
+  const int64_t pr = op.idx2 ? (int64_t)op.idx2[r] : r;
+  return reinterpret_cast<const T*>(op.ptr2) + pr * op.ld2;
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md T1): blocks that share an
+// XCD (same bid % 8) get a contiguous range of logical tiles.
+__device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
+  if (nwg < 8) return bid;
+  const int64_t q = nwg / 8, r = nwg % 8;
+  const int64_t xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// ============================================================== NT kernel
+template <typename T, bool VEC>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
+  constexpr int E = Traits<T>::ELEMS;
+  constexpr int BK = 8 * E;  // 8 chunks of 16 B per row
+  __shared__ uint4 smem[2 * (BM + BN) * 8];
+  uint4* sA0 = smem;
+  uint4* sB0 = smem + BM * 8;
+  const int buf_stride = (BM + BN) * 8;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t tilesN = (p.N + BN - 1) / BN;
+  const int64_t tilesM = (p.M + BM - 1) / BM;
+  const int64_t lt = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int64_t tm = lt / tilesN, tn = lt % tilesN;
+  const int64_t m0 = tm * BM, n0 = tn * BN;
+
+  // staging assignment: chunk c = tid + 256*i -> row (tid>>3) + 32*i, kc = tid&7
+  const int kc = tid & 7;
+  const T* pa[4];
+  const T* pa2[4];
+  const T* pb[4];
+  const T* pb2[4];
+  bool va[4], vb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    int64_t gm = m0 + r;
+    va[i] = gm < p.M;
+    gm = va[i] ? gm : (p.M - 1);
+    pa[i] = row_ptr<T>(p.A, gm);
+    pa2[i] = row_ptr2<T>(p.A, gm);
+    int64_t gn = n0 + r;
+    vb[i] = gn < p.N;
+    gn = vb[i] ? gn : (p.N - 1);
+    pb[i] = row_ptr<T>(p.B, gn);
+    pb2[i] = row_ptr2<T>(p.B, gn);
+  }
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int64_t kt) {
+    const int64_t k0 = kt * BK + kc * E;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i] = load_chunk<T, VEC>(pa[i], pa2[i], k0, p.K, va[i]);
+      rb[i] = load_chunk<T, VEC>(pb[i], pb2[i], k0, p.K, vb[i]);
+    }
+  };
+  auto lstore = [&](int buf) {
+    uint4* sA = sA0 + buf * buf_stride;
+    uint4* sB = sB0 + buf * buf_stride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      sA[r * 8 + (kc ^ (r & 7))] = ra[i];
+      sB[r * 8 + (kc ^ (r & 7))] = rb[i];
+    }
+  };
+
+  float4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = (p.K + BK - 1) / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+
+  const int g = lane >> 4, li = lane & 15;
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const uint4* sA = sA0 + buf * buf_stride;
+    const uint4* sB = sB0 + buf * buf_stride;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        short8 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm * 64 + i * 16 + li;
+          uint4 v = sA[r * 8 + ((g + 4 * s) ^ (r & 7))];
+          af[i] = *reinterpret_cast<short8*>(&v);
+          const int c = wn * 64 + i * 16 + li;
+          uint4 w = sB[c * 8 + ((g + 4 * s) ^ (c & 7))];
+          bfr[i] = *reinterpret_cast<short8*>(&w);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        float4_t af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm * 64 + i * 16 + li;
+          uint4 v = sA[r * 8 + ((kb * 4 + g) ^ (r & 7))];
+          af[i] = *reinterpret_cast<float4_t*>(&v);
+          const int c = wn * 64 + i * 16 + li;
+          uint4 w = sB[c * 8 + ((kb * 4 + g) ^ (c & 7))];
+          bfr[i] = *reinterpret_cast<float4_t*>(&w);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][t], bfr[j][t], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] -> row m0 + wm*64 + i*16 + g*4 + r, col n0 + wn*64 + j*16 + li
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = n0 + wn * 64 + j * 16 + li;
+    if (col >= p.N) continue;
+    const float bias = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + g * 4 + r;
+        if (row >= p.M) continue;
+        float v = p.alpha * acc[i][j][r] + bias;
+        if (p.act == LLP_ACT_RELU) {
+          v = fmaxf(v, 0.f);
+        } else if (p.act == LLP_ACT_RELU_BWD) {
+          const float a = p.aux_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p.aux)[row * p.ld_aux + col])
+                                     : reinterpret_cast<const float*>(p.aux)[row * p.ld_aux + col];
+          v = a > 0.f ? v : 0.f;
+        }
+        if (p.drop_p > 0.f) {
+          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)(row * p.N + col));
+          v = (x >> 8) >= p.drop_thresh ? v * p.drop_scale : 0.f;
+        }
+        if (p.c_bf16)
+          reinterpret_cast<bf16_t*>(p.C)[row * p.ldc + col] = f2bf(v);
+        else
+          reinterpret_cast<float*>(p.C)[row * p.ldc + col] = v;
+      }
+    }
+  }
+}
+
+// ============================================================== TN kernel
+// C[p,q] = sum_m A[m,p] B[m,q]; block (tile, split z) writes ws[z][P][Q].
+// bf16: BKm = 64 rows of m per step; LDS image [m][128 cols] (256 B rows),
+//       swizzle ch ^ (((row&3)<<2) | ((row>>2)&3))  (T10 image (b)),
+//       fragments via ds_read_b64_tr_b16.
+// f32 : BKm = 32; LDS image [m][128 + 16 pad] floats; ds_read_b32.
+__device__ __forceinline__ int tr_swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
+  constexpr int E = Traits<T>::ELEMS;
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int BKM = BF ? 64 : 32;
+  constexpr int CPR = BF ? 16 : 32;               // 16-B chunks per 128-col row
+  constexpr int ROWU4 = BF ? 16 : 36;             // uint4 per LDS row (f32 padded by 16 floats)
+  constexpr int TILE_U4 = BKM * ROWU4;
+  __shared__ uint4 smem[2 * 2 * TILE_U4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wp = wave >> 1, wq = wave & 1;
+  const int64_t tilesQ = (p.Q + BN - 1) / BN;
+  const int64_t tilesP = (p.P + BM - 1) / BM;
+  const int64_t ntile = tilesP * tilesQ;
+  const int64_t splits = p.splits;
+  const int64_t lt = xcd_remap(blockIdx.x, ntile * splits);
+  // the splits of one tile are adjacent in logical order -> tile = lt / splits
+  const int64_t tile = lt / splits, z = lt % splits;
+  const int64_t tp = tile / tilesQ, tq = tile % tilesQ;
+  const int64_t p0 = tp * BM, q0 = tq * BN;
+  const int64_t mbeg = z * p.mchunk;
+  const int64_t mend = min(p.M, mbeg + p.mchunk);
+
+  // staging: chunk c = tid + 256*i -> m row c / CPR, chunk (c % CPR)
+  constexpr int ROWS_PER_PASS = NTHREADS / CPR;  // 16 (bf16) or 8 (f32)
+  const int cc = tid % CPR;
+  const int rr = tid / CPR;
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int64_t mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = mt + rr + ROWS_PER_PASS * i;
+      const bool v = m < mend;
+      const int64_t mm = v ? m : mbeg;
+      const T* a0 = row_ptr<T>(p.A, mm);
+      const T* a1 = row_ptr2<T>(p.A, mm);
+      const T* b0 = row_ptr<T>(p.B, mm);
+      const T* b1 = row_ptr2<T>(p.B, mm);
+      // columns beyond P / Q read 0 (k-bound = P / Q on the column axis)
+      ra[i] = load_chunk<T, VEC>(a0 + p0, a1 ? a1 + p0 : nullptr, (int64_t)cc * E, p.P - p0, v);
+      rb[i] = load_chunk<T, VEC>(b0 + q0, b1 ? b1 + q0 : nullptr, (int64_t)cc * E, p.Q - q0, v);
+    }
+  };
+  auto lstore = [&](int buf) {
+    uint4* sA = smem + buf * 2 * TILE_U4;
+    uint4* sB = sA + TILE_U4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rr + ROWS_PER_PASS * i;
+      const int ch = BF ? tr_swz(r, cc) : cc;
+      sA[r * ROWU4 + ch] = ra[i];
+      sB[r * ROWU4 + ch] = rb[i];
+    }
+  };
+
+  float4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (mbeg < mend) {
+    const int64_t nsteps = (mend - mbeg + BKM - 1) / BKM;
+    gload(mbeg);
+    lstore(0);
+    __syncthreads();
+    const int g = lane >> 4, li = lane & 15;
+    for (int64_t st = 0; st < nsteps; ++st) {
+      const int buf = st & 1;
+      if (st + 1 < nsteps) gload(mbeg + (st + 1) * BKM);
+      const uint4* sA = smem + buf * 2 * TILE_U4;
+      const uint4* sB = sA + TILE_U4;
+      if constexpr (BF) {
+        typedef __attribute__((address_space(3))) short4_t lds_s4;
+        const int q4 = li >> 2, pp = li & 3;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          short8 af[4], bfr[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int col = wp * 64 + i * 16 + 4 * pp;
+            const int colb = wq * 64 + i * 16 + 4 * pp;
+#pragma unroll
+            for (int hlf = 0; hlf < 2; ++hlf) {
+              const int row = s * 32 + 8 * g + 4 * hlf + q4;
+              const int offa = row * 256 + 16 * tr_swz(row, col >> 3) + 8 * ((col >> 2) & 1);
+              const int offb = row * 256 + 16 * tr_swz(row, colb >> 3) + 8 * ((colb >> 2) & 1);
+              short4_t ta = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                  (lds_s4*)((__attribute__((address_space(3))) char*)((__attribute__((address_space(3))) uint4*)sA) + offa));
+              short4_t tb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                  (lds_s4*)((__attribute__((address_space(3))) char*)((__attribute__((address_space(3))) uint4*)sB) + offb));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                af[i][4 * hlf + e] = ta[e];
+                bfr[i][4 * hlf + e] = tb[e];
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+      } else {
+        const float* fA = reinterpret_cast<const float*>(sA);
+        const float* fB = reinterpret_cast<const float*>(sB);
+#pragma unroll
+        for (int t = 0; t < BKM / 4; ++t) {
+          const int row = 4 * t + g;
+          float af[4], bfr[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            af[i] = fA[row * (ROWU4 * 4) + wp * 64 + i * 16 + li];
+            bfr[i] = fB[row * (ROWU4 * 4) + wq * 64 + i * 16 + li];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      if (st + 1 < nsteps) lstore(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // slab store: ws[z][row][col]
+  const int g = lane >> 4, li = lane & 15;
+  float* out = p.ws + z * p.P * p.Q;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = q0 + wq * 64 + j * 16 + li;
+    if (col >= p.Q) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = p0 + wp * 64 + i * 16 + g * 4 + r;
+        if (row < p.P) out[row * p.Q + col] = acc[i][j][r];
+      }
+  }
+}
+
+__global__ void slab_reduce_kernel(const float* __restrict__ ws, int64_t splits, int64_t P, int64_t Q,
+                                   float* __restrict__ C, int64_t ldc, int accumulate) {
+  const int64_t n = P * Q;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t z = 0; z < splits; ++z) s += ws[z * n + e];
+    const int64_t r = e / Q, c = e % Q;
+    float* dst = C + r * ldc + c;
+    *dst = accumulate ? *dst + s : s;
+  }
+}
+
+Op to_op(const llp_operand* o) {
+  Op r;
+  r.ptr = reinterpret_cast<const char*>(o->ptr);
+  r.idx = o->idx;
+  r.ptr2 = reinterpret_cast<const char*>(o->ptr2);
+  r.idx2 = o->idx2;
+  r.ld = o->ld;
+  r.ld2 = o->ptr2 ? o->ld2 : 0;
+  return r;
+}
+
+bool aligned_op(const llp_operand* o, int esize, int64_t extent_mult) {
+  auto al = [&](const void* p, int64_t ld) {
+    return ((uintptr_t)p % 16 == 0) && ((ld * esize) % 16 == 0);
+  };
+  bool ok = al(o->ptr, o->ld);
+  if (o->ptr2) ok = ok && al(o->ptr2, o->ld2);
+  return ok && (extent_mult % (16 / esize) == 0);
+}
+
+int64_t tn_splits(int dtype, int64_t M, int64_t P, int64_t Q) {
+  const int64_t tiles = ((P + BM - 1) / BM) * ((Q + BN - 1) / BN);
+  const int64_t bkm = dtype == LLP_BF16 ? 64 : 32;
+  int64_t splits = (1024 + tiles - 1) / tiles;
+  const int64_t maxs = (M + bkm * 8 - 1) / (bkm * 8);  // at least 8 m-steps per split
+  if (splits > maxs) splits = maxs;
+  if (splits < 1) splits = 1;
+  return splits;
+}
+
+}  // namespace
+
+extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp_operand* A,
+                           const llp_operand* B, void* C, int64_t ldc, int c_dtype, const float* bias,
+                           int act, const void* aux, int64_t ld_aux, int aux_dtype, float alpha,
+                           const llp_dropout* dropout, void* stream) {
+  LLP_CHECK_ARG(A && B && C, "llp_gemm_nt: null operand");
+  LLP_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "llp_gemm_nt: negative size");
+  LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_nt: bad dtype %d", dtype);
+  LLP_CHECK_ARG(act != LLP_ACT_RELU_BWD || aux, "llp_gemm_nt: RELU_BWD needs aux");
+  if (M == 0 || N == 0) return LLP_OK;
+  NTParams p;
+  p.A = to_op(A);
+  p.B = to_op(B);
+  p.M = M; p.N = N; p.K = K;
+  p.C = C; p.ldc = ldc; p.c_bf16 = c_dtype == LLP_BF16;
+  p.bias = bias; p.act = act; p.aux = aux; p.ld_aux = ld_aux; p.aux_bf16 = aux_dtype == LLP_BF16;
+  p.alpha = alpha;
+  p.drop_p = 0.f;
+  p.drop_thresh = 0;
+  p.drop_scale = 1.f;
+  p.drop_seed = 0;
+  p.drop_ctr = nullptr;
+  p.drop_stream = 0;
+  if (dropout && dropout->p > 0.f) {
+    LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_gemm_nt: dropout p in (0,1) needs step_ctr");
+    p.drop_p = dropout->p;
+    p.drop_thresh = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    p.drop_scale = 1.f / (1.f - dropout->p);
+    p.drop_seed = dropout->seed;
+    p.drop_ctr = dropout->step_ctr;
+    p.drop_stream = dropout->stream_offset;
+  }
+  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  LLP_CHECK_ARG(tiles < (1ll << 31), "llp_gemm_nt: too many tiles");
+  hipStream_t s = (hipStream_t)stream;
+  const int es = dtype == LLP_BF16 ? 2 : 4;
+  const bool vec = aligned_op(A, es, K) && aligned_op(B, es, K);
+  dim3 grid((unsigned)tiles);
+  if (dtype == LLP_BF16) {
+    if (vec) hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, true>), grid, dim3(NTHREADS), 0, s, p);
+    else hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, false>), grid, dim3(NTHREADS), 0, s, p);
+  } else {
+    if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true>), grid, dim3(NTHREADS), 0, s, p);
+    else hipLaunchKernelGGL((gemm_nt_kernel<float, false>), grid, dim3(NTHREADS), 0, s, p);
+  }
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q) {
+  return tn_splits(dtype, M, P, Q) * P * Q * (int64_t)sizeof(float);
+}
+
+extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A,
+                           const llp_operand* B, float* C, int64_t ldc, int accumulate, void* workspace,
+                           int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(A && B && C, "llp_gemm_tn: null operand");
+  LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_tn: bad dtype %d", dtype);
+  if (P == 0 || Q == 0) return LLP_OK;
+  const int64_t splits = tn_splits(dtype, M, P, Q);
+  if (workspace_bytes < splits * P * Q * (int64_t)sizeof(float) || !workspace)
+    return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace %lld < %lld", (long long)workspace_bytes,
+                          (long long)(splits * P * Q * 4));
+  TNParams p;
+  p.A = to_op(A);
+  p.B = to_op(B);
+  p.M = M; p.P = P; p.Q = Q;
+  const int64_t bkm = dtype == LLP_BF16 ? 64 : 32;
+  int64_t mchunk = (M + splits - 1) / splits;
+  mchunk = (mchunk + bkm - 1) / bkm * bkm;
+  p.mchunk = mchunk > 0 ? mchunk : bkm;
+  p.ws = reinterpret_cast<float*>(workspace);
+  const int64_t tiles = ((P + BM - 1) / BM) * ((Q + BN - 1) / BN);
+  hipStream_t s = (hipStream_t)stream;
+  const int es = dtype == LLP_BF16 ? 2 : 4;
+  const bool vec = aligned_op(A, es, P) && aligned_op(B, es, Q);
+  p.splits = splits;
+  TNParams pp = p;
+  dim3 g2((unsigned)(tiles * splits));
+  if (dtype == LLP_BF16) {
+    if (vec) hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, true>), g2, dim3(NTHREADS), 0, s, pp);
+    else hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, false>), g2, dim3(NTHREADS), 0, s, pp);
+  } else {
+    if (vec) hipLaunchKernelGGL((gemm_tn_kernel<float, true>), g2, dim3(NTHREADS), 0, s, pp);
+    else hipLaunchKernelGGL((gemm_tn_kernel<float, false>), g2, dim3(NTHREADS), 0, s, pp);
+  }
+  LLP_LAUNCH_CHECK();
+  const int64_t n = P * Q;
+  unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, (const float*)workspace, splits, P, Q, C, ldc,
+                     accumulate);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}

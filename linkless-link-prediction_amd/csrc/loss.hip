@@ -1,0 +1,338 @@
+// Fused distillation losses and the link-predictor head.
+//
+//   llp_llp_loss : one wavefront per anchor — sigmoid, softmax/KL (LLP_D),
+//                  all-pairs margin rank (LLP_R), plus the label BCE rows, and
+//                  d(loss)/d(logit) for every predictor row.  Replaces
+//                  src/main.py:98-130 (which materialises B x C(C-1)/2 pair
+//                  tensors and a host-built numpy pair index every step).
+//   llp_head_fwd / llp_head_bwd : last Linear(H,1)+sigmoid of LinkPredictor
+//                  (src/models.py:146,150) as a row-dot, and its backward with
+//                  the ReLU of the layer below fused.
+#include "llp_common.h"
+
+namespace {
+
+constexpr int MAXC = 1024;
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + expf(-z)); }
+
+// partial sums per block: [bce, kl, rank]
+__global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, const float* __restrict__ s_logit,
+                                                         const float* __restrict__ t_prob, double B_total,
+                                                         float margin, float T, float w_d, float w_r,
+                                                         float loss_scale, float* __restrict__ dlogit,
+                                                         float* __restrict__ partial) {
+  __shared__ float ss[WAVES][MAXC];
+  __shared__ float tt[WAVES][MAXC];
+  __shared__ float red[WAVES][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * WAVES + w;
+  float kl_acc = 0.f, rk_acc = 0.f;
+  if (b < B) {
+    const float* sl = s_logit + b * C;
+    const float* tp = t_prob + b * C;
+    float* sw = ss[w];
+    float* tw = tt[w];
+    // sigmoid probabilities (Q4) and the softmax statistics of s/T and t/T
+    float ms = -INFINITY, mt = -INFINITY;
+    for (int c = lane; c < C; c += 64) {
+      const float s = sigmoidf_(sl[c]);
+      const float t = tp[c];
+      sw[c] = s;
+      tw[c] = t;
+      ms = fmaxf(ms, s / T);
+      mt = fmaxf(mt, t / T);
+    }
+    ms = wave_max(ms);
+    mt = wave_max(mt);
+    float zs = 0.f, zt = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      zs += expf(sw[c] / T - ms);
+      zt += expf(tw[c] / T - mt);
+    }
+    zs = wave_sum(zs);
+    zt = wave_sum(zt);
+    const float lse_s = logf(zs) + ms, lse_t = logf(zt) + mt;
+    const float inv_b = (float)(1.0 / B_total);
+    const double npairs = (double)C * (double)(C - 1) / 2.0;
+    const float inv_bp = npairs > 0 ? (float)(1.0 / (B_total * npairs)) : 0.f;
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < C; i += 64) {
+      const float si = sw[i], ti = tw[i];
+      // KL(p_t || q_s) pointwise, kl_div(log q, p, 'sum') = p (log p - log q)
+      const float logq = si / T - lse_s, logp = ti / T - lse_t;
+      const float pt = expf(logp), qs = expf(logq);
+      kl_acc += pt * (logp - logq);
+      const float dkl = T * (qs - pt) * inv_b;  // d/ds of KL * T^2 / B
+      // rank: pairs (i, j) lexicographic, i < j  (itertools.combinations)
+      float gi = 0.f;
+      for (int j = 0; j < C; ++j) {
+        if (j == i) continue;
+        const float sj = sw[j], tj = tw[j];
+        if (j > i) {
+          const float y = ti > tj + margin ? 1.f : (ti < tj - margin ? -1.f : 0.f);
+          const float h = -y * (si - sj) + margin;
+          rk_acc += fmaxf(h, 0.f);
+          if (h >= 0.f) gi -= y;
+        } else {
+          const float y = tj > ti + margin ? 1.f : (tj < ti - margin ? -1.f : 0.f);
+          const float h = -y * (sj - si) + margin;
+          if (h >= 0.f) gi += y;
+        }
+      }
+      const float ds = w_d * dkl + w_r * gi * inv_bp;
+      dlogit[b * C + i] = loss_scale * ds * si * (1.f - si);  // through the sigmoid
+    }
+    kl_acc = wave_sum(kl_acc) * (T * T) * inv_b;
+    rk_acc = wave_sum(rk_acc) * inv_bp;
+  }
+  if (lane == 0) {
+    red[w][0] = kl_acc;
+    red[w][1] = rk_acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float k = 0.f, r = 0.f;
+    for (int i = 0; i < WAVES; ++i) {
+      k += red[i][0];
+      r += red[i][1];
+    }
+    partial[blockIdx.x * 3 + 0] = 0.f;
+    partial[blockIdx.x * 3 + 1] = k;
+    partial[blockIdx.x * 3 + 2] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void bce_kernel(int64_t n, int64_t n_pos, const float* __restrict__ logit,
+                                                  double n_total, float w_label, float loss_scale,
+                                                  float* __restrict__ dlogit, float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (r < n) {
+    const float o = sigmoidf_(logit[r]);
+    const float y = r < n_pos ? 1.f : 0.f;
+    // nn.BCELoss: -(y*max(log o, -100) + (1-y)*max(log(1-o), -100)), mean
+    const float lo = fmaxf(logf(o), -100.f), l1o = fmaxf(logf(1.f - o), -100.f);
+    l = -(y * lo + (1.f - y) * l1o);
+    const float go = (o - y) / fmaxf((1.f - o) * o, 1e-12f) / (float)n_total;
+    dlogit[r] = loss_scale * w_label * go * o * (1.f - o);
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x * 3 + 0] = (red[0] + red[1] + red[2] + red[3]) / (float)n_total;
+    partial[blockIdx.x * 3 + 1] = 0.f;
+    partial[blockIdx.x * 3 + 2] = 0.f;
+  }
+}
+
+__global__ void loss_finalize_kernel(const float* __restrict__ partial, int64_t nblocks, float w_label, float w_d,
+                                     float w_r, float* __restrict__ terms, int accumulate) {
+  __shared__ double red[3][256];
+  double a[3] = {0, 0, 0};
+  for (int64_t i = threadIdx.x; i < nblocks; i += blockDim.x)
+    for (int k = 0; k < 3; ++k) a[k] += (double)partial[i * 3 + k];
+  for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = a[k];
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float bce = (float)red[0][0], kl = (float)red[1][0], rk = (float)red[2][0];
+    const float loss = w_label * bce + w_d * kl + w_r * rk;
+    if (accumulate) {
+      terms[0] += loss; terms[1] += bce; terms[2] += kl; terms[3] += rk;
+    } else {
+      terms[0] = loss; terms[1] = bce; terms[2] = kl; terms[3] = rk;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ head
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, int64_t i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+
+// one wave per row
+template <typename T>
+__global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
+                                                       const T* __restrict__ Z2, int64_t ldz2,
+                                                       const int32_t* __restrict__ iz, const int32_t* __restrict__ iz2,
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       float* __restrict__ logit, float* __restrict__ prob) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const T* z = Z + (iz ? (int64_t)iz[r] : r) * ldz;
+  const T* z2 = Z2 ? Z2 + (iz2 ? (int64_t)iz2[r] : r) * ldz2 : nullptr;
+  float acc = 0.f;
+  for (int64_t n = lane; n < H; n += 64) {
+    float v = ldf<T>(z, n);
+    if (z2) v *= ldf<T>(z2, n);
+    acc += w ? v * w[n] : v;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const float lg = acc + (b ? b[0] : 0.f);
+    if (logit) logit[r] = lg;
+    if (prob) prob[r] = sigmoidf_(lg);
+  }
+}
+
+// Block = 256 threads owns columns {tid, tid+256, ...}; rows [r0, r0+RB).
+// weight[r] (NULL = 1) ; writes dZ if requested; slab[blk][H] of column sums,
+// slab_b[blk] of sum(weight).
+constexpr int HB_ROWS = 256;
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
+                                                     const float* __restrict__ weight, const float* __restrict__ w,
+                                                     int relu_mask, float alpha, T* __restrict__ dZ, int64_t lddz,
+                                                     float* __restrict__ slab, float* __restrict__ slab_b) {
+  const int64_t r0 = (int64_t)blockIdx.x * HB_ROWS;
+  const int64_t r1 = min(R, r0 + HB_ROWS);
+  for (int64_t n = threadIdx.x; n < H; n += blockDim.x) {
+    const float wn = w ? w[n] : 1.f;
+    float acc = 0.f;
+    for (int64_t r = r0; r < r1; ++r) {
+      const float z = ldf<T>(Z + r * ldz, n);
+      const float g = weight ? weight[r] : 1.f;
+      acc += g * z;
+      if (dZ) {
+        float d = alpha * g * wn;
+        if (relu_mask && !(z > 0.f)) d = 0.f;
+        if constexpr (sizeof(T) == 2)
+          dZ[r * lddz + n] = f2bf(d);
+        else
+          dZ[r * lddz + n] = d;
+      }
+    }
+    slab[blockIdx.x * H + n] = acc;
+  }
+  if (slab_b && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += weight ? weight[r] : 1.f;
+    slab_b[blockIdx.x] = s;
+  }
+}
+
+__global__ void slab_sum_kernel(const float* __restrict__ slab, int64_t nslab, int64_t H, float* __restrict__ out,
+                                int accumulate) {
+  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (n >= H) return;
+  float s = 0.f;
+  for (int64_t i = 0; i < nslab; ++i) s += slab[i * H + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+}  // namespace
+
+extern "C" int64_t llp_llp_loss_workspace_bytes(int64_t B, int64_t n_lab) {
+  const int64_t nb = (B + WAVES - 1) / WAVES + (n_lab + 255) / 256 + 1;
+  return nb * 3 * (int64_t)sizeof(float);
+}
+
+extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob, int64_t n_lab,
+                            int64_t n_pos, const float* out_logit, double B_total, double n_lab_total, float margin,
+                            float T, float w_label, float w_d, float w_r, float loss_scale, float* dlogit_ctx,
+                            float* dlogit_lab, float* terms_out, int accumulate, void* workspace,
+                            int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(C <= MAXC, "llp_llp_loss: contexts per anchor C=%lld > %d", (long long)C, MAXC);
+  LLP_CHECK_ARG(terms_out && workspace, "llp_llp_loss: null terms/workspace");
+  LLP_CHECK_ARG(workspace_bytes >= llp_llp_loss_workspace_bytes(B, n_lab), "llp_llp_loss: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* partial = reinterpret_cast<float*>(workspace);
+  const int64_t nba = B > 0 ? (B + WAVES - 1) / WAVES : 0;
+  const int64_t nbl = (n_lab + 255) / 256;
+  if (nba > 0) {
+    LLP_CHECK_ARG(s_logit && t_prob && dlogit_ctx, "llp_llp_loss: null context buffers");
+    hipLaunchKernelGGL(llp_anchor_kernel, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob, B_total,
+                       margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial);
+    LLP_LAUNCH_CHECK();
+  }
+  if (nbl > 0) {
+    LLP_CHECK_ARG(out_logit && dlogit_lab, "llp_llp_loss: null label buffers");
+    hipLaunchKernelGGL(bce_kernel, dim3((unsigned)nbl), dim3(256), 0, s, n_lab, n_pos, out_logit, n_lab_total,
+                       w_label, loss_scale, dlogit_lab, partial + nba * 3);
+    LLP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partial, nba + nbl, w_label, w_d, w_r,
+                     terms_out, accumulate);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_head_fwd(int dtype, int64_t R, int64_t H, const void* Z, int64_t ldz, const void* Z2, int64_t ldz2,
+                            const int32_t* iz, const int32_t* iz2, const float* w, const float* b, float* logit,
+                            float* prob, void* stream) {
+  LLP_CHECK_ARG(Z, "llp_head_fwd: null Z");
+  if (R == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(ceil_div_u(R, 4));
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz,
+                       (const bf16_t*)Z2, ldz2, iz, iz2, w, b, logit, prob);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<float>, grid, dim3(256), 0, s, R, H, (const float*)Z, ldz, (const float*)Z2,
+                       ldz2, iz, iz2, w, b, logit, prob);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+static int64_t colsum_slabs(int64_t R) { return (R + HB_ROWS - 1) / HB_ROWS; }
+
+extern "C" int64_t llp_head_bwd_workspace_bytes(int64_t R, int64_t H) {
+  return colsum_slabs(R) * (H + 1) * (int64_t)sizeof(float);
+}
+extern "C" int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N) { return llp_head_bwd_workspace_bytes(M, N); }
+
+static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t ldz, const float* weight,
+                         const float* w, int relu_mask, float alpha, void* dZ, int64_t lddz, float* dw, float* db,
+                         int accumulate,
+                         void* workspace, int64_t workspace_bytes, hipStream_t s) {
+  LLP_CHECK_ARG(workspace_bytes >= llp_head_bwd_workspace_bytes(R, H), "colsum: workspace too small");
+  const int64_t ns = colsum_slabs(R);
+  float* slab = reinterpret_cast<float*>(workspace);
+  float* slab_b = slab + ns * H;
+  if (ns > 0) {
+    if (dtype == LLP_BF16)
+      hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz,
+                         weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr);
+    else
+      hipLaunchKernelGGL(colsum_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
+                         weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr);
+    LLP_LAUNCH_CHECK();
+  }
+  if (dw) {
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, 256)), dim3(256), 0, s, slab, ns, H, dw, accumulate);
+    LLP_LAUNCH_CHECK();
+  }
+  if (db) {
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(1), dim3(256), 0, s, slab_b, ns, (int64_t)1, db, accumulate);
+    LLP_LAUNCH_CHECK();
+  }
+  return LLP_OK;
+}
+
+extern "C" int llp_head_bwd(int dtype, int64_t R, int64_t H, const float* dlogit, const void* Z, int64_t ldz,
+                            const float* w, int relu_mask, float alpha, void* dZ, int64_t lddz, float* dw,
+                            float* db, int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(dlogit && Z, "llp_head_bwd: null input");
+  LLP_CHECK_ARG(!dZ || w, "llp_head_bwd: dZ needs w");
+  return colsum_launch(dtype, R, H, Z, ldz, dlogit, w, relu_mask, alpha, dZ, lddz, dw, db, accumulate, workspace,
+                       workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(Y && out, "llp_colsum: null input");
+  return colsum_launch(dtype, M, N, Y, ldy, nullptr, nullptr, 0, 1.f, nullptr, 0, out, nullptr, accumulate, workspace,
+                       workspace_bytes, (hipStream_t)stream);
+}

@@ -1,0 +1,191 @@
+// CSR neighbour mean-aggregation for the GraphSAGE teacher.
+//
+// PyG MessagePassing(aggr='mean') over edge_index (src/models.py:113 via
+// SAGEConv, src/sageconv_updated.py:71-72): out[i] = mean over edges e with
+// dst[e] = i of x[src[e]], duplicates counted (Q2), empty rows -> 0.  The PyG
+// GPU path materialises an E x F message tensor; here one wavefront owns a
+// destination row, streams its neighbour rows straight from HBM/L2 with
+// 16-byte loads (4 neighbour rows in flight per lane group) and writes the row
+// once: HBM traffic = E*F*s (neighbours) + 4E (col) + 4(N+1) (rowptr) + N*F*s.
+#include "llp_common.h"
+
+namespace {
+
+template <typename T>
+struct V16;
+template <>
+struct V16<float> {
+  static constexpr int E = 4;
+  __device__ static void add(float* a, uint4 v, float w) {
+    a[0] += w * __uint_as_float(v.x); a[1] += w * __uint_as_float(v.y);
+    a[2] += w * __uint_as_float(v.z); a[3] += w * __uint_as_float(v.w);
+  }
+  __device__ static uint4 pack(const float* a) {
+    return make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3]));
+  }
+};
+template <>
+struct V16<bf16_t> {
+  static constexpr int E = 8;
+  __device__ static void add(float* a, uint4 v, float w) {
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[2 * i] += w * __uint_as_float(u[i] << 16);
+      a[2 * i + 1] += w * __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  }
+  __device__ static uint4 pack(const float* a) {
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = (uint32_t)f2bf(a[2 * i]) | ((uint32_t)f2bf(a[2 * i + 1]) << 16);
+    return make_uint4(u[0], u[1], u[2], u[3]);
+  }
+};
+
+// Row of F elements = NCH 16-B chunks.  A wave processes one row; lanes are
+// split into G = 64 / NCH_eff groups, each group walks every G-th neighbour and
+// the groups are summed through LDS at the end.
+template <typename T>
+__global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_t F, const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col, const T* __restrict__ x,
+                                                          int64_t ldx, const float* __restrict__ inv_deg, int mode,
+                                                          T* __restrict__ out, int64_t ldo, int accumulate) {
+  constexpr int E = V16<T>::E;
+  __shared__ float red[4][64 * E];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nch = F / E;                 // chunks per row (F % E == 0 here)
+  const int64_t row = (int64_t)blockIdx.x * 4 + w;
+  if (row >= n_rows) return;
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  // chunk sweep: columns in blocks of 64 chunks
+  for (int64_t c0 = 0; c0 < nch; c0 += 64) {
+    const int64_t cw = min((int64_t)64, nch - c0);           // chunks in this sweep
+    const int G = cw >= 64 ? 1 : (cw >= 32 ? 2 : (cw >= 16 ? 4 : (cw >= 8 ? 8 : (cw >= 4 ? 16 : (cw >= 2 ? 32 : 64)))));
+    const int lanes_per_group = 64 / G;
+    const int grp = lane / lanes_per_group, gl = lane % lanes_per_group;
+    const bool active = gl < cw;
+    float acc[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] = 0.f;
+    if (active) {
+      const int64_t ch = c0 + gl;
+      int64_t e = beg + grp;
+      // 4 neighbours in flight per group
+      for (; e + 3 * G < end; e += 4 * G) {
+        const int32_t j0 = col[e], j1 = col[e + G], j2 = col[e + 2 * G], j3 = col[e + 3 * G];
+        const uint4 v0 = *reinterpret_cast<const uint4*>(x + (int64_t)j0 * ldx + ch * E);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(x + (int64_t)j1 * ldx + ch * E);
+        const uint4 v2 = *reinterpret_cast<const uint4*>(x + (int64_t)j2 * ldx + ch * E);
+        const uint4 v3 = *reinterpret_cast<const uint4*>(x + (int64_t)j3 * ldx + ch * E);
+        const float w0 = mode ? inv_deg[j0] : 1.f, w1 = mode ? inv_deg[j1] : 1.f;
+        const float w2 = mode ? inv_deg[j2] : 1.f, w3 = mode ? inv_deg[j3] : 1.f;
+        V16<T>::add(acc, v0, w0);
+        V16<T>::add(acc, v1, w1);
+        V16<T>::add(acc, v2, w2);
+        V16<T>::add(acc, v3, w3);
+      }
+      for (; e < end; e += G) {
+        const int32_t j = col[e];
+        const uint4 v = *reinterpret_cast<const uint4*>(x + (int64_t)j * ldx + ch * E);
+        V16<T>::add(acc, v, mode ? inv_deg[j] : 1.f);
+      }
+    }
+    if (G > 1) {
+      // reduce the G groups through LDS (fixed order -> deterministic)
+      float* r = red[w];
+      __builtin_amdgcn_wave_barrier();
+      if (grp > 0 && active)
+#pragma unroll
+        for (int i = 0; i < E; ++i) r[(grp * lanes_per_group + gl) * E + i] = acc[i];
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (grp == 0 && active)
+        for (int g2 = 1; g2 < G; ++g2)
+#pragma unroll
+          for (int i = 0; i < E; ++i) acc[i] += r[(g2 * lanes_per_group + gl) * E + i];
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (grp == 0 && active) {
+      const float sc = mode ? 1.f : 1.f / (float)max(end - beg, (int64_t)1);
+#pragma unroll
+      for (int i = 0; i < E; ++i) acc[i] *= sc;
+      uint4* dst = reinterpret_cast<uint4*>(out + row * ldo + (c0 + gl) * E);
+      if (accumulate) {
+        float prev[E];
+#pragma unroll
+        for (int i = 0; i < E; ++i) prev[i] = 0.f;
+        V16<T>::add(prev, *dst, 1.f);
+#pragma unroll
+        for (int i = 0; i < E; ++i) acc[i] += prev[i];
+      }
+      *dst = V16<T>::pack(acc);
+    }
+  }
+}
+
+// Scalar fallback for feature widths that are not a multiple of the vector.
+template <typename T>
+__global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int64_t F,
+                                                             const int32_t* __restrict__ rowptr,
+                                                             const int32_t* __restrict__ col, const T* __restrict__ x,
+                                                             int64_t ldx, const float* __restrict__ inv_deg, int mode,
+                                                             T* __restrict__ out, int64_t ldo, int accumulate) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  const float sc = mode ? 1.f : 1.f / (float)max(end - beg, (int64_t)1);
+  for (int64_t f = lane; f < F; f += 64) {
+    float acc = 0.f;
+    for (int64_t e = beg; e < end; ++e) {
+      const int32_t j = col[e];
+      float v;
+      if constexpr (sizeof(T) == 2) v = bf2f(x[(int64_t)j * ldx + f]); else v = x[(int64_t)j * ldx + f];
+      acc += (mode ? inv_deg[j] : 1.f) * v;
+    }
+    acc *= sc;
+    T* d = out + row * ldo + f;
+    if constexpr (sizeof(T) == 2) {
+      if (accumulate) acc += bf2f(*d);
+      *d = f2bf(acc);
+    } else {
+      if (accumulate) acc += *d;
+      *d = acc;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
+                                 const void* x, int64_t ldx, const float* inv_deg, int mode, void* out, int64_t ldo,
+                                 int accumulate, void* stream) {
+  LLP_CHECK_ARG(rowptr && x && out, "llp_csr_aggregate: null pointer");
+  LLP_CHECK_ARG(mode == 0 || (mode == 1 && inv_deg), "llp_csr_aggregate: mode 1 needs inv_deg");
+  if (n_rows == 0 || F == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int es = dtype == LLP_BF16 ? 2 : 4;
+  const int E = 16 / es;
+  const bool vec = (F % E == 0) && (ldx % E == 0) && (ldo % E == 0) && ((uintptr_t)x % 16 == 0) &&
+                   ((uintptr_t)out % 16 == 0);
+  dim3 grid(ceil_div_u(n_rows, 4));
+  if (dtype == LLP_BF16) {
+    if (vec)
+      hipLaunchKernelGGL(csr_agg_vec_kernel<bf16_t>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const bf16_t*)x,
+                         ldx, inv_deg, mode, (bf16_t*)out, ldo, accumulate);
+    else
+      hipLaunchKernelGGL(csr_agg_scalar_kernel<bf16_t>, grid, dim3(256), 0, s, n_rows, F, rowptr, col,
+                         (const bf16_t*)x, ldx, inv_deg, mode, (bf16_t*)out, ldo, accumulate);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL(csr_agg_vec_kernel<float>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const float*)x, ldx,
+                         inv_deg, mode, (float*)out, ldo, accumulate);
+    else
+      hipLaunchKernelGGL(csr_agg_scalar_kernel<float>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const float*)x,
+                         ldx, inv_deg, mode, (float*)out, ldo, accumulate);
+  }
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}

@@ -1,0 +1,154 @@
+// Device-side samplers and per-step index builders.
+//
+// The reference samples on the host: torch_cluster random_walk on CPU for the
+// minibatch path (src/main.py:93 -> :33-50, then .to("cuda") at :50) and
+// torch.randint (src/main.py:47,84).  Here everything is drawn on the GPU from
+// a counter-based Philox stream keyed by a DEVICE step counter, so a captured
+// hipGraph replays a fresh sample every step and no host sync is needed.  Draw
+// indices are global (b + b_offset), so a rank holding a shard of the anchors
+// draws exactly what one GPU would draw for those anchors.
+#include "llp_common.h"
+
+namespace {
+
+// One thread per (anchor, walk).  Walk semantics: torch_cluster random_walk,
+// p = q = 1: next = col[rowptr[cur] + floor(u * deg(cur))]; deg 0 -> stay.
+__global__ void context_walk_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                    const int32_t* __restrict__ start, int64_t B, int64_t b_offset, int n_walks,
+                                    int walk_len, int ps_nb, int64_t C1, uint64_t seed,
+                                    const int64_t* __restrict__ step_ctr, int64_t stream_offset,
+                                    int32_t* __restrict__ samples) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= B * n_walks) return;
+  const int64_t b = t % B;
+  const int w = (int)(t / B);
+  const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_offset + w);
+  const int64_t bg = b + b_offset;
+  int32_t cur = start[b];
+  int32_t* out = samples + b * C1;
+  if (w == 0) out[0] = cur;
+  // column of step l (1-based) of walk w: rw -> l ; nb -> w*hops + l
+  const int64_t colbase = ps_nb ? (int64_t)w * walk_len : 0;
+  for (int l = 0; l < walk_len; ++l) {
+    const uint32_t x = philox_u32(seed, stream, (uint64_t)(bg * walk_len + l));
+    const int32_t lo = rowptr[cur];
+    const int32_t deg = rowptr[cur + 1] - lo;
+    if (deg > 0) cur = col[lo + uniform_index(x, deg)];
+    out[colbase + l + 1] = cur;
+  }
+}
+
+__global__ void context_neg_kernel(int64_t B, int64_t b_offset, int64_t nneg, int64_t num_nodes, int64_t col0,
+                                   int64_t C1, uint64_t seed, const int64_t* __restrict__ step_ctr,
+                                   int64_t stream_rel, int32_t* __restrict__ samples) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= B * nneg) return;
+  const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_rel);
+  const int64_t b = t / nneg, q = t % nneg;
+  const uint32_t x = philox_u32(seed, stream, (uint64_t)((b + b_offset) * nneg + q));
+  samples[b * C1 + col0 + q] = (int32_t)randint_index(x, num_nodes);
+}
+
+__global__ void randint_pairs_kernel(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
+                                     const int64_t* __restrict__ step_ctr, int64_t stream_offset,
+                                     int32_t* __restrict__ out) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= 2 * n) return;
+  const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_offset);
+  const int64_t side = t / n, i = t % n;
+  const uint64_t draw = (uint64_t)(side * n_total + offset + i);
+  out[t] = (int32_t)randint_index(philox_u32(seed, stream, draw), num_nodes);
+}
+
+__global__ void build_targets_kernel(int64_t BC1, const int32_t* __restrict__ samples,
+                                     const int32_t* __restrict__ pairs, const int32_t* __restrict__ perm,
+                                     const int64_t* __restrict__ step_ctr, int64_t perm_stride, int64_t P,
+                                     const int32_t* __restrict__ neg, int32_t* __restrict__ target) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t total = BC1 + 4 * P;
+  if (t >= total) return;
+  if (t < BC1) {
+    target[t] = samples[t];
+    return;
+  }
+  const int64_t u = t - BC1;           // [0, 4P): src(2P) then dst(2P)
+  const int64_t side = u / (2 * P);    // 0 = src (train_edges[0]), 1 = dst
+  const int64_t i = u % (2 * P);
+  int32_t v;
+  if (i < P) {
+    const int64_t e = perm[(step_ctr ? *step_ctr : 0) * perm_stride + i];
+    v = pairs[2 * e + side];           // pos_train_edge[link_perm].t() (main.py:78)
+  } else {
+    v = neg[side * P + (i - P)];       // neg_edge[side] (main.py:84)
+  }
+  target[t] = v;
+}
+
+__global__ void pair_index_kernel(int64_t B, int64_t C, const int32_t* __restrict__ samples,
+                                  int32_t* __restrict__ ia, int32_t* __restrict__ ib) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= B * C) return;
+  const int64_t b = t / C, c = t % C;
+  ia[t] = samples[b * (C + 1)];
+  ib[t] = samples[b * (C + 1) + 1 + c];
+}
+
+}  // namespace
+
+extern "C" int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
+                                   const int32_t* start, int64_t B, int64_t b_offset, int ps_method, int rw_step,
+                                   int hops, int ns_rate, uint64_t seed, const int64_t* step_ctr,
+                                   int64_t stream_offset, int32_t* samples, void* stream) {
+  LLP_CHECK_ARG(rowptr && col && start && samples && step_ctr, "llp_context_sampler: null pointer");
+  LLP_CHECK_ARG(ps_method == 0 || ps_method == 1, "llp_context_sampler: ps_method must be 0 (rw) or 1 (nb)");
+  LLP_CHECK_ARG(rw_step >= 1 && hops >= 1 && ns_rate >= 0 && rw_step < 15, "llp_context_sampler: bad step/hops");
+  if (B == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t C1 = 1 + (int64_t)rw_step * hops * (1 + ns_rate);
+  const int n_walks = ps_method == 1 ? rw_step : 1;
+  const int walk_len = ps_method == 1 ? hops : rw_step * hops;
+  const int64_t nt = B * n_walks;
+  hipLaunchKernelGGL(context_walk_kernel, dim3(ceil_div_u(nt, 256)), dim3(256), 0, s, rowptr, col, start, B, b_offset,
+                     n_walks, walk_len, ps_method, C1, seed, step_ctr, stream_offset, samples);
+  LLP_LAUNCH_CHECK();
+  const int64_t nneg = (int64_t)rw_step * hops * ns_rate;
+  if (nneg > 0) {
+    hipLaunchKernelGGL(context_neg_kernel, dim3(ceil_div_u(B * nneg, 256)), dim3(256), 0, s, B, b_offset, nneg,
+                       num_nodes, 1 + (int64_t)rw_step * hops, C1, seed, step_ctr, stream_offset + rw_step, samples);
+    LLP_LAUNCH_CHECK();
+  }
+  return LLP_OK;
+}
+
+extern "C" int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
+                                 const int64_t* step_ctr, int64_t stream_offset, int32_t* out, void* stream) {
+  LLP_CHECK_ARG(out && step_ctr, "llp_randint_pairs: null pointer");
+  LLP_CHECK_ARG(offset + n <= n_total, "llp_randint_pairs: shard out of range");
+  if (n == 0) return LLP_OK;
+  hipLaunchKernelGGL(randint_pairs_kernel, dim3(ceil_div_u(2 * n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     num_nodes, n, n_total, offset, seed, step_ctr, stream_offset, out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
+                                 const int32_t* perm, const int64_t* step_ctr, int64_t perm_stride, int64_t P,
+                                 const int32_t* neg, int32_t* target, void* stream) {
+  LLP_CHECK_ARG(samples && pairs && perm && neg && target, "llp_build_targets: null pointer");
+  const int64_t total = B * C1 + 4 * P;
+  if (total == 0) return LLP_OK;
+  hipLaunchKernelGGL(build_targets_kernel, dim3(ceil_div_u(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     B * C1, samples, pairs, perm, step_ctr, perm_stride, P, neg, target);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* samples, int32_t* ia, int32_t* ib,
+                                           void* stream) {
+  LLP_CHECK_ARG(samples && ia && ib, "llp_pair_index_from_samples: null pointer");
+  if (B * C == 0) return LLP_OK;
+  hipLaunchKernelGGL(pair_index_kernel, dim3(ceil_div_u(B * C, 256)), dim3(256), 0, (hipStream_t)stream, B, C,
+                     samples, ia, ib);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}

@@ -1,0 +1,419 @@
+"""MI355X LLP distillation engine: one relational-distillation step (sampling,
+student MLP + LinkPredictor forward/backward, frozen teacher predictor, fused
+LLP_D / LLP_R / BCE loss, clip_grad_norm_ per group, Adam) as a fixed sequence
+of hand-written gfx950 kernels on preallocated HBM buffers.
+
+Reference: ``train_minibatch`` (src/main.py:52-144) and ``train``
+(src/main.py:147-236).  The nn.Modules stay the source of truth for the
+weights (their ``.data``/``.grad``/optimizer state are the engine's buffers),
+so ``state_dict()`` / ``torch.save`` interoperate with the reference's files.
+
+Layout in HBM (minibatch path, one step, rows of h follow src/main.py:95):
+    target  int32[R1]        node id per student row: samples.flat | src(2P) | dst(2P)
+    H_l     dtype[R1, H]     student activations, R1 = B*(C+1) + 4P
+    Z_l     dtype[R2, H]     predictor activations, R2 = B*C + 2P
+    logit   f32[R2]          predictor logits: B*C context pairs | 2P label pairs
+    T1      dtype[B*C, 256]  teacher predictor hidden layer
+Weights: f32 masters (the modules' parameters) + a compute-dtype copy and a
+transposed copy, refreshed by the Adam kernel.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import llp_hip as K
+
+_DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
+
+
+def build_sampler_csr(row: np.ndarray, col: np.ndarray, num_nodes: int, sorted_: bool = False):
+    """CSR for the context sampler with torch_cluster random_walk semantics
+    (coalesced=False, src/main.py:37-45): rowptr = prefix sum of row degrees,
+    col kept in the given (possibly unsorted) order.  ``sorted_``
+    (--rw_sorted) sorts by (row, col) instead."""
+    row = np.asarray(row, np.int64)
+    col = np.asarray(col, np.int64)
+    if sorted_:
+        perm = np.argsort(row * num_nodes + col, kind="stable")
+        col = col[perm]
+    deg = np.bincount(row, minlength=num_nodes)
+    rowptr = np.zeros(num_nodes + 1, np.int64)
+    np.cumsum(deg, out=rowptr[1:])
+    assert rowptr[-1] < 2 ** 31
+    return rowptr.astype(np.int32), col.astype(np.int32)
+
+
+class _Linear:
+    """Device view of one nn.Linear: f32 master W/b (the module's params), their
+    grads (views into the flat grad buffer), compute copies."""
+
+    def __init__(self, lin: torch.nn.Linear, dtype, need_t: bool, need_c: bool):
+        self.W = lin.weight.data
+        self.b = lin.bias.data
+        self.out_f, self.in_f = self.W.shape
+        self.Wc = None
+        self.Wt = None
+        if need_c and dtype != torch.float32:
+            self.Wc = torch.empty_like(self.W, dtype=dtype)
+        if need_t:
+            self.Wt = torch.empty(self.in_f, self.out_f, dtype=dtype, device=self.W.device)
+        self.lin = lin
+
+    @property
+    def Wcomp(self):
+        return self.Wc if self.Wc is not None else self.W
+
+
+class DistillEngine:
+    """Holds every device buffer of the distillation step.
+
+    Parameters mirror ``train_minibatch``'s arguments (src/main.py:52): the
+    student ``model`` (MLP), ``predictor`` (LinkPredictor), the frozen
+    ``teacher_predictor`` and teacher embeddings ``t_h``; ``x`` the node
+    features; ``row``/``col`` the sampler graph (data.adj_t, src/main.py:56);
+    ``optimizer`` a torch.optim.Adam over model+predictor parameters whose
+    hyper-parameters and state this engine uses.
+    """
+
+    def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
+                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None):
+        self.dev = torch.device(device) if device is not None else x.device
+        if self.dev.type != "cuda":
+            raise RuntimeError("DistillEngine runs only on a HIP device (no CPU fallback)")
+        K.lib()
+        self.dtype = _DT[dtype]
+        self.dc = K.dtype_code(self.dtype)
+        self.args = args
+        self.N = int(num_nodes)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.group = group
+        self.world = dist.get_world_size(group) if (group is not None or (dist.is_available() and dist.is_initialized())) else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        if args.predictor not in ("mlp", "inner"):
+            raise ValueError(args.predictor)
+        self.predictor_kind = args.predictor
+
+        # ---------------- parameters
+        self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
+        stu = list(model.layers)
+        prd = list(predictor.lins)
+        self.stu = [_Linear(l, self.dtype, need_t=(i > 0), need_c=True) for i, l in enumerate(stu)]
+        if self.predictor_kind == "mlp":
+            self.prd = [_Linear(l, self.dtype, need_t=True, need_c=True) for l in prd[:-1]]
+            self.head = prd[-1]
+        else:
+            self.prd, self.head = [], None
+        self.all_params = [p for l in stu for p in (l.weight, l.bias)] + [p for l in prd for p in (l.weight, l.bias)]
+        self.n_stu_params = 2 * len(stu)
+        total = sum(p.numel() for p in self.all_params)
+        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=self.dev)
+        off = 0
+        for p in self.all_params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.optimizer = optimizer
+        self._init_optimizer_state()
+
+        # teacher predictor (frozen; dropout stays live as in the reference, Q3)
+        tl = list(teacher_predictor.lins)
+        self.t_kind = teacher_predictor.predictor
+        self.t_hidden = []
+        for l in tl[:-1]:
+            W = l.weight.data.to(self.dev)
+            self.t_hidden.append((W.to(self.dtype).contiguous(), l.bias.data.to(self.dev).float().contiguous()))
+        self.t_head = (tl[-1].weight.data.to(self.dev).float().reshape(-1).contiguous(),
+                       tl[-1].bias.data.to(self.dev).float().contiguous())
+        self.t_dropout = float(getattr(teacher_predictor, "dropout", 0.0)) if teacher_predictor.training else 0.0
+
+        # ---------------- data
+        self.x = x.to(self.dev).to(self.dtype).contiguous()
+        self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
+        rowptr, colv = build_sampler_csr(np.asarray(row), np.asarray(col), self.N, rw_sorted)
+        self.rowptr = torch.from_numpy(rowptr).to(self.dev)
+        self.col = torch.from_numpy(colv).to(self.dev)
+
+        # ---------------- step state (device)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)   # RNG stream counter
+        self.terms = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        self._bufs = {}
+        self._shape = None
+        self._build_descs()
+
+    # ------------------------------------------------------------------ setup
+    def _init_optimizer_state(self):
+        opt = self.optimizer
+        if not isinstance(opt, torch.optim.Adam):
+            raise NotImplementedError("the LLP engine implements torch.optim.Adam (src/main.py:400-402)")
+        g = opt.param_groups
+        if len(g) != 1 or g[0]["weight_decay"] != 0 or g[0]["amsgrad"] or g[0].get("maximize", False):
+            raise NotImplementedError("Adam with one param group, no weight decay / amsgrad / maximize")
+        ids = {id(p) for p in g[0]["params"]}
+        if ids != {id(p) for p in self.all_params}:
+            raise ValueError("optimizer must hold exactly model.parameters() + predictor.parameters()")
+        step0 = 0
+        for p in self.all_params:
+            st = opt.state[p]
+            if "exp_avg" not in st:
+                st["step"] = torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            step0 = int(float(st["step"]))
+        self.adam_step = torch.full((1,), step0, dtype=torch.int64, device=self.dev)
+
+    def _build_descs(self):
+        opt = self.optimizer
+        descs = []
+        shadow_dt = self.dc
+        lin_of = {}
+        for l in self.stu + self.prd:
+            lin_of[id(l.lin.weight)] = l
+        for i, p in enumerate(self.all_params):
+            st = opt.state[p]
+            L = lin_of.get(id(p))
+            shadow = L.Wc if L is not None else None
+            shadow_t = L.Wt if L is not None else None
+            rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+            descs.append(K.TensorDesc(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
+                                      st["exp_avg_sq"].data_ptr(), K.ptr(shadow), K.ptr(shadow_t), p.numel(), rows,
+                                      cols, 0 if i < self.n_stu_params else 1, shadow_dt))
+        self.n_desc = len(descs)
+        self.max_numel = max(p.numel() for p in self.all_params)
+        self.descs_dev = K.descs_to_device(descs, self.dev)
+        self.sumsq = torch.zeros(2, dtype=torch.float32, device=self.dev)
+        self.ws_sumsq = torch.empty(K.grad_sumsq_ws_bytes(self.n_desc, self.max_numel) // 4 + 1, dtype=torch.float32,
+                                    device=self.dev)
+        K.refresh_shadows(self.descs_dev, self.n_desc, self.max_numel)
+
+    def refresh_weights(self):
+        """Call after loading weights into the modules (reset_parameters, load_state_dict)."""
+        K.refresh_shadows(self.descs_dev, self.n_desc, self.max_numel)
+
+    def _buf(self, name, shape, dtype):
+        numel = int(np.prod(shape))
+        b = self._bufs.get(name)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, device=self.dev)
+            self._bufs[name] = b
+        return b[:numel].view(*shape)
+
+    def _ws(self, name, nbytes):
+        return self._buf(name, (nbytes // 4 + 16,), torch.float32)
+
+    # ------------------------------------------------------------------ helpers
+    def _dropout(self, p, stream_off):
+        if p <= 0.0:
+            return None
+        return K.Dropout(float(p), self.seed ^ 0xD0D0, self.step_ctr.data_ptr(), stream_off)
+
+    def _rows_index(self, B, C, P2):
+        """Predictor-row -> h-row index for the minibatch layout (static per shape)."""
+        key = ("rows", B, C, P2)
+        if key not in self._bufs:
+            C1 = C + 1
+            b = torch.arange(B, device=self.dev, dtype=torch.int64).repeat_interleave(C)
+            c = torch.arange(C, device=self.dev, dtype=torch.int64).repeat(B)
+            ia_ctx = b * C1
+            ib_ctx = b * C1 + 1 + c
+            lab = torch.arange(P2, device=self.dev, dtype=torch.int64)
+            ia_lab = B * C1 + lab
+            ib_lab = B * C1 + P2 + lab
+            ia = torch.cat([ia_ctx, ia_lab]).to(torch.int32).contiguous()
+            ib = torch.cat([ib_ctx, ib_lab]).to(torch.int32).contiguous()
+            self._bufs[key] = (ia, ib)
+        return self._bufs[key]
+
+    # ------------------------------------------------------------------ the step
+    def step_minibatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
+                       samples=None, neg=None, kernel_events=None):
+        """One link batch of train_minibatch (src/main.py:73-143).
+
+        anchors  int32[B]   this rank's slice of node_perm (src/main.py:76)
+        link_ids int32[P]   this rank's slice of link_perm (src/main.py:73,78)
+        pairs    int32[E,2] pos_train_edge (src/main.py:55)
+        samples / neg: optional injected samples int32[B, 1+C] / negatives int32[2, P]
+        (parity tests); otherwise drawn on the device.
+        Returns nothing; the loss terms stay on the device (self.terms).
+        """
+        a = self.args
+        B = int(anchors.numel())
+        P = int(link_ids.numel())
+        B_total = B if B_total is None else int(B_total)
+        P_total = P if P_total is None else int(P_total)
+        rw_step, hops, ns_rate = int(a.rw_step), int(a.hops), int(a.ns_rate)
+        C = rw_step * hops * (1 + ns_rate)
+        C1 = C + 1
+        H = self.stu[-1].out_f
+        dt, dc = self.dtype, self.dc
+        R1 = B * C1 + 4 * P
+        R2 = B * C + 2 * P
+        P2 = 2 * P
+
+        # ---- a1-a3: samples and negatives (src/main.py:84,93)
+        samp = self._buf("samples", (B, C1), torch.int32)
+        if samples is not None:
+            samp.copy_(samples.to(torch.int32))
+        else:
+            K.context_sampler(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
+                              self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
+        negb = self._buf("neg", (2, P), torch.int32)
+        if neg is not None:
+            negb.copy_(neg.to(torch.int32))
+        else:
+            K.randint_pairs(self.N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)
+        target = self._buf("target", (R1,), torch.int32)
+        K.build_targets(B, C1, samp, pairs, link_ids, None, 0, P, negb, target)
+        t_ia = self._buf("t_ia", (B * C,), torch.int32)
+        t_ib = self._buf("t_ib", (B * C,), torch.int32)
+        K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
+        ia, ib = self._rows_index(B, C, P2)
+
+        # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
+        acts = []
+        A = K.operand(self.x, target)
+        p_drop = float(a.dropout)
+        for l, lin in enumerate(self.stu):
+            last = l == len(self.stu) - 1
+            out = self._buf(f"H{l}", (R1, lin.out_f), dt)
+            timed = kernel_events is not None and l == 1
+            if timed:   # the dominant MFMA kernel, timed on the launch stream (bench.py roofline)
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            K.gemm_nt(A, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, dc, bias=lin.b,
+                      act=K.ACT_NONE if last else K.ACT_RELU,
+                      dropout=None if last else self._dropout(p_drop, 1 + l))
+            if timed:
+                ev[1].record()
+                kernel_events.append(ev)
+            acts.append(out)
+            A = K.operand(out)
+        h = acts[-1]
+
+        # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
+        logit = self._buf("logit", (R2,), torch.float32)
+        zacts = []
+        A = K.operand(h, ia, h, ib)
+        for l, lin in enumerate(self.prd):
+            out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
+            K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
+                      dropout=self._dropout(p_drop, 5 + l))
+            zacts.append(out)
+            A = K.operand(out)
+        if self.predictor_kind == "mlp":
+            K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
+                       logit=logit)
+        else:
+            K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
+
+        # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
+        t_r = self._buf("t_r", (B * C,), torch.float32)
+        self._teacher_forward(B * C, t_ia, t_ib, t_r)
+
+        # ---- a7-a9: fused LLP_D + LLP_R + BCE and d(loss)/d(logit) (src/main.py:107-130)
+        if not (a.LLP_D or a.LLP_R):
+            raise UnboundLocalError("train_minibatch: loss is only defined when LLP_D or LLP_R is set "
+                                    "(src/main.py:129-130)")
+        dlogit = self._buf("dlogit", (R2,), torch.float32)
+        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(B, P2))
+        K.llp_loss(B, C, logit, t_r, P2, P, logit[B * C:], B_total, 2 * P_total, float(a.margin), 1.0,
+                   float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms, ws)
+
+        # ---- a10: backward
+        dZ0 = self._predictor_backward(dlogit, R2, h, ia, ib, zacts, p_drop)
+        dh = self._buf("gS0", (R1, H), dt)
+        if self.predictor_kind == "mlp":
+            K.hadamard_bwd_blocks(B, C, P2, H, dZ0, h, dh)
+        else:
+            K.hadamard_bwd_blocks(B, C, P2, H, None, h, dh, drow=dlogit)
+        self._student_backward(dh, R1, target, acts, p_drop)
+        self._allreduce_and_update()
+        K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
+        K.increment(self.step_ctr)
+
+    def _teacher_forward(self, R, t_ia, t_ib, t_r):
+        dt, dc = self.dtype, self.dc
+        if self.t_kind == "inner":
+            K.head_fwd(self.t_h, R, self.t_h.shape[1], None, None, prob=t_r, Z2=self.t_h, iz=t_ia, iz2=t_ib)
+            return
+        A = K.operand(self.t_h, t_ia, self.t_h, t_ib)
+        out = None
+        for l, (W, b) in enumerate(self.t_hidden):
+            out = self._buf(f"T{l}", (R, W.shape[0]), dt)
+            K.gemm_nt(A, K.operand(W), R, W.shape[0], W.shape[1], out, dc, bias=b, act=K.ACT_RELU,
+                      dropout=self._dropout(self.t_dropout, 9 + l))
+            A = K.operand(out)
+        w, b = self.t_head
+        K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
+
+    def _predictor_backward(self, dlogit, R2, h, ia, ib, zacts, p_drop):
+        dt, dc = self.dtype, self.dc
+        if self.predictor_kind != "mlp":
+            return None
+        alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
+        Zl = zacts[-1]
+        Hh = Zl.shape[1]
+        g = self._buf("gP0", (R2, Hh), dt)
+        ws = self._ws("ws_col", K.head_bwd_ws_bytes(R2, max(Hh, 1)))
+        K.head_bwd(dlogit, Zl, R2, Hh, self.head.weight.data.view(-1), True, g, self.head.weight.grad.view(-1),
+                   self.head.bias.grad, ws, alpha=alpha)
+        cur, nxt = "gP0", "gP1"
+        for l in range(len(self.prd) - 1, -1, -1):
+            lin = self.prd[l]
+            gcur = self._buf(cur, (R2, lin.out_f), dt)
+            A_in = K.operand(zacts[l - 1]) if l > 0 else K.operand(h, ia, h, ib)
+            wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
+            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb))
+            K.colsum(gcur, R2, lin.out_f, lin.lin.bias.grad, self._ws("ws_col", K.colsum_ws_bytes(R2, lin.out_f)))
+            gnext = self._buf(nxt, (R2, lin.in_f), dt)
+            if l > 0:
+                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
+                          act=K.ACT_RELU_BWD, aux=zacts[l - 1], alpha=alpha)
+            else:
+                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
+            cur, nxt = nxt, cur
+        return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
+
+    def _student_backward(self, dh, R1, target, acts, p_drop):
+        dt, dc = self.dtype, self.dc
+        alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
+        cur, nxt = "gS0", "gS1"
+        for l in range(len(self.stu) - 1, -1, -1):
+            lin = self.stu[l]
+            gcur = self._buf(cur, (R1, lin.out_f), dt)
+            A_in = K.operand(acts[l - 1]) if l > 0 else K.operand(self.x, target)
+            wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.in_f)
+            K.gemm_tn(K.operand(gcur), A_in, R1, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb))
+            K.colsum(gcur, R1, lin.out_f, lin.lin.bias.grad, self._ws("ws_col", K.colsum_ws_bytes(R1, lin.out_f)))
+            if l > 0:
+                gnext = self._buf(nxt, (R1, lin.in_f), dt)
+                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
+                          act=K.ACT_RELU_BWD, aux=acts[l - 1], alpha=alpha)
+                cur, nxt = nxt, cur
+
+    def _allreduce_and_update(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+        g = self.optimizer.param_groups[0]
+        K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, 2, self.sumsq, self.ws_sumsq)
+        b1, b2 = g["betas"]
+        K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
+                    float(b2), float(g["eps"]), self.adam_step)
+
+    # ------------------------------------------------------------------ epoch bookkeeping
+    def begin_epoch(self):
+        self.loss_sum.zero_()
+
+    def end_epoch(self, total_examples):
+        """Returns total_loss / total_examples (src/main.py:141-144); one host sync."""
+        tot = self.loss_sum
+        if self.world > 1:
+            tot = tot.clone()
+            dist.all_reduce(tot, group=self.group)
+        steps = int(self.adam_step.item())
+        for p in self.all_params:
+            self.optimizer.state[p]["step"] = torch.tensor(float(steps))
+        return float(tot.item()) / max(total_examples, 1)

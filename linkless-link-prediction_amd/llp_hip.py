@@ -1,0 +1,337 @@
+"""ctypes binding of libllp_hip.so (the C ABI in include/llp_hip.h).
+
+This is the only way the product reaches the GPU: every op below launches a
+hand-written gfx950 kernel on torch's current HIP stream.  There is no CPU
+fallback — if the library or a GPU is missing, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libllp_hip.so")
+
+LLP_F32, LLP_BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_RELU_BWD = 0, 1, 2
+
+c_i64 = C.c_int64
+c_int = C.c_int
+c_f32 = C.c_float
+c_f64 = C.c_double
+c_vp = C.c_void_p
+c_u64 = C.c_uint64
+
+
+class Operand(C.Structure):
+    _fields_ = [("ptr", c_vp), ("idx", c_vp), ("ptr2", c_vp), ("idx2", c_vp), ("ld", c_i64), ("ld2", c_i64)]
+
+
+class Dropout(C.Structure):
+    _fields_ = [("p", c_f32), ("seed", c_u64), ("step_ctr", c_vp), ("stream_offset", c_i64)]
+
+
+class TensorDesc(C.Structure):
+    _fields_ = [("param", c_vp), ("grad", c_vp), ("exp_avg", c_vp), ("exp_avg_sq", c_vp), ("shadow", c_vp),
+                ("shadow_t", c_vp), ("numel", c_i64), ("rows", c_i64), ("cols", c_i64), ("group", C.c_int32),
+                ("shadow_dtype", C.c_int32)]
+
+
+_SIGS = {
+    "llp_version": (c_int, []),
+    "llp_last_error": (C.c_char_p, []),
+    "llp_device_count": (c_int, []),
+    "llp_gemm_nt": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
+                            c_vp, c_int, c_vp, c_i64, c_int, c_f32, C.POINTER(Dropout), c_vp]),
+    "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
+    "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
+                            c_vp, c_i64, c_vp]),
+    "llp_colsum_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_colsum": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp]),
+    "llp_head_fwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_head_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_head_bwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_vp, c_i64, c_vp, c_vp,
+                             c_int, c_vp, c_i64, c_vp]),
+    "llp_llp_loss_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_llp_loss": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32,
+                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_vp]),
+    "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_hadamard_bwd_scatter": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_context_sampler": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
+                                    c_i64, c_vp, c_vp]),
+    "llp_randint_pairs": (c_int, [c_i64, c_i64, c_i64, c_i64, c_u64, c_vp, c_i64, c_vp, c_vp]),
+    "llp_build_targets": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "llp_pair_index_from_samples": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_csr_aggregate": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_int, c_vp]),
+    "llp_grad_sumsq_workspace_bytes": (c_i64, [c_int, c_i64]),
+    "llp_grad_sumsq": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
+    "llp_adam_step": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
+    "llp_refresh_shadows": (c_int, [c_vp, c_int, c_i64, c_vp]),
+    "llp_convert": (c_int, [c_int, c_int, c_i64, c_vp, c_vp, c_vp]),
+    "llp_accumulate": (c_int, [c_i64, c_vp, c_f32, c_vp, c_vp]),
+    "llp_increment": (c_int, [c_vp, c_vp]),
+    "llp_zero": (c_int, [c_vp, c_i64, c_vp]),
+    "llp_relu_bwd": (c_int, [c_int, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
+    "llp_transpose": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "llp_mul": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_row_scale": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_sigmoid_bwd": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """dlopen the library (works without a GPU: no compute call is made)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise RuntimeError(f"libllp_hip.so not found at {path}: run `python build_lib.py` (or "
+                               f"__graft_entry__.build()) first — there is no CPU fallback")
+        lib = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def lib():
+    """The library, for compute: requires a visible GPU."""
+    L = load()
+    if not torch.cuda.is_available():
+        raise RuntimeError("libllp_hip: no HIP device visible — the LLP hot path runs only on MI355X (gfx950)")
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.llp_last_error().decode() if _lib else ""
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(t: torch.dtype) -> int:
+    if t == torch.float32:
+        return LLP_F32
+    if t == torch.bfloat16:
+        return LLP_BF16
+    raise TypeError(f"unsupported dtype {t}")
+
+
+def operand(t, idx=None, t2=None, idx2=None) -> Operand:
+    """Operand over the row-major 2-D tensor ``t`` (rows optionally gathered by
+    int32 ``idx``), optionally times ``t2[idx2]`` elementwise."""
+    assert t.dim() == 2 and t.stride(1) == 1
+    if idx is not None:
+        assert idx.dtype == torch.int32 and idx.is_contiguous()
+    o = Operand(t.data_ptr(), ptr(idx), ptr(t2), ptr(idx2), t.stride(0), t2.stride(0) if t2 is not None else 0)
+    return o
+
+
+# ------------------------------------------------------------------ op wrappers
+def gemm_nt(A: Operand, B: Operand, M, N, K, C_out, dtype, bias=None, act=ACT_NONE, aux=None, alpha=1.0,
+            dropout: Dropout | None = None):
+    L = lib()
+    check(L.llp_gemm_nt(dtype, M, N, K, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0),
+                        dtype_code(C_out.dtype), ptr(bias), act, ptr(aux), aux.stride(0) if aux is not None else 0,
+                        dtype_code(aux.dtype) if aux is not None else 0, alpha,
+                        C.byref(dropout) if dropout is not None else None, stream_ptr()), "llp_gemm_nt")
+
+
+def gemm_tn_ws_bytes(dtype, M, P, Q):
+    return load().llp_gemm_tn_workspace_bytes(dtype, M, P, Q)
+
+
+def gemm_tn(A: Operand, B: Operand, M, P, Q, C_out, dtype, ws, accumulate=False):
+    L = lib()
+    check(L.llp_gemm_tn(dtype, M, P, Q, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0), int(accumulate),
+                        ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_gemm_tn")
+
+
+def colsum_ws_bytes(M, N):
+    return load().llp_colsum_workspace_bytes(M, N)
+
+
+def colsum(Y, M, N, out, ws, accumulate=False):
+    L = lib()
+    check(L.llp_colsum(dtype_code(Y.dtype), M, N, Y.data_ptr(), Y.stride(0), out.data_ptr(), int(accumulate),
+                       ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_colsum")
+
+
+def head_fwd(Z, R, H, w, b, logit=None, prob=None, Z2=None, iz=None, iz2=None):
+    L = lib()
+    check(L.llp_head_fwd(dtype_code(Z.dtype), R, H, Z.data_ptr(), Z.stride(0), ptr(Z2),
+                         Z2.stride(0) if Z2 is not None else 0, ptr(iz), ptr(iz2), ptr(w), ptr(b), ptr(logit),
+                         ptr(prob), stream_ptr()), "llp_head_fwd")
+
+
+def head_bwd_ws_bytes(R, H):
+    return load().llp_head_bwd_workspace_bytes(R, H)
+
+
+def head_bwd(dlogit, Z, R, H, w, relu_mask, dZ, dw, db, ws, accumulate=False, alpha=1.0):
+    L = lib()
+    check(L.llp_head_bwd(dtype_code(Z.dtype), R, H, dlogit.data_ptr(), Z.data_ptr(), Z.stride(0), ptr(w),
+                         int(relu_mask), alpha, ptr(dZ), dZ.stride(0) if dZ is not None else 0, ptr(dw), ptr(db),
+                         int(accumulate), ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()),
+          "llp_head_bwd")
+
+
+def llp_loss_ws_bytes(B, n_lab):
+    return load().llp_llp_loss_workspace_bytes(B, n_lab)
+
+
+def llp_loss(B, Cc, s_logit, t_prob, n_lab, n_pos, out_logit, B_total, n_lab_total, margin, T, w_label, w_d, w_r,
+             dlogit_ctx, dlogit_lab, terms, ws, accumulate=False, loss_scale=1.0):
+    L = lib()
+    check(L.llp_llp_loss(B, Cc, ptr(s_logit), ptr(t_prob), n_lab, n_pos, ptr(out_logit), float(B_total),
+                         float(n_lab_total), margin, T, w_label, w_d, w_r, loss_scale, ptr(dlogit_ctx),
+                         ptr(dlogit_lab), terms.data_ptr(), int(accumulate), ws.data_ptr(),
+                         ws.numel() * ws.element_size(), stream_ptr()), "llp_llp_loss")
+
+
+def hadamard_bwd_blocks(B, Cc, L2, H, dZ, h, dh, drow=None):
+    L = lib()
+    check(L.llp_hadamard_bwd_blocks(dtype_code(h.dtype), B, Cc, L2, H, ptr(dZ), ptr(drow), h.data_ptr(),
+                                    dh.data_ptr(), stream_ptr()), "llp_hadamard_bwd_blocks")
+
+
+def hadamard_bwd_scatter(R, H, dZ, ia, ib, h, dh, drow=None):
+    L = lib()
+    check(L.llp_hadamard_bwd_scatter(dtype_code(h.dtype), R, H, ptr(dZ), ptr(drow), ia.data_ptr(), ib.data_ptr(),
+                                     h.data_ptr(), dh.data_ptr(), stream_ptr()), "llp_hadamard_bwd_scatter")
+
+
+def context_sampler(rowptr, col, num_nodes, start, B, ps_method, rw_step, hops, ns_rate, seed, step_ctr,
+                    stream_offset, samples, b_offset=0):
+    L = lib()
+    check(L.llp_context_sampler(rowptr.data_ptr(), col.data_ptr(), num_nodes, start.data_ptr(), B, b_offset,
+                                1 if ps_method == "nb" else 0, rw_step, hops, ns_rate, seed, step_ctr.data_ptr(),
+                                stream_offset, samples.data_ptr(), stream_ptr()), "llp_context_sampler")
+
+
+def randint_pairs(num_nodes, n, seed, step_ctr, stream_offset, out, n_total=None, offset=0):
+    L = lib()
+    n_total = n if n_total is None else n_total
+    check(L.llp_randint_pairs(num_nodes, n, n_total, offset, seed, step_ctr.data_ptr(), stream_offset,
+                              out.data_ptr(), stream_ptr()), "llp_randint_pairs")
+
+
+def build_targets(B, C1, samples, pairs, perm, step_ctr, perm_stride, P, neg, target):
+    L = lib()
+    check(L.llp_build_targets(B, C1, samples.data_ptr(), pairs.data_ptr(), perm.data_ptr(), ptr(step_ctr),
+                              perm_stride, P, neg.data_ptr(), target.data_ptr(), stream_ptr()), "llp_build_targets")
+
+
+def pair_index_from_samples(B, Cc, samples, ia, ib):
+    L = lib()
+    check(L.llp_pair_index_from_samples(B, Cc, samples.data_ptr(), ia.data_ptr(), ib.data_ptr(), stream_ptr()),
+          "llp_pair_index_from_samples")
+
+
+def csr_aggregate(n_rows, F, rowptr, col, x, inv_deg, mode, out, accumulate=False):
+    L = lib()
+    check(L.llp_csr_aggregate(dtype_code(x.dtype), n_rows, F, rowptr.data_ptr(), col.data_ptr(), x.data_ptr(),
+                              x.stride(0), ptr(inv_deg), mode, out.data_ptr(), out.stride(0), int(accumulate),
+                              stream_ptr()), "llp_csr_aggregate")
+
+
+def grad_sumsq_ws_bytes(n, max_numel):
+    return load().llp_grad_sumsq_workspace_bytes(n, max_numel)
+
+
+def grad_sumsq(descs_dev, n, max_numel, n_groups, sumsq, ws):
+    L = lib()
+    check(L.llp_grad_sumsq(descs_dev.data_ptr(), n, max_numel, n_groups, sumsq.data_ptr(), ws.data_ptr(),
+                           ws.numel() * ws.element_size(), stream_ptr()), "llp_grad_sumsq")
+
+
+def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step):
+    L = lib()
+    check(L.llp_adam_step(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
+                          step.data_ptr(), stream_ptr()), "llp_adam_step")
+
+
+def refresh_shadows(descs_dev, n, max_numel):
+    L = lib()
+    check(L.llp_refresh_shadows(descs_dev.data_ptr(), n, max_numel, stream_ptr()), "llp_refresh_shadows")
+
+
+def convert(src, dst):
+    L = lib()
+    assert src.numel() == dst.numel() and src.is_contiguous() and dst.is_contiguous()
+    check(L.llp_convert(dtype_code(src.dtype), dtype_code(dst.dtype), src.numel(), src.data_ptr(), dst.data_ptr(),
+                        stream_ptr()), "llp_convert")
+
+
+def accumulate(src, weight, dst):
+    L = lib()
+    check(L.llp_accumulate(src.numel(), src.data_ptr(), weight, dst.data_ptr(), stream_ptr()), "llp_accumulate")
+
+
+def zero_(t):
+    L = lib()
+    check(L.llp_zero(t.data_ptr(), t.numel() * t.element_size(), stream_ptr()), "llp_zero")
+
+
+def increment(ctr):
+    L = lib()
+    check(L.llp_increment(ctr.data_ptr(), stream_ptr()), "llp_increment")
+
+
+def descs_to_device(descs, device):
+    """Pack a list of TensorDesc into a device byte tensor."""
+    arr = (TensorDesc * len(descs))(*descs)
+    raw = bytes(C.string_at(C.addressof(arr), C.sizeof(arr)))
+    host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    return host.to(device)
+
+
+def relu_bwd(gy, y, alpha, out):
+    L = lib()
+    check(L.llp_relu_bwd(dtype_code(gy.dtype), gy.numel(), gy.data_ptr(), ptr(y), alpha, out.data_ptr(),
+                         stream_ptr()), "llp_relu_bwd")
+
+
+def transpose(W):
+    L = lib()
+    rows, cols = W.shape
+    out = torch.empty(cols, rows, dtype=W.dtype, device=W.device)
+    check(L.llp_transpose(dtype_code(W.dtype), rows, cols, W.data_ptr(), out.data_ptr(), stream_ptr()),
+          "llp_transpose")
+    return out
+
+
+def mul(a, b):
+    L = lib()
+    a, b = a.contiguous(), b.contiguous()
+    out = torch.empty_like(a)
+    check(L.llp_mul(dtype_code(a.dtype), a.numel(), a.data_ptr(), b.data_ptr(), out.data_ptr(), stream_ptr()),
+          "llp_mul")
+    return out
+
+
+def row_scale(z, s):
+    L = lib()
+    z = z.contiguous()
+    out = torch.empty_like(z)
+    check(L.llp_row_scale(dtype_code(z.dtype), z.shape[0], z.shape[1], z.data_ptr(), s.data_ptr(), out.data_ptr(),
+                          stream_ptr()), "llp_row_scale")
+    return out
+
+
+def sigmoid_bwd(gprob, prob, out):
+    L = lib()
+    check(L.llp_sigmoid_bwd(prob.numel(), gprob.data_ptr(), prob.data_ptr(), out.data_ptr(), stream_ptr()),
+          "llp_sigmoid_bwd")

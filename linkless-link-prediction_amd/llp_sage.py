@@ -1,0 +1,105 @@
+"""GraphSAGE teacher pieces on MI355X: the CSR graph layout and the SAGEConv
+layers used by the reference's SAGE encoder (src/models.py:82-119).
+
+  SAGEConv          — torch_geometric 2.2.0 SAGEConv(aggr='mean') semantics
+                      (restated, the package is not installed): mean over
+                      incoming edges, then lin_l (bias) + lin_r (no bias) on the
+                      root (used at src/train_teacher_gnn.py:381-383).
+  SAGEConv_updated  — src/sageconv_updated.py:9-93: lin_l FIRST, then the
+                      mean, then + lin_r(x) (used for coauthor-physics).
+
+State-dict keys (``lin_l.weight``, ``lin_l.bias``, ``lin_r.weight``) match
+PyG's, so the reference's saved teacher weights load here.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+import llp_ops as ops
+
+
+class Graph:
+    """edge_index (2, E) as CSR by destination (PyG flow source_to_target):
+    row i lists the sources of the edges into i, duplicates kept.
+    Also the transposed CSR (by source) and 1/deg for the backward."""
+
+    def __init__(self, edge_index, num_nodes: int, device):
+        ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
+        src = ei[0].astype(np.int64)
+        dst = ei[1].astype(np.int64)
+        N = int(num_nodes)
+        assert src.size < 2 ** 31
+        order = np.argsort(dst, kind="stable")
+        deg = np.bincount(dst, minlength=N)
+        rowptr = np.zeros(N + 1, np.int64)
+        np.cumsum(deg, out=rowptr[1:])
+        order_t = np.argsort(src, kind="stable")
+        deg_t = np.bincount(src, minlength=N)
+        rowptr_t = np.zeros(N + 1, np.int64)
+        np.cumsum(deg_t, out=rowptr_t[1:])
+        dev = torch.device(device)
+        self.num_dst = N
+        self.num_edges = int(src.size)
+        self.rowptr = torch.from_numpy(rowptr.astype(np.int32)).to(dev)
+        self.col = torch.from_numpy(src[order].astype(np.int32)).to(dev)
+        self.rowptr_t = torch.from_numpy(rowptr_t.astype(np.int32)).to(dev)
+        self.col_t = torch.from_numpy(dst[order_t].astype(np.int32)).to(dev)
+        self.inv_deg = torch.from_numpy((1.0 / np.maximum(deg, 1)).astype(np.float32)).to(dev)
+
+
+_GRAPH_CACHE = {}
+
+
+def as_graph(edge_index, num_nodes, device):
+    """Cache the CSR per edge_index tensor (the reference re-passes the same
+    data.adj_t every step, src/train_teacher_gnn.py:43)."""
+    if isinstance(edge_index, Graph):
+        return edge_index
+    key = (id(edge_index), int(num_nodes), str(device))
+    g = _GRAPH_CACHE.get(key)
+    if g is None or g[0] is not edge_index:
+        g = (edge_index, Graph(edge_index, num_nodes, device))
+        _GRAPH_CACHE[key] = g
+    return g[1]
+
+
+class SAGEConv(nn.Module):
+    def __init__(self, in_channels, out_channels, normalize=False, root_weight=True, bias=True, **kwargs):
+        super().__init__()
+        if normalize:
+            raise NotImplementedError("SAGEConv(normalize=True) is not used by the reference")
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.root_weight = root_weight
+        self.lin_l = nn.Linear(in_channels, out_channels, bias=bias)
+        if root_weight:
+            self.lin_r = nn.Linear(in_channels, out_channels, bias=False)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.lin_l.reset_parameters()
+        if self.root_weight:
+            self.lin_r.reset_parameters()
+
+    def forward(self, x, edge_index):
+        g = as_graph(edge_index, x.shape[0], x.device)
+        out = ops.linear(ops.mean_aggregate(x, g), self.lin_l.weight, self.lin_l.bias)
+        if self.root_weight:
+            out = out + ops.linear(x, self.lin_r.weight, None)
+        return out
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, aggr=mean)"
+
+
+class SAGEConv_updated(SAGEConv):
+    """src/sageconv_updated.py:65-81: out = mean_j(W_l x_j + b) + W_r x_i."""
+
+    def forward(self, x, edge_index):
+        g = as_graph(edge_index, x.shape[0], x.device)
+        out = ops.mean_aggregate(ops.linear(x, self.lin_l.weight, self.lin_l.bias), g)
+        if self.root_weight:
+            out = out + ops.linear(x, self.lin_r.weight, None)
+        return out

@@ -1,0 +1,88 @@
+"""Model classes with the reference's constructor signatures and state_dict keys
+(src/models.py), computing on MI355X through libllp_hip (llp_ops.py).
+
+  MLP(num_layers, input_dim, hidden_dim, output_dim, dropout_ratio, norm_type='none')   src/models.py:6-54
+  SAGE(data_name, in, hidden, out, num_layers, dropout, conv_layer, norm_type='none')   src/models.py:82-119
+  LinkPredictor(predictor, in, hidden, out, num_layers, dropout)                        src/models.py:121-150
+
+State-dict keys match (``layers.{i}.weight``, ``lins.{i}.weight``,
+``convs.{i}.lin_l.weight`` ...), so teacher/student checkpoints written by the
+reference load here and vice versa.  Forward/backward run as HIP kernels; a CPU
+tensor raises (no fallback).  norm_type 'batch'/'layer' and the GCN encoder are
+out of scope.
+"""
+import torch
+import torch.nn as nn
+
+import llp_ops as ops
+
+
+class MLP(nn.Module):
+    def __init__(self, num_layers, input_dim, hidden_dim, output_dim, dropout_ratio, norm_type="none"):
+        super().__init__()
+        if norm_type != "none":
+            raise NotImplementedError("MLP norm_type other than 'none' (not on the LLP path, SURVEY §8f)")
+        self.num_layers = num_layers
+        self.norm_type = norm_type
+        self.dropout = nn.Dropout(dropout_ratio)
+        self.layers = nn.ModuleList()
+        self.norms = nn.ModuleList()
+        if num_layers == 1:
+            self.layers.append(nn.Linear(input_dim, output_dim))
+        else:
+            self.layers.append(nn.Linear(input_dim, hidden_dim))
+            for _ in range(num_layers - 2):
+                self.layers.append(nn.Linear(hidden_dim, hidden_dim))
+            self.layers.append(nn.Linear(hidden_dim, output_dim))
+
+    def reset_parameters(self):
+        for layer in self.layers:
+            layer.reset_parameters()
+
+    def forward(self, feats):
+        # Linear, then ReLU + dropout on every layer but the last (src/models.py:45-54),
+        # ReLU and dropout fused into the GEMM epilogue.
+        h = feats
+        for l, layer in enumerate(self.layers):
+            last = l == self.num_layers - 1
+            h = ops.linear(h, layer.weight, layer.bias, relu=not last,
+                           dropout=0.0 if last else self.dropout.p, training=self.training)
+        return h
+
+
+class LinkPredictor(nn.Module):
+    def __init__(self, predictor, in_channels, hidden_channels, out_channels, num_layers, dropout):
+        super().__init__()
+        self.predictor = predictor
+        self.lins = nn.ModuleList()
+        self.lins.append(nn.Linear(in_channels, hidden_channels))
+        for _ in range(num_layers - 2):
+            self.lins.append(nn.Linear(hidden_channels, hidden_channels))
+        self.lins.append(nn.Linear(hidden_channels, out_channels))
+        self.dropout = dropout
+
+    def reset_parameters(self):
+        for lin in self.lins:
+            lin.reset_parameters()
+
+    def forward(self, x_i, x_j):
+        # sigmoid(Lin_L(...ReLU/dropout(Lin_1(x_i * x_j)))) (src/models.py:139-150);
+        # x_i * x_j is formed while the first GEMM stages its A tile.
+        if x_i.shape != x_j.shape:
+            x_i, x_j = torch.broadcast_tensors(x_i, x_j)
+        if self.predictor == "mlp":
+            if self.lins[-1].out_features != 1:
+                raise NotImplementedError("LinkPredictor out_channels != 1")
+            x = None
+            for l, lin in enumerate(self.lins[:-1]):
+                if l == 0:
+                    x = ops.linear(x_i, lin.weight, lin.bias, relu=True, dropout=self.dropout,
+                                   training=self.training, x2=x_j)
+                else:
+                    x = ops.linear(x, lin.weight, lin.bias, relu=True, dropout=self.dropout, training=self.training)
+            if x is None:
+                raise NotImplementedError("LinkPredictor with num_layers < 2")
+            return ops.head(x, self.lins[-1].weight, self.lins[-1].bias)
+        elif self.predictor == "inner":
+            return ops.head(x_i, z2=x_j)
+        raise ValueError(self.predictor)

@@ -1,0 +1,64 @@
+"""The fused HIP distillation step (llp_engine) replayed on the golden vectors
+produced by the reference's own train_minibatch (tests/golden/gen_golden.py),
+with every random tensor injected.  fp32 path: logits/losses within 1e-4."""
+import pytest
+import torch
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _grad_close(got, ref, rtol=2e-4):
+    err = (got - ref).abs().max().item()
+    return err <= rtol * max(ref.abs().max().item(), 1e-6) + 1e-7, err
+
+
+@pytest.mark.parametrize("name", G.MINIBATCH_CASES)
+def test_engine_replays_reference_minibatch(name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import llp_engine
+    import models
+    case = G.load_case(name)
+    a = case.args
+    model = models.MLP(case.L, case.F, case.H, case.H, float(a.dropout)).to(DEV)
+    pred = models.LinkPredictor(a.predictor, case.H, case.H, 1, case.L, float(a.dropout)).to(DEV)
+    tpred = models.LinkPredictor(a.predictor, 256, 256, 1, 2, float(a.dropout)).to(DEV)
+    with torch.no_grad():
+        for p, v in zip(list(model.parameters()) + list(pred.parameters()), case.stu0 + case.pred0):
+            p.copy_(v)
+        for p, v in zip(tpred.parameters(), case.tpred):
+            p.copy_(v)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=float(a.lr))
+    ei = case.edge_index
+    eng = llp_engine.DistillEngine(model, pred, tpred, case.x.to(DEV), case.t_h.to(DEV), ei[0].numpy(),
+                                   ei[1].numpy(), case.N, a, opt, dtype="fp32", seed=1)
+    pairs = case.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+    steps_per_epoch = len(case.steps) // len(case.epoch_losses)
+    tot_ex = 0
+    eng.begin_epoch()
+    for i, st in enumerate(case.steps):
+        eng.step_minibatch(st.node_perm.to(torch.int32).to(DEV), st.link_perm.to(torch.int32).to(DEV), pairs,
+                           samples=st.samples.to(DEV), neg=st.neg_edge.to(DEV))
+        torch.cuda.synchronize()
+        t = eng.terms.cpu()
+        assert abs(t[1].item() - st.bce) <= 1e-4 * max(1, abs(st.bce)), ("bce", t[1].item(), st.bce)
+        assert abs(t[2].item() - st.llp_d) <= 1e-4 * max(1, abs(st.llp_d)), ("kl", t[2].item(), st.llp_d)
+        assert abs(t[3].item() - st.llp_r) <= 1e-4 * max(1, abs(st.llp_r)), ("rank", t[3].item(), st.llp_r)
+        for p, ref in zip(list(model.parameters()) + list(pred.parameters()), st.grads):
+            ok, err = _grad_close(p.grad.detach().cpu(), ref)
+            assert ok, (name, i, tuple(p.shape), err, ref.abs().max().item())
+        tot_ex += st.edge.size(1)
+        if (i + 1) % steps_per_epoch == 0:
+            ep = eng.end_epoch(tot_ex)
+            assert abs(ep - case.epoch_losses[(i + 1) // steps_per_epoch - 1]) < 1e-4, ep
+            tot_ex = 0
+            eng.begin_epoch()
+    # final parameters after several Adam steps
+    for p, ref in zip(list(model.parameters()) + list(pred.parameters()), case.stu_final + case.pred_final):
+        d = (p.detach().cpu() - ref).abs()
+        assert (d <= 1e-4).float().mean().item() > 0.999, (name, tuple(p.shape), d.max().item())

@@ -1,0 +1,318 @@
+"""Parity of each libllp_hip kernel against the CPU oracle / a torch fp32
+reference of the same op.  Run on the MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import llp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import llp_hip
+    llp_hip.lib()
+
+
+def K():
+    import llp_hip
+    return llp_hip
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+# ------------------------------------------------------------------ GEMM NT
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,N,Kd", [(300, 70, 37), (1000, 256, 128), (129, 128, 64), (64, 1, 16), (5, 300, 520)])
+def test_gemm_nt(dt, M, N, Kd):
+    k = K()
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(M, Kd, generator=g)
+    W = torch.randn(N, Kd, generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    Ad, Wd = A.to(DEV, tdt), W.to(DEV, tdt)
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    k.gemm_nt(k.operand(Ad), k.operand(Wd), M, N, Kd, out, k.dtype_code(tdt), bias=b.to(DEV), act=k.ACT_RELU)
+    ref = F.relu(F.linear(A if dt == "fp32" else _bf(A), W if dt == "fp32" else _bf(W), b))
+    tol = 1e-5 if dt == "fp32" else 2e-3
+    assert torch.allclose(out.cpu(), ref, rtol=tol, atol=tol * (1 + ref.abs().max().item())), \
+        (out.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_gemm_nt_gather_hadamard_and_relu_bwd(dt):
+    k = K()
+    g = torch.Generator().manual_seed(1)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    N0, H, M, N = 50, 72, 333, 96
+    X = torch.randn(N0, H, generator=g)
+    ia = torch.randint(0, N0, (M,), generator=g)
+    ib = torch.randint(0, N0, (M,), generator=g)
+    W = torch.randn(N, H, generator=g) * 0.2
+    aux = torch.randn(M, N, generator=g)
+    Xd = X.to(DEV, tdt)
+    out = torch.empty(M, N, device=DEV, dtype=tdt)
+    k.gemm_nt(k.operand(Xd, ia.to(DEV, torch.int32), Xd, ib.to(DEV, torch.int32)), k.operand(W.to(DEV, tdt)), M, N, H,
+              out, k.dtype_code(tdt), act=k.ACT_RELU_BWD, aux=aux.to(DEV, tdt), alpha=2.0)
+    Xr = X if dt == "fp32" else _bf(X)
+    prod = Xr[ia] * Xr[ib]
+    if dt == "bf16":
+        prod = _bf(prod)
+    ref = 2.0 * F.linear(prod, W if dt == "fp32" else _bf(W)) * ((aux if dt == "fp32" else _bf(aux)) > 0)
+    tol = 1e-5 if dt == "fp32" else 1e-2
+    assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * (1 + ref.abs().max().item()))
+
+
+def test_gemm_nt_dropout_is_deterministic_and_unbiased():
+    k = K()
+    M, N, Kd = 512, 256, 64
+    A = torch.randn(M, Kd, device=DEV)
+    W = torch.randn(N, Kd, device=DEV) * 0.1
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    outs = []
+    for _ in range(2):
+        o = torch.empty(M, N, device=DEV)
+        k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, o, 0, act=k.ACT_NONE,
+                  dropout=k.Dropout(0.5, 1234, ctr.data_ptr(), 3))
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1])
+    full = A @ W.t()
+    kept = outs[0] != 0
+    frac = kept.float().mean().item()
+    assert 0.48 < frac < 0.52
+    assert torch.allclose(outs[0][kept], 2.0 * full[kept], rtol=1e-4, atol=1e-4)
+
+
+# ------------------------------------------------------------------ GEMM TN (weight grads)
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,P,Q", [(1000, 64, 48), (5000, 256, 128), (77, 130, 20), (20000, 128, 256)])
+def test_gemm_tn(dt, M, P, Q):
+    k = K()
+    g = torch.Generator().manual_seed(M + P)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    A = torch.randn(M, P, generator=g)
+    B = torch.randn(M, Q, generator=g)
+    out = torch.empty(P, Q, device=DEV)
+    ws = torch.empty(k.gemm_tn_ws_bytes(k.dtype_code(tdt), M, P, Q) // 4 + 16, device=DEV)
+    k.gemm_tn(k.operand(A.to(DEV, tdt)), k.operand(B.to(DEV, tdt)), M, P, Q, out, k.dtype_code(tdt), ws)
+    ref = (A if dt == "fp32" else _bf(A)).double().t() @ (B if dt == "fp32" else _bf(B)).double()
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= (1e-4 if dt == "fp32" else 2e-3) * (1 + ref.abs().max().item()), err
+
+
+def test_gemm_tn_gathered_hadamard_operand():
+    k = K()
+    g = torch.Generator().manual_seed(3)
+    M, P, Q, N0 = 3000, 64, 96, 200
+    A = torch.randn(M, P, generator=g)
+    X = torch.randn(N0, Q, generator=g)
+    ia = torch.randint(0, N0, (M,), generator=g)
+    ib = torch.randint(0, N0, (M,), generator=g)
+    out = torch.empty(P, Q, device=DEV)
+    ws = torch.empty(k.gemm_tn_ws_bytes(0, M, P, Q) // 4 + 16, device=DEV)
+    Xd = X.to(DEV)
+    k.gemm_tn(k.operand(A.to(DEV)), k.operand(Xd, ia.to(DEV, torch.int32), Xd, ib.to(DEV, torch.int32)), M, P, Q,
+              out, 0, ws)
+    ref = A.double().t() @ (X[ia] * X[ib]).double()
+    assert (out.cpu().double() - ref).abs().max().item() < 1e-3
+
+
+# ------------------------------------------------------------------ heads, colsum
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_head_fwd_bwd_and_colsum(dt):
+    k = K()
+    g = torch.Generator().manual_seed(4)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    R, H = 1000, 200
+    Z = torch.relu(torch.randn(R, H, generator=g))
+    w = torch.randn(H, generator=g)
+    b = torch.randn(1, generator=g)
+    Zd = Z.to(DEV, tdt)
+    Zr = Z if dt == "fp32" else _bf(Z)
+    logit = torch.empty(R, device=DEV)
+    prob = torch.empty(R, device=DEV)
+    k.head_fwd(Zd, R, H, w.to(DEV), b.to(DEV), logit=logit, prob=prob)
+    ref = Zr @ w + b
+    assert torch.allclose(logit.cpu(), ref, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(prob.cpu(), torch.sigmoid(ref), rtol=1e-5, atol=1e-6)
+    dlogit = torch.randn(R, generator=g)
+    dZ = torch.empty(R, H, device=DEV, dtype=tdt)
+    dw = torch.empty(H, device=DEV)
+    db = torch.empty(1, device=DEV)
+    ws = torch.empty(k.head_bwd_ws_bytes(R, H) // 4 + 16, device=DEV)
+    k.head_bwd(dlogit.to(DEV), Zd, R, H, w.to(DEV), True, dZ, dw, db, ws, alpha=1.5)
+    ref_dZ = 1.5 * dlogit[:, None] * w[None, :] * (Zr > 0)
+    tol = 1e-6 if dt == "fp32" else 1e-2
+    assert torch.allclose(dZ.float().cpu(), ref_dZ, rtol=tol, atol=tol)
+    assert torch.allclose(dw.cpu(), dlogit @ Zr, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(db.cpu(), dlogit.sum().reshape(1), rtol=1e-5, atol=1e-4)
+    cs = torch.empty(H, device=DEV)
+    k.colsum(Zd, R, H, cs, ws)
+    assert torch.allclose(cs.cpu(), Zr.sum(0), rtol=1e-5, atol=1e-3)
+
+
+# ------------------------------------------------------------------ fused LLP loss
+@pytest.mark.parametrize("B,C,margin", [(37, 12, 0.1), (64, 36, 0.01), (5, 70, 0.2), (3, 2, 0.05)])
+def test_llp_loss_matches_oracle(B, C, margin):
+    k = K()
+    g = torch.Generator().manual_seed(B * C)
+    s_logit = torch.randn(B, C, generator=g) * 2
+    t_prob = torch.rand(B, C, generator=g)
+    t_prob[0, :2] = 0.5   # exact ties -> y = 0 pairs (Q5)
+    n_pos = 50
+    out_logit = torch.randn(2 * n_pos, generator=g) * 3
+    wl, wd, wr = 0.7, 1.3, 2.1
+    dlog = torch.empty(B * C + 2 * n_pos, device=DEV)
+    terms = torch.zeros(4, device=DEV)
+    ws = torch.empty(k.llp_loss_ws_bytes(B, 2 * n_pos) // 4 + 16, device=DEV)
+    sl = s_logit.reshape(-1).to(DEV)
+    ol = out_logit.to(DEV)
+    k.llp_loss(B, C, sl, t_prob.reshape(-1).to(DEV), 2 * n_pos, n_pos, ol, B, 2 * n_pos, margin, 1.0, wl, wd, wr,
+               dlog, dlog[B * C:], terms, ws)
+    # oracle through torch autograd (fp64)
+    s = s_logit.double().requires_grad_()
+    o = out_logit.double().requires_grad_()
+    sp = torch.sigmoid(s)
+    kl = O.kl_loss(sp, t_prob.double(), 1)
+    rk = O.rank_loss(sp, t_prob.double(), margin)
+    lab = torch.cat([torch.ones(n_pos), torch.zeros(n_pos)]).double()
+    bce = O.bce_loss(torch.sigmoid(o), lab)
+    loss = wl * bce + wd * kl + wr * rk
+    loss.backward()
+    t = terms.cpu()
+    assert abs(t[0].item() - loss.item()) < 1e-5 * max(1, abs(loss.item()))
+    assert abs(t[1].item() - bce.item()) < 1e-5
+    assert abs(t[2].item() - kl.item()) < 1e-5
+    assert abs(t[3].item() - rk.item()) < 1e-5
+    d = dlog.cpu().double()
+    assert torch.allclose(d[:B * C], s.grad.reshape(-1), rtol=1e-4, atol=1e-7)
+    assert torch.allclose(d[B * C:], o.grad, rtol=1e-4, atol=1e-7)
+
+
+# ------------------------------------------------------------------ samplers (bit-exact)
+@pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 1, 15, 0)])
+@pytest.mark.parametrize("sorted_", [False, True])
+def test_context_sampler_bit_exact(ps, rw_step, hops, ns_rate, sorted_):
+    import llp_engine
+    k = K()
+    rng = np.random.default_rng(5)
+    N = 500
+    u = rng.integers(0, N, 3000)
+    v = rng.integers(0, N, 3000)
+    pairs = np.stack([u, v], 1)
+    ei = np.stack([pairs, pairs[:, ::-1]], 1).reshape(-1, 2).T   # interleaved, unsorted (Q1)
+    ei = ei[:, ei[0] % 17 != 3]                                   # leave some isolated nodes (deg 0)
+    rowptr, col = llp_engine.build_sampler_csr(ei[0], ei[1], N, sorted_)
+    start = rng.permutation(N)[:123].astype(np.int32)
+    C1 = 1 + rw_step * hops * (1 + ns_rate)
+    out = torch.empty(123, C1, dtype=torch.int32, device=DEV)
+    ctr = torch.tensor([7], dtype=torch.int64, device=DEV)
+    k.context_sampler(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(col).to(DEV), N,
+                      torch.from_numpy(start).to(DEV), 123, ps, rw_step, hops, ns_rate, 99, ctr, 0, out, b_offset=0)
+    pos, neg = O.neighbor_samplers(rowptr.astype(np.int64), col.astype(np.int64), start, N, rw_step, ps, ns_rate,
+                                   hops, seed=99, stream_base=16 * 7)
+    ref = np.concatenate([pos, neg], 1)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    # shard invariance: anchors [60, 123) drawn by a second "rank" match
+    out2 = torch.empty(63, C1, dtype=torch.int32, device=DEV)
+    k.context_sampler(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(col).to(DEV), N,
+                      torch.from_numpy(start[60:]).to(DEV), 63, ps, rw_step, hops, ns_rate, 99, ctr, 0, out2,
+                      b_offset=60)
+    assert np.array_equal(out2.cpu().numpy(), ref[60:])
+
+
+def test_random_walk_follows_unsorted_csr_semantics():
+    """Q1: with coalesced=False the walk indexes col in array order."""
+    import llp_engine
+    row = np.array([1, 0, 2, 0, 1, 2])
+    col = np.array([0, 1, 0, 2, 2, 1])
+    rowptr, colv = llp_engine.build_sampler_csr(row, col, 3, False)
+    assert rowptr.tolist() == [0, 2, 4, 6]
+    assert colv.tolist() == [0, 1, 0, 2, 2, 1]   # node 0's "neighbours" = col[0:2] = [0, 1] (unsorted order)
+
+
+def test_randint_pairs_bit_exact_and_sharded():
+    k = K()
+    ctr = torch.tensor([3], dtype=torch.int64, device=DEV)
+    out = torch.empty(2, 1000, dtype=torch.int32, device=DEV)
+    k.randint_pairs(12345, 1000, 77, ctr, 15, out)
+    ref = O.randint_edges(12345, 1000, seed=77, stream=16 * 3 + 15)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    part = torch.empty(2, 300, dtype=torch.int32, device=DEV)
+    k.randint_pairs(12345, 300, 77, ctr, 15, part, n_total=1000, offset=500)
+    assert np.array_equal(part.cpu().numpy(), ref[:, 500:800])
+
+
+# ------------------------------------------------------------------ SAGE aggregate
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("F_", [128, 256, 30, 8])
+def test_csr_mean_aggregate_fwd_bwd(dt, F_):
+    import llp_sage
+    k = K()
+    rng = np.random.default_rng(F_)
+    N = 700
+    u = rng.integers(0, N, 5000)
+    v = rng.integers(0, N, 5000)
+    ei = torch.from_numpy(np.stack([np.concatenate([u, v, u[:100]]), np.concatenate([v, u, v[:100]])]))  # dup edges
+    g = llp_sage.Graph(ei, N, DEV)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    x = torch.randn(N, F_)
+    xr = x if dt == "fp32" else _bf(x)
+    out = torch.empty(N, F_, device=DEV, dtype=tdt)
+    k.csr_aggregate(N, F_, g.rowptr, g.col, x.to(DEV, tdt), None, 0, out)
+    ref = O.sage_mean_aggregate(xr, ei[0], ei[1], N)
+    tol = 1e-5 if dt == "fp32" else 1e-2
+    assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol)
+    # backward: d/dx of sum(out * gout)
+    gout = torch.randn(N, F_)
+    xg = xr.clone().requires_grad_()
+    (O.sage_mean_aggregate(xg, ei[0], ei[1], N) * (gout if dt == "fp32" else _bf(gout))).sum().backward()
+    gx = torch.empty(N, F_, device=DEV, dtype=tdt)
+    k.csr_aggregate(N, F_, g.rowptr_t, g.col_t, gout.to(DEV, tdt), g.inv_deg, 1, gx)
+    assert torch.allclose(gx.float().cpu(), xg.grad, rtol=tol, atol=tol * 2)
+
+
+# ------------------------------------------------------------------ clip + Adam
+def test_clip_and_adam_match_oracle():
+    k = K()
+    g = torch.Generator().manual_seed(9)
+    shapes = [(64, 32), (64,), (1, 64), (1,)]
+    params = [torch.randn(*s, generator=g) for s in shapes]
+    grads = [torch.randn(*s, generator=g) * 3 for s in shapes]
+    groups = [0, 0, 1, 1]
+    dp = [p.to(DEV).clone() for p in params]
+    dg = [x.to(DEV).clone() for x in grads]
+    m = [torch.zeros_like(p) for p in dp]
+    v = [torch.zeros_like(p) for p in dp]
+    descs = []
+    for i, p in enumerate(dp):
+        rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+        descs.append(k.TensorDesc(p.data_ptr(), dg[i].data_ptr(), m[i].data_ptr(), v[i].data_ptr(), None, None,
+                                  p.numel(), rows, cols, groups[i], 0))
+    dd = k.descs_to_device(descs, DEV)
+    sumsq = torch.zeros(2, device=DEV)
+    ws = torch.empty(k.grad_sumsq_ws_bytes(4, 64 * 32) // 4 + 16, device=DEV)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    adam = O.AdamState(params, lr=0.01)
+    cur = [p.clone() for p in params]
+    for it in range(3):
+        gs = [x * (it + 1) for x in grads]
+        for i in range(4):
+            dg[i].copy_(gs[i].to(DEV))
+        k.grad_sumsq(dd, 4, 64 * 32, 2, sumsq, ws)
+        k.adam_step(dd, 4, 64 * 32, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step)
+        c0, _ = O.clip_grad_norm(gs[:2])
+        c1, _ = O.clip_grad_norm(gs[2:])
+        cur = adam.step(cur, c0 + c1)
+    assert step.item() == 3
+    for a, b in zip(dp, cur):
+        assert torch.allclose(a.cpu(), b, rtol=1e-5, atol=1e-6)
