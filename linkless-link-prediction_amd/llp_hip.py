@@ -136,6 +136,7 @@ def operand(t, idx=None, t2=None, idx2=None) -> Operand:
     if idx is not None:
         assert idx.dtype == torch.int32 and idx.is_contiguous()
     o = Operand(t.data_ptr(), ptr(idx), ptr(t2), ptr(idx2), t.stride(0), t2.stride(0) if t2 is not None else 0)
+    o._keep = (t, idx, t2, idx2)   # the struct holds raw pointers: keep the tensors alive with it
     return o
 
 
