@@ -132,6 +132,13 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
                  float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
                  void* workspace, int64_t workspace_bytes, void* stream);
 
+/* out[r, :] = a[ia[r], :] * b[ib[r], :]   (ia/ib NULL = identity) — the
+ * predictor input x_i * x_j (src/models.py:140) materialised once per step so
+ * the first predictor layer's forward and weight-gradient GEMMs both stream it
+ * with global_load_lds.  Rows of 16-byte multiples. */
+int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a, const int32_t* ia, const void* b,
+                      const int32_t* ib, void* out, void* stream);
+
 /* ---------------------------------------------------------------- Hadamard backward
  * Backward of x_i * x_j (src/models.py:140) for the minibatch row layout of
  * src/main.py:95-105 (h rows: B anchor blocks of (1 + C) rows, then 2L src

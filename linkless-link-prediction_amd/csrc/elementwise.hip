@@ -73,6 +73,35 @@ __global__ __launch_bounds__(256) void hadamard_bwd_scatter_kernel(int64_t R, in
   }
 }
 
+// out[r, :] = a[ia[r], :] * b[ib[r], :]  — 16-byte chunks, one per thread.
+template <typename T>
+__global__ __launch_bounds__(256) void hadamard_rows_kernel(int64_t R, int64_t H, const T* __restrict__ a,
+                                                             const int32_t* __restrict__ ia, const T* __restrict__ b,
+                                                             const int32_t* __restrict__ ib, T* __restrict__ out) {
+  constexpr int E = 16 / sizeof(T);
+  const int64_t cpr = H / E;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= R * cpr) return;
+  const int64_t r = t / cpr, c = t % cpr;
+  const int64_t ra = ia ? (int64_t)ia[r] : r, rb = ib ? (int64_t)ib[r] : r;
+  const uint4 x = *reinterpret_cast<const uint4*>(a + ra * H + c * E);
+  const uint4 y = *reinterpret_cast<const uint4*>(b + rb * H + c * E);
+  uint4 o;
+  if constexpr (sizeof(T) == 2) {
+    auto m2 = [](uint32_t p, uint32_t q) {
+      return (uint32_t)f2bf(__uint_as_float(p << 16) * __uint_as_float(q << 16)) |
+             ((uint32_t)f2bf(__uint_as_float(p & 0xFFFF0000u) * __uint_as_float(q & 0xFFFF0000u)) << 16);
+    };
+    o = make_uint4(m2(x.x, y.x), m2(x.y, y.y), m2(x.z, y.z), m2(x.w, y.w));
+  } else {
+    o = make_uint4(__float_as_uint(__uint_as_float(x.x) * __uint_as_float(y.x)),
+                   __float_as_uint(__uint_as_float(x.y) * __uint_as_float(y.y)),
+                   __float_as_uint(__uint_as_float(x.z) * __uint_as_float(y.z)),
+                   __float_as_uint(__uint_as_float(x.w) * __uint_as_float(y.w)));
+  }
+  *reinterpret_cast<uint4*>(out + r * H + c * E) = o;
+}
+
 // ---------------------------------------------------------------- optimiser
 constexpr int OPT_CHUNK = 4096;  // elements per block
 
@@ -199,6 +228,25 @@ extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t 
   else
     hipLaunchKernelGGL(hadamard_bwd_blocks_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, B, C, L2, H,
                        (const float*)dZ, drow, (const float*)h, (float*)dh);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a, const int32_t* ia, const void* b,
+                                 const int32_t* ib, void* out, void* stream) {
+  LLP_CHECK_ARG(a && b && out, "llp_hadamard_rows: null pointer");
+  const int es = dtype == LLP_BF16 ? 2 : 4;
+  LLP_CHECK_ARG((H * es) % 16 == 0 && (uintptr_t)a % 16 == 0 && (uintptr_t)b % 16 == 0 && (uintptr_t)out % 16 == 0,
+                "llp_hadamard_rows: rows must be 16-byte multiples and aligned");
+  const int64_t n = R * (H * es / 16);
+  if (n == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(hadamard_rows_kernel<bf16_t>, dim3(ceil_div_u(n, 256)), dim3(256), 0, s, R, H,
+                       (const bf16_t*)a, ia, (const bf16_t*)b, ib, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(hadamard_rows_kernel<float>, dim3(ceil_div_u(n, 256)), dim3(256), 0, s, R, H, (const float*)a,
+                       ia, (const float*)b, ib, (float*)out);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

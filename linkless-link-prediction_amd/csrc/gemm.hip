@@ -17,6 +17,14 @@
 //         ds_read_b32 (TN).
 #include "llp_common.h"
 
+int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
+                         int64_t ldc, const float* bias, int act, const void* aux, int64_t ld_aux, float alpha,
+                         float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
+                         const int64_t* drop_ctr, int64_t drop_stream, hipStream_t s);
+int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q);
+int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
+                         int64_t splits, hipStream_t s);
+
 namespace {
 
 constexpr int BM = 128;
@@ -534,6 +542,17 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   LLP_CHECK_ARG(tiles < (1ll << 31), "llp_gemm_nt: too many tiles");
   hipStream_t s = (hipStream_t)stream;
+  // Large-tile bf16 kernel (gemm256.hip) whenever the layout allows it.
+  static const bool force_v1 = getenv("LLP_GEMM_V1") != nullptr;
+  auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
+  if (!force_v1 && dtype == LLP_BF16 && c_dtype == LLP_BF16 && K > 0 && K % 64 == 0 && N % 8 == 0 && !B->ptr2 &&
+      a16(A->ptr, A->ld) && (!A->ptr2 || a16(A->ptr2, A->ld2)) && a16(B->ptr, B->ld) && a16(C, ldc) &&
+      (act != LLP_ACT_RELU_BWD || (aux_dtype == LLP_BF16 && a16(aux, ld_aux)))) {
+    const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, aux, ld_aux, alpha, p.drop_p,
+                                        p.drop_thresh, p.drop_scale, p.drop_seed, p.drop_ctr, p.drop_stream, s);
+    if (rc != 0) return llp::set_error(rc, "llp_gemm_nt (256 tile): %s", hipGetErrorString((hipError_t)rc));
+    return LLP_OK;
+  }
   const int es = dtype == LLP_BF16 ? 2 : 4;
   const bool vec = aligned_op(A, es, K) && aligned_op(B, es, K);
   dim3 grid((unsigned)tiles);
@@ -549,7 +568,9 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
 }
 
 extern "C" int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q) {
-  return tn_splits(dtype, M, P, Q) * P * Q * (int64_t)sizeof(float);
+  int64_t s = tn_splits(dtype, M, P, Q);
+  if (dtype == LLP_BF16) s = std::max(s, llp_gemm_tn_256_splits(M, P, Q));
+  return s * P * Q * (int64_t)sizeof(float);
 }
 
 extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A,
@@ -558,6 +579,24 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
   LLP_CHECK_ARG(A && B && C, "llp_gemm_tn: null operand");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_tn: bad dtype %d", dtype);
   if (P == 0 || Q == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  static const bool force_v1 = getenv("LLP_GEMM_V1") != nullptr;
+  auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
+  if (!force_v1 && dtype == LLP_BF16 && P % 8 == 0 && Q % 8 == 0 && !A->ptr2 && !B->ptr2 && a16(A->ptr, A->ld) &&
+      a16(B->ptr, B->ld)) {
+    // large-tile glds kernel (gemm256_tn.hip)
+    const int64_t sp = llp_gemm_tn_256_splits(M, P, Q);
+    if (workspace_bytes < sp * P * Q * (int64_t)sizeof(float) || !workspace)
+      return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace too small");
+    const int rc = llp_gemm_tn_bf16_256(A, B, M, P, Q, reinterpret_cast<float*>(workspace), sp, s);
+    if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (256 tile): %s", hipGetErrorString((hipError_t)rc));
+    const int64_t n = P * Q;
+    unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, (const float*)workspace, sp, P, Q, C, ldc,
+                       accumulate);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
   const int64_t splits = tn_splits(dtype, M, P, Q);
   if (workspace_bytes < splits * P * Q * (int64_t)sizeof(float) || !workspace)
     return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace %lld < %lld", (long long)workspace_bytes,
@@ -572,7 +611,6 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
   p.mchunk = mchunk > 0 ? mchunk : bkm;
   p.ws = reinterpret_cast<float*>(workspace);
   const int64_t tiles = ((P + BM - 1) / BM) * ((Q + BN - 1) / BN);
-  hipStream_t s = (hipStream_t)stream;
   const int es = dtype == LLP_BF16 ? 2 : 4;
   const bool vec = aligned_op(A, es, P) && aligned_op(B, es, Q);
   p.splits = splits;

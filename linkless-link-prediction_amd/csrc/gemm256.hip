@@ -1,0 +1,264 @@
+// Large-tile bf16 MFMA GEMM (NT form) for the LLP hot path — the kernel that
+// carries the student MLP / LinkPredictor / teacher-predictor Linear layers
+// (src/models.py:48,143,146) and their data-gradients.
+//
+//   C[m, n] = epi(alpha * sum_k A[m, k] * B[n, k])      bf16 in, f32 accumulate, bf16 out
+//
+// Geometry: 256 x 256 output tile per 512-thread workgroup (8 waves as 2 (m) x
+// 4 (n), 128 x 64 per wave), BK = 64, one workgroup per CU (128 KiB of LDS
+// double-buffered stages).  Staging: global_load_lds_dwordx4 (per-lane source
+// address = gathered row, XOR-swizzled 16-B chunks, lane-linear LDS image) for
+// plain / gathered operands; register staging (two loads, multiply, ds_write)
+// when A is a Hadamard product x_i * x_j (src/models.py:140).
+// MFMA roles are swapped (weights = MFMA A operand, activations = MFMA B
+// operand) so that a lane's accumulator holds 4 CONSECUTIVE output columns of
+// one output row: the epilogue (bias, ReLU, dropout) runs in registers, the
+// tile is staged row-major through LDS and written with 16-byte coalesced
+// stores; the ReLU-backward mask (aux) is read with the same 16-byte pattern.
+#include "llp_common.h"
+
+namespace {
+
+constexpr int TM = 256, TN = 256, TK = 64;
+constexpr int NT2 = 512;
+constexpr int STAGE_U4 = (TM + TN) * 8;          // uint4 per stage (A then B), 64 KiB
+constexpr int EPI_ROW_U4 = TN / 8 + 1;           // 16-B chunks per staged C row (+1 pad)
+constexpr int SMEM_U4_LOOP = 2 * STAGE_U4;       // 128 KiB
+constexpr int SMEM_U4_EPI = TM * EPI_ROW_U4;     // 132 KiB
+constexpr int SMEM_U4 = SMEM_U4_LOOP > SMEM_U4_EPI ? SMEM_U4_LOOP : SMEM_U4_EPI;
+
+struct P256 {
+  const bf16_t* A;  const int32_t* ia;  const bf16_t* A2; const int32_t* ia2; int64_t lda, lda2;
+  const bf16_t* B;  const int32_t* ib;  int64_t ldb;
+  int64_t M, N, K;
+  bf16_t* C; int64_t ldc;
+  const float* bias;
+  int act;
+  const bf16_t* aux; int64_t ld_aux;
+  float alpha;
+  float drop_p; uint32_t drop_thresh; float drop_scale; uint64_t drop_seed; const int64_t* drop_ctr;
+  int64_t drop_stream;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int64_t xcd_remap2(int64_t bid, int64_t nwg) {
+  if (nwg < 8) return bid;
+  const int64_t q = nwg / 8, r = nwg % 8;
+  const int64_t xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+__device__ __forceinline__ uint32_t mulbf2(uint32_t a, uint32_t b) {
+  const float a0 = __uint_as_float(a << 16), a1 = __uint_as_float(a & 0xFFFF0000u);
+  const float b0 = __uint_as_float(b << 16), b1 = __uint_as_float(b & 0xFFFF0000u);
+  return (uint32_t)f2bf(a0 * b0) | ((uint32_t)f2bf(a1 * b1) << 16);
+}
+
+template <bool HADA>
+__global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[SMEM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TM - 1) / TM;
+  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
+  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+
+  // ---------------- staging addresses
+  // glds: wave w stages rows [32w, 32w+32) of A and of B: 4 instructions each,
+  // instruction i covers rows 32w + 8i + (lane>>3), physical chunk lane&7.
+  const int srow0 = 32 * w + (lane >> 3);
+  const int pch = lane & 7;
+  const bf16_t* ga[4];
+  const bf16_t* gb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = srow0 + 8 * i;
+    const int lc = pch ^ (r & 7);                      // logical chunk stored at physical pch
+    int64_t m = m0 + r;
+    m = m < p.M ? m : p.M - 1;
+    const int64_t pm = p.ia ? (int64_t)p.ia[m] : m;
+    ga[i] = p.A + pm * p.lda + lc * 8;
+    int64_t n = n0 + r;
+    n = n < p.N ? n : p.N - 1;
+    const int64_t pn = p.ib ? (int64_t)p.ib[n] : n;
+    gb[i] = p.B + pn * p.ldb + lc * 8;
+  }
+  // register staging of a Hadamard A: thread t owns chunks t + 512*i (i < 4):
+  // row (t>>3) + 64 i, logical chunk t & 7.
+  const bf16_t* ha[4];
+  const bf16_t* ha2[4];
+  if (HADA) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t m = m0 + (tid >> 3) + 64 * i;
+      m = m < p.M ? m : p.M - 1;
+      ha[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + (tid & 7) * 8;
+      ha2[i] = p.A2 + (p.ia2 ? (int64_t)p.ia2[m] : m) * p.lda2 + (tid & 7) * 8;
+    }
+  }
+  uint4 hr[4], hr2[4];
+
+  auto stage_glds = [&](int buf, int64_t kt) {
+    uint4* sA = smem + buf * STAGE_U4;
+    uint4* sB = sA + TM * 8;
+    const int64_t koff = kt * TK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!HADA)
+        __builtin_amdgcn_global_load_lds((const void*)(ga[i] + koff), (lds_void*)(sA + (32 * w + 8 * i) * 8), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gb[i] + koff), (lds_void*)(sB + (32 * w + 8 * i) * 8), 16, 0, 0);
+    }
+  };
+  auto hada_load = [&](int64_t kt) {
+    const int64_t koff = kt * TK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hr[i] = *reinterpret_cast<const uint4*>(ha[i] + koff);
+      hr2[i] = *reinterpret_cast<const uint4*>(ha2[i] + koff);
+    }
+  };
+  auto hada_store = [&](int buf) {
+    uint4* sA = smem + buf * STAGE_U4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 64 * i, c = tid & 7;
+      uint4 v;
+      v.x = mulbf2(hr[i].x, hr2[i].x); v.y = mulbf2(hr[i].y, hr2[i].y);
+      v.z = mulbf2(hr[i].z, hr2[i].z); v.w = mulbf2(hr[i].w, hr2[i].w);
+      sA[r * 8 + (c ^ (r & 7))] = v;
+    }
+  };
+
+  // ---------------- main loop
+  const int wm = w >> 2, wn = w & 3;
+  float4_t acc[4][8];   // [n-tile jn][m-tile im]: rows n = 16 jn + 4 g + r, col m = 16 im + li
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = p.K / TK;
+  if (HADA) hada_load(0);
+  stage_glds(0, 0);
+  if (HADA) hada_store(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int buf = (int)(kt & 1);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      if (HADA) hada_load(kt + 1);
+      stage_glds(buf ^ 1, kt + 1);
+    }
+    const uint4* sA = smem + buf * STAGE_U4;
+    const uint4* sB = sA + TM * 8;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      short8 fw[4], fx[8];
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) {
+        const int r = wn * 64 + jn * 16 + li;
+        uint4 v = sB[r * 8 + ((g + 4 * s) ^ (r & 7))];
+        fw[jn] = *reinterpret_cast<short8*>(&v);
+      }
+#pragma unroll
+      for (int im = 0; im < 8; ++im) {
+        const int r = wm * 128 + im * 16 + li;
+        uint4 v = sA[r * 8 + ((g + 4 * s) ^ (r & 7))];
+        fx[im] = *reinterpret_cast<short8*>(&v);
+      }
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+        for (int im = 0; im < 8; ++im)
+          acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
+    }
+    if (more && HADA) hada_store(buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---------------- epilogue in registers: alpha, bias, ReLU, dropout
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  uint4* stg = smem;   // staged C tile: row-major [256][EPI_ROW_U4] uint4
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn) {
+    const int nl = wn * 64 + jn * 16 + g * 4;          // local column of element r = 0
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? p.bias[n0 + nl + r] : 0.f;
+    }
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int ml = wm * 128 + im * 16 + li;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = p.alpha * acc[jn][im][r] + bv[r];
+        if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (p.drop_p > 0.f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)((m0 + ml) * p.N + n0 + nl + r));
+          v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
+        }
+      }
+      const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
+      *dst = make_uint2(lo, hi);
+    }
+  }
+  __syncthreads();
+  // ---------------- coalesced write-out (+ ReLU-backward mask from aux)
+  const int chunks_per_row = TN / 8;   // 32
+#pragma unroll 4
+  for (int q = tid; q < TM * chunks_per_row; q += NT2) {
+    const int rl = q / chunks_per_row, c = q % chunks_per_row;
+    const int64_t row = m0 + rl, col = n0 + c * 8;
+    if (row >= p.M || col >= p.N) continue;
+    uint4 v = stg[rl * EPI_ROW_U4 + c];
+    if (p.act == LLP_ACT_RELU_BWD) {
+      const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
+      const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
+        const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
+        vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+      }
+      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+  }
+}
+
+}  // namespace
+
+// Called from llp_gemm_nt when the shapes allow it (gemm.hip).
+int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
+                         int64_t ldc, const float* bias, int act, const void* aux, int64_t ld_aux, float alpha,
+                         float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
+                         const int64_t* drop_ctr, int64_t drop_stream, hipStream_t s) {
+  P256 p;
+  p.A = (const bf16_t*)A->ptr; p.ia = A->idx; p.A2 = (const bf16_t*)A->ptr2; p.ia2 = A->idx2;
+  p.lda = A->ld; p.lda2 = A->ptr2 ? A->ld2 : 0;
+  p.B = (const bf16_t*)B->ptr; p.ib = B->idx; p.ldb = B->ld;
+  p.M = M; p.N = N; p.K = K;
+  p.C = (bf16_t*)C; p.ldc = ldc;
+  p.bias = bias; p.act = act; p.aux = (const bf16_t*)aux; p.ld_aux = ld_aux; p.alpha = alpha;
+  p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
+  p.drop_ctr = drop_ctr; p.drop_stream = drop_stream;
+  const int64_t tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  if (A->ptr2)
+    hipLaunchKernelGGL(gemm_nt_bf16_256<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else
+    hipLaunchKernelGGL(gemm_nt_bf16_256<false>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,181 @@
+// Large-tile bf16 MFMA weight-gradient GEMM (TN form):
+//
+//   ws[z][p][q] = sum_{m in split z} A[m, p] * B[m, q]      (A = dY, B = X; f32 slabs)
+//
+// Replaces autograd's weight-gradient of every nn.Linear on the distillation
+// path (src/main.py:132).  256 (p) x 256 (q) tile per 512-thread workgroup,
+// 64 rows of m per stage, both operands staged by global_load_lds_dwordx4 into
+// [m][256] images (512-B rows, 16-B chunks XOR-swizzled by m) and read as MFMA
+// fragments with ds_read_b64_tr_b16 (the contraction index m is the image's
+// row).  Rows past the split's end read a zero row, so no m-tail handling is
+// needed in the MFMA loop.  B rows may be gathered (x[this_target], the first
+// student layer).  MFMA roles put 4 consecutive q of one p in a lane, so the
+// f32 slab is written with 16-byte stores.
+#include "llp_common.h"
+
+namespace {
+
+constexpr int TP = 256, TQ = 256, TKM = 64;
+constexpr int NTT = 512;
+constexpr int IMG_U4 = TKM * 32;            // one [64][256] bf16 image = 2048 uint4 = 32 KiB
+constexpr int STAGE_T = 2 * IMG_U4;         // A image + B image
+
+__device__ __attribute__((aligned(16))) uint4 g_zero_row[64];   // 1 KiB of zeros (static init)
+
+struct PTN {
+  const bf16_t* A; const int32_t* ia; int64_t lda;
+  const bf16_t* B; const int32_t* ib; int64_t ldb;
+  int64_t M, P, Q, mchunk, splits;
+  float* ws;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) short4_t lds_s4;
+
+__device__ __forceinline__ int64_t xcd_remap3(int64_t bid, int64_t nwg) {
+  if (nwg < 8) return bid;
+  const int64_t q = nwg / 8, r = nwg % 8;
+  const int64_t xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// swizzle of the 16-B chunk index within a 512-B image row (low 4 bits only)
+__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+__global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * STAGE_T];   // 128 KiB
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
+  const int64_t tilesP = (p.P + TP - 1) / TP;
+  const int64_t lt = xcd_remap3(blockIdx.x, tilesP * tilesQ * p.splits);
+  const int64_t tile = lt / p.splits, z = lt % p.splits;
+  const int64_t p0 = (tile / tilesQ) * TP, q0 = (tile % tilesQ) * TQ;
+  const int64_t mbeg = z * p.mchunk;
+  const int64_t mend = min(p.M, mbeg + p.mchunk);
+
+  // glds assignment: wave w stages image rows [8w, 8w+8): instruction i covers
+  // rows 8w + 2i + (lane >> 5), physical chunk lane & 31.
+  const int pc = lane & 31;
+  const int rbase = 8 * w + (lane >> 5);
+  // columns past P / Q are clamped to a valid address (their products are never stored)
+  const int capA = (int)max((int64_t)0, (p.P - p0) - 8), capB = (int)max((int64_t)0, (p.Q - q0) - 8);
+  const bf16_t* zrow = reinterpret_cast<const bf16_t*>(g_zero_row);
+
+  auto stage = [&](int buf, int64_t mt) {
+    uint4* sA = smem + buf * STAGE_T;
+    uint4* sB = sA + IMG_U4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rbase + 2 * i;
+      const int lc8 = (pc ^ swz(r)) * 8;
+      const int ca = min(lc8, capA), cb = min(lc8, capB);
+      const int64_t m = mt + r;
+      const bool v = m < mend;
+      const int64_t mm = v ? m : mbeg;
+      const int64_t ra = p.ia ? (int64_t)p.ia[mm] : mm;
+      const int64_t rb = p.ib ? (int64_t)p.ib[mm] : mm;
+      const bf16_t* srcA = v ? p.A + ra * p.lda + p0 + ca : zrow + ca;
+      const bf16_t* srcB = v ? p.B + rb * p.ldb + q0 + cb : zrow + cb;
+      __builtin_amdgcn_global_load_lds((const void*)srcA, (lds_void*)(sA + (8 * w + 2 * i) * 32), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)srcB, (lds_void*)(sB + (8 * w + 2 * i) * 32), 16, 0, 0);
+    }
+  };
+
+  const int wq = w >> 2, wp = w & 3;
+  float4_t acc[8][4];   // [q-tile jq][p-tile ip]: rows q = 16 jq + 4 g + r, col p = 16 ip + li
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int q4 = li >> 2, pp = li & 3;
+  if (mbeg < mend) {
+    const int64_t nsteps = (mend - mbeg + TKM - 1) / TKM;
+    stage(0, mbeg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int64_t st = 0; st < nsteps; ++st) {
+      const int buf = (int)(st & 1);
+      if (st + 1 < nsteps) stage(buf ^ 1, mbeg + (st + 1) * TKM);
+      const char* sA = reinterpret_cast<const char*>(smem + buf * STAGE_T);
+      const char* sB = sA + IMG_U4 * 16;
+      typedef __attribute__((address_space(3))) char lds_char;
+      auto tr_read = [&](const char* img, int row, int col) -> short4_t {
+        const int off = row * 512 + 16 * ((col >> 3) ^ swz(row)) + 8 * ((col >> 2) & 1);
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)((lds_char*)((__attribute__((address_space(3))) uint4*)img) + off));
+      };
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int row0 = s * 32 + 8 * g + q4;    // k rows 8g..8g+3 (hlf 0) and +4 (hlf 1)
+        short8 fp[4];
+#pragma unroll
+        for (int ip = 0; ip < 4; ++ip) {
+          const int col = wp * 64 + ip * 16 + 4 * pp;
+          const short4_t t0 = tr_read(sA, row0, col), t1 = tr_read(sA, row0 + 4, col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { fp[ip][e] = t0[e]; fp[ip][4 + e] = t1[e]; }
+        }
+#pragma unroll
+        for (int jh = 0; jh < 2; ++jh) {
+          short8 fq[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int col = wq * 128 + (4 * jh + jj) * 16 + 4 * pp;
+            const short4_t t0 = tr_read(sB, row0, col), t1 = tr_read(sB, row0 + 4, col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { fq[jj][e] = t0[e]; fq[jj][4 + e] = t1[e]; }
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int ip = 0; ip < 4; ++ip)
+              acc[4 * jh + jj][ip] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[jj], fp[ip], acc[4 * jh + jj][ip], 0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // slab store: C[p][q..q+3] as one float4
+  float* out = p.ws + z * p.P * p.Q;
+#pragma unroll
+  for (int ip = 0; ip < 4; ++ip) {
+    const int64_t pr = p0 + wp * 64 + ip * 16 + li;
+    if (pr >= p.P) continue;
+#pragma unroll
+    for (int jq = 0; jq < 8; ++jq) {
+      const int64_t qc = q0 + wq * 128 + jq * 16 + 4 * g;
+      if (qc >= p.Q) continue;
+      *reinterpret_cast<float4_t*>(out + pr * p.Q + qc) = acc[jq][ip];
+    }
+  }
+}
+
+}  // namespace
+
+int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q) {
+  const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
+  int64_t splits = (768 + tiles - 1) / tiles;
+  const int64_t maxs = (M + TKM * 8 - 1) / (TKM * 8);   // >= 8 m-steps per split
+  if (splits > maxs) splits = maxs;
+  return splits < 1 ? 1 : splits;
+}
+
+int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
+                         int64_t splits, hipStream_t s) {
+  PTN p;
+  p.A = (const bf16_t*)A->ptr; p.ia = A->idx; p.lda = A->ld;
+  p.B = (const bf16_t*)B->ptr; p.ib = B->idx; p.ldb = B->ld;
+  p.M = M; p.P = P; p.Q = Q;
+  int64_t mchunk = (M + splits - 1) / splits;
+  mchunk = (mchunk + TKM - 1) / TKM * TKM;
+  p.mchunk = mchunk > 0 ? mchunk : TKM;
+  p.splits = splits;
+  p.ws = ws;
+  const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
+  hipLaunchKernelGGL(gemm_tn_bf16_256, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  return (int)hipGetLastError();
+}

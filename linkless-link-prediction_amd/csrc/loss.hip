@@ -187,10 +187,89 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, con
   }
 }
 
-// Block = 256 threads owns columns {tid, tid+256, ...}; rows [r0, r0+RB).
-// weight[r] (NULL = 1) ; writes dZ if requested; slab[blk][H] of column sums,
-// slab_b[blk] of sum(weight).
-constexpr int HB_ROWS = 256;
+// Column sums (weighted: sum_r weight[r] * Z[r, n]) with the head backward's dZ
+// write fused in.  Vector form: a row is cpr 16-byte chunks; 256 threads
+// cover rpp = 256 / cpr rows per pass and a block walks HB_ROWS rows; the rpp
+// partial rows are combined in LDS and one slab row [blk][H] is written.
+constexpr int HB_ROWS = 2048;
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
+                                                         const float* __restrict__ weight,
+                                                         const float* __restrict__ w, int relu_mask, float alpha,
+                                                         T* __restrict__ dZ, int64_t lddz, float* __restrict__ slab,
+                                                         float* __restrict__ slab_b) {
+  constexpr int CH = 16 / sizeof(T);
+  __shared__ float part[256 * CH];
+  __shared__ float partb[256];
+  const int cpr = (int)(H / CH);
+  const int rpp = 256 / cpr;
+  const int t = threadIdx.x;
+  const int c = t % cpr, rl = t / cpr;
+  const bool active = rl < rpp;
+  const int64_t r0 = (int64_t)blockIdx.x * HB_ROWS;
+  const int64_t r1 = min(R, r0 + HB_ROWS);
+  float acc[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) acc[i] = 0.f;
+  float accb = 0.f;
+  float wv[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) wv[i] = (w && active) ? alpha * w[c * CH + i] : alpha;
+  if (active) {
+    for (int64_t r = r0 + rl; r < r1; r += rpp) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(Z + r * ldz + (int64_t)c * CH);
+      float z[CH];
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          z[2 * i] = __uint_as_float(u[i] << 16);
+          z[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+        }
+      } else {
+        z[0] = __uint_as_float(raw.x); z[1] = __uint_as_float(raw.y);
+        z[2] = __uint_as_float(raw.z); z[3] = __uint_as_float(raw.w);
+      }
+      const float g = weight ? weight[r] : 1.f;
+      accb += g;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) acc[i] += g * z[i];
+      if (dZ) {
+        float d[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) d[i] = (relu_mask && !(z[i] > 0.f)) ? 0.f : g * wv[i];
+        uint4 o;
+        if constexpr (sizeof(T) == 2) {
+          o.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
+          o.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
+          o.z = (uint32_t)f2bf(d[4]) | ((uint32_t)f2bf(d[5]) << 16);
+          o.w = (uint32_t)f2bf(d[6]) | ((uint32_t)f2bf(d[7]) << 16);
+        } else {
+          o = make_uint4(__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3]));
+        }
+        *reinterpret_cast<uint4*>(dZ + r * lddz + (int64_t)c * CH) = o;
+      }
+    }
+  }
+  // combine the rpp row-lanes (fixed order -> deterministic)
+  if (active)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) part[rl * (cpr * CH) + c * CH + i] = acc[i];
+  partb[t] = active ? accb : 0.f;
+  __syncthreads();
+  for (int n = t; n < H; n += 256) {
+    float s = 0.f;
+    for (int k = 0; k < rpp; ++k) s += part[k * (cpr * CH) + n];
+    slab[blockIdx.x * H + n] = s;
+  }
+  if (slab_b && t == 0) {
+    float s = 0.f;
+    for (int k = 0; k < rpp; ++k) s += partb[k * cpr];
+    slab_b[blockIdx.x] = s;
+  }
+}
+
+// Scalar fallback for widths that are not a multiple of 16 bytes / wider than 256 chunks.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
                                                      const float* __restrict__ weight, const float* __restrict__ w,
@@ -223,13 +302,21 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const
   }
 }
 
-__global__ void slab_sum_kernel(const float* __restrict__ slab, int64_t nslab, int64_t H, float* __restrict__ out,
-                                int accumulate) {
-  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (n >= H) return;
+// out[n] (+)= sum_i slab[i][n]: 64 columns x 4 slab-lanes per block, fixed order.
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int64_t nslab, int64_t H,
+                                                       float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int64_t i = 0; i < nslab; ++i) s += slab[i * H + n];
-  out[n] = accumulate ? out[n] + s : s;
+  if (n < H)
+    for (int64_t i = sl; i < nslab; i += 4) s += slab[i * H + n];
+  red[sl][cl] = s;
+  __syncthreads();
+  if (sl == 0 && n < H) {
+    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    out[n] = accumulate ? out[n] + v : v;
+  }
 }
 
 }  // namespace
@@ -302,16 +389,29 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
   float* slab = reinterpret_cast<float*>(workspace);
   float* slab_b = slab + ns * H;
   if (ns > 0) {
-    if (dtype == LLP_BF16)
-      hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz,
-                         weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr);
-    else
-      hipLaunchKernelGGL(colsum_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
-                         weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr);
+    const int ch = dtype == LLP_BF16 ? 8 : 4;
+    const int es = dtype == LLP_BF16 ? 2 : 4;
+    const bool vec = (H % ch == 0) && (H / ch <= 256) && ((uintptr_t)Z % 16 == 0) && ((ldz * es) % 16 == 0) &&
+                     (!dZ || (((uintptr_t)dZ % 16 == 0) && ((lddz * es) % 16 == 0)));
+    if (dtype == LLP_BF16) {
+      if (vec)
+        hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z,
+                           ldz, weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr);
+      else
+        hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz,
+                           weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr);
+    } else {
+      if (vec)
+        hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
+                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr);
+      else
+        hipLaunchKernelGGL(colsum_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
+                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr);
+    }
     LLP_LAUNCH_CHECK();
   }
   if (dw) {
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, 256)), dim3(256), 0, s, slab, ns, H, dw, accumulate);
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, 64)), dim3(256), 0, s, slab, ns, H, dw, accumulate);
     LLP_LAUNCH_CHECK();
   }
   if (db) {

@@ -296,7 +296,15 @@ class DistillEngine:
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
         logit = self._buf("logit", (R2,), torch.float32)
         zacts = []
-        A = K.operand(h, ia, h, ib)
+        if (H * h.element_size()) % 16 == 0:
+            # materialise x_i * x_j once: layer-1 forward and its weight-gradient then
+            # stream a plain operand with global_load_lds
+            zin = self._buf("Zin", (R2, H), dt)
+            K.hadamard_rows(h, ia, h, ib, zin)
+            A0 = K.operand(zin)
+        else:
+            A0 = K.operand(h, ia, h, ib)
+        A = A0
         for l, lin in enumerate(self.prd):
             out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
             K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
@@ -323,7 +331,7 @@ class DistillEngine:
                    float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms, ws)
 
         # ---- a10: backward
-        dZ0 = self._predictor_backward(dlogit, R2, h, ia, ib, zacts, p_drop)
+        dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
         dh = self._buf("gS0", (R1, H), dt)
         if self.predictor_kind == "mlp":
             K.hadamard_bwd_blocks(B, C, P2, H, dZ0, h, dh)
@@ -349,7 +357,7 @@ class DistillEngine:
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _predictor_backward(self, dlogit, R2, h, ia, ib, zacts, p_drop):
+    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop):
         dt, dc = self.dtype, self.dc
         if self.predictor_kind != "mlp":
             return None
@@ -364,7 +372,7 @@ class DistillEngine:
         for l in range(len(self.prd) - 1, -1, -1):
             lin = self.prd[l]
             gcur = self._buf(cur, (R2, lin.out_f), dt)
-            A_in = K.operand(zacts[l - 1]) if l > 0 else K.operand(h, ia, h, ib)
+            A_in = K.operand(zacts[l - 1]) if l > 0 else A0
             wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
             K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb))
             K.colsum(gcur, R2, lin.out_f, lin.lin.bias.grad, self._ws("ws_col", K.colsum_ws_bytes(R2, lin.out_f)))

@@ -73,6 +73,7 @@ _SIGS = {
     "llp_accumulate": (c_int, [c_i64, c_vp, c_f32, c_vp, c_vp]),
     "llp_increment": (c_int, [c_vp, c_vp]),
     "llp_zero": (c_int, [c_vp, c_i64, c_vp]),
+    "llp_hadamard_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_relu_bwd": (c_int, [c_int, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
     "llp_transpose": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "llp_mul": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp]),
@@ -206,6 +207,13 @@ def hadamard_bwd_blocks(B, Cc, L2, H, dZ, h, dh, drow=None):
     L = lib()
     check(L.llp_hadamard_bwd_blocks(dtype_code(h.dtype), B, Cc, L2, H, ptr(dZ), ptr(drow), h.data_ptr(),
                                     dh.data_ptr(), stream_ptr()), "llp_hadamard_bwd_blocks")
+
+
+def hadamard_rows(a, ia, b, ib, out):
+    L = lib()
+    R, H = out.shape
+    check(L.llp_hadamard_rows(dtype_code(a.dtype), R, H, a.data_ptr(), ptr(ia), b.data_ptr(), ptr(ib),
+                              out.data_ptr(), stream_ptr()), "llp_hadamard_rows")
 
 
 def hadamard_bwd_scatter(R, H, dZ, ia, ib, h, dh, drow=None):

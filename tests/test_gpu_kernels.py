@@ -72,6 +72,56 @@ def test_gemm_nt_gather_hadamard_and_relu_bwd(dt):
     assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * (1 + ref.abs().max().item()))
 
 
+@pytest.mark.parametrize("M,N,Kd,act", [(1000, 256, 128, "relu_bwd"), (700, 1024, 64, "relu"), (300, 40, 192, "none")])
+def test_gemm_nt_bf16_large_tile_paths(M, N, Kd, act):
+    """Shapes that take the 256x256 glds kernel (bf16, K % 64 == 0, N % 8 == 0),
+    with a gathered Hadamard A operand (the predictor's x_i * x_j)."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N + Kd)
+    N0 = 97
+    X = torch.randn(N0, Kd, generator=g)
+    ia = torch.randint(0, N0, (M,), generator=g)
+    ib = torch.randint(0, N0, (M,), generator=g)
+    W = torch.randn(N, Kd, generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    aux = torch.randn(M, N, generator=g)
+    Xd = X.to(DEV, torch.bfloat16)
+    iad, ibd = ia.to(DEV, torch.int32), ib.to(DEV, torch.int32)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    code = {"none": k.ACT_NONE, "relu": k.ACT_RELU, "relu_bwd": k.ACT_RELU_BWD}[act]
+    auxd = aux.to(DEV, torch.bfloat16)
+    k.gemm_nt(k.operand(Xd, iad, Xd, ibd), k.operand(W.to(DEV, torch.bfloat16)), M, N, Kd, out, 1, bias=b.to(DEV),
+              act=code, aux=auxd if act == "relu_bwd" else None, alpha=0.5)
+    prod = _bf(_bf(X)[ia] * _bf(X)[ib])
+    ref = 0.5 * F.linear(prod, _bf(W)) + b
+    if act == "relu":
+        ref = F.relu(ref)
+    if act == "relu_bwd":
+        ref = ref * (_bf(aux) > 0)
+    assert torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=1e-2 * (1 + ref.abs().max().item()))
+    # plain gathered operand (no Hadamard) through the glds path
+    out2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt(k.operand(Xd, iad), k.operand(W.to(DEV, torch.bfloat16)), M, N, Kd, out2, 1)
+    ref2 = F.linear(_bf(X)[ia], _bf(W))
+    assert torch.allclose(out2.float().cpu(), ref2, rtol=1e-2, atol=1e-2 * (1 + ref2.abs().max().item()))
+
+
+def test_gemm_nt_bf16_dropout_matches_fp32_mask():
+    """The 256-tile bf16 kernel and the general kernel draw the same dropout mask."""
+    k = K()
+    M, N, Kd = 600, 256, 128
+    A = torch.randn(M, Kd, device=DEV)
+    W = torch.randn(N, Kd, device=DEV) * 0.1
+    ctr = torch.full((1,), 5, dtype=torch.int64, device=DEV)
+    o32 = torch.empty(M, N, device=DEV)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, o32, 0, act=k.ACT_NONE,
+              dropout=k.Dropout(0.3, 99, ctr.data_ptr(), 4))
+    o16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt(k.operand(A.bfloat16()), k.operand(W.bfloat16()), M, N, Kd, o16, 1, act=k.ACT_NONE,
+              dropout=k.Dropout(0.3, 99, ctr.data_ptr(), 4))
+    assert torch.equal(o32 != 0, o16.float() != 0)
+
+
 def test_gemm_nt_dropout_is_deterministic_and_unbiased():
     k = K()
     M, N, Kd = 512, 256, 64
