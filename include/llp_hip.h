@@ -83,11 +83,13 @@ int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K,
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
  * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then
  * reduced in a fixed order: deterministic.  C is f32 with leading dim ldc.
- * Replaces autograd's weight-gradient of nn.Linear (src/main.py:132). */
+ * colsum_a (f32[P], may be NULL) (+)= sum_m A[m,p]: the bias gradient, fused
+ * into the same pass over dY.  Replaces autograd's weight/bias gradient of
+ * nn.Linear (src/main.py:132). */
 int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q);
 int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q,
                 const llp_operand* A, const llp_operand* B,
-                float* C, int64_t ldc, int accumulate,
+                float* C, int64_t ldc, int accumulate, float* colsum_a,
                 void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Column sums: out[n] (+)= sum_m Y[m,n] (bias gradient).  Deterministic. */

@@ -57,6 +57,101 @@ __global__ __launch_bounds__(256) void hadamard_bwd_blocks_kernel(int64_t B, int
   }
 }
 
+// 16-byte-chunk form of hadamard_bwd_blocks_kernel.  Anchor part: a block holds
+// 256 / cpr anchors, thread = (anchor slot, chunk); label part: one thread per
+// (pair, chunk).  f32 accumulation, one rounding per output element.
+template <typename T>
+struct Chunk {
+  static constexpr int E = 16 / sizeof(T);
+  float v[16 / sizeof(T)];
+  __device__ __forceinline__ void load(const T* p) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p);
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t u[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(u[i] << 16);
+        v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+      }
+    } else {
+      v[0] = __uint_as_float(r.x); v[1] = __uint_as_float(r.y); v[2] = __uint_as_float(r.z); v[3] = __uint_as_float(r.w);
+    }
+  }
+  __device__ __forceinline__ void fill(float s) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = s;
+  }
+};
+template <typename T>
+__device__ __forceinline__ void store_chunk(T* p, const float* v) {
+  uint4 o;
+  if constexpr (sizeof(T) == 2) {
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  } else {
+    o = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+  }
+  *reinterpret_cast<uint4*>(p) = o;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void hadamard_bwd_blocks_vec_kernel(int64_t B, int64_t C, int64_t L2, int64_t H,
+                                                                       int64_t anchor_blocks,
+                                                                       const T* __restrict__ dZ,
+                                                                       const float* __restrict__ drow,
+                                                                       const T* __restrict__ h, T* __restrict__ dh) {
+  constexpr int E = 16 / sizeof(T);
+  const int cpr = (int)(H / E);
+  const int64_t C1 = C + 1;
+  if ((int64_t)blockIdx.x < anchor_blocks) {
+    const int apb = 256 / cpr;
+    const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
+    const int64_t b = (int64_t)blockIdx.x * apb + slot;
+    if (slot >= apb || b >= B) return;
+    const int64_t col = (int64_t)c * E;
+    Chunk<T> ha;
+    ha.load(h + (b * C1) * H + col);
+    float acc[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] = 0.f;
+    for (int64_t cc = 0; cc < C; ++cc) {
+      const int64_t r = b * C + cc;
+      Chunk<T> d, hc;
+      if (drow) d.fill(drow[r]); else d.load(dZ + r * H + col);
+      hc.load(h + (b * C1 + 1 + cc) * H + col);
+      float o[E];
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        acc[i] += d.v[i] * hc.v[i];
+        o[i] = d.v[i] * ha.v[i];
+      }
+      store_chunk<T>(dh + (b * C1 + 1 + cc) * H + col, o);
+    }
+    store_chunk<T>(dh + (b * C1) * H + col, acc);
+  } else {
+    const int64_t t = ((int64_t)blockIdx.x - anchor_blocks) * 256 + threadIdx.x;
+    if (t >= L2 * cpr) return;
+    const int64_t i = t / cpr;
+    const int64_t col = (t % cpr) * E;
+    const int64_t base = B * C1;
+    const int64_t r = B * C + i;
+    Chunk<T> d, hs, hd;
+    if (drow) d.fill(drow[r]); else d.load(dZ + r * H + col);
+    hs.load(h + (base + i) * H + col);
+    hd.load(h + (base + L2 + i) * H + col);
+    float o1[E], o2[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      o1[k] = d.v[k] * hd.v[k];
+      o2[k] = d.v[k] * hs.v[k];
+    }
+    store_chunk<T>(dh + (base + i) * H + col, o1);
+    store_chunk<T>(dh + (base + L2 + i) * H + col, o2);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void hadamard_bwd_scatter_kernel(int64_t R, int64_t H, const T* __restrict__ dZ,
                                                                     const float* __restrict__ drow,
@@ -222,6 +317,26 @@ extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t 
   const int64_t nblk = B + (L2 + 63) / 64;
   if (nblk == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
+  {
+    const int es = dtype == LLP_BF16 ? 2 : 4;
+    const int64_t cpr = H * es / 16;
+    const bool vec = (H * es) % 16 == 0 && cpr <= 256 && (uintptr_t)h % 16 == 0 && (uintptr_t)dh % 16 == 0 &&
+                     (!dZ || (uintptr_t)dZ % 16 == 0);
+    if (vec) {
+      const int64_t apb = 256 / cpr;
+      const int64_t ab = (B + apb - 1) / apb;
+      const int64_t lb = (L2 * cpr + 255) / 256;
+      if (ab + lb == 0) return LLP_OK;
+      if (dtype == LLP_BF16)
+        hipLaunchKernelGGL(hadamard_bwd_blocks_vec_kernel<bf16_t>, dim3((unsigned)(ab + lb)), dim3(256), 0, s, B, C,
+                           L2, H, ab, (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh);
+      else
+        hipLaunchKernelGGL(hadamard_bwd_blocks_vec_kernel<float>, dim3((unsigned)(ab + lb)), dim3(256), 0, s, B, C,
+                           L2, H, ab, (const float*)dZ, drow, (const float*)h, (float*)dh);
+      LLP_LAUNCH_CHECK();
+      return LLP_OK;
+    }
+  }
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(hadamard_bwd_blocks_kernel<bf16_t>, dim3((unsigned)nblk), dim3(256), 0, s, B, C, L2, H,
                        (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh);

@@ -23,7 +23,7 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
                          const int64_t* drop_ctr, int64_t drop_stream, hipStream_t s);
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q);
 int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
-                         int64_t splits, hipStream_t s);
+                         float* ws_colsum, int64_t splits, hipStream_t s);
 
 namespace {
 
@@ -567,40 +567,63 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   return LLP_OK;
 }
 
+extern "C" int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N);
+extern "C" int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
+                          void* workspace, int64_t workspace_bytes, void* stream);
+
+// workspace = [weight slabs: splits*P*Q f32][column-sum region]
+static int64_t tn_colsum_region(int dtype, int64_t M, int64_t P) {
+  int64_t r = llp_colsum_workspace_bytes(M, P);
+  if (dtype == LLP_BF16) r = std::max(r, llp_gemm_tn_256_splits(M, P, 256) * P * (int64_t)sizeof(float));
+  return r;
+}
+
 extern "C" int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q) {
   int64_t s = tn_splits(dtype, M, P, Q);
   if (dtype == LLP_BF16) s = std::max(s, llp_gemm_tn_256_splits(M, P, Q));
-  return s * P * Q * (int64_t)sizeof(float);
+  return s * P * Q * (int64_t)sizeof(float) + tn_colsum_region(dtype, M, P);
 }
 
 extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A,
-                           const llp_operand* B, float* C, int64_t ldc, int accumulate, void* workspace,
-                           int64_t workspace_bytes, void* stream) {
+                           const llp_operand* B, float* C, int64_t ldc, int accumulate, float* colsum_a,
+                           void* workspace, int64_t workspace_bytes, void* stream) {
   LLP_CHECK_ARG(A && B && C, "llp_gemm_tn: null operand");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_tn: bad dtype %d", dtype);
+  LLP_CHECK_ARG(!colsum_a || (!A->idx && !A->ptr2), "llp_gemm_tn: colsum_a needs a plain A operand");
   if (P == 0 || Q == 0) return LLP_OK;
+  if (workspace_bytes < llp_gemm_tn_workspace_bytes(dtype, M, P, Q) || !workspace)
+    return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace %lld < %lld", (long long)workspace_bytes,
+                          (long long)llp_gemm_tn_workspace_bytes(dtype, M, P, Q));
   hipStream_t s = (hipStream_t)stream;
   static const bool force_v1 = getenv("LLP_GEMM_V1") != nullptr;
   auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
   if (!force_v1 && dtype == LLP_BF16 && P % 8 == 0 && Q % 8 == 0 && !A->ptr2 && !B->ptr2 && a16(A->ptr, A->ld) &&
       a16(B->ptr, B->ld)) {
-    // large-tile glds kernel (gemm256_tn.hip)
+    // large-tile glds kernel (gemm256_tn.hip), bias gradient fused
     const int64_t sp = llp_gemm_tn_256_splits(M, P, Q);
-    if (workspace_bytes < sp * P * Q * (int64_t)sizeof(float) || !workspace)
-      return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace too small");
-    const int rc = llp_gemm_tn_bf16_256(A, B, M, P, Q, reinterpret_cast<float*>(workspace), sp, s);
+    float* ws = reinterpret_cast<float*>(workspace);
+    float* wcs = colsum_a ? ws + sp * P * Q : nullptr;
+    const int rc = llp_gemm_tn_bf16_256(A, B, M, P, Q, ws, wcs, sp, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (256 tile): %s", hipGetErrorString((hipError_t)rc));
     const int64_t n = P * Q;
     unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, (const float*)workspace, sp, P, Q, C, ldc,
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, (const float*)ws, sp, P, Q, C, ldc,
                        accumulate);
     LLP_LAUNCH_CHECK();
+    if (colsum_a) {
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3(ceil_div_u(P, 256)), dim3(256), 0, s, (const float*)wcs, sp, P,
+                         (int64_t)1, colsum_a, (int64_t)1, accumulate);
+      LLP_LAUNCH_CHECK();
+    }
     return LLP_OK;
   }
   const int64_t splits = tn_splits(dtype, M, P, Q);
-  if (workspace_bytes < splits * P * Q * (int64_t)sizeof(float) || !workspace)
-    return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace %lld < %lld", (long long)workspace_bytes,
-                          (long long)(splits * P * Q * 4));
+  if (colsum_a) {
+    char* region = reinterpret_cast<char*>(workspace) + splits * P * Q * (int64_t)sizeof(float);
+    const int rc = llp_colsum(dtype, M, P, A->ptr, A->ld, colsum_a, accumulate, region,
+                              tn_colsum_region(dtype, M, P), stream);
+    if (rc != 0) return rc;
+  }
   TNParams p;
   p.A = to_op(A);
   p.B = to_op(B);

@@ -151,7 +151,9 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
     const bool more = kt + 1 < nk;
     if (more) {
       if (HADA) hada_load(kt + 1);
+#ifndef LLP_ABLATE_NOLOAD   // tools/gemm_ablate.cpp: time the loop without its staging loads
       stage_glds(buf ^ 1, kt + 1);
+#endif
     }
     const uint4* sA = smem + buf * STAGE_U4;
     const uint4* sB = sA + TM * 8;
@@ -170,11 +172,18 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
         uint4 v = sA[r * 8 + ((g + 4 * s) ^ (r & 7))];
         fx[im] = *reinterpret_cast<short8*>(&v);
       }
+#ifndef LLP_ABLATE_NOMFMA
 #pragma unroll
       for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
         for (int im = 0; im < 8; ++im)
           acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
+#else
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
+#pragma unroll
+      for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
+#endif
     }
     if (more && HADA) hada_store(buf ^ 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -239,6 +248,189 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined variant for plain / gathered A (no Hadamard): BK = 32 per stage
+// (32 KiB: A and B images of [256 rows][64 B]), NS-stage LDS ring, NS-1
+// stages of global_load_lds in flight across raw barriers with a counted
+// vmcnt (cdna_hip_programming.md §5 "Pipelining across barriers").  The
+// single-stage-in-flight loop above measured latency-bound (no-load ablation
+// 1.28 PF/s vs 0.79 PF/s full, L2->CU traffic ~19 GB/s per CU).
+// 64-B image rows: 16-B chunk swizzle phys = logical ^ ((row >> 2) & 2) is
+// conflict-free for ds_read_b128 fragment reads of 16 consecutive rows
+// (checked against the four 16-lane bank groups of ds_read_b128).
+constexpr int PK = 32;
+constexpr int PSTAGE_U4 = (TM + TN) * 4;   // 2048 uint4 = 32 KiB
+
+__device__ __forceinline__ int swz64(int row) { return (row >> 2) & 2; }
+
+// global_load_lds_dwordx4 issued from inline asm: hipcc's waitcnt pass then does
+// not see the LDS-DMA and does not put s_waitcnt vmcnt(0) in front of every
+// ds_read of the ring (it cannot prove the reads do not alias the DMA).  The
+// kernel owns the counting: vm_wait_stages + s_barrier before a stage is read.
+__device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_addr_uniform) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr),
+               "s"(lds_addr_uniform)
+               : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)p);
+}
+
+template <int NS>
+__device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
+  // each stage is 4 global_load_lds per wave; wait until only `ahead` stages remain
+  if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+template <int NS>
+__global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
+  constexpr int LOOP_U4 = NS * PSTAGE_U4;
+  constexpr int SM_U4 = LOOP_U4 > SMEM_U4_EPI ? LOOP_U4 : SMEM_U4_EPI;
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TM - 1) / TM;
+  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
+  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+
+  // glds: wave w stages rows [32w, 32w+32): 2 instructions per operand, each 16
+  // rows x 64 B; lane -> row 32w + 16i + (lane>>2), physical chunk lane & 3.
+  const bf16_t* ga[2];
+  const bf16_t* gb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 32 * w + 16 * i + (lane >> 2);
+    const int lc = (lane & 3) ^ swz64(r);
+    int64_t m = m0 + r;
+    m = m < p.M ? m : p.M - 1;
+    ga[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
+    int64_t n = n0 + r;
+    n = n < p.N ? n : p.N - 1;
+    gb[i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
+  }
+  const uint32_t lds0 = lds_u32(smem);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto issue = [&](int64_t kt) {
+    const uint32_t sA = lds0 + (uint32_t)((kt % NS) * PSTAGE_U4 * 16);
+    const uint32_t sB = sA + TM * 4 * 16;
+    const int64_t koff = kt * PK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t off = (uint32_t)((32 * wu + 16 * i) * 4 * 16);
+      glds16(ga[i] + koff, __builtin_amdgcn_readfirstlane(sA + off));
+      glds16(gb[i] + koff, __builtin_amdgcn_readfirstlane(sB + off));
+    }
+  };
+
+  const int wm = w >> 2, wn = w & 3;
+  float4_t acc[4][8];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = p.K / PK;
+  for (int64_t s = 0; s < NS - 1 && s < nk; ++s) issue(s);
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int64_t last_issued = min(nk - 1, kt + NS - 2);
+    vm_wait_stages<NS>(last_issued - kt);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);   // into the buffer of stage kt-1 (all waves are past it)
+    const uint4* sA = smem + (int)(kt % NS) * PSTAGE_U4;
+    const uint4* sB = sA + TM * 4;
+    short8 fw[4], fx[8];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      const int r = wn * 64 + jn * 16 + li;
+      uint4 v = sB[r * 4 + (g ^ swz64(r))];
+      fw[jn] = *reinterpret_cast<short8*>(&v);
+    }
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int r = wm * 128 + im * 16 + li;
+      uint4 v = sA[r * 4 + (g ^ swz64(r))];
+      fx[im] = *reinterpret_cast<short8*>(&v);
+    }
+#ifndef LLP_ABLATE_NOMFMA
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+      for (int im = 0; im < 8; ++im)
+        acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#else
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
+#pragma unroll
+    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
+#endif
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---------------- epilogue (as gemm_nt_bf16_256)
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  uint4* stg = smem;
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn) {
+    const int nl = wn * 64 + jn * 16 + g * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? p.bias[n0 + nl + r] : 0.f;
+    }
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int ml = wm * 128 + im * 16 + li;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = p.alpha * acc[jn][im][r] + bv[r];
+        if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (p.drop_p > 0.f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)((m0 + ml) * p.N + n0 + nl + r));
+          v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
+        }
+      }
+      const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
+      *dst = make_uint2(lo, hi);
+    }
+  }
+  __syncthreads();
+  const int chunks_per_row = TN / 8;
+#pragma unroll 4
+  for (int q = tid; q < TM * chunks_per_row; q += NT2) {
+    const int rl = q / chunks_per_row, c = q % chunks_per_row;
+    const int64_t row = m0 + rl, col = n0 + c * 8;
+    if (row >= p.M || col >= p.N) continue;
+    uint4 v = stg[rl * EPI_ROW_U4 + c];
+    if (p.act == LLP_ACT_RELU_BWD) {
+      const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
+      const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
+        const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
+        vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+      }
+      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+  }
+}
+
 }  // namespace
 
 // Called from llp_gemm_nt when the shapes allow it (gemm.hip).
@@ -256,8 +448,15 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
   p.drop_ctr = drop_ctr; p.drop_stream = drop_stream;
   const int64_t tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  static const int pipe = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
   if (A->ptr2)
     hipLaunchKernelGGL(gemm_nt_bf16_256<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (pipe == 5)
+    hipLaunchKernelGGL(gemm_nt_bf16_256p<5>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (pipe == 4)
+    hipLaunchKernelGGL(gemm_nt_bf16_256p<4>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (pipe == 3)
+    hipLaunchKernelGGL(gemm_nt_bf16_256p<3>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else
     hipLaunchKernelGGL(gemm_nt_bf16_256<false>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   return (int)hipGetLastError();

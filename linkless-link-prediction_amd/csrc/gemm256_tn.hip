@@ -1,24 +1,29 @@
 // Large-tile bf16 MFMA weight-gradient GEMM (TN form):
 //
 //   ws[z][p][q] = sum_{m in split z} A[m, p] * B[m, q]      (A = dY, B = X; f32 slabs)
+//   ws_colsum[z][p] = sum_{m in split z} A[m, p]            (bias gradient, optional)
 //
-// Replaces autograd's weight-gradient of every nn.Linear on the distillation
-// path (src/main.py:132).  256 (p) x 256 (q) tile per 512-thread workgroup,
-// 64 rows of m per stage, both operands staged by global_load_lds_dwordx4 into
-// [m][256] images (512-B rows, 16-B chunks XOR-swizzled by m) and read as MFMA
-// fragments with ds_read_b64_tr_b16 (the contraction index m is the image's
-// row).  Rows past the split's end read a zero row, so no m-tail handling is
-// needed in the MFMA loop.  B rows may be gathered (x[this_target], the first
-// student layer).  MFMA roles put 4 consecutive q of one p in a lane, so the
-// f32 slab is written with 16-byte stores.
+// Replaces autograd's weight/bias-gradient of every nn.Linear on the
+// distillation path (src/main.py:132).  256 (p) x 256 (q) tile per 512-thread
+// workgroup.  The contraction index m is the ROW of both operands, so a stage
+// of 32 rows keeps full 512-B row segments: both operands are staged by
+// global_load_lds_dwordx4 (issued from inline asm, see gemm256.hip glds16) into
+// [32][256] images (16-B chunks XOR-swizzled by row) held in a 4-stage LDS
+// ring with 3 stages in flight (counted vmcnt + raw barriers), and read as
+// MFMA fragments with ds_read_b64_tr_b16.  Rows past the split's end read a
+// zero row.  B rows may be gathered (x[this_target], the first student layer).
+// MFMA roles put 4 consecutive q of one p in a lane (16-byte slab stores).
+// The bias gradient rides along: waves of the q0 == 0 tiles multiply their A
+// fragments by a ones fragment (4 extra MFMAs per 32 on those waves).
 #include "llp_common.h"
 
 namespace {
 
-constexpr int TP = 256, TQ = 256, TKM = 64;
+constexpr int TP = 256, TQ = 256, TKM = 32;
 constexpr int NTT = 512;
-constexpr int IMG_U4 = TKM * 32;            // one [64][256] bf16 image = 2048 uint4 = 32 KiB
-constexpr int STAGE_T = 2 * IMG_U4;         // A image + B image
+constexpr int NS = 4;                          // LDS ring depth (stages of TKM rows)
+constexpr int IMG_U4 = TKM * 32;               // one [32][256] bf16 image = 1024 uint4 = 16 KiB
+constexpr int STAGE_T = 2 * IMG_U4;            // A image + B image = 32 KiB
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_row[64];   // 1 KiB of zeros (static init)
 
@@ -27,10 +32,11 @@ struct PTN {
   const bf16_t* B; const int32_t* ib; int64_t ldb;
   int64_t M, P, Q, mchunk, splits;
   float* ws;
+  float* ws_colsum;   // [splits][P] column sums of A (bias gradient), or NULL
 };
 
-typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) short4_t lds_s4;
+typedef __attribute__((address_space(3))) char lds_char;
 
 __device__ __forceinline__ int64_t xcd_remap3(int64_t bid, int64_t nwg) {
   if (nwg < 8) return bid;
@@ -39,11 +45,25 @@ __device__ __forceinline__ int64_t xcd_remap3(int64_t bid, int64_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-// swizzle of the 16-B chunk index within a 512-B image row (low 4 bits only)
+// swizzle of the 16-B chunk index within a 512-B image row (low 4 bits only):
+// T10 image (b); conflict-free for the transposed reads below.
 __device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
+__device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_addr_uniform) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr),
+               "s"(lds_addr_uniform)
+               : "memory", "m0");
+}
+
+__device__ __forceinline__ void vm_wait(int64_t ahead) {   // 4 glds per wave per stage
+  if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
 __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * STAGE_T];   // 128 KiB
+  __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE_T];   // 128 KiB
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
@@ -54,19 +74,22 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
   const int64_t mbeg = z * p.mchunk;
   const int64_t mend = min(p.M, mbeg + p.mchunk);
 
-  // glds assignment: wave w stages image rows [8w, 8w+8): instruction i covers
-  // rows 8w + 2i + (lane >> 5), physical chunk lane & 31.
+  // glds: wave w stages image rows [4w, 4w+4) of each operand: instruction i
+  // covers rows 4w + 2i + (lane >> 5), physical chunk lane & 31.
   const int pc = lane & 31;
-  const int rbase = 8 * w + (lane >> 5);
+  const int rbase = 4 * w + (lane >> 5);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   // columns past P / Q are clamped to a valid address (their products are never stored)
   const int capA = (int)max((int64_t)0, (p.P - p0) - 8), capB = (int)max((int64_t)0, (p.Q - q0) - 8);
   const bf16_t* zrow = reinterpret_cast<const bf16_t*>(g_zero_row);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)smem);
 
-  auto stage = [&](int buf, int64_t mt) {
-    uint4* sA = smem + buf * STAGE_T;
-    uint4* sB = sA + IMG_U4;
+  auto issue = [&](int64_t st) {
+    const int64_t mt = mbeg + st * TKM;
+    const uint32_t sA = lds0 + (uint32_t)((st % NS) * STAGE_T * 16);
+    const uint32_t sB = sA + IMG_U4 * 16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 2; ++i) {
       const int r = rbase + 2 * i;
       const int lc8 = (pc ^ swz(r)) * 8;
       const int ca = min(lc8, capA), cb = min(lc8, capB);
@@ -77,8 +100,9 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
       const int64_t rb = p.ib ? (int64_t)p.ib[mm] : mm;
       const bf16_t* srcA = v ? p.A + ra * p.lda + p0 + ca : zrow + ca;
       const bf16_t* srcB = v ? p.B + rb * p.ldb + q0 + cb : zrow + cb;
-      __builtin_amdgcn_global_load_lds((const void*)srcA, (lds_void*)(sA + (8 * w + 2 * i) * 32), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)srcB, (lds_void*)(sB + (8 * w + 2 * i) * 32), 16, 0, 0);
+      const uint32_t off = (uint32_t)((4 * wu + 2 * i) * 32 * 16);
+      glds16(srcA, __builtin_amdgcn_readfirstlane(sA + off));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(sB + off));
     }
   };
 
@@ -90,53 +114,71 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
     for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   const int q4 = li >> 2, pp = li & 3;
+  const bool do_cs = p.ws_colsum != nullptr && q0 == 0 && wq == 0;
+  float4_t accb[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) accb[b] = float4_t{0.f, 0.f, 0.f, 0.f};
+  short8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;   // bf16 1.0
+
+  auto tr_read = [&](const char* img, int row, int col) -> short4_t {
+    const int off = row * 512 + 16 * ((col >> 3) ^ swz(row)) + 8 * ((col >> 2) & 1);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)((lds_char*)((__attribute__((address_space(3))) uint4*)img) + off));
+  };
+
   if (mbeg < mend) {
     const int64_t nsteps = (mend - mbeg + TKM - 1) / TKM;
-    stage(0, mbeg);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    for (int64_t s = 0; s < NS - 1 && s < nsteps; ++s) issue(s);
     for (int64_t st = 0; st < nsteps; ++st) {
-      const int buf = (int)(st & 1);
-      if (st + 1 < nsteps) stage(buf ^ 1, mbeg + (st + 1) * TKM);
-      const char* sA = reinterpret_cast<const char*>(smem + buf * STAGE_T);
+      vm_wait(min(nsteps - 1, st + NS - 2) - st);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (st + NS - 1 < nsteps) issue(st + NS - 1);   // into the buffer of stage st-1
+      const char* sA = reinterpret_cast<const char*>(smem + (int)(st % NS) * STAGE_T);
       const char* sB = sA + IMG_U4 * 16;
-      typedef __attribute__((address_space(3))) char lds_char;
-      auto tr_read = [&](const char* img, int row, int col) -> short4_t {
-        const int off = row * 512 + 16 * ((col >> 3) ^ swz(row)) + 8 * ((col >> 2) & 1);
-        return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s4*)((lds_char*)((__attribute__((address_space(3))) uint4*)img) + off));
-      };
+      const int row0 = 8 * g + q4;    // k rows 8g..8g+3 and 8g+4..8g+7
+      short8 fp[4];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int row0 = s * 32 + 8 * g + q4;    // k rows 8g..8g+3 (hlf 0) and +4 (hlf 1)
-        short8 fp[4];
+      for (int ip = 0; ip < 4; ++ip) {
+        const int col = wp * 64 + ip * 16 + 4 * pp;
+        const short4_t t0 = tr_read(sA, row0, col), t1 = tr_read(sA, row0 + 4, col);
 #pragma unroll
-        for (int ip = 0; ip < 4; ++ip) {
-          const int col = wp * 64 + ip * 16 + 4 * pp;
-          const short4_t t0 = tr_read(sA, row0, col), t1 = tr_read(sA, row0 + 4, col);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { fp[ip][e] = t0[e]; fp[ip][4 + e] = t1[e]; }
-        }
-#pragma unroll
-        for (int jh = 0; jh < 2; ++jh) {
-          short8 fq[4];
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int col = wq * 128 + (4 * jh + jj) * 16 + 4 * pp;
-            const short4_t t0 = tr_read(sB, row0, col), t1 = tr_read(sB, row0 + 4, col);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { fq[jj][e] = t0[e]; fq[jj][4 + e] = t1[e]; }
-          }
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-            for (int ip = 0; ip < 4; ++ip)
-              acc[4 * jh + jj][ip] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[jj], fp[ip], acc[4 * jh + jj][ip], 0, 0, 0);
-        }
+        for (int e = 0; e < 4; ++e) { fp[ip][e] = t0[e]; fp[ip][4 + e] = t1[e]; }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (do_cs) {
+#pragma unroll
+        for (int ip = 0; ip < 4; ++ip)
+          accb[ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fp[ip], accb[ip], 0, 0, 0);
+      }
+#pragma unroll
+      for (int jh = 0; jh < 2; ++jh) {
+        short8 fq[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int col = wq * 128 + (4 * jh + jj) * 16 + 4 * pp;
+          const short4_t t0 = tr_read(sB, row0, col), t1 = tr_read(sB, row0 + 4, col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { fq[jj][e] = t0[e]; fq[jj][4 + e] = t1[e]; }
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int ip = 0; ip < 4; ++ip)
+            acc[4 * jh + jj][ip] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[jj], fp[ip], acc[4 * jh + jj][ip], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (do_cs && g == 0) {   // every row of the ones-product holds the column sums: take row 0
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) {
+      const int64_t pr = p0 + wp * 64 + ip * 16 + li;
+      if (pr < p.P) p.ws_colsum[z * p.P + pr] = accb[ip][0];
     }
   }
   // slab store: C[p][q..q+3] as one float4
@@ -159,14 +201,15 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
   int64_t splits = (768 + tiles - 1) / tiles;
-  const int64_t maxs = (M + TKM * 8 - 1) / (TKM * 8);   // >= 8 m-steps per split
+  const int64_t maxs = (M + TKM * 16 - 1) / (TKM * 16);   // >= 16 m-steps per split
   if (splits > maxs) splits = maxs;
   return splits < 1 ? 1 : splits;
 }
 
 int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
-                         int64_t splits, hipStream_t s) {
+                         float* ws_colsum, int64_t splits, hipStream_t s) {
   PTN p;
+  p.ws_colsum = ws_colsum;
   p.A = (const bf16_t*)A->ptr; p.ia = A->idx; p.lda = A->ld;
   p.B = (const bf16_t*)B->ptr; p.ib = B->idx; p.ldb = B->ld;
   p.M = M; p.P = P; p.Q = Q;

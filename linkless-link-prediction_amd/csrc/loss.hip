@@ -174,10 +174,48 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, con
   const T* z = Z + (iz ? (int64_t)iz[r] : r) * ldz;
   const T* z2 = Z2 ? Z2 + (iz2 ? (int64_t)iz2[r] : r) * ldz2 : nullptr;
   float acc = 0.f;
-  for (int64_t n = lane; n < H; n += 64) {
-    float v = ldf<T>(z, n);
-    if (z2) v *= ldf<T>(z2, n);
-    acc += w ? v * w[n] : v;
+  constexpr int E = 16 / sizeof(T);
+  const bool vec = (H % E == 0) && ((uintptr_t)z % 16 == 0) && (!z2 || (uintptr_t)z2 % 16 == 0) &&
+                   (!w || (uintptr_t)w % 16 == 0);
+  if (vec) {
+    // 16-byte chunks of the row per lane (the row is streamed once, 1 KiB per wave-instruction)
+    for (int64_t c = lane; c < H / E; c += 64) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(z + c * E);
+      float v[E];
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[2 * i] = __uint_as_float(u[i] << 16);
+          v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+        }
+      } else {
+        v[0] = __uint_as_float(raw.x); v[1] = __uint_as_float(raw.y);
+        v[2] = __uint_as_float(raw.z); v[3] = __uint_as_float(raw.w);
+      }
+      if (z2) {
+        const uint4 r2 = *reinterpret_cast<const uint4*>(z2 + c * E);
+        if constexpr (sizeof(T) == 2) {
+          const uint32_t u[4] = {r2.x, r2.y, r2.z, r2.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[2 * i] *= __uint_as_float(u[i] << 16);
+            v[2 * i + 1] *= __uint_as_float(u[i] & 0xFFFF0000u);
+          }
+        } else {
+          v[0] *= __uint_as_float(r2.x); v[1] *= __uint_as_float(r2.y);
+          v[2] *= __uint_as_float(r2.z); v[3] *= __uint_as_float(r2.w);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < E; ++i) acc += w ? v[i] * w[c * E + i] : v[i];
+    }
+  } else {
+    for (int64_t n = lane; n < H; n += 64) {
+      float v = ldf<T>(z, n);
+      if (z2) v *= ldf<T>(z2, n);
+      acc += w ? v * w[n] : v;
+    }
   }
   acc = wave_sum(acc);
   if (lane == 0) {

@@ -374,8 +374,8 @@ class DistillEngine:
             gcur = self._buf(cur, (R2, lin.out_f), dt)
             A_in = K.operand(zacts[l - 1]) if l > 0 else A0
             wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
-            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb))
-            K.colsum(gcur, R2, lin.out_f, lin.lin.bias.grad, self._ws("ws_col", K.colsum_ws_bytes(R2, lin.out_f)))
+            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
+                      colsum_a=lin.lin.bias.grad)
             gnext = self._buf(nxt, (R2, lin.in_f), dt)
             if l > 0:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
@@ -394,8 +394,8 @@ class DistillEngine:
             gcur = self._buf(cur, (R1, lin.out_f), dt)
             A_in = K.operand(acts[l - 1]) if l > 0 else K.operand(self.x, target)
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.in_f)
-            K.gemm_tn(K.operand(gcur), A_in, R1, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb))
-            K.colsum(gcur, R1, lin.out_f, lin.lin.bias.grad, self._ws("ws_col", K.colsum_ws_bytes(R1, lin.out_f)))
+            K.gemm_tn(K.operand(gcur), A_in, R1, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
+                      colsum_a=lin.lin.bias.grad)
             if l > 0:
                 gnext = self._buf(nxt, (R1, lin.in_f), dt)
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,

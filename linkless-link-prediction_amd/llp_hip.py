@@ -47,7 +47,7 @@ _SIGS = {
                             c_vp, c_int, c_vp, c_i64, c_int, c_f32, C.POINTER(Dropout), c_vp]),
     "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
     "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
-                            c_vp, c_i64, c_vp]),
+                            c_vp, c_vp, c_i64, c_vp]),
     "llp_colsum_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_colsum": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp]),
     "llp_head_fwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -155,10 +155,10 @@ def gemm_tn_ws_bytes(dtype, M, P, Q):
     return load().llp_gemm_tn_workspace_bytes(dtype, M, P, Q)
 
 
-def gemm_tn(A: Operand, B: Operand, M, P, Q, C_out, dtype, ws, accumulate=False):
+def gemm_tn(A: Operand, B: Operand, M, P, Q, C_out, dtype, ws, accumulate=False, colsum_a=None):
     L = lib()
     check(L.llp_gemm_tn(dtype, M, P, Q, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0), int(accumulate),
-                        ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_gemm_tn")
+                        ptr(colsum_a), ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_gemm_tn")
 
 
 def colsum_ws_bytes(M, N):
