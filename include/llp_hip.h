@@ -80,6 +80,20 @@ int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K,
                 const float* bias, int act, const void* aux, int64_t ld_aux, int aux_dtype,
                 float alpha, const llp_dropout* dropout, void* stream);
 
+/* bf16 GEMM with the LinkPredictor's last Linear(N, 1) fused into the epilogue
+ * (src/models.py:143-146): y = act(alpha * A.B^T + bias) (+dropout) is stored to
+ * C (C may be NULL when only the head is needed) and each 256-column tile t
+ * writes head_part[t][m] = sum_{n in tile} y[m, n] * head_w[n] (f32, exact
+ * activations before bf16 rounding).  llp_head_finish sums the
+ * llp_gemm_nt_head_parts(N) partials in a fixed order, adds the bias and
+ * applies torch.sigmoid (src/models.py:150). */
+int64_t llp_gemm_nt_head_parts(int64_t N);
+int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B,
+                     void* C, int64_t ldc, const float* bias, int act, float alpha,
+                     const llp_dropout* dropout, const float* head_w, float* head_part, void* stream);
+int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit,
+                    float* prob, void* stream);
+
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
  * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then
  * reduced in a fixed order: deterministic.  C is f32 with leading dim ldc.

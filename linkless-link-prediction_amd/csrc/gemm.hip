@@ -20,7 +20,8 @@
 int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
                          int64_t ldc, const float* bias, int act, const void* aux, int64_t ld_aux, float alpha,
                          float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
-                         const int64_t* drop_ctr, int64_t drop_stream, hipStream_t s);
+                         const int64_t* drop_ctr, int64_t drop_stream, const float* head_w, float* head_part,
+                         hipStream_t s);
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q);
 int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
                          float* ws_colsum, int64_t splits, hipStream_t s);
@@ -549,7 +550,8 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
       a16(A->ptr, A->ld) && (!A->ptr2 || a16(A->ptr2, A->ld2)) && a16(B->ptr, B->ld) && a16(C, ldc) &&
       (act != LLP_ACT_RELU_BWD || (aux_dtype == LLP_BF16 && a16(aux, ld_aux)))) {
     const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, aux, ld_aux, alpha, p.drop_p,
-                                        p.drop_thresh, p.drop_scale, p.drop_seed, p.drop_ctr, p.drop_stream, s);
+                                        p.drop_thresh, p.drop_scale, p.drop_seed, p.drop_ctr, p.drop_stream,
+                                        nullptr, nullptr, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_nt (256 tile): %s", hipGetErrorString((hipError_t)rc));
     return LLP_OK;
   }
@@ -563,6 +565,60 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<float, false>), grid, dim3(NTHREADS), 0, s, p);
   }
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+namespace {
+__global__ void head_finish_kernel(int64_t parts, int64_t M, const float* __restrict__ part, const float* __restrict__ b,
+                                   float* __restrict__ logit, float* __restrict__ prob) {
+  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float s = b ? b[0] : 0.f;
+  for (int64_t t = 0; t < parts; ++t) s += part[t * M + m];   // fixed order: deterministic
+  if (logit) logit[m] = s;
+  if (prob) prob[m] = 1.f / (1.f + expf(-s));
+}
+}  // namespace
+
+extern "C" int64_t llp_gemm_nt_head_parts(int64_t N) { return (N + 255) / 256; }
+
+extern "C" int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B, void* C,
+                                int64_t ldc, const float* bias, int act, float alpha, const llp_dropout* dropout,
+                                const float* head_w, float* head_part, void* stream) {
+  LLP_CHECK_ARG(A && B && head_w && head_part, "llp_gemm_nt_head: null pointer");
+  LLP_CHECK_ARG(act == LLP_ACT_NONE || act == LLP_ACT_RELU, "llp_gemm_nt_head: act must be NONE or RELU");
+  auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
+  LLP_CHECK_ARG(K > 0 && K % 64 == 0 && N % 8 == 0 && !A->ptr2 && !B->ptr2 && a16(A->ptr, A->ld) && a16(B->ptr, B->ld) &&
+                    (!C || a16(C, ldc)),
+                "llp_gemm_nt_head: needs bf16 rows of 16-B multiples, K %% 64 == 0, N %% 8 == 0, plain operands");
+  if (M == 0) return LLP_OK;
+  float dp = 0.f, ds = 1.f;
+  uint32_t dth = 0;
+  uint64_t dseed = 0;
+  const int64_t* dctr = nullptr;
+  int64_t dstr = 0;
+  if (dropout && dropout->p > 0.f) {
+    LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_gemm_nt_head: dropout p in (0,1) needs step_ctr");
+    dp = dropout->p;
+    dth = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    ds = 1.f / (1.f - dropout->p);
+    dseed = dropout->seed;
+    dctr = dropout->step_ctr;
+    dstr = dropout->stream_offset;
+  }
+  const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, nullptr, 0, alpha, dp, dth, ds, dseed, dctr,
+                                      dstr, head_w, head_part, (hipStream_t)stream);
+  if (rc != 0) return llp::set_error(rc, "llp_gemm_nt_head: %s", hipGetErrorString((hipError_t)rc));
+  return LLP_OK;
+}
+
+extern "C" int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit, float* prob,
+                               void* stream) {
+  LLP_CHECK_ARG(part, "llp_head_finish: null part");
+  if (M == 0) return LLP_OK;
+  hipLaunchKernelGGL(head_finish_kernel, dim3(ceil_div_u(M, 256)), dim3(256), 0, (hipStream_t)stream, parts, M, part,
+                     b, logit, prob);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

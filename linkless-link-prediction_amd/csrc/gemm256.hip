@@ -38,6 +38,10 @@ struct P256 {
   float alpha;
   float drop_p; uint32_t drop_thresh; float drop_scale; uint64_t drop_seed; const int64_t* drop_ctr;
   int64_t drop_stream;
+  // fused Linear(N, 1) head (LinkPredictor's last layer, src/models.py:146):
+  // head_part[tn][m] = sum over this tile's columns of y[m, n] * head_w[n]
+  const float* head_w;
+  float* head_part;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -289,7 +293,7 @@ template <int NS>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   constexpr int LOOP_U4 = NS * PSTAGE_U4;
   constexpr int SM_U4 = LOOP_U4 > SMEM_U4_EPI ? LOOP_U4 : SMEM_U4_EPI;
-  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4 + 256];   // + 4 KiB head partials
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int64_t tilesN = (p.N + TN - 1) / TN;
@@ -374,16 +378,22 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---------------- epilogue (as gemm_nt_bf16_256)
+  // ---------------- epilogue: alpha, bias, ReLU, dropout, fused head partials
   const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
   uint4* stg = smem;
+  float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn) {
     const int nl = wn * 64 + jn * 16 + g * 4;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    float hw[4] = {0.f, 0.f, 0.f, 0.f};
     if (p.bias) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? p.bias[n0 + nl + r] : 0.f;
+    }
+    if (p.head_w) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hw[r] = (n0 + nl + r < p.N) ? p.head_w[n0 + nl + r] : 0.f;
     }
 #pragma unroll
     for (int im = 0; im < 8; ++im) {
@@ -401,13 +411,31 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
           v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
         }
       }
+      hp[im] += v[0] * hw[0] + v[1] * hw[1] + v[2] * hw[2] + v[3] * hw[3];
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
       *dst = make_uint2(lo, hi);
     }
   }
+  if (p.head_w) {
+    // rows ml = wm*128 + im*16 + li: sum the 4 lane groups, then the 4 waves (wn) in LDS
+    float* part = reinterpret_cast<float*>(smem + SM_U4);   // [4 wn][256 rows]
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      float v = hp[im];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) part[wn * 256 + wm * 128 + im * 16 + li] = v;
+    }
+  }
   __syncthreads();
+  if (p.head_w && tid < TM && m0 + tid < p.M) {
+    const float* part = reinterpret_cast<const float*>(smem + SM_U4);
+    const float s = part[tid] + part[256 + tid] + part[512 + tid] + part[768 + tid];
+    p.head_part[(n0 / TN) * p.M + m0 + tid] = s;
+  }
+  if (!p.C) return;
   const int chunks_per_row = TN / 8;
 #pragma unroll 4
   for (int q = tid; q < TM * chunks_per_row; q += NT2) {
@@ -437,8 +465,12 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
 int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
                          int64_t ldc, const float* bias, int act, const void* aux, int64_t ld_aux, float alpha,
                          float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
-                         const int64_t* drop_ctr, int64_t drop_stream, hipStream_t s) {
+                         const int64_t* drop_ctr, int64_t drop_stream, const float* head_w, float* head_part,
+                         hipStream_t s) {
   P256 p;
+  p.head_w = head_w;
+  p.head_part = head_part;
+  if ((head_w || !C) && A->ptr2) return (int)hipErrorInvalidValue;   // fused head: pipelined kernel only
   p.A = (const bf16_t*)A->ptr; p.ia = A->idx; p.A2 = (const bf16_t*)A->ptr2; p.ia2 = A->idx2;
   p.lda = A->ld; p.lda2 = A->ptr2 ? A->ld2 : 0;
   p.B = (const bf16_t*)B->ptr; p.ib = B->idx; p.ldb = B->ld;
@@ -448,12 +480,11 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
   p.drop_ctr = drop_ctr; p.drop_stream = drop_stream;
   const int64_t tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  static const int pipe = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
+  static const int pipe_env = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
+  const int pipe = ((head_w || !C) && (pipe_env < 3 || pipe_env > 5)) ? 4 : pipe_env;
   if (A->ptr2)
     hipLaunchKernelGGL(gemm_nt_bf16_256<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (pipe == 5)
-    hipLaunchKernelGGL(gemm_nt_bf16_256p<5>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (pipe == 4)
+  else if (pipe == 4 || pipe == 5)
     hipLaunchKernelGGL(gemm_nt_bf16_256p<4>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (pipe == 3)
     hipLaunchKernelGGL(gemm_nt_bf16_256p<3>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);

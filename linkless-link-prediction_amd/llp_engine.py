@@ -296,7 +296,8 @@ class DistillEngine:
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
         logit = self._buf("logit", (R2,), torch.float32)
         zacts = []
-        if (H * h.element_size()) % 16 == 0:
+        zin_ok = (H * h.element_size()) % 16 == 0
+        if zin_ok:
             # materialise x_i * x_j once: layer-1 forward and its weight-gradient then
             # stream a plain operand with global_load_lds
             zin = self._buf("Zin", (R2, H), dt)
@@ -305,15 +306,27 @@ class DistillEngine:
         else:
             A0 = K.operand(h, ia, h, ib)
         A = A0
+        fused = False
         for l, lin in enumerate(self.prd):
             out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
-            K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
-                      dropout=self._dropout(p_drop, 5 + l))
+            last = l == len(self.prd) - 1
+            if last and self._fusable(lin.in_f, lin.out_f) and (A0 is not A or zin_ok):
+                # last hidden layer + Linear(H,1) head in one GEMM (partials per 256 columns)
+                parts = K.head_parts(lin.out_f)
+                hpart = self._buf("hpart", (parts, R2), torch.float32)
+                K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, self.head.weight.data.view(-1),
+                               hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, 5 + l))
+                K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
+                fused = True
+            else:
+                K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
+                          dropout=self._dropout(p_drop, 5 + l))
             zacts.append(out)
             A = K.operand(out)
         if self.predictor_kind == "mlp":
-            K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
-                       logit=logit)
+            if not fused:
+                K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
+                           logit=logit)
         else:
             K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
 
@@ -342,10 +355,27 @@ class DistillEngine:
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
 
+    def _fusable(self, K_in, N_out):
+        return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0
+
     def _teacher_forward(self, R, t_ia, t_ib, t_r):
         dt, dc = self.dtype, self.dc
         if self.t_kind == "inner":
             K.head_fwd(self.t_h, R, self.t_h.shape[1], None, None, prob=t_r, Z2=self.t_h, iz=t_ia, iz2=t_ib)
+            return
+        Ht = self.t_h.shape[1]
+        if len(self.t_hidden) == 1 and self._fusable(Ht, self.t_hidden[0][0].shape[0]):
+            # t_h[a] * t_h[c] materialised, then hidden layer + head in one GEMM; the
+            # hidden activations are never stored (no backward through the teacher)
+            tin = self._buf("Tin", (R, Ht), dt)
+            K.hadamard_rows(self.t_h, t_ia, self.t_h, t_ib, tin)
+            W, b = self.t_hidden[0]
+            w2, b2 = self.t_head
+            parts = K.head_parts(W.shape[0])
+            tpart = self._buf("tpart", (parts, R), torch.float32)
+            K.gemm_nt_head(K.operand(tin), K.operand(W), R, W.shape[0], W.shape[1], None, w2, tpart, bias=b,
+                           act=K.ACT_RELU, dropout=self._dropout(self.t_dropout, 9))
+            K.head_finish(parts, R, tpart, b2, prob=t_r)
             return
         A = K.operand(self.t_h, t_ia, self.t_h, t_ib)
         out = None

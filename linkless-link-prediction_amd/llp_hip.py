@@ -45,6 +45,10 @@ _SIGS = {
     "llp_device_count": (c_int, []),
     "llp_gemm_nt": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_int, c_vp, c_i64, c_int, c_f32, C.POINTER(Dropout), c_vp]),
+    "llp_gemm_nt_head_parts": (c_i64, [c_i64]),
+    "llp_gemm_nt_head": (c_int, [c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_vp, c_int,
+                                 c_f32, C.POINTER(Dropout), c_vp, c_vp, c_vp]),
+    "llp_head_finish": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
     "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_vp, c_i64, c_vp]),
@@ -149,6 +153,25 @@ def gemm_nt(A: Operand, B: Operand, M, N, K, C_out, dtype, bias=None, act=ACT_NO
                         dtype_code(C_out.dtype), ptr(bias), act, ptr(aux), aux.stride(0) if aux is not None else 0,
                         dtype_code(aux.dtype) if aux is not None else 0, alpha,
                         C.byref(dropout) if dropout is not None else None, stream_ptr()), "llp_gemm_nt")
+
+
+def head_parts(N):
+    return load().llp_gemm_nt_head_parts(N)
+
+
+def gemm_nt_head(A: Operand, B: Operand, M, N, K, C_out, head_w, head_part, bias=None, act=ACT_RELU, alpha=1.0,
+                 dropout: Dropout | None = None):
+    """bf16 GEMM with the Linear(N,1) head fused (C_out may be None)."""
+    L = lib()
+    check(L.llp_gemm_nt_head(M, N, K, C.byref(A), C.byref(B), ptr(C_out), C_out.stride(0) if C_out is not None else 0,
+                             ptr(bias), act, alpha, C.byref(dropout) if dropout is not None else None, head_w.data_ptr(),
+                             head_part.data_ptr(), stream_ptr()), "llp_gemm_nt_head")
+
+
+def head_finish(parts, M, head_part, b, logit=None, prob=None):
+    L = lib()
+    check(L.llp_head_finish(parts, M, head_part.data_ptr(), ptr(b), ptr(logit), ptr(prob), stream_ptr()),
+          "llp_head_finish")
 
 
 def gemm_tn_ws_bytes(dtype, M, P, Q):

@@ -15,6 +15,57 @@ def _grad_close(got, ref, rtol=2e-4):
     return err <= rtol * max(ref.abs().max().item(), 1e-6) + 1e-7, err
 
 
+def _make_engine(dtype, N, F_, H, L, seed, args, x, t_h, ei):
+    import llp_engine
+    import models
+    torch.manual_seed(seed)
+    model = models.MLP(L, F_, H, H, float(args.dropout)).to(DEV)
+    pred = models.LinkPredictor(args.predictor, H, H, 1, L, float(args.dropout)).to(DEV)
+    tpred = models.LinkPredictor(args.predictor, 256, 256, 1, 2, float(args.dropout)).to(DEV)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=float(args.lr))
+    eng = llp_engine.DistillEngine(model, pred, tpred, x.to(DEV), t_h.to(DEV), ei[0].numpy(), ei[1].numpy(), N, args,
+                                   opt, dtype=dtype, seed=5)
+    return eng, model, pred
+
+
+def test_engine_bf16_fast_paths_track_fp32():
+    """bf16 engine (256-tile glds GEMMs, fused heads, materialised Hadamard
+    inputs) against the fp32 engine on the same samples: same loss terms to
+    bf16 accuracy, gradients pointing the same way."""
+    import types
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, F_, H, L = 3000, 128, 256, 3
+    args = types.SimpleNamespace(rw_step=3, hops=3, ns_rate=3, ps_method="nb", dropout=0.0, margin=0.01,
+                                 LLP_D=1.0, LLP_R=1.0, True_label=1.0, predictor="mlp", lr=0.001)
+    g = torch.Generator().manual_seed(0)
+    u = torch.randint(0, N, (20000,), generator=g)
+    v = torch.randint(0, N, (20000,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
+    x = torch.randn(N, F_, generator=g) * 0.3
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    res = {}
+    for dt in ("fp32", "bf16"):
+        eng, model, pred = _make_engine(dt, N, F_, H, L, 3, args, x, t_h, ei)
+        anchors = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:300].to(torch.int32).to(DEV)
+        link = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(2))[:2048]
+        eng.step_minibatch(anchors, link.to(torch.int32).to(DEV), pairs.to(torch.int32).to(DEV))
+        torch.cuda.synchronize()
+        res[dt] = (eng.terms.cpu().clone(), [p.grad.detach().cpu().clone() for p in
+                                             list(model.parameters()) + list(pred.parameters())])
+    t32, g32 = res["fp32"]
+    t16, g16 = res["bf16"]
+    for i in range(4):
+        assert abs(t16[i] - t32[i]) <= 2e-2 * max(abs(t32[i].item()), 1e-3), (i, t16[i].item(), t32[i].item())
+    for a, b in zip(g16, g32):
+        cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+        assert cos > 0.98, (tuple(a.shape), cos)
+
+
 @pytest.mark.parametrize("name", G.MINIBATCH_CASES)
 def test_engine_replays_reference_minibatch(name):
     if not torch.cuda.is_available():

@@ -106,6 +106,34 @@ def test_gemm_nt_bf16_large_tile_paths(M, N, Kd, act):
     assert torch.allclose(out2.float().cpu(), ref2, rtol=1e-2, atol=1e-2 * (1 + ref2.abs().max().item()))
 
 
+@pytest.mark.parametrize("M,N,Kd", [(1000, 1024, 128), (513, 256, 256)])
+def test_gemm_nt_head_fused(M, N, Kd):
+    """Linear(N,1) head fused into the GEMM epilogue == separate head pass."""
+    k = K()
+    g = torch.Generator().manual_seed(M)
+    A = (torch.randn(M, Kd, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    hw = torch.randn(N, generator=g).to(DEV)
+    hb = torch.randn(1, generator=g).to(DEV)
+    parts = k.head_parts(N)
+    hpart = torch.empty(parts, M, device=DEV)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C, hw, hpart, bias=b, act=k.ACT_RELU)
+    logit = torch.empty(M, device=DEV)
+    prob = torch.empty(M, device=DEV)
+    k.head_finish(parts, M, hpart, hb, logit=logit, prob=prob)
+    y = F.relu(A.float() @ W.float().t() + b)
+    ref = y @ hw + hb
+    assert torch.allclose(C.float(), y, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(logit, ref, rtol=1e-3, atol=1e-3 * (1 + ref.abs().max().item()))
+    assert torch.allclose(prob, torch.sigmoid(ref), atol=1e-4)
+    # head only (C = None)
+    hpart2 = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, None, hw, hpart2, bias=b, act=k.ACT_RELU)
+    assert torch.equal(hpart, hpart2)
+
+
 def test_gemm_nt_bf16_dropout_matches_fp32_mask():
     """The 256-tile bf16 kernel and the general kernel draw the same dropout mask."""
     k = K()
