@@ -358,6 +358,22 @@ class DistillEngine:
     def _fusable(self, K_in, N_out):
         return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0
 
+    def capture_minibatch(self, anchors, link_ids, pairs, **kw):
+        """Capture one step_minibatch into a hipGraph (torch.cuda.CUDAGraph).
+
+        ``anchors`` / ``link_ids`` must be persistent device buffers: refill them
+        (e.g. ``anchors.copy_(node_perm[i*B:(i+1)*B])``) before each ``replay()``.
+        Every random draw is keyed by device counters (Philox stream = 16 *
+        step_ctr + offset; Adam's step), so each replay is a fresh step.  Call
+        after at least one eager step (kernels and buffers already loaded)."""
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.graph(g, stream=s):
+            self.step_minibatch(anchors, link_ids, pairs, **kw)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        return g
+
     def _teacher_forward(self, R, t_ia, t_ib, t_r):
         dt, dc = self.dtype, self.dc
         if self.t_kind == "inner":

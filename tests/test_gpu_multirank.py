@@ -1,0 +1,115 @@
+"""Data-parallel distillation step: R ranks each take a shard of the anchor and
+link batches (global normalisers, global Philox draw indices) and all-reduce
+the gradients; the result must equal the single-rank step.  Runs 2 processes
+on the one GPU of the test box over gloo (the RCCL path is the same code with
+backend 'nccl'; it is exercised by the driver's multi-GPU bench)."""
+import os
+import socket
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _problem():
+    N, F_, H, L = 2000, 64, 128, 3
+    g = torch.Generator().manual_seed(0)
+    u = torch.randint(0, N, (12000,), generator=g)
+    v = torch.randint(0, N, (12000,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
+    x = torch.randn(N, F_, generator=g) * 0.3
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    anchors = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:256].to(torch.int32)
+    links = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(2))[:1024].to(torch.int32)
+    args = types.SimpleNamespace(rw_step=2, hops=2, ns_rate=2, ps_method="nb", dropout=0.0, margin=0.05, LLP_D=1.0,
+                                 LLP_R=1.0, True_label=0.5, predictor="mlp", lr=0.01)
+    return N, F_, H, L, pairs, ei, x, t_h, anchors, links, args
+
+
+def _run(rank, world, dtype, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "linkless-link-prediction_amd"))
+    import llp_engine
+    import models
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, F_, H, L, pairs, ei, x, t_h, anchors, links, args = _problem()
+    torch.manual_seed(3)
+    model = models.MLP(L, F_, H, H, 0.0).to(dev)
+    pred = models.LinkPredictor("mlp", H, H, 1, L, 0.0).to(dev)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
+    eng = llp_engine.DistillEngine(model, pred, tpred, x.to(dev), t_h.to(dev), ei[0].numpy(), ei[1].numpy(), N, args,
+                                   opt, dtype=dtype, seed=11)
+    B, P = anchors.numel(), links.numel()
+    b0, b1 = rank * B // world, (rank + 1) * B // world
+    p0, p1 = rank * P // world, (rank + 1) * P // world
+    pr = pairs.to(torch.int32).to(dev).contiguous()
+    eng.begin_epoch()
+    for _ in range(2):
+        eng.step_minibatch(anchors[b0:b1].to(dev), links[p0:p1].to(dev), pr, b_offset=b0, p_offset=p0, B_total=B,
+                           P_total=P)
+    loss = eng.end_epoch(2 * P)
+    torch.cuda.synchronize()
+    if rank == 0:   # numpy copies: torch tensors through an mp.Queue share fds with an exiting child
+        out["loss"] = loss
+        out["params"] = [p.detach().cpu().numpy().copy() for p in list(model.parameters()) + list(pred.parameters())]
+        out["grads"] = [p.grad.detach().cpu().numpy().copy() for p in
+                        list(model.parameters()) + list(pred.parameters())]
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _worker(rank, world, dtype, port, q):
+    out = {}
+    _run(rank, world, dtype, port, out)
+    if rank == 0:
+        q.put(out)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_two_ranks_equal_one_rank(dtype):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    single = {}
+    _run(0, 1, dtype, 0, single)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, dtype, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    multi = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    tol = 1e-4 if dtype == "fp32" else 2e-2
+    assert abs(multi["loss"] - single["loss"]) <= tol * max(1.0, abs(single["loss"])), (multi["loss"], single["loss"])
+    for a, b in zip(multi["grads"], single["grads"]):
+        err = float(abs(a - b).max())
+        assert err <= (2e-3 if dtype == "fp32" else 5e-2) * max(float(abs(b).max()), 1e-6) + 1e-7, err
+    for a, b in zip(multi["params"], single["params"]):
+        d = abs(a - b)
+        assert float((d <= 1e-4).mean()) > 0.99
