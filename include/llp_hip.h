@@ -207,6 +207,44 @@ int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, const int32
 int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* samples,
                                 int32_t* ia, int32_t* ib, void* stream);
 
+/* ---------------------------------------------------------------- full-batch step (src/main.py:147-236)
+ * Dense negative sampling, replacing PyG 2.2.0 negative_sampling(edge_index,
+ * num_nodes, num_neg_samples, method='dense') (src/main.py:206,
+ * src/train_teacher_gnn.py:50).  edge_keys: sorted unique int64 keys
+ * row*(N-1) + col - (row < col) of the non-self-loop edges.  sample_size =
+ * int(1.1*num_neg/prob) as PyG computes it (host, with duplicate edges counted).
+ * population = N(N-1) <= sample_size: the non-edges in ascending order (bit-exact
+ * with PyG).  Otherwise `rounds` * sample_size Philox candidates (stream
+ * 16*(*step_ctr)+stream_offset), duplicates and existing edges dropped, first
+ * num_neg kept in draw order — the law of PyG's sample-without-replacement
+ * rounds.  out = int32[2, ld_out] (row 0 = source); *count = columns written
+ * (may be < num_neg, as PyG's may). */
+int64_t llp_neg_sample_dense_workspace_bytes(int64_t max_candidates);
+int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys, int64_t num_neg,
+                         int64_t sample_size, int rounds, uint64_t seed, const int64_t* step_ctr,
+                         int64_t stream_offset, int32_t* out, int64_t ld_out, int32_t* count,
+                         void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Predictor-row indices of the full-batch step: rows [0, B*C) are (anchor,
+ * context) pairs from samples[B, C1] (src/main.py:184-186), then P positives
+ * pairs[perm[i]] and n_neg negatives neg[:, i] (train_edges, src/main.py:212). */
+int llp_fullbatch_pairs(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
+                        const int32_t* perm, int64_t P, const int32_t* neg, int64_t ld_neg, int64_t n_neg,
+                        int32_t* ia, int32_t* ib, void* stream);
+
+/* KD terms of the full-batch loss (src/main.py:218-219):
+ *   KD_LM = mse(sigmoid(out_logit), t_prob_lab)  over n_lab rows (normaliser n_lab_total);
+ *           dlogit_lab += loss_scale * w_lm * d/dlogit
+ *   KD_RM = 1 - mean_b cos(h[idx_rm[b]], t_h[idx_rm[b]])  (src/main.py:24-25; normaliser
+ *           B_rm_total); dh[idx_rm[b]] += loss_scale * w_rm * d/dh  (dh f32, may be NULL)
+ * terms_out[4] = KD_RM share, terms_out[5] = KD_LM share, terms_out[0] += weighted sum. */
+int64_t llp_kd_terms_workspace_bytes(int64_t B_rm, int64_t n_lab);
+int llp_kd_terms(int dtype, int64_t n_lab, const float* out_logit, const float* t_prob_lab,
+                 double n_lab_total, float w_lm, int64_t B_rm, int64_t H, const void* h, int64_t ldh,
+                 const void* t_h, int64_t ldt, const int32_t* idx_rm, double B_rm_total, float w_rm,
+                 float loss_scale, float* dlogit_lab, float* dh, int64_t lddh, float* terms_out,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- SAGE aggregate
  * out[i] = scale_i * sum_{e in [rowptr[i], rowptr[i+1])} w_e * x[col[e]]
  *   mode 0 (forward mean):   scale_i = 1/max(deg_i,1), w_e = 1

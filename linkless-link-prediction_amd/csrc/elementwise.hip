@@ -206,13 +206,6 @@ __device__ __forceinline__ void put_elem(void* base, int64_t i, float v, int dt)
   else
     reinterpret_cast<float*>(base)[i] = v;
 }
-__device__ __forceinline__ void put_shadows(const llp_tensor_desc& d, int64_t e, float v) {
-  if (d.shadow) put_elem(d.shadow, e, v, d.shadow_dtype);
-  if (d.shadow_t) {
-    const int64_t r = e / d.cols, c = e % d.cols;
-    put_elem(d.shadow_t, c * d.rows + r, v, d.shadow_dtype);
-  }
-}
 
 __global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* __restrict__ descs, int64_t max_chunks,
                                                          float* __restrict__ partial) {
@@ -233,23 +226,43 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* 
   if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors, int64_t max_chunks,
-                                    const float* __restrict__ partial, int n_groups, float* __restrict__ sumsq) {
-  // one thread per group; fixed order -> deterministic
-  const int gidx = threadIdx.x;
-  if (gidx >= n_groups) return;
-  double s = 0.0;
+__global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors,
+                                                           int64_t max_chunks, const float* __restrict__ partial,
+                                                           int n_groups, float* __restrict__ sumsq) {
+  // one block; per tensor the 256 threads reduce its chunk partials in a fixed
+  // tree (deterministic), thread 0 adds the tensor total to its group.
+  __shared__ double red[4];
+  double gs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int t = 0; t < n_tensors; ++t) {
-    if (descs[t].group != gidx) continue;
     const int64_t nch = (descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK;
-    // per-tensor norm first, as torch.norm(stack([norm(g) for g])) does
     double ts = 0.0;
-    for (int64_t c = 0; c < nch; ++c) ts += (double)partial[t * max_chunks + c];
-    s += ts;
+    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) ts += (double)partial[t * max_chunks + c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ts += __shfl_xor(ts, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ts;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int gidx = descs[t].group;
+      if (gidx >= 0 && gidx < 8) gs[gidx] += (red[0] + red[1]) + (red[2] + red[3]);
+    }
+    __syncthreads();
   }
-  sumsq[gidx] = (float)s;
+  if (threadIdx.x == 0)
+    for (int gidx = 0; gidx < n_groups; ++gidx) sumsq[gidx] = (float)gs[gidx];
 }
 
+__device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float beta1, float beta2, float eps,
+                                           float bc2s, float step_size) {
+  m = beta1 * m + (1.f - beta1) * g;
+  v = beta2 * v + (1.f - beta2) * g * g;
+  const float denom = sqrtf(v) / bc2s + eps;
+  return p - step_size * (m / denom);
+}
+
+// torch.optim.Adam (foreach=False semantics, see reference main.py:train_minibatch
+// optimizer.step) after clip_grad_norm_.  Each block owns OPT_CHUNK elements of
+// one tensor; 16-byte vector path when the tensor's buffers allow it.  The
+// transposed shadow is written by shadow_t_kernel (LDS-tiled) afterwards.
 __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __restrict__ descs,
                                                    const float* __restrict__ sumsq, float max_norm, float lr,
                                                    float beta1, float beta2, float eps,
@@ -267,17 +280,74 @@ __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __rest
   const float bc1 = (float)(1.0 - pow((double)beta1, t));
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, t));
   const float step_size = lr / bc1;
+  const bool vec = ((d.numel & 3) == 0) &&
+                   ((((uintptr_t)d.grad) | ((uintptr_t)d.exp_avg) | ((uintptr_t)d.exp_avg_sq) | ((uintptr_t)d.param) |
+                     (d.shadow ? (uintptr_t)d.shadow : 0)) & 15) == 0;
+  if (vec) {
+    for (int64_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
+      float4 g = *reinterpret_cast<const float4*>(d.grad + e);
+      if (coef != 1.f) {
+        g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
+        *reinterpret_cast<float4*>(d.grad + e) = g;   // clip_grad_norm_ scales .grad in place
+      }
+      float4 m = *reinterpret_cast<const float4*>(d.exp_avg + e);
+      float4 v = *reinterpret_cast<const float4*>(d.exp_avg_sq + e);
+      float4 p = *reinterpret_cast<const float4*>(d.param + e);
+      p.x = adam_elem(g.x, m.x, v.x, p.x, beta1, beta2, eps, bc2s, step_size);
+      p.y = adam_elem(g.y, m.y, v.y, p.y, beta1, beta2, eps, bc2s, step_size);
+      p.z = adam_elem(g.z, m.z, v.z, p.z, beta1, beta2, eps, bc2s, step_size);
+      p.w = adam_elem(g.w, m.w, v.w, p.w, beta1, beta2, eps, bc2s, step_size);
+      *reinterpret_cast<float4*>(d.exp_avg + e) = m;
+      *reinterpret_cast<float4*>(d.exp_avg_sq + e) = v;
+      *reinterpret_cast<float4*>(d.param + e) = p;
+      if (d.shadow) {
+        if (d.shadow_dtype == LLP_BF16) {
+          uint2 o;
+          o.x = (uint32_t)f2bf(p.x) | ((uint32_t)f2bf(p.y) << 16);
+          o.y = (uint32_t)f2bf(p.z) | ((uint32_t)f2bf(p.w) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(d.shadow) + e) = o;
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(d.shadow) + e) = p;
+        }
+      }
+    }
+    return;
+  }
   for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
     const float g = d.grad[e] * coef;
-    if (coef != 1.f) d.grad[e] = g;   // clip_grad_norm_ scales the .grad in place
-    const float m = beta1 * d.exp_avg[e] + (1.f - beta1) * g;
-    const float v = beta2 * d.exp_avg_sq[e] + (1.f - beta2) * g * g;
+    if (coef != 1.f) d.grad[e] = g;
+    float m = d.exp_avg[e], v = d.exp_avg_sq[e];
+    const float pnew = adam_elem(g, m, v, d.param[e], beta1, beta2, eps, bc2s, step_size);
     d.exp_avg[e] = m;
     d.exp_avg_sq[e] = v;
-    const float denom = sqrtf(v) / bc2s + eps;
-    const float pnew = d.param[e] - step_size * (m / denom);
     d.param[e] = pnew;
-    put_shadows(d, e, pnew);
+    if (d.shadow) put_elem(d.shadow, e, pnew, d.shadow_dtype);
+  }
+}
+
+// shadow_t[c, r] = param[r, c] in the shadow dtype, 64x64 tiles through LDS so
+// both the read and the write are row-coalesced.  Grid-strided over tiles.
+__global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __restrict__ descs) {
+  __shared__ float tile[64][65];
+  const llp_tensor_desc d = descs[blockIdx.y];
+  if (!d.shadow_t) return;
+  const int64_t rows = d.rows, cols = d.cols;
+  const int64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int64_t tI = blockIdx.x; tI < tr * tc; tI += gridDim.x) {
+    const int64_t r0 = (tI / tc) * 64, c0 = (tI % tc) * 64;
+#pragma unroll 4
+    for (int i = ty; i < 64; i += 4) {
+      const int64_t r = r0 + i, c = c0 + tx;
+      tile[i][tx] = (r < rows && c < cols) ? d.param[r * cols + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int i = ty; i < 64; i += 4) {   // output row = column c0+i, output col = r0+tx
+      const int64_t c = c0 + i, r = r0 + tx;
+      if (c < cols && r < rows) put_elem(d.shadow_t, c * rows + r, tile[tx][i], d.shadow_dtype);
+    }
+    __syncthreads();
   }
 }
 
@@ -286,7 +356,8 @@ __global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __re
   const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
   if (e0 >= d.numel) return;
   const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) put_shadows(d, e, d.param[e]);
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
+    if (d.shadow) put_elem(d.shadow, e, d.param[e], d.shadow_dtype);
 }
 
 __global__ void increment_kernel(int64_t* ctr) { *ctr += 1; }
@@ -399,7 +470,7 @@ extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64
   hipLaunchKernelGGL(grad_sumsq_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, mc,
                      (float*)workspace);
   LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(grad_sumsq_finalize, dim3(1), dim3(64), 0, s, descs, n_tensors, mc, (const float*)workspace,
+  hipLaunchKernelGGL(grad_sumsq_finalize, dim3(1), dim3(256), 0, s, descs, n_tensors, mc, (const float*)workspace,
                      n_groups, sumsq);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
@@ -414,6 +485,8 @@ extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, sumsq, max_norm, lr,
                      beta1, beta2, eps, (const int64_t*)step);
   LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs);
+  LLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(increment_kernel, dim3(1), dim3(1), 0, s, step);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
@@ -423,6 +496,9 @@ extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, 
   LLP_CHECK_ARG(descs, "llp_refresh_shadows: null pointer");
   const int64_t mc = max_chunks_of(max_numel);
   hipLaunchKernelGGL(shadow_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream, descs);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream,
+                     descs);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -1,0 +1,351 @@
+// Full-batch distillation step helpers (reference ``train``, src/main.py:147-236):
+//   * dense negative sampling on the device (a3; PyG 2.2.0 negative_sampling,
+//     method='dense', called at src/main.py:206 and src/train_teacher_gnn.py:50),
+//   * predictor-row index build for h[samples] / h[train_edges] (src/main.py:184-186,213),
+//   * the KD_RM (cosine, src/main.py:24-25) and KD_LM (MSE, src/main.py:219) terms
+//     with their gradients.
+#include "llp_common.h"
+
+namespace {
+
+constexpr uint64_t kEmpty = ~0ull;
+
+__device__ __forceinline__ bool in_sorted(const int64_t* __restrict__ keys, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const int64_t k = keys[mid];
+    if (k < v) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && keys[lo] == v;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+
+__global__ void neg_table_init(uint64_t* __restrict__ tkeys, int32_t* __restrict__ tmin, int64_t T) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < T) {
+    tkeys[i] = kEmpty;
+    tmin[i] = 0x7fffffff;
+  }
+}
+
+// Candidate i of the round stream: the population index itself (population <=
+// sample_size: PyG enumerates range(population)) or a 64-bit Philox draw
+// floor(u64 * population / 2^64).  Candidates that are existing edges are
+// marked -1; the others are inserted in an open-addressing table keeping the
+// smallest draw index per value (first occurrence = sampling without replacement).
+__global__ void neg_candidates(int64_t M, int enumerate_all, uint64_t population, uint64_t seed,
+                               const int64_t* __restrict__ step_ctr, int64_t stream_offset,
+                               const int64_t* __restrict__ edge_keys, int64_t n_keys, int64_t* __restrict__ cand,
+                               int32_t* __restrict__ slot, uint64_t* __restrict__ tkeys, int32_t* __restrict__ tmin,
+                               int64_t T) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  uint64_t c;
+  if (enumerate_all) {
+    c = (uint64_t)(i % (int64_t)population);
+  } else {
+    const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_offset);
+    const uint64_t lo = philox_u32(seed, stream, 2 * (uint64_t)i);
+    const uint64_t hi = philox_u32(seed, stream, 2 * (uint64_t)i + 1);
+    c = __umul64hi((hi << 32) | lo, population);
+  }
+  cand[i] = (int64_t)c;
+  if (in_sorted(edge_keys, n_keys, (int64_t)c)) {
+    slot[i] = -1;
+    return;
+  }
+  uint32_t h = mix32(c) & (uint32_t)(T - 1);
+  while (true) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[h], (unsigned long long)kEmpty,
+                                              (unsigned long long)c);
+    if (prev == kEmpty || prev == c) {
+      atomicMin(&tmin[h], (int32_t)i);
+      slot[i] = (int32_t)h;
+      return;
+    }
+    h = (h + 1) & (uint32_t)(T - 1);
+  }
+}
+
+// Ordered compaction of the valid candidates (one block): the first num_neg of
+// them in stream order, decoded as PyG does: row = idx / (N-1), col = idx %
+// (N-1), col += (row <= col).
+__global__ __launch_bounds__(1024) void neg_compact(int64_t M, int64_t num_nodes, int64_t num_neg,
+                                                    const int64_t* __restrict__ cand,
+                                                    const int32_t* __restrict__ slot,
+                                                    const int32_t* __restrict__ tmin, int32_t* __restrict__ out,
+                                                    int64_t ld_out, int32_t* __restrict__ count) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t base_s;
+  const int tid = threadIdx.x;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  const int64_t per = 2048;   // candidates per pass: 1024 threads x 2
+  for (int64_t p0 = 0; p0 < M; p0 += per) {
+    const int base = base_s;
+    if (base >= num_neg) break;
+    int v[2];
+    int64_t idx[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      idx[k] = p0 + 2 * tid + k;
+      v[k] = 0;
+      if (idx[k] < M) {
+        const int32_t s = slot[idx[k]];
+        v[k] = (s >= 0 && tmin[s] == (int32_t)idx[k]) ? 1 : 0;
+      }
+    }
+    int mine = v[0] + v[1];
+    // block exclusive scan of mine
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if ((tid & 63) >= o) incl += y;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < (tid >> 6); ++w) wbase += wsum[w];
+    int pos = base + wbase + incl - mine;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (v[k]) {
+        if (pos < num_neg) {
+          const int64_t c = cand[idx[k]];
+          const int64_t r = c / (num_nodes - 1);
+          int64_t cc = c % (num_nodes - 1);
+          if (r <= cc) cc += 1;
+          out[pos] = (int32_t)r;
+          out[ld_out + pos] = (int32_t)cc;
+        }
+        ++pos;
+      }
+    }
+    __syncthreads();
+    if (tid == 1023) base_s = min((int64_t)pos, num_neg);
+    __syncthreads();
+  }
+  if (tid == 0) *count = base_s;
+}
+
+// ia/ib for the full-batch predictor rows: B*C context pairs (anchor, context)
+// then P positive and n_neg negative label pairs (train_edges, src/main.py:212).
+__global__ void fullbatch_pairs_kernel(int64_t B, int64_t C1, const int32_t* __restrict__ samples,
+                                       const int32_t* __restrict__ pairs, const int32_t* __restrict__ perm, int64_t P,
+                                       const int32_t* __restrict__ neg, int64_t ld_neg, int64_t n_neg,
+                                       int32_t* __restrict__ ia, int32_t* __restrict__ ib) {
+  const int64_t C = C1 - 1;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t BC = B * C;
+  if (t < BC) {
+    const int64_t b = t / C, c = t % C;
+    ia[t] = samples[b * C1];
+    ib[t] = samples[b * C1 + 1 + c];
+    return;
+  }
+  const int64_t u = t - BC;
+  if (u < P) {
+    const int64_t e = perm[u];
+    ia[t] = pairs[2 * e];
+    ib[t] = pairs[2 * e + 1];
+  } else if (u < P + n_neg) {
+    ia[t] = neg[u - P];
+    ib[t] = neg[ld_neg + u - P];
+  }
+}
+
+// KD_LM: mse(sigmoid(z), t) mean over n_total label rows; adds the gradient.
+__global__ __launch_bounds__(256) void kd_lm_kernel(int64_t n, const float* __restrict__ logit,
+                                                    const float* __restrict__ t_prob, double n_total, float w,
+                                                    float loss_scale, float* __restrict__ dlogit,
+                                                    float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (r < n) {
+    const float z = logit[r];
+    const float o = 1.f / (1.f + __expf(-z));
+    const float d = o - t_prob[r];
+    l = d * d;
+    dlogit[r] += loss_scale * w * (2.f * d / (float)n_total) * o * (1.f - o);
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) / (float)n_total;
+}
+
+// KD_RM: 1 - mean_b cos(h[idx_b], t_h[idx_b]) (torch cosine_similarity, eps 1e-8
+// clamp on each norm); one wave per row; dh[idx_b] += d/dh.
+template <typename T>
+__global__ __launch_bounds__(256) void kd_rm_kernel(int64_t B, int64_t H, const T* __restrict__ h, int64_t ldh,
+                                                    const T* __restrict__ t_h, int64_t ldt,
+                                                    const int32_t* __restrict__ idx, double B_total, float w,
+                                                    float loss_scale, float* __restrict__ dh, int64_t lddh,
+                                                    float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x * 4 + wv;
+  float cosv = 0.f;
+  if (b < B) {
+    const int64_t row = idx[b];
+    const T* hr = h + row * ldh;
+    const T* tr = t_h + row * ldt;
+    float dot = 0.f, n1 = 0.f, n2 = 0.f;
+    for (int64_t j = lane; j < H; j += 64) {
+      float a, c;
+      if constexpr (sizeof(T) == 2) { a = bf2f(hr[j]); c = bf2f(tr[j]); } else { a = hr[j]; c = tr[j]; }
+      dot += a * c; n1 += a * a; n2 += c * c;
+    }
+    dot = wave_sum(dot); n1 = wave_sum(n1); n2 = wave_sum(n2);
+    const float na = fmaxf(sqrtf(n1), 1e-8f), nb = fmaxf(sqrtf(n2), 1e-8f);
+    cosv = dot / (na * nb);
+    if (dh) {
+      const float g = -loss_scale * w / (float)B_total;
+      float* dr = dh + row * lddh;
+      for (int64_t j = lane; j < H; j += 64) {
+        float a, c;
+        if constexpr (sizeof(T) == 2) { a = bf2f(hr[j]); c = bf2f(tr[j]); } else { a = hr[j]; c = tr[j]; }
+        atomicAdd(&dr[j], g * (c / (na * nb) - cosv * a / (na * na)));
+      }
+    }
+    cosv = 1.f - cosv;   // this row's (1 - cos); summed / B_total = its share of the loss
+  }
+  if (lane == 0) red[wv] = cosv;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) / (float)B_total;
+}
+
+__global__ void kd_finalize(const float* __restrict__ partial, int64_t n_rm, int64_t n_lm, float w_rm, float w_lm,
+                            float* __restrict__ terms) {
+  __shared__ double red[2][256];
+  double a = 0, c = 0;
+  for (int64_t i = threadIdx.x; i < n_rm; i += blockDim.x) a += (double)partial[i];
+  for (int64_t i = threadIdx.x; i < n_lm; i += blockDim.x) c += (double)partial[n_rm + i];
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = c;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float rm = (float)red[0][0], lm = (float)red[1][0];
+    terms[4] = rm;
+    terms[5] = lm;
+    terms[0] += w_rm * rm + w_lm * lm;
+  }
+}
+
+int64_t pow2_at_least(int64_t v) {
+  int64_t t = 1;
+  while (t < v) t <<= 1;
+  return t;
+}
+
+}  // namespace
+
+extern "C" int64_t llp_neg_sample_dense_workspace_bytes(int64_t max_candidates) {
+  const int64_t T = pow2_at_least(2 * max_candidates);
+  return T * 8 + T * 4 + max_candidates * 8 + max_candidates * 4 + 64;
+}
+
+extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys,
+                                    int64_t num_neg, int64_t sample_size, int rounds, uint64_t seed,
+                                    const int64_t* step_ctr, int64_t stream_offset, int32_t* out, int64_t ld_out,
+                                    int32_t* count, void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(out && count && workspace && step_ctr, "llp_neg_sample_dense: null pointer");
+  LLP_CHECK_ARG(num_nodes >= 2 && num_nodes < (1ll << 31), "llp_neg_sample_dense: num_nodes out of range");
+  LLP_CHECK_ARG(n_keys == 0 || edge_keys, "llp_neg_sample_dense: null edge keys");
+  LLP_CHECK_ARG(rounds >= 1 && sample_size >= 0 && num_neg >= 0 && ld_out >= num_neg,
+                "llp_neg_sample_dense: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t population = (uint64_t)num_nodes * (uint64_t)(num_nodes - 1);
+  const int enumerate_all = population <= (uint64_t)sample_size;
+  // population <= sample_size: every round enumerates range(population); the
+  // later rounds can add nothing, so one pass suffices.
+  const int64_t M = enumerate_all ? (int64_t)population : (int64_t)rounds * sample_size;
+  LLP_CHECK_ARG(workspace_bytes >= llp_neg_sample_dense_workspace_bytes(M), "llp_neg_sample_dense: workspace too small");
+  LLP_CHECK_ARG(M < (1ll << 31), "llp_neg_sample_dense: too many candidates");
+  const int64_t T = pow2_at_least(2 * M);
+  char* w = reinterpret_cast<char*>(workspace);
+  uint64_t* tkeys = reinterpret_cast<uint64_t*>(w);
+  int32_t* tmin = reinterpret_cast<int32_t*>(w + T * 8);
+  int64_t* cand = reinterpret_cast<int64_t*>(w + T * 12);
+  int32_t* slot = reinterpret_cast<int32_t*>(w + T * 12 + M * 8);
+  if (M > 0) {
+    hipLaunchKernelGGL(neg_table_init, dim3(ceil_div_u(T, 256)), dim3(256), 0, s, tkeys, tmin, T);
+    LLP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(neg_candidates, dim3(ceil_div_u(M, 256)), dim3(256), 0, s, M, enumerate_all, population, seed,
+                       step_ctr, stream_offset, edge_keys, n_keys, cand, slot, tkeys, tmin, T);
+    LLP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(neg_compact, dim3(1), dim3(1024), 0, s, M, num_nodes, num_neg, cand, slot, tmin, out, ld_out,
+                     count);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_fullbatch_pairs(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
+                                   const int32_t* perm, int64_t P, const int32_t* neg, int64_t ld_neg, int64_t n_neg,
+                                   int32_t* ia, int32_t* ib, void* stream) {
+  LLP_CHECK_ARG(ia && ib, "llp_fullbatch_pairs: null output");
+  LLP_CHECK_ARG(B == 0 || (samples && C1 >= 2), "llp_fullbatch_pairs: null samples");
+  LLP_CHECK_ARG(P == 0 || (pairs && perm), "llp_fullbatch_pairs: null pairs");
+  LLP_CHECK_ARG(n_neg == 0 || neg, "llp_fullbatch_pairs: null negatives");
+  const int64_t n = B * (C1 > 0 ? C1 - 1 : 0) + P + n_neg;
+  if (n == 0) return LLP_OK;
+  hipLaunchKernelGGL(fullbatch_pairs_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, B, C1,
+                     samples, pairs, perm, P, neg, ld_neg, n_neg, ia, ib);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int64_t llp_kd_terms_workspace_bytes(int64_t B_rm, int64_t n_lab) {
+  return ((B_rm + 3) / 4 + (n_lab + 255) / 256 + 2) * (int64_t)sizeof(float);
+}
+
+extern "C" int llp_kd_terms(int dtype, int64_t n_lab, const float* out_logit, const float* t_prob_lab,
+                            double n_lab_total, float w_lm, int64_t B_rm, int64_t H, const void* h, int64_t ldh,
+                            const void* t_h, int64_t ldt, const int32_t* idx_rm, double B_rm_total, float w_rm,
+                            float loss_scale, float* dlogit_lab, float* dh, int64_t lddh, float* terms_out,
+                            void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(terms_out && workspace, "llp_kd_terms: null terms/workspace");
+  LLP_CHECK_ARG(workspace_bytes >= llp_kd_terms_workspace_bytes(B_rm, n_lab), "llp_kd_terms: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* partial = reinterpret_cast<float*>(workspace);
+  const int64_t nrm = B_rm > 0 ? (B_rm + 3) / 4 : 0;
+  const int64_t nlm = n_lab > 0 ? (n_lab + 255) / 256 : 0;
+  if (nrm > 0) {
+    LLP_CHECK_ARG(h && t_h && idx_rm, "llp_kd_terms: null KD_RM buffers");
+    if (dtype == LLP_BF16)
+      hipLaunchKernelGGL(kd_rm_kernel<bf16_t>, dim3((unsigned)nrm), dim3(256), 0, s, B_rm, H, (const bf16_t*)h, ldh,
+                         (const bf16_t*)t_h, ldt, idx_rm, B_rm_total, w_rm, loss_scale, dh, lddh, partial);
+    else
+      hipLaunchKernelGGL(kd_rm_kernel<float>, dim3((unsigned)nrm), dim3(256), 0, s, B_rm, H, (const float*)h, ldh,
+                         (const float*)t_h, ldt, idx_rm, B_rm_total, w_rm, loss_scale, dh, lddh, partial);
+    LLP_LAUNCH_CHECK();
+  }
+  if (nlm > 0) {
+    LLP_CHECK_ARG(out_logit && t_prob_lab && dlogit_lab, "llp_kd_terms: null KD_LM buffers");
+    hipLaunchKernelGGL(kd_lm_kernel, dim3((unsigned)nlm), dim3(256), 0, s, n_lab, out_logit, t_prob_lab, n_lab_total,
+                       w_lm, loss_scale, dlogit_lab, partial + nrm);
+    LLP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(kd_finalize, dim3(1), dim3(256), 0, s, partial, nrm, nlm, w_rm, w_lm, terms_out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}

@@ -132,6 +132,8 @@ class DistillEngine:
         # ---------------- data
         self.x = x.to(self.dev).to(self.dtype).contiguous()
         self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
+        self._row_np_for_neg, self._col_np_for_neg = np.asarray(row), np.asarray(col)
+        self._neg_keys = None
         rowptr, colv = build_sampler_csr(np.asarray(row), np.asarray(col), self.N, rw_sorted)
         self.rowptr = torch.from_numpy(rowptr).to(self.dev)
         self.col = torch.from_numpy(colv).to(self.dev)
@@ -354,6 +356,182 @@ class DistillEngine:
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
+
+    # ------------------------------------------------------------------ full-batch step
+    def _neg_setup(self):
+        """Keys of the negative-sampling graph edge_index = stack([col, row])
+        (src/main.py:156) in PyG's dense encoding (host, once per engine)."""
+        if getattr(self, "_neg_keys", None) is None:
+            r = self._row_np_for_neg
+            c = self._col_np_for_neg
+            src, dst = c.astype(np.int64), r.astype(np.int64)      # edge_index = [col, row]
+            m = src != dst
+            src, dst = src[m], dst[m]
+            key = src * (self.N - 1) + dst - (src < dst)
+            self._neg_n_idx = int(key.size)                         # duplicates counted, as PyG does
+            self._neg_keys = torch.from_numpy(np.unique(key)).to(self.dev)
+        return self._neg_keys
+
+    def neg_sample_size(self, num_neg):
+        """int(1.1 * num_neg / prob), prob = 1 - |idx| / (N(N-1)) (PyG 2.2.0)."""
+        self._neg_setup()
+        population = self.N * (self.N - 1)
+        if self._neg_n_idx >= population:
+            return 0
+        prob = 1.0 - self._neg_n_idx / population
+        return int(1.1 * num_neg / prob)
+
+    def step_fullbatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
+                       samples=None, neg=None, dense_negatives=True):
+        """One link batch of ``train`` (src/main.py:167-235): the student MLP runs
+        over all N nodes (src/main.py:173), the predictor over h[samples] context
+        pairs and h[train_edges] label pairs, plus KD_RM / KD_LM.
+
+        anchors  int32[B]  this rank's slice of node_perm (src/main.py:169)
+        link_ids int32[P]  this rank's slice of link_perm
+        pairs    int32[E,2] pos_train_edge (data.edge_index.t() for production, src/main.py:153)
+        dense_negatives: PyG dense negative sampling (non-collab, src/main.py:205-207)
+            else torch.randint pairs (collab, src/main.py:208-209).
+        neg      optional injected negatives int32[2, n_neg] (parity tests).
+        Returns the number of negatives used (host int; the dense sampler's count
+        is read back, one sync, as the reference's shapes are host-known)."""
+        a = self.args
+        B = int(anchors.numel())
+        P = int(link_ids.numel())
+        B_total = B if B_total is None else int(B_total)
+        P_total = P if P_total is None else int(P_total)
+        use_llp = bool(a.LLP_D or a.LLP_R)
+        rw_step, hops, ns_rate = int(a.rw_step), int(a.hops), int(a.ns_rate)
+        C = rw_step * hops * (1 + ns_rate)
+        C1 = C + 1
+        Bc = B if use_llp else 0
+        N = self.N
+        H = self.stu[-1].out_f
+        dt, dc = self.dtype, self.dc
+        p_drop = float(a.dropout)
+
+        # ---- samples (src/main.py:180-183)
+        samp = None
+        if use_llp:
+            samp = self._buf("samples", (B, C1), torch.int32)
+            if samples is not None:
+                samp.copy_(samples.to(torch.int32))
+            else:
+                K.context_sampler(self.rowptr, self.col, N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
+                                  self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
+        # ---- negatives (src/main.py:205-209)
+        if neg is not None:
+            n_neg = int(neg.shape[1])
+            n_neg_total = n_neg if P_total == P else int(round(n_neg * P_total / max(P, 1)))
+            negb = self._buf("neg", (2, max(n_neg, 1)), torch.int32)
+            negb[:, :n_neg].copy_(neg.to(torch.int32))
+        elif dense_negatives:
+            keys = self._neg_setup()
+            ss = self.neg_sample_size(P_total)
+            population = N * (N - 1)
+            M = population if population <= ss else 3 * ss
+            negg = self._buf("neg_all", (2, max(P_total, 1)), torch.int32)
+            cnt = self._buf("neg_count", (1,), torch.int32)
+            ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
+            K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, 14, negg, cnt, ws)
+            n_neg_total = int(cnt.item())
+            lo = min(p_offset, n_neg_total)
+            hi = min(p_offset + P, n_neg_total) if self.world > 1 else n_neg_total
+            n_neg = hi - lo
+            negb = negg[:, lo:hi]
+        else:
+            n_neg, n_neg_total = P, P_total
+            negb = self._buf("neg", (2, max(P, 1)), torch.int32)
+            K.randint_pairs(N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)
+        n_lab = P + n_neg
+        n_lab_total = P_total + n_neg_total
+        BC = Bc * C
+        R2 = BC + n_lab
+        ia = self._buf("fb_ia", (max(R2, 1),), torch.int32)[:R2]
+        ib = self._buf("fb_ib", (max(R2, 1),), torch.int32)[:R2]
+        K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
+
+        # ---- a4: student MLP over all nodes (src/main.py:173)
+        acts = []
+        A = K.operand(self.x)
+        for l, lin in enumerate(self.stu):
+            last = l == len(self.stu) - 1
+            out = self._buf(f"H{l}", (N, lin.out_f), dt)
+            K.gemm_nt(A, K.operand(lin.Wcomp), N, lin.out_f, lin.in_f, out, dc, bias=lin.b,
+                      act=K.ACT_NONE if last else K.ACT_RELU,
+                      dropout=None if last else self._dropout(p_drop, 1 + l))
+            acts.append(out)
+            A = K.operand(out)
+        h = acts[-1]
+
+        # ---- a5: predictor over context + label pairs (src/main.py:186,213)
+        logit = self._buf("logit", (R2,), torch.float32)
+        zacts = []
+        zin_ok = (H * h.element_size()) % 16 == 0
+        if self.predictor_kind == "mlp":
+            if zin_ok:
+                zin = self._buf("Zin", (R2, H), dt)
+                K.hadamard_rows(h, ia, h, ib, zin)
+                A0 = K.operand(zin)
+            else:
+                A0 = K.operand(h, ia, h, ib)
+            A = A0
+            for l, lin in enumerate(self.prd):
+                out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
+                K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
+                          dropout=self._dropout(p_drop, 5 + l))
+                zacts.append(out)
+                A = K.operand(out)
+            K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
+                       logit=logit)
+        else:
+            A0 = None
+            K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
+
+        # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215)
+        R_t = R2 if float(a.KD_LM) != 0.0 else BC
+        t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
+        if R_t > 0:
+            self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r)
+
+        # ---- a7-a9: LLP_D + LLP_R + BCE, then KD_RM / KD_LM (src/main.py:217-222)
+        dlogit = self._buf("dlogit", (R2,), torch.float32)
+        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(Bc, n_lab))
+        K.llp_loss(Bc, C, logit, t_r, n_lab, P, logit[BC:], B_total if use_llp else 1, n_lab_total,
+                   float(a.margin), 1.0, float(a.True_label), float(a.LLP_D) if use_llp else 0.0,
+                   float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws)
+        # d(loss)/dh accumulates in f32 (scatter-add over the gathered rows); in
+        # fp32 mode it IS the student backward's first gradient buffer
+        dh32 = self._buf("gS0" if dt == torch.float32 else "dh32", (N, H), torch.float32)
+        dh32.zero_()
+        w_rm, w_lm = float(a.KD_RM), float(a.KD_LM)
+        if w_rm != 0.0 or w_lm != 0.0:
+            if w_rm != 0.0 and self.t_h.shape[1] != H:
+                raise ValueError("KD_RM needs the student width to equal the teacher's (src/main.py:218)")
+            wsk = self._ws("ws_kd", K.kd_terms_ws_bytes(B, n_lab))
+            K.kd_terms(self.terms, wsk, n_lab=n_lab if w_lm != 0.0 else 0, out_logit=logit[BC:],
+                       t_prob_lab=t_r[BC:R2] if w_lm != 0.0 else None, n_lab_total=n_lab_total, w_lm=w_lm,
+                       dlogit_lab=dlogit[BC:], B_rm=B if w_rm != 0.0 else 0, h=h, t_h=self.t_h, idx_rm=anchors,
+                       B_rm_total=B_total, w_rm=w_rm, dh=dh32)
+        else:
+            self.terms[4:6].zero_()
+
+        # ---- a10: backward
+        dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
+        if self.predictor_kind == "mlp":
+            K.hadamard_bwd_scatter(R2, H, dZ0, ia, ib, h, dh32)
+        else:
+            K.hadamard_bwd_scatter(R2, H, None, ia, ib, h, dh32, drow=dlogit)
+        if dt == torch.float32:
+            dh = dh32
+        else:
+            dh = self._buf("gS0", (N, H), dt)
+            K.convert(dh32, dh)
+        self._student_backward(dh, N, None, acts, p_drop)
+        self._allreduce_and_update()
+        K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
+        K.increment(self.step_ctr)
+        return n_neg
 
     def _fusable(self, K_in, N_out):
         return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0

@@ -68,6 +68,13 @@ _SIGS = {
     "llp_randint_pairs": (c_int, [c_i64, c_i64, c_i64, c_i64, c_u64, c_vp, c_i64, c_vp, c_vp]),
     "llp_build_targets": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "llp_pair_index_from_samples": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_neg_sample_dense_workspace_bytes": (c_i64, [c_i64]),
+    "llp_neg_sample_dense": (c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                     c_vp, c_i64, c_vp]),
+    "llp_fullbatch_pairs": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "llp_kd_terms_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_kd_terms": (c_int, [c_int, c_i64, c_vp, c_vp, c_f64, c_f32, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
+                             c_f64, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "llp_csr_aggregate": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_int, c_vp]),
     "llp_grad_sumsq_workspace_bytes": (c_i64, [c_int, c_i64]),
     "llp_grad_sumsq": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
@@ -270,6 +277,43 @@ def pair_index_from_samples(B, Cc, samples, ia, ib):
     L = lib()
     check(L.llp_pair_index_from_samples(B, Cc, samples.data_ptr(), ia.data_ptr(), ib.data_ptr(), stream_ptr()),
           "llp_pair_index_from_samples")
+
+
+def neg_sample_ws_bytes(max_candidates):
+    return load().llp_neg_sample_dense_workspace_bytes(max_candidates)
+
+
+def neg_sample_dense(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr, stream_offset, out, count, ws,
+                     rounds=3):
+    """out: int32[2, ld] (ld >= num_neg); count: int32[1] on the device."""
+    L = lib()
+    check(L.llp_neg_sample_dense(num_nodes, ptr(edge_keys), 0 if edge_keys is None else edge_keys.numel(), num_neg,
+                                 sample_size, rounds, seed, step_ctr.data_ptr(), stream_offset, out.data_ptr(),
+                                 out.stride(0), count.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
+                                 stream_ptr()), "llp_neg_sample_dense")
+
+
+def fullbatch_pairs(B, C1, samples, pairs, perm, P, neg, n_neg, ia, ib):
+    L = lib()
+    check(L.llp_fullbatch_pairs(B, C1, ptr(samples), ptr(pairs), ptr(perm), P, ptr(neg),
+                                neg.stride(0) if neg is not None else 0, n_neg, ia.data_ptr(), ib.data_ptr(),
+                                stream_ptr()), "llp_fullbatch_pairs")
+
+
+def kd_terms_ws_bytes(B_rm, n_lab):
+    return load().llp_kd_terms_workspace_bytes(B_rm, n_lab)
+
+
+def kd_terms(terms, ws, n_lab=0, out_logit=None, t_prob_lab=None, n_lab_total=1.0, w_lm=0.0, dlogit_lab=None,
+             B_rm=0, h=None, t_h=None, idx_rm=None, B_rm_total=1.0, w_rm=0.0, dh=None, loss_scale=1.0):
+    L = lib()
+    dc = dtype_code(h.dtype) if h is not None else LLP_F32
+    H = h.shape[1] if h is not None else 0
+    check(L.llp_kd_terms(dc, n_lab, ptr(out_logit), ptr(t_prob_lab), float(n_lab_total), float(w_lm), B_rm, H, ptr(h),
+                         h.stride(0) if h is not None else 0, ptr(t_h), t_h.stride(0) if t_h is not None else 0,
+                         ptr(idx_rm), float(B_rm_total), float(w_rm), float(loss_scale), ptr(dlogit_lab), ptr(dh),
+                         dh.stride(0) if dh is not None else 0, terms.data_ptr(), ws.data_ptr(),
+                         ws.numel() * ws.element_size(), stream_ptr()), "llp_kd_terms")
 
 
 def csr_aggregate(n_rows, F, rowptr, col, x, inv_deg, mode, out, accumulate=False):

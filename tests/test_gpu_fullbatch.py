@@ -1,0 +1,170 @@
+"""Full-batch distillation step (reference ``train``, src/main.py:147-236) on the
+GPU: the dense negative sampler against its restatement (bit-exact) and
+against PyG's enumerate branch, the KD_RM / KD_LM kernel against autograd,
+and the engine replaying the reference's own full-batch golden steps."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_io as G
+from oracle import llp_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import llp_hip as K
+    return K
+
+
+def _graph(N, n_und, seed):
+    g = np.random.default_rng(seed)
+    u = g.integers(0, N, n_und)
+    v = g.integers(0, N, n_und)
+    return np.stack([np.concatenate([u, v]), np.concatenate([v, u])], 0)   # with self loops / duplicates
+
+
+@pytest.mark.parametrize("N,n_und,num_neg", [(12, 20, 200), (50, 300, 400), (2000, 9000, 4096), (3, 1, 10)])
+def test_neg_sample_dense_bit_exact(N, n_und, num_neg):
+    K = _K()
+    ei = _graph(N, n_und, N)
+    keys, n_idx = O.dense_neg_keys(ei, N)
+    ss = O.dense_neg_sample_size(n_idx, N, num_neg)
+    seed, step, off = 77, 3, 14
+    exp = O.negative_sampling_dense_philox(ei, N, num_neg, seed, 16 * step + off)
+    pop = N * (N - 1)
+    M = pop if pop <= ss else 3 * ss
+    out = torch.full((2, num_neg), -1, dtype=torch.int32, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(K.neg_sample_ws_bytes(M) // 4 + 16, dtype=torch.float32, device=DEV)
+    ctr = torch.full((1,), step, dtype=torch.int64, device=DEV)
+    K.neg_sample_dense(N, torch.from_numpy(keys).to(DEV), num_neg, ss, seed, ctr, off, out, cnt, ws)
+    torch.cuda.synchronize()
+    n = int(cnt.item())
+    assert n == exp.shape[1]
+    got = out[:, :n].cpu().numpy().astype(np.int64)
+    assert np.array_equal(got, exp)
+    # properties of PyG's output: no self loops, no existing edge, no repeats
+    assert (got[0] != got[1]).all()
+    es = set(map(tuple, ei.T.tolist()))
+    assert not any((int(a), int(b)) in es for a, b in got.T)
+    assert len(set(map(tuple, got.T.tolist()))) == n
+    if pop <= ss:   # enumerate branch: exactly PyG's (deterministic) result
+        ref = O.negative_sampling_dense(torch.from_numpy(ei), N, num_neg).numpy()
+        assert np.array_equal(got, ref)
+
+
+def test_kd_terms_match_autograd():
+    K = _K()
+    torch.manual_seed(0)
+    N, H, B, n_lab = 300, 256, 70, 500
+    for dt in (torch.float32, torch.bfloat16):
+        h = (torch.randn(N, H) * 0.5).to(DEV).to(dt)
+        t_h = (torch.randn(N, H) * 0.5).to(DEV).to(dt)
+        idx = torch.randperm(N)[:B].to(torch.int32).to(DEV)
+        logit = torch.randn(n_lab, device=DEV)
+        tp = torch.rand(n_lab, device=DEV)
+        terms = torch.zeros(8, device=DEV)
+        terms[0] = 1.5
+        dlog = torch.full((n_lab,), 0.25, device=DEV)
+        dh = torch.zeros(N, H, device=DEV)
+        ws = torch.empty(K.kd_terms_ws_bytes(B, n_lab) // 4 + 16, device=DEV)
+        K.kd_terms(terms, ws, n_lab=n_lab, out_logit=logit, t_prob_lab=tp, n_lab_total=n_lab, w_lm=0.7,
+                   dlogit_lab=dlog, B_rm=B, h=h, t_h=t_h, idx_rm=idx, B_rm_total=B, w_rm=0.3, dh=dh)
+        torch.cuda.synchronize()
+        hf = h.float().cpu().double().requires_grad_()
+        zf = logit.cpu().double().requires_grad_()
+        ii = idx.long().cpu()
+        rm = 1 - F.cosine_similarity(hf[ii], t_h.float().cpu().double()[ii], dim=-1).mean()
+        lm = F.mse_loss(torch.sigmoid(zf), tp.cpu().double())
+        (0.3 * rm + 0.7 * lm).backward()
+        assert abs(terms[4].item() - rm.item()) < 1e-5
+        assert abs(terms[5].item() - lm.item()) < 1e-5
+        assert abs(terms[0].item() - (1.5 + 0.3 * rm.item() + 0.7 * lm.item())) < 1e-5
+        assert torch.allclose(dlog.cpu().double(), 0.25 + zf.grad, atol=1e-7, rtol=1e-4)
+        assert torch.allclose(dh.cpu().double(), hf.grad, atol=1e-7, rtol=1e-3)
+
+
+def _engine(case, dtype="fp32"):
+    import llp_engine
+    import models
+    a = case.args
+    model = models.MLP(case.L, case.F, case.H, case.H, float(a.dropout)).to(DEV)
+    pred = models.LinkPredictor(a.predictor, case.H, case.H, 1, case.L, float(a.dropout)).to(DEV)
+    tpred = models.LinkPredictor(a.predictor, 256, 256, 1, 2, float(a.dropout)).to(DEV)
+    with torch.no_grad():
+        for p, v in zip(list(model.parameters()) + list(pred.parameters()), case.stu0 + case.pred0):
+            p.copy_(v)
+        for p, v in zip(tpred.parameters(), case.tpred):
+            p.copy_(v)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=float(a.lr))
+    ei = case.edge_index
+    eng = llp_engine.DistillEngine(model, pred, tpred, case.x.to(DEV), case.t_h.to(DEV), ei[0].numpy(),
+                                   ei[1].numpy(), case.N, a, opt, dtype=dtype, seed=1)
+    return eng, model, pred
+
+
+@pytest.mark.parametrize("name", G.FULLBATCH_CASES)
+def test_engine_replays_reference_fullbatch(name):
+    _K()
+    case = G.load_case(name)
+    a = case.args
+    eng, model, pred = _engine(case)
+    pairs = case.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+    steps_per_epoch = len(case.steps) // len(case.epoch_losses)
+    tot_ex = 0
+    eng.begin_epoch()
+    for i, st in enumerate(case.steps):
+        n_neg = eng.step_fullbatch(st.node_perm.to(torch.int32).to(DEV), st.link_perm.to(torch.int32).to(DEV), pairs,
+                                   samples=None if st.samples is None else st.samples.to(DEV),
+                                   neg=st.neg_edge.to(DEV))
+        assert n_neg == st.neg_edge.shape[1]
+        torch.cuda.synchronize()
+        t = eng.terms.cpu()
+        assert abs(t[1].item() - st.bce) <= 1e-4 * max(1, abs(st.bce)), ("bce", t[1].item(), st.bce)
+        if st.llp_d is not None:
+            assert abs(t[2].item() - st.llp_d) <= 1e-4 * max(1, abs(st.llp_d)), ("kl", t[2].item(), st.llp_d)
+            assert abs(t[3].item() - st.llp_r) <= 1e-4 * max(1, abs(st.llp_r)), ("rank", t[3].item(), st.llp_r)
+        rtol = 2e-4 if i == 0 else 2e-3
+        for p, ref in zip(list(model.parameters()) + list(pred.parameters()), st.grads):
+            err = (p.grad.detach().cpu() - ref).abs().max().item()
+            assert err <= rtol * max(ref.abs().max().item(), 1e-6) + 1e-7, (name, i, tuple(p.shape), err)
+        tot_ex += st.edge.size(1)
+        if (i + 1) % steps_per_epoch == 0:
+            ep = eng.end_epoch(tot_ex)
+            assert abs(ep - case.epoch_losses[(i + 1) // steps_per_epoch - 1]) < 1e-4, ep
+            tot_ex = 0
+            eng.begin_epoch()
+    lr = float(a.lr)
+    for p, ref in zip(list(model.parameters()) + list(pred.parameters()), case.stu_final + case.pred_final):
+        d = (p.detach().cpu() - ref).abs()
+        assert (d <= 1e-4).float().mean().item() > 0.99, (name, tuple(p.shape), d.max().item())
+        assert d.max().item() <= 2 * lr * len(case.steps), (name, tuple(p.shape), d.max().item())
+
+
+def test_fullbatch_device_negatives_and_bf16():
+    """No injection: device samples + dense negatives; bf16 engine tracks fp32."""
+    _K()
+    case = G.load_case("fullbatch_cora_small")
+    res = {}
+    for dt in ("fp32", "bf16"):
+        eng, model, pred = _engine(case, dt)
+        pairs = case.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+        st = case.steps[0]
+        n_neg = eng.step_fullbatch(st.node_perm.to(torch.int32).to(DEV), st.link_perm.to(torch.int32).to(DEV), pairs)
+        torch.cuda.synchronize()
+        assert n_neg == st.link_perm.numel()
+        res[dt] = (eng.terms.cpu().clone(), [p.grad.detach().cpu().clone() for p in
+                                             list(model.parameters()) + list(pred.parameters())])
+        assert torch.isfinite(res[dt][0]).all()
+    for i in range(6):
+        a, b = res["bf16"][0][i].item(), res["fp32"][0][i].item()
+        assert abs(a - b) <= 3e-2 * max(abs(b), 1e-2), (i, a, b)
+    for a, b in zip(res["bf16"][1], res["fp32"][1]):
+        assert F.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.97
