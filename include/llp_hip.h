@@ -245,6 +245,18 @@ int llp_kd_terms(int dtype, int64_t n_lab, const float* out_logit, const float* 
                  float loss_scale, float* dlogit_lab, float* dh, int64_t lddh, float* terms_out,
                  void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- evaluation (src/train_teacher_gnn.py:76-268)
+ * Hits@K as ogb 1.3.6 Evaluator computes it (src/train_teacher_gnn.py:121-143,
+ * 227-247): kth = topk(neg, K)[-1] (exact radix select), hits = #(pos > kth) /
+ * n_pos; n_neg < K -> 1.0.  One result per entry of Ks[n_K] (device int32). */
+int llp_hits_at_k(const float* pos, int64_t n_pos, const float* neg, int64_t n_neg, const int32_t* Ks,
+                  int n_K, double* hits_out, void* stream);
+/* sklearn roc_auc_score(y, score) with y = [1]*n_pos + [0]*n_neg
+ * (src/train_teacher_gnn.py:153,263): Mann-Whitney U / (n_pos*n_neg), ties 1/2. */
+int64_t llp_auc_workspace_bytes(int64_t n_pos, int64_t n_neg);
+int llp_auc(const float* pos, int64_t n_pos, const float* neg, int64_t n_neg, double* auc_out,
+            void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- SAGE aggregate
  * out[i] = scale_i * sum_{e in [rowptr[i], rowptr[i+1])} w_e * x[col[e]]
  *   mode 0 (forward mean):   scale_i = 1/max(deg_i,1), w_e = 1
@@ -272,6 +284,9 @@ typedef struct llp_tensor_desc {
   int64_t cols;
   int32_t group;       /* clip group id (0..7)                                   */
   int32_t shadow_dtype;/* element type of shadow / shadow_t: LLP_F32 or LLP_BF16 */
+  int64_t shadow_ld;   /* row stride of shadow (0 = cols): lets two parameters share one
+                          K-concatenated GEMM operand, e.g. [W_l | W_r] of a SAGEConv  */
+  int64_t shadow_t_ld; /* row stride of shadow_t (0 = rows)                            */
 } llp_tensor_desc;
 
 /* sumsq[g] = sum of grad^2 over tensors of group g (n_groups <= 8). */
@@ -302,6 +317,13 @@ int llp_zero(void* p, int64_t bytes, void* stream);
  * out[r, :] = z[r, :] * s[r]                      — 'inner' predictor backward
  * out = gprob * prob * (1 - prob)                 — torch.sigmoid backward (src/models.py:150) */
 int llp_relu_bwd(int dtype, int64_t n, const void* gy, const void* y, float alpha, void* out, void* stream);
+/* Strided [rows, cols] forms for the SAGE teacher's concatenated layouts:
+ * y = dropout(act(x)) (act NONE/RELU; dropout draw #(r*cols+c), as the GEMM
+ * epilogue; src/models.py:117-118) and out = alpha * gy * (y > 0). */
+int llp_act_2d(int dtype, int64_t rows, int64_t cols, const void* x, int64_t ldx, void* y, int64_t ldy,
+               int act, const llp_dropout* dropout, void* stream);
+int llp_relu_bwd_2d(int dtype, int64_t rows, int64_t cols, const void* gy, int64_t ldg, const void* y,
+                    int64_t ldy, float alpha, void* out, int64_t ldo, void* stream);
 int llp_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* dst, void* stream);
 int llp_mul(int dtype, int64_t n, const void* a, const void* b, void* out, void* stream);
 int llp_row_scale(int dtype, int64_t rows, int64_t cols, const void* z, const float* s, void* out, void* stream);

@@ -200,6 +200,13 @@ __global__ __launch_bounds__(256) void hadamard_rows_kernel(int64_t R, int64_t H
 // ---------------------------------------------------------------- optimiser
 constexpr int OPT_CHUNK = 4096;  // elements per block
 
+// element e = (r, c) of a [rows, cols] parameter -> its slot in a shadow with
+// leading dimension shadow_ld (0 = packed)
+__device__ __forceinline__ int64_t shadow_index(const llp_tensor_desc& d, int64_t e) {
+  if (d.shadow_ld == 0 || d.shadow_ld == d.cols) return e;
+  return (e / d.cols) * d.shadow_ld + e % d.cols;
+}
+
 __device__ __forceinline__ void put_elem(void* base, int64_t i, float v, int dt) {
   if (dt == LLP_BF16)
     reinterpret_cast<bf16_t*>(base)[i] = f2bf(v);
@@ -282,7 +289,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __rest
   const float step_size = lr / bc1;
   const bool vec = ((d.numel & 3) == 0) &&
                    ((((uintptr_t)d.grad) | ((uintptr_t)d.exp_avg) | ((uintptr_t)d.exp_avg_sq) | ((uintptr_t)d.param) |
-                     (d.shadow ? (uintptr_t)d.shadow : 0)) & 15) == 0;
+                     (d.shadow ? (uintptr_t)d.shadow : 0)) & 15) == 0 &&
+                   (d.shadow_ld == 0 || d.shadow_ld == d.cols);
   if (vec) {
     for (int64_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
       float4 g = *reinterpret_cast<const float4*>(d.grad + e);
@@ -321,7 +329,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __rest
     d.exp_avg[e] = m;
     d.exp_avg_sq[e] = v;
     d.param[e] = pnew;
-    if (d.shadow) put_elem(d.shadow, e, pnew, d.shadow_dtype);
+    if (d.shadow) put_elem(d.shadow, shadow_index(d, e), pnew, d.shadow_dtype);
   }
 }
 
@@ -332,6 +340,7 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
   const llp_tensor_desc d = descs[blockIdx.y];
   if (!d.shadow_t) return;
   const int64_t rows = d.rows, cols = d.cols;
+  const int64_t ldt = d.shadow_t_ld ? d.shadow_t_ld : rows;
   const int64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int64_t tI = blockIdx.x; tI < tr * tc; tI += gridDim.x) {
@@ -345,7 +354,7 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
 #pragma unroll 4
     for (int i = ty; i < 64; i += 4) {   // output row = column c0+i, output col = r0+tx
       const int64_t c = c0 + i, r = r0 + tx;
-      if (c < cols && r < rows) put_elem(d.shadow_t, c * rows + r, tile[tx][i], d.shadow_dtype);
+      if (c < cols && r < rows) put_elem(d.shadow_t, c * ldt + r, tile[tx][i], d.shadow_dtype);
     }
     __syncthreads();
   }
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __re
   if (e0 >= d.numel) return;
   const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
   for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
-    if (d.shadow) put_elem(d.shadow, e, d.param[e], d.shadow_dtype);
+    if (d.shadow) put_elem(d.shadow, shadow_index(d, e), d.param[e], d.shadow_dtype);
 }
 
 __global__ void increment_kernel(int64_t* ctr) { *ctr += 1; }

@@ -63,7 +63,83 @@ __global__ void sigmoid_bwd_kernel(int64_t n, const float* __restrict__ gprob, c
 
 unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384)); }
 
+// y = dropout(relu(x)) on a strided [rows, cols] view; draw #(r*cols + c) of
+// Philox stream 16*(*ctr) + stream_off, as the GEMM epilogue draws.
+template <typename T>
+__global__ void act_2d_kernel(int64_t rows, int64_t cols, const T* __restrict__ x, int64_t ldx, T* __restrict__ y,
+                              int64_t ldy, int relu, uint32_t thr, float scale, uint64_t seed,
+                              const int64_t* __restrict__ ctr, int64_t stream_off) {
+  const int64_t n = rows * cols;
+  const uint64_t stream = ctr ? (uint64_t)(16 * (*ctr) + stream_off) : 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols, c = i % cols;
+    float v = ldv<T>(x, r * ldx + c);
+    if (relu) v = fmaxf(v, 0.f);
+    if (thr) v = ((philox_u32(seed, stream, (uint64_t)i) >> 8) >= thr) ? v * scale : 0.f;
+    stv<T>(y, r * ldy + c, v);
+  }
+}
+
+template <typename T>
+__global__ void relu_bwd_2d_kernel(int64_t rows, int64_t cols, const T* __restrict__ gy, int64_t ldg,
+                                   const T* __restrict__ y, int64_t ldy, float alpha, T* __restrict__ out,
+                                   int64_t ldo) {
+  const int64_t n = rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols, c = i % cols;
+    float g = alpha * ldv<T>(gy, r * ldg + c);
+    if (!(ldv<T>(y, r * ldy + c) > 0.f)) g = 0.f;
+    stv<T>(out, r * ldo + c, g);
+  }
+}
+
 }  // namespace
+
+extern "C" int llp_act_2d(int dtype, int64_t rows, int64_t cols, const void* x, int64_t ldx, void* y, int64_t ldy,
+                          int act, const llp_dropout* dropout, void* stream) {
+  LLP_CHECK_ARG(x && y, "llp_act_2d: null pointer");
+  LLP_CHECK_ARG(act == LLP_ACT_NONE || act == LLP_ACT_RELU, "llp_act_2d: act must be NONE or RELU");
+  if (rows == 0 || cols == 0) return LLP_OK;
+  uint32_t thr = 0;
+  float scale = 1.f;
+  uint64_t seed = 0;
+  const int64_t* ctr = nullptr;
+  int64_t off = 0;
+  if (dropout && dropout->p > 0.f) {
+    LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_act_2d: dropout p in (0,1) needs step_ctr");
+    thr = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    scale = 1.f / (1.f - dropout->p);
+    seed = dropout->seed;
+    ctr = dropout->step_ctr;
+    off = dropout->stream_offset;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = rows * cols;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(act_2d_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, rows, cols, (const bf16_t*)x, ldx,
+                       (bf16_t*)y, ldy, act == LLP_ACT_RELU, thr, scale, seed, ctr, off);
+  else
+    hipLaunchKernelGGL(act_2d_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, rows, cols, (const float*)x, ldx,
+                       (float*)y, ldy, act == LLP_ACT_RELU, thr, scale, seed, ctr, off);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_relu_bwd_2d(int dtype, int64_t rows, int64_t cols, const void* gy, int64_t ldg, const void* y,
+                               int64_t ldy, float alpha, void* out, int64_t ldo, void* stream) {
+  LLP_CHECK_ARG(gy && y && out, "llp_relu_bwd_2d: null pointer");
+  if (rows == 0 || cols == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = rows * cols;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(relu_bwd_2d_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, rows, cols, (const bf16_t*)gy,
+                       ldg, (const bf16_t*)y, ldy, alpha, (bf16_t*)out, ldo);
+  else
+    hipLaunchKernelGGL(relu_bwd_2d_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, rows, cols, (const float*)gy,
+                       ldg, (const float*)y, ldy, alpha, (float*)out, ldo);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
 
 extern "C" int llp_relu_bwd(int dtype, int64_t n, const void* gy, const void* y, float alpha, void* out,
                             void* stream) {

@@ -61,8 +61,9 @@ __global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_
   // chunk sweep: columns in blocks of 64 chunks
   for (int64_t c0 = 0; c0 < nch; c0 += 64) {
     const int64_t cw = min((int64_t)64, nch - c0);           // chunks in this sweep
-    const int G = cw >= 64 ? 1 : (cw >= 32 ? 2 : (cw >= 16 ? 4 : (cw >= 8 ? 8 : (cw >= 4 ? 16 : (cw >= 2 ? 32 : 64)))));
-    const int lanes_per_group = 64 / G;
+    // lanes per group = the smallest power of two >= cw (every chunk has a lane)
+    const int lanes_per_group = cw > 32 ? 64 : (cw > 16 ? 32 : (cw > 8 ? 16 : (cw > 4 ? 8 : (cw > 2 ? 4 : (int)cw))));
+    const int G = 64 / lanes_per_group;
     const int grp = lane / lanes_per_group, gl = lane % lanes_per_group;
     const bool active = gl < cw;
     float acc[E];

@@ -68,47 +68,35 @@ class _Linear:
         return self.Wc if self.Wc is not None else self.W
 
 
-class DistillEngine:
-    """Holds every device buffer of the distillation step.
+class EngineBase:
+    """Device state shared by the distillation and teacher engines: the flat
+    f32 gradient buffer the parameters' ``.grad`` view, Adam state in the
+    torch optimizer, the device descriptor table of the fused clip+Adam
+    kernel (with each weight's compute-dtype / transposed shadows), the
+    LinkPredictor's forward/backward, scratch buffers and the loss counters."""
 
-    Parameters mirror ``train_minibatch``'s arguments (src/main.py:52): the
-    student ``model`` (MLP), ``predictor`` (LinkPredictor), the frozen
-    ``teacher_predictor`` and teacher embeddings ``t_h``; ``x`` the node
-    features; ``row``/``col`` the sampler graph (data.adj_t, src/main.py:56);
-    ``optimizer`` a torch.optim.Adam over model+predictor parameters whose
-    hyper-parameters and state this engine uses.
-    """
-
-    def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
-                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None):
-        self.dev = torch.device(device) if device is not None else x.device
+    def _init_device(self, x_device, device, dtype, seed, group, name):
+        self.dev = torch.device(device) if device is not None else x_device
         if self.dev.type != "cuda":
-            raise RuntimeError("DistillEngine runs only on a HIP device (no CPU fallback)")
+            raise RuntimeError(f"{name} runs only on a HIP device (no CPU fallback)")
         K.lib()
         self.dtype = _DT[dtype]
         self.dc = K.dtype_code(self.dtype)
-        self.args = args
-        self.N = int(num_nodes)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.group = group
         self.world = dist.get_world_size(group) if (group is not None or (dist.is_available() and dist.is_initialized())) else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
-        if args.predictor not in ("mlp", "inner"):
-            raise ValueError(args.predictor)
-        self.predictor_kind = args.predictor
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)   # RNG stream counter
+        self.terms = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        self._bufs = {}
+        self._shadows = {}
 
-        # ---------------- parameters
-        self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
-        stu = list(model.layers)
-        prd = list(predictor.lins)
-        self.stu = [_Linear(l, self.dtype, need_t=(i > 0), need_c=True) for i, l in enumerate(stu)]
-        if self.predictor_kind == "mlp":
-            self.prd = [_Linear(l, self.dtype, need_t=True, need_c=True) for l in prd[:-1]]
-            self.head = prd[-1]
-        else:
-            self.prd, self.head = [], None
-        self.all_params = [p for l in stu for p in (l.weight, l.bias)] + [p for l in prd for p in (l.weight, l.bias)]
-        self.n_stu_params = 2 * len(stu)
+    def _init_params(self, all_params, groups, optimizer):
+        """``groups[i]``: clip group of all_params[i] (clip_grad_norm_ per module, Q9)."""
+        self.all_params = list(all_params)
+        self.param_groups_of = list(groups)
+        self.n_groups = max(self.param_groups_of) + 1
         total = sum(p.numel() for p in self.all_params)
         self.flat_grad = torch.zeros(total, dtype=torch.float32, device=self.dev)
         off = 0
@@ -118,33 +106,24 @@ class DistillEngine:
         self.optimizer = optimizer
         self._init_optimizer_state()
 
-        # teacher predictor (frozen; dropout stays live as in the reference, Q3)
-        tl = list(teacher_predictor.lins)
-        self.t_kind = teacher_predictor.predictor
-        self.t_hidden = []
-        for l in tl[:-1]:
-            W = l.weight.data.to(self.dev)
-            self.t_hidden.append((W.to(self.dtype).contiguous(), l.bias.data.to(self.dev).float().contiguous()))
-        self.t_head = (tl[-1].weight.data.to(self.dev).float().reshape(-1).contiguous(),
-                       tl[-1].bias.data.to(self.dev).float().contiguous())
-        self.t_dropout = float(getattr(teacher_predictor, "dropout", 0.0)) if teacher_predictor.training else 0.0
+    def _set_shadow(self, p, shadow=None, shadow_t=None, ld=0, ld_t=0):
+        """Register the compute-dtype copy (row stride ld) and/or transposed copy
+        (row stride ld_t) the Adam kernel refreshes for parameter p."""
+        self._shadows[id(p)] = (shadow, shadow_t, int(ld), int(ld_t))
 
-        # ---------------- data
-        self.x = x.to(self.dev).to(self.dtype).contiguous()
-        self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
-        self._row_np_for_neg, self._col_np_for_neg = np.asarray(row), np.asarray(col)
-        self._neg_keys = None
-        rowptr, colv = build_sampler_csr(np.asarray(row), np.asarray(col), self.N, rw_sorted)
-        self.rowptr = torch.from_numpy(rowptr).to(self.dev)
-        self.col = torch.from_numpy(colv).to(self.dev)
-
-        # ---------------- step state (device)
-        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)   # RNG stream counter
-        self.terms = torch.zeros(8, dtype=torch.float32, device=self.dev)
-        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.dev)
-        self._bufs = {}
-        self._shape = None
-        self._build_descs()
+    def _setup_predictor(self, predictor, kind):
+        if kind not in ("mlp", "inner"):
+            raise ValueError(kind)
+        self.predictor_kind = kind
+        prd = list(predictor.lins)
+        if kind == "mlp":
+            self.prd = [_Linear(l, self.dtype, need_t=True, need_c=True) for l in prd[:-1]]
+            self.head = prd[-1]
+        else:
+            self.prd, self.head = [], None
+        for l in self.prd:
+            self._set_shadow(l.lin.weight, l.Wc, l.Wt)
+        return [p for l in prd for p in (l.weight, l.bias)]
 
     # ------------------------------------------------------------------ setup
     def _init_optimizer_state(self):
@@ -170,23 +149,17 @@ class DistillEngine:
     def _build_descs(self):
         opt = self.optimizer
         descs = []
-        shadow_dt = self.dc
-        lin_of = {}
-        for l in self.stu + self.prd:
-            lin_of[id(l.lin.weight)] = l
-        for i, p in enumerate(self.all_params):
+        for p, grp in zip(self.all_params, self.param_groups_of):
             st = opt.state[p]
-            L = lin_of.get(id(p))
-            shadow = L.Wc if L is not None else None
-            shadow_t = L.Wt if L is not None else None
+            shadow, shadow_t, ld, ld_t = self._shadows.get(id(p), (None, None, 0, 0))
             rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
             descs.append(K.TensorDesc(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                                       st["exp_avg_sq"].data_ptr(), K.ptr(shadow), K.ptr(shadow_t), p.numel(), rows,
-                                      cols, 0 if i < self.n_stu_params else 1, shadow_dt))
+                                      cols, grp, self.dc, ld, ld_t))
         self.n_desc = len(descs)
         self.max_numel = max(p.numel() for p in self.all_params)
         self.descs_dev = K.descs_to_device(descs, self.dev)
-        self.sumsq = torch.zeros(2, dtype=torch.float32, device=self.dev)
+        self.sumsq = torch.zeros(self.n_groups, dtype=torch.float32, device=self.dev)
         self.ws_sumsq = torch.empty(K.grad_sumsq_ws_bytes(self.n_desc, self.max_numel) // 4 + 1, dtype=torch.float32,
                                     device=self.dev)
         K.refresh_shadows(self.descs_dev, self.n_desc, self.max_numel)
@@ -206,12 +179,211 @@ class DistillEngine:
     def _ws(self, name, nbytes):
         return self._buf(name, (nbytes // 4 + 16,), torch.float32)
 
-    # ------------------------------------------------------------------ helpers
     def _dropout(self, p, stream_off):
         if p <= 0.0:
             return None
         return K.Dropout(float(p), self.seed ^ 0xD0D0, self.step_ctr.data_ptr(), stream_off)
 
+    def _fusable(self, K_in, N_out):
+        return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0
+
+    # ------------------------------------------------------------------ negatives
+    def _neg_setup(self):
+        """Keys of the negative-sampling graph ``edge_index = stack([col, row])``
+        (src/main.py:156, src/train_teacher_gnn.py:28) in PyG's dense encoding
+        (host, once per engine); ``self._neg_rc`` = (row, col) numpy arrays."""
+        if getattr(self, "_neg_keys", None) is None:
+            r, c = self._neg_rc
+            src, dst = np.asarray(c, np.int64), np.asarray(r, np.int64)   # edge_index = [col, row]
+            m = src != dst
+            src, dst = src[m], dst[m]
+            key = src * (self.N - 1) + dst - (src < dst)
+            self._neg_n_idx = int(key.size)                              # duplicates counted, as PyG does
+            self._neg_keys = torch.from_numpy(np.unique(key)).to(self.dev)
+        return self._neg_keys
+
+    def neg_sample_size(self, num_neg):
+        """int(1.1 * num_neg / prob), prob = 1 - |idx| / (N(N-1)) (PyG 2.2.0)."""
+        self._neg_setup()
+        population = self.N * (self.N - 1)
+        if self._neg_n_idx >= population:
+            return 0
+        prob = 1.0 - self._neg_n_idx / population
+        return int(1.1 * num_neg / prob)
+
+    def _negatives(self, P, P_total, p_offset, neg, dense):
+        """This rank's negative edges: injected, PyG-dense (non-collab) or
+        randint (collab) — src/main.py:205-209, src/train_teacher_gnn.py:49-54.
+        Returns (int32[2, n] view, n, n_total)."""
+        N = self.N
+        if neg is not None:
+            n_neg = int(neg.shape[1])
+            n_neg_total = n_neg if P_total == P else int(round(n_neg * P_total / max(P, 1)))
+            negb = self._buf("neg", (2, max(n_neg, 1)), torch.int32)
+            negb[:, :n_neg].copy_(neg.to(torch.int32))
+            return negb[:, :n_neg], n_neg, n_neg_total
+        if dense:
+            # every rank draws the same global list and keeps its column slice
+            keys = self._neg_setup()
+            ss = self.neg_sample_size(P_total)
+            population = N * (N - 1)
+            M = population if population <= ss else 3 * ss
+            negg = self._buf("neg_all", (2, max(P_total, 1)), torch.int32)
+            cnt = self._buf("neg_count", (1,), torch.int32)
+            ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
+            K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, 14, negg, cnt, ws)
+            n_neg_total = int(cnt.item())
+            lo = min(p_offset, n_neg_total)
+            hi = min(p_offset + P, n_neg_total) if self.world > 1 else n_neg_total
+            return negg[:, lo:hi], hi - lo, n_neg_total
+        negb = self._buf("neg", (2, max(P, 1)), torch.int32)
+        K.randint_pairs(N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)
+        return negb, P, P_total
+
+    def _predictor_forward(self, h, ia, ib, R2, logit, p_drop):
+        """LinkPredictor(h[ia], h[ib]) logits (src/models.py:139-150).  Returns
+        (A0, zacts): the first layer's input operand and hidden activations."""
+        H = h.shape[1]
+        dt, dc = self.dtype, self.dc
+        zacts = []
+        if self.predictor_kind != "mlp":
+            K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
+            return None, zacts
+        zin_ok = (H * h.element_size()) % 16 == 0
+        if zin_ok:
+            # materialise x_i * x_j once: layer-1 forward and its weight-gradient then
+            # stream a plain operand with global_load_lds
+            zin = self._buf("Zin", (R2, H), dt)
+            K.hadamard_rows(h, ia, h, ib, zin)
+            A0 = K.operand(zin)
+        else:
+            A0 = K.operand(h, ia, h, ib)
+        A = A0
+        fused = False
+        for l, lin in enumerate(self.prd):
+            out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
+            last = l == len(self.prd) - 1
+            if last and self._fusable(lin.in_f, lin.out_f) and (A0 is not A or zin_ok):
+                # last hidden layer + Linear(H,1) head in one GEMM (partials per 256 columns)
+                parts = K.head_parts(lin.out_f)
+                hpart = self._buf("hpart", (parts, R2), torch.float32)
+                K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, self.head.weight.data.view(-1),
+                               hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, 5 + l))
+                K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
+                fused = True
+            else:
+                K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
+                          dropout=self._dropout(p_drop, 5 + l))
+            zacts.append(out)
+            A = K.operand(out)
+        if not fused:
+            K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
+                       logit=logit)
+        return A0, zacts
+
+    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop):
+        dt, dc = self.dtype, self.dc
+        if self.predictor_kind != "mlp":
+            return None
+        alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
+        Zl = zacts[-1]
+        Hh = Zl.shape[1]
+        g = self._buf("gP0", (R2, Hh), dt)
+        ws = self._ws("ws_col", K.head_bwd_ws_bytes(R2, max(Hh, 1)))
+        K.head_bwd(dlogit, Zl, R2, Hh, self.head.weight.data.view(-1), True, g, self.head.weight.grad.view(-1),
+                   self.head.bias.grad, ws, alpha=alpha)
+        cur, nxt = "gP0", "gP1"
+        for l in range(len(self.prd) - 1, -1, -1):
+            lin = self.prd[l]
+            gcur = self._buf(cur, (R2, lin.out_f), dt)
+            A_in = K.operand(zacts[l - 1]) if l > 0 else A0
+            wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
+            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
+                      colsum_a=lin.lin.bias.grad)
+            gnext = self._buf(nxt, (R2, lin.in_f), dt)
+            if l > 0:
+                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
+                          act=K.ACT_RELU_BWD, aux=zacts[l - 1], alpha=alpha)
+            else:
+                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
+            cur, nxt = nxt, cur
+        return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
+
+    def _allreduce_and_update(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+        g = self.optimizer.param_groups[0]
+        K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq)
+        b1, b2 = g["betas"]
+        K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
+                    float(b2), float(g["eps"]), self.adam_step)
+
+    # ------------------------------------------------------------------ epoch bookkeeping
+    def begin_epoch(self):
+        self.loss_sum.zero_()
+
+    def end_epoch(self, total_examples):
+        """Returns total_loss / total_examples (src/main.py:141-144); one host sync."""
+        tot = self.loss_sum
+        if self.world > 1:
+            tot = tot.clone()
+            dist.all_reduce(tot, group=self.group)
+        steps = int(self.adam_step.item())
+        for p in self.all_params:
+            self.optimizer.state[p]["step"] = torch.tensor(float(steps))
+        return float(tot.item()) / max(total_examples, 1)
+
+
+class DistillEngine(EngineBase):
+    """Holds every device buffer of the distillation step.
+
+    Parameters mirror ``train_minibatch``'s arguments (src/main.py:52): the
+    student ``model`` (MLP), ``predictor`` (LinkPredictor), the frozen
+    ``teacher_predictor`` and teacher embeddings ``t_h``; ``x`` the node
+    features; ``row``/``col`` the sampler graph (data.adj_t, src/main.py:56);
+    ``optimizer`` a torch.optim.Adam over model+predictor parameters whose
+    hyper-parameters and state this engine uses.
+    """
+
+    def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
+                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None):
+        self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
+        self.args = args
+        self.N = int(num_nodes)
+
+        # ---------------- parameters
+        self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
+        stu = list(model.layers)
+        self.stu = [_Linear(l, self.dtype, need_t=(i > 0), need_c=True) for i, l in enumerate(stu)]
+        for l in self.stu:
+            self._set_shadow(l.lin.weight, l.Wc, l.Wt)
+        stu_params = [p for l in stu for p in (l.weight, l.bias)]
+        prd_params = self._setup_predictor(predictor, args.predictor)
+        self._init_params(stu_params + prd_params, [0] * len(stu_params) + [1] * len(prd_params), optimizer)
+
+        # teacher predictor (frozen; dropout stays live as in the reference, Q3)
+        tl = list(teacher_predictor.lins)
+        self.t_kind = teacher_predictor.predictor
+        self.t_hidden = []
+        for l in tl[:-1]:
+            W = l.weight.data.to(self.dev)
+            self.t_hidden.append((W.to(self.dtype).contiguous(), l.bias.data.to(self.dev).float().contiguous()))
+        self.t_head = (tl[-1].weight.data.to(self.dev).float().reshape(-1).contiguous(),
+                       tl[-1].bias.data.to(self.dev).float().contiguous())
+        self.t_dropout = float(getattr(teacher_predictor, "dropout", 0.0)) if teacher_predictor.training else 0.0
+
+        # ---------------- data
+        self.x = x.to(self.dev).to(self.dtype).contiguous()
+        self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
+        self._neg_rc = (np.asarray(row), np.asarray(col))
+        self._neg_keys = None
+        rowptr, colv = build_sampler_csr(np.asarray(row), np.asarray(col), self.N, rw_sorted)
+        self.rowptr = torch.from_numpy(rowptr).to(self.dev)
+        self.col = torch.from_numpy(colv).to(self.dev)
+
+        self._build_descs()
+
+    # ------------------------------------------------------------------ helpers
     def _rows_index(self, B, C, P2):
         """Predictor-row -> h-row index for the minibatch layout (static per shape)."""
         key = ("rows", B, C, P2)
@@ -297,40 +469,7 @@ class DistillEngine:
 
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
         logit = self._buf("logit", (R2,), torch.float32)
-        zacts = []
-        zin_ok = (H * h.element_size()) % 16 == 0
-        if zin_ok:
-            # materialise x_i * x_j once: layer-1 forward and its weight-gradient then
-            # stream a plain operand with global_load_lds
-            zin = self._buf("Zin", (R2, H), dt)
-            K.hadamard_rows(h, ia, h, ib, zin)
-            A0 = K.operand(zin)
-        else:
-            A0 = K.operand(h, ia, h, ib)
-        A = A0
-        fused = False
-        for l, lin in enumerate(self.prd):
-            out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
-            last = l == len(self.prd) - 1
-            if last and self._fusable(lin.in_f, lin.out_f) and (A0 is not A or zin_ok):
-                # last hidden layer + Linear(H,1) head in one GEMM (partials per 256 columns)
-                parts = K.head_parts(lin.out_f)
-                hpart = self._buf("hpart", (parts, R2), torch.float32)
-                K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, self.head.weight.data.view(-1),
-                               hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, 5 + l))
-                K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
-                fused = True
-            else:
-                K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
-                          dropout=self._dropout(p_drop, 5 + l))
-            zacts.append(out)
-            A = K.operand(out)
-        if self.predictor_kind == "mlp":
-            if not fused:
-                K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
-                           logit=logit)
-        else:
-            K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
+        A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop)
 
         # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
         t_r = self._buf("t_r", (B * C,), torch.float32)
@@ -358,29 +497,6 @@ class DistillEngine:
         K.increment(self.step_ctr)
 
     # ------------------------------------------------------------------ full-batch step
-    def _neg_setup(self):
-        """Keys of the negative-sampling graph edge_index = stack([col, row])
-        (src/main.py:156) in PyG's dense encoding (host, once per engine)."""
-        if getattr(self, "_neg_keys", None) is None:
-            r = self._row_np_for_neg
-            c = self._col_np_for_neg
-            src, dst = c.astype(np.int64), r.astype(np.int64)      # edge_index = [col, row]
-            m = src != dst
-            src, dst = src[m], dst[m]
-            key = src * (self.N - 1) + dst - (src < dst)
-            self._neg_n_idx = int(key.size)                         # duplicates counted, as PyG does
-            self._neg_keys = torch.from_numpy(np.unique(key)).to(self.dev)
-        return self._neg_keys
-
-    def neg_sample_size(self, num_neg):
-        """int(1.1 * num_neg / prob), prob = 1 - |idx| / (N(N-1)) (PyG 2.2.0)."""
-        self._neg_setup()
-        population = self.N * (self.N - 1)
-        if self._neg_n_idx >= population:
-            return 0
-        prob = 1.0 - self._neg_n_idx / population
-        return int(1.1 * num_neg / prob)
-
     def step_fullbatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
                        samples=None, neg=None, dense_negatives=True):
         """One link batch of ``train`` (src/main.py:167-235): the student MLP runs
@@ -420,29 +536,7 @@ class DistillEngine:
                 K.context_sampler(self.rowptr, self.col, N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                   self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
         # ---- negatives (src/main.py:205-209)
-        if neg is not None:
-            n_neg = int(neg.shape[1])
-            n_neg_total = n_neg if P_total == P else int(round(n_neg * P_total / max(P, 1)))
-            negb = self._buf("neg", (2, max(n_neg, 1)), torch.int32)
-            negb[:, :n_neg].copy_(neg.to(torch.int32))
-        elif dense_negatives:
-            keys = self._neg_setup()
-            ss = self.neg_sample_size(P_total)
-            population = N * (N - 1)
-            M = population if population <= ss else 3 * ss
-            negg = self._buf("neg_all", (2, max(P_total, 1)), torch.int32)
-            cnt = self._buf("neg_count", (1,), torch.int32)
-            ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
-            K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, 14, negg, cnt, ws)
-            n_neg_total = int(cnt.item())
-            lo = min(p_offset, n_neg_total)
-            hi = min(p_offset + P, n_neg_total) if self.world > 1 else n_neg_total
-            n_neg = hi - lo
-            negb = negg[:, lo:hi]
-        else:
-            n_neg, n_neg_total = P, P_total
-            negb = self._buf("neg", (2, max(P, 1)), torch.int32)
-            K.randint_pairs(N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)
+        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
         n_lab = P + n_neg
         n_lab_total = P_total + n_neg_total
         BC = Bc * C
@@ -466,27 +560,7 @@ class DistillEngine:
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
-        zacts = []
-        zin_ok = (H * h.element_size()) % 16 == 0
-        if self.predictor_kind == "mlp":
-            if zin_ok:
-                zin = self._buf("Zin", (R2, H), dt)
-                K.hadamard_rows(h, ia, h, ib, zin)
-                A0 = K.operand(zin)
-            else:
-                A0 = K.operand(h, ia, h, ib)
-            A = A0
-            for l, lin in enumerate(self.prd):
-                out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
-                K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
-                          dropout=self._dropout(p_drop, 5 + l))
-                zacts.append(out)
-                A = K.operand(out)
-            K.head_fwd(zacts[-1], R2, zacts[-1].shape[1], self.head.weight.data.view(-1), self.head.bias.data,
-                       logit=logit)
-        else:
-            A0 = None
-            K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
+        A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop)
 
         # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215)
         R_t = R2 if float(a.KD_LM) != 0.0 else BC
@@ -533,9 +607,6 @@ class DistillEngine:
         K.increment(self.step_ctr)
         return n_neg
 
-    def _fusable(self, K_in, N_out):
-        return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0
-
     def capture_minibatch(self, anchors, link_ids, pairs, **kw):
         """Capture one step_minibatch into a hipGraph (torch.cuda.CUDAGraph).
 
@@ -581,34 +652,6 @@ class DistillEngine:
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop):
-        dt, dc = self.dtype, self.dc
-        if self.predictor_kind != "mlp":
-            return None
-        alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
-        Zl = zacts[-1]
-        Hh = Zl.shape[1]
-        g = self._buf("gP0", (R2, Hh), dt)
-        ws = self._ws("ws_col", K.head_bwd_ws_bytes(R2, max(Hh, 1)))
-        K.head_bwd(dlogit, Zl, R2, Hh, self.head.weight.data.view(-1), True, g, self.head.weight.grad.view(-1),
-                   self.head.bias.grad, ws, alpha=alpha)
-        cur, nxt = "gP0", "gP1"
-        for l in range(len(self.prd) - 1, -1, -1):
-            lin = self.prd[l]
-            gcur = self._buf(cur, (R2, lin.out_f), dt)
-            A_in = K.operand(zacts[l - 1]) if l > 0 else A0
-            wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
-            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
-                      colsum_a=lin.lin.bias.grad)
-            gnext = self._buf(nxt, (R2, lin.in_f), dt)
-            if l > 0:
-                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
-                          act=K.ACT_RELU_BWD, aux=zacts[l - 1], alpha=alpha)
-            else:
-                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
-            cur, nxt = nxt, cur
-        return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
-
     def _student_backward(self, dh, R1, target, acts, p_drop):
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
@@ -625,27 +668,3 @@ class DistillEngine:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
                           act=K.ACT_RELU_BWD, aux=acts[l - 1], alpha=alpha)
                 cur, nxt = nxt, cur
-
-    def _allreduce_and_update(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
-        g = self.optimizer.param_groups[0]
-        K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, 2, self.sumsq, self.ws_sumsq)
-        b1, b2 = g["betas"]
-        K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
-                    float(b2), float(g["eps"]), self.adam_step)
-
-    # ------------------------------------------------------------------ epoch bookkeeping
-    def begin_epoch(self):
-        self.loss_sum.zero_()
-
-    def end_epoch(self, total_examples):
-        """Returns total_loss / total_examples (src/main.py:141-144); one host sync."""
-        tot = self.loss_sum
-        if self.world > 1:
-            tot = tot.clone()
-            dist.all_reduce(tot, group=self.group)
-        steps = int(self.adam_step.item())
-        for p in self.all_params:
-            self.optimizer.state[p]["step"] = torch.tensor(float(steps))
-        return float(tot.item()) / max(total_examples, 1)

@@ -36,7 +36,7 @@ class Dropout(C.Structure):
 class TensorDesc(C.Structure):
     _fields_ = [("param", c_vp), ("grad", c_vp), ("exp_avg", c_vp), ("exp_avg_sq", c_vp), ("shadow", c_vp),
                 ("shadow_t", c_vp), ("numel", c_i64), ("rows", c_i64), ("cols", c_i64), ("group", C.c_int32),
-                ("shadow_dtype", C.c_int32)]
+                ("shadow_dtype", C.c_int32), ("shadow_ld", c_i64), ("shadow_t_ld", c_i64)]
 
 
 _SIGS = {
@@ -75,6 +75,9 @@ _SIGS = {
     "llp_kd_terms_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_kd_terms": (c_int, [c_int, c_i64, c_vp, c_vp, c_f64, c_f32, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
                              c_f64, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "llp_hits_at_k": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp]),
+    "llp_auc_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_auc": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "llp_csr_aggregate": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_int, c_vp]),
     "llp_grad_sumsq_workspace_bytes": (c_i64, [c_int, c_i64]),
     "llp_grad_sumsq": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
@@ -86,6 +89,8 @@ _SIGS = {
     "llp_zero": (c_int, [c_vp, c_i64, c_vp]),
     "llp_hadamard_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_relu_bwd": (c_int, [c_int, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
+    "llp_act_2d": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, C.POINTER(Dropout), c_vp]),
+    "llp_relu_bwd_2d": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp]),
     "llp_transpose": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "llp_mul": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_row_scale": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
@@ -314,6 +319,46 @@ def kd_terms(terms, ws, n_lab=0, out_logit=None, t_prob_lab=None, n_lab_total=1.
                          ptr(idx_rm), float(B_rm_total), float(w_rm), float(loss_scale), ptr(dlogit_lab), ptr(dh),
                          dh.stride(0) if dh is not None else 0, terms.data_ptr(), ws.data_ptr(),
                          ws.numel() * ws.element_size(), stream_ptr()), "llp_kd_terms")
+
+
+def act_2d(x, y, act=ACT_RELU, dropout: Dropout | None = None):
+    """y = dropout(act(x)) on (strided) 2-D views of equal shape."""
+    L = lib()
+    check(L.llp_act_2d(dtype_code(x.dtype), x.shape[0], x.shape[1], x.data_ptr(), x.stride(0), y.data_ptr(),
+                       y.stride(0), act, C.byref(dropout) if dropout is not None else None, stream_ptr()),
+          "llp_act_2d")
+
+
+def relu_bwd_2d(gy, y, alpha, out):
+    L = lib()
+    check(L.llp_relu_bwd_2d(dtype_code(gy.dtype), gy.shape[0], gy.shape[1], gy.data_ptr(), gy.stride(0), y.data_ptr(),
+                            y.stride(0), float(alpha), out.data_ptr(), out.stride(0), stream_ptr()), "llp_relu_bwd_2d")
+
+
+def hits_at_k(pos, neg, Ks):
+    """Hits@K for every K in ``Ks`` (device computation, one sync); list of floats."""
+    L = lib()
+    Ks = [int(k) for k in Ks]
+    if any(k <= 0 for k in Ks):
+        raise ValueError("K must be positive")
+    kd = torch.tensor(Ks, dtype=torch.int32).to(pos.device)
+    out = torch.empty(len(Ks), dtype=torch.float64, device=pos.device)
+    pos = pos.float().contiguous()
+    neg = neg.float().contiguous()
+    check(L.llp_hits_at_k(pos.data_ptr(), pos.numel(), neg.data_ptr(), neg.numel(), kd.data_ptr(), len(Ks),
+                          out.data_ptr(), stream_ptr()), "llp_hits_at_k")
+    return out.tolist()
+
+
+def auc(pos, neg):
+    L = lib()
+    pos = pos.float().contiguous()
+    neg = neg.float().contiguous()
+    ws = torch.empty(L.llp_auc_workspace_bytes(pos.numel(), neg.numel()), dtype=torch.uint8, device=pos.device)
+    out = torch.empty(1, dtype=torch.float64, device=pos.device)
+    check(L.llp_auc(pos.data_ptr(), pos.numel(), neg.data_ptr(), neg.numel(), out.data_ptr(), ws.data_ptr(),
+                    ws.numel(), stream_ptr()), "llp_auc")
+    return float(out.item())
 
 
 def csr_aggregate(n_rows, F, rowptr, col, x, inv_deg, mode, out, accumulate=False):

@@ -112,6 +112,37 @@ def linear(x, weight, bias=None, relu=False, dropout=0.0, training=False, x2=Non
     return y.reshape(*shp[:-1], weight.shape[0])
 
 
+class _ReluDropout(torch.autograd.Function):
+    """F.dropout(F.relu(x)) between SAGE layers (src/models.py:117-118)."""
+
+    @staticmethod
+    def forward(ctx, x, p, training):
+        y = torch.empty_like(x)
+        drop = None
+        if training and p > 0:
+            ctr = _dropout_state(x.device)
+            drop = K.Dropout(float(p), _dropout_seed(), ctr.data_ptr(), 4)
+        K.act_2d(x, y, act=K.ACT_RELU, dropout=drop)
+        if drop is not None:
+            K.increment(_dropout_state(x.device))
+        ctx.save_for_backward(y)
+        ctx.alpha = 1.0 / (1.0 - p) if (training and p > 0) else 1.0
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        gx = torch.empty_like(y)
+        K.relu_bwd_2d(gy.contiguous(), y, ctx.alpha, gx)
+        return gx, None, None
+
+
+def relu_dropout(x, p=0.0, training=False):
+    _require_cuda(x)
+    x2d = _row2d(x)
+    return _ReluDropout.apply(x2d, float(p), bool(training)).reshape(x.shape)
+
+
 class _Head(torch.autograd.Function):
     """sigmoid(z w + b) (w = None: sigmoid(sum(z * z2))) — LinkPredictor's tail."""
 

@@ -1,0 +1,218 @@
+"""MI355X GraphSAGE teacher engine: one link batch of the teacher's ``train``
+(src/train_teacher_gnn.py:21-73) — full-graph SAGE encoder forward/backward,
+LinkPredictor on h[train_edges], BCE, clip_grad_norm_ per module, Adam — as a
+fixed sequence of hand-written gfx950 kernels.
+
+Encoder layer l (in F, out O), both conv flavours the reference uses:
+
+  SAGEConv (PyG 2.2.0, aggr='mean', src/train_teacher_gnn.py:381-383)
+      out = mean_j x_j . W_l^T + b + x . W_r^T
+      HBM layout: XA_l = [agg | x] (N x 2F, one buffer): the CSR aggregate
+      writes the left half, the previous layer's GEMM epilogue (bias, ReLU,
+      dropout) writes x into the right half, and ONE K-concatenated MFMA GEMM
+      against Wcat = [W_l | W_r] (O x 2F) produces the layer.
+  SAGEConv_updated (src/sageconv_updated.py:65-81, coauthor-physics)
+      out = mean_j (x_j . W_l^T + b) + x . W_r^T
+      ONE GEMM against Wst = [W_l ; W_r] (2O x F) gives [U | R] (N x 2O); the
+      aggregate of U accumulates into R in place.
+
+Backward (both flavours): with dOut the layer's output gradient and
+G = mean-backward(dOut) over the transposed CSR, dX = [G | dOut] . [W_l^T | W_r^T]
+is ONE K-concatenated GEMM whose epilogue applies the previous layer's
+ReLU/dropout mask; weight gradients are TN GEMMs with the bias gradient fused.
+The weight copies (Wcat / Wst and the shared [W_l^T | W_r^T]) are shadows the
+Adam kernel refreshes through descriptor leading dimensions.
+
+Aggregation follows PyG: messages flow edge_index[0] -> edge_index[1],
+duplicates counted, isolated nodes get 0.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import llp_hip as K
+from llp_engine import EngineBase
+from llp_sage import Graph, SAGEConv_updated
+
+
+class TeacherEngine(EngineBase):
+    """``model``: models.SAGE (convs of SAGEConv or SAGEConv_updated, root_weight,
+    norm_type 'none'); ``predictor``: LinkPredictor; ``x``: node features;
+    ``edge_index``: the message-passing graph (data.adj_t / data.edge_index,
+    src/train_teacher_gnn.py:23-27,43-46); ``optimizer``: Adam over
+    model.parameters() + predictor.parameters()."""
+
+    def __init__(self, model, predictor, x, edge_index, num_nodes, optimizer, dtype="fp32", seed=0, group=None,
+                 device=None):
+        self._init_device(x.device, device, dtype, seed, group, "TeacherEngine")
+        self.N = int(num_nodes)
+        N = self.N
+        dt = self.dtype
+        self.model, self.predictor = model, predictor
+        if getattr(model, "norm_type", "none") != "none":
+            raise NotImplementedError("SAGE norm_type other than 'none' (not used by the reference scripts)")
+        self.convs = list(model.convs)
+        self.updated = isinstance(self.convs[0], SAGEConv_updated)
+        if any(isinstance(c, SAGEConv_updated) != self.updated or not c.root_weight for c in self.convs):
+            raise NotImplementedError("all convs of one flavour, with root_weight")
+        self.p_drop = float(model.dropout)
+        ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
+        self.graph = Graph(ei, N, self.dev)
+        self._neg_rc = (ei[0], ei[1])        # row, col = data.adj_t (src/train_teacher_gnn.py:23)
+        self.num_edges = int(ei.shape[1])
+
+        # ---------------- per-layer weights and shadows
+        self.layers = []
+        for l, conv in enumerate(self.convs):
+            Wl, bl, Wr = conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight
+            O, F = Wl.shape
+            L = dict(F=F, O=O, conv=conv)
+            WT = torch.empty(F, 2 * O, dtype=dt, device=self.dev)          # [W_l^T | W_r^T]
+            if self.updated:
+                Wst = torch.empty(2 * O, F, dtype=dt, device=self.dev)      # [W_l ; W_r]
+                self._set_shadow(Wl, Wst[:O], WT[:, :O], 0, 2 * O)
+                self._set_shadow(Wr, Wst[O:], WT[:, O:], 0, 2 * O)
+                bias2 = torch.zeros(2 * O, dtype=torch.float32, device=self.dev)
+                bias2[:O].copy_(bl.data)
+                bl.data = bias2[:O]                                         # the module's bias now lives here
+                L.update(Wf=Wst, bias=bias2)
+            else:
+                Wcat = torch.empty(O, 2 * F, dtype=dt, device=self.dev)     # [W_l | W_r]
+                self._set_shadow(Wl, Wcat[:, :F], WT[:, :O], 2 * F, 2 * O)
+                self._set_shadow(Wr, Wcat[:, F:], WT[:, O:], 2 * F, 2 * O)
+                L.update(Wf=Wcat, bias=bl.data)
+            L["WT"] = WT
+            self.layers.append(L)
+        enc_params = [p for p in model.parameters()]
+        prd_params = self._setup_predictor(predictor, predictor.predictor)
+        self.pred_drop = float(predictor.dropout)
+        self._init_params(enc_params + prd_params, [0] * len(enc_params) + [1] * len(prd_params), optimizer)
+
+        # ---------------- activations (HBM-resident for the whole run)
+        x = x.to(self.dev)
+        for l, L in enumerate(self.layers):
+            F, O = L["F"], L["O"]
+            if self.updated:
+                L["X"] = x.to(dt).contiguous() if l == 0 else torch.empty(N, F, dtype=dt, device=self.dev)
+                L["YY"] = torch.empty(N, 2 * O, dtype=dt, device=self.dev)
+            else:
+                XA = torch.empty(N, 2 * F, dtype=dt, device=self.dev)
+                if l == 0:
+                    XA[:, F:].copy_(x.to(dt))
+                L["XA"] = XA
+                L["X"] = XA[:, F:]
+            L["G"] = torch.empty(N, 2 * O, dtype=dt, device=self.dev)        # [mean-bwd(dOut) | dOut]
+        self.out_dim = self.layers[-1]["O"]
+        self.h = torch.empty(N, self.out_dim, dtype=dt, device=self.dev)
+        self._build_descs()
+
+    # ------------------------------------------------------------------ encoder
+    def _encode(self, training: bool):
+        """SAGE.forward (src/models.py:110-119): conv, ReLU, dropout between layers."""
+        g = self.graph
+        dc = self.dc
+        N = self.N
+        nl = len(self.layers)
+        for l, L in enumerate(self.layers):
+            F, O = L["F"], L["O"]
+            last = l == nl - 1
+            drop = None if (last or not training) else self._dropout(self.p_drop, 1 + l)
+            act = K.ACT_NONE if last else K.ACT_RELU
+            nxt = None if last else self.layers[l + 1]
+            if self.updated:
+                YY = L["YY"]
+                K.gemm_nt(K.operand(L["X"]), K.operand(L["Wf"]), N, 2 * O, F, YY, dc, bias=L["bias"])
+                K.csr_aggregate(N, O, g.rowptr, g.col, YY[:, :O], None, 0, YY[:, O:], accumulate=True)
+                K.act_2d(YY[:, O:], self.h if last else nxt["X"], act=act, dropout=drop)
+            else:
+                XA = L["XA"]
+                K.csr_aggregate(N, F, g.rowptr, g.col, XA[:, F:], None, 0, XA[:, :F])
+                out = self.h if last else nxt["X"]
+                K.gemm_nt(K.operand(XA), K.operand(L["Wf"]), N, O, 2 * F, out, dc, bias=L["bias"], act=act,
+                          dropout=drop)
+        return self.h
+
+    def _encode_backward(self, dh32):
+        """Backward of _encode from d(loss)/dh (f32 [N, O])."""
+        g = self.graph
+        dt, dc = self.dtype, self.dc
+        N = self.N
+        alpha = 1.0 / (1.0 - self.p_drop) if self.p_drop > 0 else 1.0
+        nl = len(self.layers)
+        last = self.layers[-1]
+        O = last["O"]
+        Gl = last["G"]
+        if dt == torch.float32:
+            K.act_2d(dh32, Gl[:, O:], act=K.ACT_NONE)
+        else:
+            dh = self._buf("dh_c", (N, O), dt)
+            K.convert(dh32, dh)
+            K.act_2d(dh, Gl[:, O:], act=K.ACT_NONE)
+        for l in range(nl - 1, -1, -1):
+            L = self.layers[l]
+            F, O = L["F"], L["O"]
+            G = L["G"]
+            dOut = G[:, O:]
+            conv = L["conv"]
+            # G = mean-backward(dOut) over the transposed CSR (scale 1/deg of the destination)
+            K.csr_aggregate(N, O, g.rowptr_t, g.col_t, dOut, g.inv_deg, 1, G[:, :O])
+            wsb = K.gemm_tn_ws_bytes(dc, N, O, F)
+            ws = self._ws("ws_tn", wsb)
+            if self.updated:
+                # U = x W_l^T + b is aggregated: dW_l = G^T x, db = colsum(G); dW_r = dOut^T x
+                K.gemm_tn(K.operand(G[:, :O]), K.operand(L["X"]), N, O, F, conv.lin_l.weight.grad, dc, ws,
+                          colsum_a=conv.lin_l.bias.grad)
+            else:
+                # dW_l = dOut^T agg(x), db = colsum(dOut); dW_r = dOut^T x
+                K.gemm_tn(K.operand(dOut), K.operand(L["XA"][:, :F]), N, O, F, conv.lin_l.weight.grad, dc, ws,
+                          colsum_a=conv.lin_l.bias.grad)
+            K.gemm_tn(K.operand(dOut), K.operand(L["X"]), N, O, F, conv.lin_r.weight.grad, dc, ws)
+            if l > 0:
+                # dX = [G | dOut] . [W_l^T | W_r^T]^T, ReLU/dropout mask of layer l-1 in the epilogue,
+                # written straight into layer l-1's output-gradient slot
+                prev = self.layers[l - 1]
+                K.gemm_nt(K.operand(G), K.operand(L["WT"]), N, F, 2 * O, prev["G"][:, prev["O"]:], dc,
+                          act=K.ACT_RELU_BWD, aux=L["X"], alpha=alpha)
+
+    # ------------------------------------------------------------------ the step
+    def step(self, link_ids, pairs, p_offset=0, P_total=None, neg=None, dense_negatives=True):
+        """One batch of train() (src/train_teacher_gnn.py:33-71).
+
+        link_ids int32[P]   this rank's slice of the DataLoader permutation
+        pairs    int32[E,2] pos_train_edge (src/train_teacher_gnn.py:25,28)
+        dense_negatives: PyG dense sampler (non-collab) else randint (collab).
+        Returns the number of negatives used."""
+        P = int(link_ids.numel())
+        P_total = P if P_total is None else int(P_total)
+        N, O = self.N, self.out_dim
+        h = self._encode(training=True)
+        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+        R = P + n_neg
+        ia = self._buf("t_ia", (max(R, 1),), torch.int32)[:R]
+        ib = self._buf("t_ib", (max(R, 1),), torch.int32)[:R]
+        K.fullbatch_pairs(0, 0, None, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
+        logit = self._buf("logit", (R,), torch.float32)
+        A0, zacts = self._predictor_forward(h, ia, ib, R, logit, self.pred_drop)
+        dlogit = self._buf("dlogit", (R,), torch.float32)
+        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(0, R))
+        # BCE only (src/train_teacher_gnn.py:56-58)
+        K.llp_loss(0, 1, None, None, R, P, logit, 1, P_total + n_neg_total, 0.0, 1.0, 1.0, 0.0, 0.0, None, dlogit,
+                   self.terms, ws)
+        dh32 = self._buf("dh32", (N, O), torch.float32)
+        dh32.zero_()
+        dZ0 = self._predictor_backward(dlogit, R, A0, zacts, self.pred_drop)
+        if self.predictor_kind == "mlp":
+            K.hadamard_bwd_scatter(R, O, dZ0, ia, ib, h, dh32)
+        else:
+            K.hadamard_bwd_scatter(R, O, None, ia, ib, h, dh32, drow=dlogit)
+        self._encode_backward(dh32)
+        self._allreduce_and_update()
+        K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
+        K.increment(self.step_ctr)
+        return n_neg
+
+    @torch.no_grad()
+    def embed(self):
+        """model(x, adj_t) in eval mode (src/train_teacher_gnn.py:87) -> f32 [N, O]."""
+        return self._encode(training=False).float()

@@ -50,6 +50,37 @@ class MLP(nn.Module):
         return h
 
 
+class SAGE(nn.Module):
+    """src/models.py:82-119: conv_layer is llp_sage.SAGEConv (PyG SAGEConv
+    semantics) or llp_sage.SAGEConv_updated.  The training hot path is
+    llp_teacher.TeacherEngine; this module is the eval / autograd surface."""
+
+    def __init__(self, data_name, in_channels, hidden_channels, out_channels, num_layers, dropout, conv_layer,
+                 norm_type="none"):
+        super().__init__()
+        if norm_type != "none":
+            raise NotImplementedError("SAGE norm_type other than 'none' (not used by the reference scripts)")
+        self.data_name = data_name
+        self.norm_type = norm_type
+        self.convs = nn.ModuleList()
+        self.norms = nn.ModuleList()
+        self.convs.append(conv_layer(in_channels, hidden_channels))
+        for _ in range(num_layers - 2):
+            self.convs.append(conv_layer(hidden_channels, hidden_channels))
+        self.convs.append(conv_layer(hidden_channels, out_channels))
+        self.dropout = dropout
+
+    def reset_parameters(self):
+        for conv in self.convs:
+            conv.reset_parameters()
+
+    def forward(self, x, adj_t):
+        for conv in self.convs[:-1]:
+            x = conv(x, adj_t)
+            x = ops.relu_dropout(x, self.dropout, self.training)
+        return self.convs[-1](x, adj_t)
+
+
 class LinkPredictor(nn.Module):
     def __init__(self, predictor, in_channels, hidden_channels, out_channels, num_layers, dropout):
         super().__init__()

@@ -385,8 +385,186 @@ def run_model_case(name, ref_models, seed):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
+# ----------------------------------------------------------------------------
+# Teacher: src/train_teacher_gnn.py:21-73 (train) with the reference's own
+# SAGE (src/models.py:82-119) and SAGEConv_updated (src/sageconv_updated.py).
+# PyG pieces they build on are restated: SAGEConv -> oracle.sage_conv,
+# MessagePassing.propagate(aggr='mean') -> oracle.sage_mean_aggregate,
+# torch_geometric Linear -> nn.Linear (weights are overwritten anyway).
+# ----------------------------------------------------------------------------
+class _RestatedSAGEConv(nn.Module):
+    def __init__(self, in_channels, out_channels, normalize=False, root_weight=True, bias=True, **kw):
+        super().__init__()
+        self.lin_l = nn.Linear(in_channels, out_channels, bias=bias)
+        self.lin_r = nn.Linear(in_channels, out_channels, bias=False)
+
+    def reset_parameters(self):
+        self.lin_l.reset_parameters()
+        self.lin_r.reset_parameters()
+
+    def forward(self, x, edge_index):
+        return O.sage_conv(x, edge_index, self.lin_l.weight, self.lin_l.bias, self.lin_r.weight)
+
+
+class _MessagePassing(nn.Module):
+    def __init__(self, aggr="mean", **kw):
+        super().__init__()
+        assert aggr == "mean"
+        self.aggr = aggr
+
+    def propagate(self, edge_index, x, size=None):
+        xs = x[0]
+        return O.sage_mean_aggregate(self.message(xs[edge_index[0]]), torch.arange(edge_index.size(1)),
+                                     edge_index[1], xs.size(0))
+
+
+def load_reference_sage():
+    """Exec src/models.py and src/sageconv_updated.py over restated PyG stubs."""
+    stubs = {}
+    pyg = types.ModuleType("torch_geometric")
+    pyg_nn = types.ModuleType("torch_geometric.nn")
+    for n in ("GCNConv", "GATConv", "APPNP"):
+        setattr(pyg_nn, n, type(n, (), {}))
+    pyg_nn.SAGEConv = _RestatedSAGEConv
+    conv = types.ModuleType("torch_geometric.nn.conv")
+    conv.MessagePassing = _MessagePassing
+    dense = types.ModuleType("torch_geometric.nn.dense")
+    lin = types.ModuleType("torch_geometric.nn.dense.linear")
+    lin.Linear = nn.Linear
+    typ = types.ModuleType("torch_geometric.typing")
+    typ.OptPairTensor = typ.Adj = typ.Size = object
+    tsp = types.ModuleType("torch_sparse")
+    tsp.SparseTensor = type("SparseTensor", (), {})
+    tsp.matmul = None
+    pyg.nn = pyg_nn
+    for k, v in {"torch_geometric": pyg, "torch_geometric.nn": pyg_nn, "torch_geometric.nn.conv": conv,
+                 "torch_geometric.nn.dense": dense, "torch_geometric.nn.dense.linear": lin,
+                 "torch_geometric.typing": typ, "torch_sparse": tsp}.items():
+        stubs[k] = sys.modules.get(k)
+        sys.modules[k] = v
+    try:
+        mods = types.ModuleType("ref_models_sage")
+        exec(compile(_compile_file(os.path.join(REF, "models.py")), os.path.join(REF, "models.py"), "exec"),
+             mods.__dict__)
+        upd = types.ModuleType("ref_sageconv_updated")
+        p = os.path.join(REF, "sageconv_updated.py")
+        exec(compile(_compile_file(p), p, "exec"), upd.__dict__)
+    finally:
+        for k, v in stubs.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return mods, upd.SAGEConv_updated
+
+
+def load_reference_teacher_train(rec: Recorder, neg_seed: int):
+    src = _compile_file(os.path.join(REF, "train_teacher_gnn.py"))
+    tree = ast.parse(src)
+    body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "train"]
+    mod_ast = ast.Module(body=body, type_ignores=[])
+    ast.fix_missing_locations(mod_ast)
+    neg_rng = random.Random(neg_seed)
+
+    def negative_sampling(edge_index, num_nodes=None, num_neg_samples=None, method="sparse"):
+        assert method == "dense"
+        out = O.negative_sampling_dense(edge_index, num_nodes, num_neg_samples, rng=neg_rng)
+        rec.add("negative_sampling", out)
+        return out
+
+    class RecDataLoader:
+        def __init__(self, *a, **k):
+            self.dl = torch.utils.data.DataLoader(*a, **k)
+
+        def __iter__(self):
+            for b in self.dl:
+                rec.add("perm", b)
+                yield b
+
+    class NNProxy(types.ModuleType):
+        def __getattr__(self, name):
+            return getattr(nn, name)
+
+    nproxy = NNProxy("nn")
+
+    class RecBCELoss(nn.BCELoss):
+        def forward(self, a, b):
+            out = super().forward(a, b)
+            rec.add("bce", out)
+            return out
+
+    nproxy.BCELoss = RecBCELoss
+
+    class TorchProxy(types.ModuleType):
+        def __getattr__(self, name):
+            return getattr(torch, name)
+
+    tproxy = TorchProxy("torch")
+
+    def randint(*a, **k):
+        out = torch.randint(*a, **k)
+        rec.add("randint", out)
+        return out
+
+    tproxy.randint = randint
+    ns = dict(torch=tproxy, nn=nproxy, F=F, DataLoader=RecDataLoader, negative_sampling=negative_sampling)
+    exec(compile(mod_ast, os.path.join(REF, "train_teacher_gnn.py"), "exec"), ns)
+    return ns["train"]
+
+
+def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, dataset="cora", epochs=2):
+    rec = Recorder()
+    ref_mods, ref_updated = load_reference_sage()
+    train = load_reference_teacher_train(rec, neg_seed=seed + 31)
+    torch.manual_seed(seed)
+    pairs, ei = synth_graph(N, E_und, seed, interleave=False)
+    x = torch.randn(N, F_) * 0.5
+    conv_layer = ref_updated if updated else ref_mods.SAGE.__init__.__globals__["SAGEConv"]
+    model = ref_mods.SAGE(dataset, F_, H, H, L, 0.0, conv_layer)
+    predictor = ref_mods.LinkPredictor("mlp", H, H, 1, 2, 0.0)
+    init_enc = {k: v.clone() for k, v in model.state_dict().items()}
+    init_pred = {k: v.clone() for k, v in predictor.state_dict().items()}
+    opt = RecAdam(list(model.parameters()) + list(predictor.parameters()), rec, lr=0.005)
+    if transductive == "transductive":
+        # non-collab: adj_t = split_edge['train']['edge'].t() (one direction, src/train_teacher_gnn.py:317-318)
+        data = types.SimpleNamespace(x=x, adj_t=pairs.t().contiguous())
+        split_edge = {"train": {"edge": pairs}}
+    else:
+        data = types.SimpleNamespace(x=x, edge_index=ei)
+        split_edge = None
+    losses = [train(model, predictor, data, split_edge, opt, bs, "sage", dataset, transductive)
+              for _ in range(epochs)]
+    mp_edges = data.adj_t if transductive == "transductive" else ei
+    out = dict(N=N, F=F_, H=H, L=L, x=x.numpy(), edge_index=mp_edges.numpy(), train_pairs=pairs.numpy(),
+               epoch_losses=np.array(losses, np.float64), updated=np.array(int(updated)), batch_size=np.array(bs),
+               transductive=np.array(transductive), dataset=np.array(dataset))
+    for k, v in init_enc.items():
+        out[f"init/enc/{k}"] = v.numpy()
+    for k, v in init_pred.items():
+        out[f"init/pred/{k}"] = v.numpy()
+    for k, v in model.state_dict().items():
+        out[f"final/enc/{k}"] = v.numpy()
+    for k, v in predictor.state_dict().items():
+        out[f"final/pred/{k}"] = v.numpy()
+    out["enc_keys"] = np.array(list(init_enc.keys()))
+    out["pred_keys"] = np.array(list(init_pred.keys()))
+    _dump_log(out, rec, kind_order="teacher", args=None)
+    # eval-mode embedding after training (src/train_teacher_gnn.py:87): the saved teacher features
+    model.eval()
+    with torch.no_grad():
+        out["h_eval"] = model(x, mp_edges).numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "steps:", out["nsteps"], "epoch losses:", losses)
+
+
 def main():
     ref_models = load_reference_models()
+    run_teacher_case("teacher_sage_small", N=110, F_=24, H=64, L=2, E_und=400, bs=160, updated=False,
+                     transductive="transductive", seed=7)
+    run_teacher_case("teacher_sage3_collab_small", N=130, F_=16, H=32, L=3, E_und=500, bs=200, updated=False,
+                     transductive="transductive", seed=9, dataset="collab")
+    run_teacher_case("teacher_updated_production_small", N=100, F_=48, H=64, L=2, E_und=350, bs=256,
+                     updated=True, transductive="production", seed=8)
     run_kl_rank_case("kl_loss", 1)
     run_model_case("models_fwd_bwd", ref_models, 2)
     # collab-style minibatch path (main.py:52-144), C = 3*3*(1+3) = 36 like the

@@ -100,5 +100,35 @@ def load_case(name):
     return case
 
 
+def load_teacher_case(name):
+    """Fixtures of the reference teacher's train() (src/train_teacher_gnn.py:21-73)."""
+    z = load(name)
+    enc_keys = [str(k) for k in z["enc_keys"]]
+    pred_keys = [str(k) for k in z["pred_keys"]]
+    c = types.SimpleNamespace(
+        name=name, N=int(z["N"]), F=int(z["F"]), H=int(z["H"]), L=int(z["L"]), updated=bool(int(z["updated"])),
+        batch_size=int(z["batch_size"]), transductive=str(z["transductive"]), dataset=str(z["dataset"]),
+        x=torch.from_numpy(z["x"].copy()), edge_index=torch.from_numpy(z["edge_index"].copy()),
+        train_pairs=torch.from_numpy(z["train_pairs"].copy()), epoch_losses=z["epoch_losses"],
+        enc0=_params(z, "init/enc", enc_keys), pred0=_params(z, "init/pred", pred_keys),
+        enc_final=_params(z, "final/enc", enc_keys), pred_final=_params(z, "final/pred", pred_keys),
+        h_eval=torch.from_numpy(z["h_eval"].copy()), steps=[])
+    c.pos_train_edge = c.train_pairs if c.transductive == "transductive" else c.edge_index.t()
+    ng = len(c.enc0) + len(c.pred0)
+    for s in range(int(z["nsteps"])):
+        st = types.SimpleNamespace()
+        st.link_perm = torch.from_numpy(z[f"perm/{s}"].copy())
+        st.edge = c.pos_train_edge[st.link_perm].t()
+        if f"step{s}/neg_edge" in z.files:
+            st.neg_edge = torch.from_numpy(z[f"step{s}/neg_edge"].copy())
+        else:
+            st.neg_edge = torch.from_numpy(z[f"step{s}/randint0"].copy())
+        st.bce = float(z[f"step{s}/bce"])
+        st.grads = [torch.from_numpy(z[f"step{s}/grad{i}"].copy()) for i in range(ng)]
+        c.steps.append(st)
+    return c
+
+
+TEACHER_CASES = ["teacher_sage_small", "teacher_sage3_collab_small", "teacher_updated_production_small"]
 MINIBATCH_CASES = ["minibatch_collab_small", "minibatch_rw_small"]
 FULLBATCH_CASES = ["fullbatch_cora_small", "fullbatch_production_small"]

@@ -332,7 +332,7 @@ def test_randint_pairs_bit_exact_and_sharded():
 
 # ------------------------------------------------------------------ SAGE aggregate
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
-@pytest.mark.parametrize("F_", [128, 256, 30, 8])
+@pytest.mark.parametrize("F_", [128, 256, 30, 8, 24, 48, 200, 1000])
 def test_csr_mean_aggregate_fwd_bwd(dt, F_):
     import llp_sage
     k = K()

@@ -89,3 +89,40 @@ def test_oracle_replays_reference_steps(name):
         if (i + 1) % steps_per_epoch == 0:
             assert abs(tot / n - case.epoch_losses[ep]) < 1e-5
             tot, n, ep = 0.0, 0, ep + 1
+
+
+def _oracle_teacher_replay(c):
+    """Oracle restatement of the teacher's train() on the recorded permutations
+    and negatives: SAGE forward, LinkPredictor, BCE, clip per module, Adam."""
+    enc = [p.clone().requires_grad_() for p in c.enc0]
+    pred = [p.clone().requires_grad_() for p in c.pred0]
+    adam = O.AdamState(enc + pred, lr=0.005)
+    recs = []
+    for st in c.steps:
+        convs = [tuple(enc[3 * i:3 * i + 3]) for i in range(c.L)]
+        h = O.sage_forward(c.x, c.edge_index, convs, 0.0, updated=c.updated)
+        tr = torch.cat([st.edge, st.neg_edge], 1)
+        out = O.link_predictor_forward(h[tr[0]], h[tr[1]], pred[0::2], pred[1::2]).squeeze(-1)
+        label = torch.cat([torch.ones(st.edge.size(1)), torch.zeros(st.neg_edge.size(1))])
+        loss = O.bce_loss(out, label)
+        new, grads, _ = O.distill_step(enc, pred, adam, loss)
+        recs.append((float(loss), grads))
+        enc = [p.clone().requires_grad_() for p in new[:len(enc)]]
+        pred = [p.clone().requires_grad_() for p in new[len(enc):]]
+    return recs, enc, pred
+
+
+@pytest.mark.parametrize("name", G.TEACHER_CASES)
+def test_oracle_replays_reference_teacher(name):
+    c = G.load_teacher_case(name)
+    recs, enc, pred = _oracle_teacher_replay(c)
+    for st, (loss, grads) in zip(c.steps, recs):
+        assert abs(loss - st.bce) <= 1e-6
+        for g, ref in zip(grads, st.grads):
+            assert torch.allclose(g, ref, rtol=1e-4, atol=1e-6), (name, (g - ref).abs().max())
+    for p, ref in zip(enc + pred, c.enc_final + c.pred_final):
+        assert torch.allclose(p.detach(), ref, rtol=1e-4, atol=1e-5), (name, (p - ref).abs().max())
+    convs = [tuple(enc[3 * i:3 * i + 3]) for i in range(c.L)]
+    h = O.sage_forward(c.x, c.edge_index, [tuple(t.detach() for t in cv) for cv in convs], 0.0, training=False,
+                       updated=c.updated)
+    assert torch.allclose(h, c.h_eval, rtol=1e-4, atol=1e-5)
