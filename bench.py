@@ -99,6 +99,87 @@ def cpu_baseline(data, a, t_h, init_params, B_full, P_full, sample_P=8192, steps
                        f"(H=1024, L=3, C={C}); {dt:.1f} s on {nthreads} threads")
 
 
+def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, n):
+    """One real step (buffers filled), then the dominant kernel alone n times:
+    the command rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes profile."""
+    import llp_hip as K
+    eng.step_minibatch(node_perm[b0:b1], link_perm[p0:p1], pairs, b_offset=b0, p_offset=p0, B_total=B_full,
+                       P_total=P_full)
+    lin = eng.stu[1]
+    A = eng._bufs["H0"]
+    R1 = (b1 - b0) * (eng.args.rw_step * eng.args.hops * (1 + eng.args.ns_rate) + 1) + 4 * (p1 - p0)
+    out = eng._buf("H1", (R1, lin.out_f), eng.dtype)
+    a_op = K.operand(A[:R1 * lin.in_f].view(R1, lin.in_f))
+    for _ in range(n):
+        K.gemm_nt(a_op, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, eng.dc, bias=lin.b, act=K.ACT_RELU)
+    torch.cuda.synchronize()
+
+
+PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_dominant.json")
+
+
+def pmc_traffic(rows, H, dtype):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC passes (profiles/r01_pmc_dominant.json, tools/pmc_summary.py):
+    2 x FETCH_SIZE (gfx950 reports half of a wide streaming read) + WRITE_SIZE,
+    per dispatch.  None when the profile is absent or for another shape."""
+    try:
+        with open(PMC_FILE) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if p.get("rows") != rows or p.get("H") != H or p.get("dtype") != dtype:
+        return None
+    return p.get("traffic_bytes_per_launch")
+
+
+def evaluate(model, pred, data, dev):
+    """Hits@K / AUC on the synthetic held-out split through the device eval
+    path (llp_eval: test_transductive, src/train_teacher_gnn.py:76-155), fp32."""
+    import llp_eval
+    t0 = time.perf_counter()
+    model.eval()
+    pred.eval()
+    h = llp_eval.embed_mlp(model, data.x.to(dev))
+    score = llp_eval.EdgeScorer(pred)
+    out = {}
+    for split in ("valid", "test"):
+        p = score(h, data.split_edge[split]["edge"].to(dev))
+        n = score(h, data.split_edge[split]["edge_neg"].to(dev))
+        for k, v in zip((10, 20, 50, 100), llp_eval.K.hits_at_k(p, n, (10, 20, 50, 100))):
+            out.setdefault(f"Hits@{k}", {})[split] = v
+    torch.cuda.synchronize()
+    return {"hits@20": out["Hits@20"], "hits": out, "eval_ms": (time.perf_counter() - t0) * 1e3,
+            "hits_note": "after the timed steps from random init on synthetic data (not a converged model)"}
+
+
+def sage_aggregate(data, dev):
+    """SAGE teacher's CSR mean aggregate (a11) at the collab shape, F=128 f32,
+    event-timed: algorithmic bytes E*F*4 + 4E + 4(N+1) + N*F*4 per launch."""
+    import llp_hip as K
+    import llp_sage
+    g = llp_sage.Graph(data.edge_index, data.N, dev)
+    x = data.x.to(dev)
+    out = torch.empty_like(x)
+    F_ = x.shape[1]
+    for _ in range(3):
+        K.csr_aggregate(data.N, F_, g.rowptr, g.col, x, None, 0, out)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 20
+    s.record()
+    for _ in range(n):
+        K.csr_aggregate(data.N, F_, g.rowptr, g.col, x, None, 0, out)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / n
+    nbytes = g.num_edges * F_ * 4 + 4 * g.num_edges + 4 * (data.N + 1) + data.N * F_ * 4
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"kernel": "csr_agg_vec_kernel<float> fwd", "N": data.N, "E": g.num_edges, "F": F_, "ms": ms,
+            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+            "algorithmic_bytes": nbytes,
+            "note": "x (121 MB) stays resident in the 256 MiB Infinity Cache across the ~10 neighbour re-reads"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,6 +190,11 @@ def main():
     ap.add_argument("--cpu-sample-edges", type=int, default=8192)
     ap.add_argument("--scale", type=float, default=1.0, help="dataset scale (1.0 = ogbl-collab shape)")
     ap.add_argument("--profile-kernels", action="store_true", help="exit right after the timed region")
+    ap.add_argument("--dominant-only", type=int, default=0,
+                    help="run only the dominant kernel this many times (rocprofv3 --pmc passes) and exit")
+    ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph (N=1)")
+    ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-sage", action="store_true")
     opt = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,7 +210,7 @@ def main():
     import models
 
     a = collab_args()
-    data = llp_data.synthetic_collab(seed=0, scale=opt.scale, with_eval=False)
+    data = llp_data.synthetic_collab(seed=0, scale=opt.scale, with_eval=not opt.no_eval)
     N, F, H, L = data.N, data.F, a.hidden_channels, a.num_layers
     E_train = data.train_pairs.shape[0]
     P_full = a.link_batch_size
@@ -163,8 +249,21 @@ def main():
         eng.step_minibatch(anchors, links, pairs, b_offset=b0, p_offset=p0, B_total=B_full, P_total=P_full,
                            kernel_events=kern_ev if timed else None)
 
+    if opt.dominant_only:
+        dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, opt.dominant_only)
+        return
+    use_graph = opt.graph and world == 1
     for s in range(opt.warmup):
         one_step(s, False)
+    graph = None
+    if use_graph:
+        # persistent input slots, refilled before each replay (device-to-device copies)
+        g_anchors = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
+        g_links = torch.empty(p1 - p0, dtype=torch.int32, device=dev)
+        g_anchors.copy_(node_perm[b0:b1])
+        g_links.copy_(link_perm[p0:p1])
+        graph = eng.capture_minibatch(g_anchors, g_links, pairs, b_offset=b0, p_offset=p0, B_total=B_full,
+                                      P_total=P_full)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -172,7 +271,13 @@ def main():
     eng.begin_epoch()
     t0 = time.perf_counter()
     for s in range(opt.steps):
-        one_step(opt.warmup + s, True)
+        if graph is not None:
+            j = (opt.warmup + s) % n_full
+            g_anchors.copy_(node_perm[j * B_full + b0: j * B_full + b1])
+            g_links.copy_(link_perm[j * P_full + p0: j * P_full + p1])
+            graph.replay()
+        else:
+            one_step(opt.warmup + s, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -190,6 +295,10 @@ def main():
 
     # dominant kernel: student layer-2 forward GEMM (rows_mlp x 1024 x 1024, bf16 MFMA)
     rows_mlp = (b1 - b0) * (C + 1) + 4 * (p1 - p0)
+    if not kern_ev:   # graph mode: time the dominant kernel in a few eager steps after the timed region
+        for s in range(3):
+            one_step(opt.warmup + opt.steps + s, True)
+        torch.cuda.synchronize()
     kt = [s.elapsed_time(e) for s, e in kern_ev]
     k_ms = float(np.mean(kt)) if kt else float("nan")
     k_flop = 2.0 * rows_mlp * H * H
@@ -211,11 +320,17 @@ def main():
                        "edges_per_step": P_full, "global_batch": P_full, "parallelism": f"dp{world}",
                        "step_tflop": flop_step / 1e12, "mfma_util_step": flop_step / (dt / opt.steps) / 1e12 / peak
                        / world},
-            "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<bf16> student layer-2 forward "
+            "roofline": {"bound": "mfma", "kernel": "gemm_nt_bf16_256p student layer-2 forward "
                          f"({rows_mlp}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None, "kernel_ms": k_ms},
+                         "frac": achieved / peak, "traffic": pmc_traffic(rows_mlp, H, opt.dtype),
+                         "algorithmic_bytes": 2.0 * rows_mlp * H * 2 + 2.0 * H * H, "kernel_ms": k_ms},
             "loss": loss,
+            "hipgraph": bool(graph is not None),
         }
+        if not opt.no_eval:
+            res.update(evaluate(model, pred, data, dev))
+        if not opt.no_sage:
+            res["sage_aggregate"] = sage_aggregate(data, dev)
         if world == 1 and not opt.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, a, t_h, init, B_full, P_full, sample_P=opt.cpu_sample_edges)
         print(json.dumps(res), flush=True)

@@ -18,8 +18,11 @@ import torch
 COLLAB = dict(N=235_868, F=128, E_train=1_179_052, n_valid=60_084, n_test=46_329, n_neg=100_000)
 
 
-def planted_pairs(N: int, n_pairs: int, n_comm: int, p_intra: float, dup_frac: float, rng):
-    comm = rng.integers(0, n_comm, N)
+def planted_pairs(N: int, n_pairs: int, n_comm: int, p_intra: float, dup_frac: float, rng, comm=None):
+    """Undirected pairs, a fraction p_intra inside the planted community of u.
+    ``comm`` (node -> community) is drawn when not given."""
+    if comm is None:
+        comm = rng.integers(0, n_comm, N)
     members = [np.flatnonzero(comm == c) for c in range(n_comm)]
     n_dup = int(n_pairs * dup_frac)
     n_base = n_pairs - n_dup
@@ -39,6 +42,7 @@ def planted_pairs(N: int, n_pairs: int, n_comm: int, p_intra: float, dup_frac: f
     dup = pairs[rng.integers(0, n_base, n_dup)]
     pairs = np.concatenate([pairs, dup], 0)
     pairs = pairs[rng.permutation(pairs.shape[0])]
+    planted_pairs.last_comm = comm
     return pairs
 
 
@@ -55,12 +59,18 @@ def synthetic_collab(seed: int = 0, scale: float = 1.0, with_eval: bool = True, 
     Fd = COLLAB["F"] if F is None else F
     E = int(COLLAB["E_train"] * scale)
     pairs = planted_pairs(N, E, max(10, int(1000 * scale)), 0.9, 0.05, rng)
-    x = (rng.standard_normal((N, Fd), dtype=np.float32) * 0.1).astype(np.float32)
+    comm = planted_pairs.last_comm
+    # features carry the planted community (centroid + noise), so the student
+    # MLP can learn the link structure from x as it does from real features
+    n_comm = max(10, int(1000 * scale))
+    cent = rng.standard_normal((n_comm, Fd), dtype=np.float32)
+    x = (0.07 * (cent[comm] + rng.standard_normal((N, Fd), dtype=np.float32))).astype(np.float32)
     d = types.SimpleNamespace(N=N, F=Fd, x=torch.from_numpy(x), train_pairs=torch.from_numpy(pairs),
                               edge_index=torch.from_numpy(interleave(pairs)))
     if with_eval:
         nv, nt, nn_ = (int(COLLAB[k] * scale) for k in ("n_valid", "n_test", "n_neg"))
-        held = planted_pairs(N, nv + nt, max(10, int(1000 * scale)), 0.9, 0.0, rng)
+        # held-out positives from the SAME planted communities as the training graph
+        held = planted_pairs(N, nv + nt, max(10, int(1000 * scale)), 0.9, 0.0, rng, comm=comm)
         d.split_edge = {
             "train": {"edge": d.train_pairs},
             "valid": {"edge": torch.from_numpy(held[:nv]),

@@ -1,0 +1,40 @@
+"""Per-launch duration of bench.py's dominant kernel (student layer-2 forward
+GEMM = the 2nd gemm_nt_bf16_256p dispatch after each step's context_walk_kernel)
+from a rocprofv3 --kernel-trace CSV, to check against bench.py's event timing.
+
+    python tools/dominant_from_trace.py gpurun_out/prof_r01/bench_kernel_trace.csv [out.json]
+"""
+import csv
+import json
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    durs = []
+    k = None
+    for s, e, name in rows:
+        if "context_walk_kernel" in name:
+            k = 0
+            continue
+        if k is not None and "gemm_nt_bf16_256p" in name:
+            k += 1
+            if k == 2:
+                durs.append(e - s)
+    out = {"kernel": "gemm_nt_bf16_256p (student layer-2 forward, 2nd NT launch of each step)",
+           "launches": len(durs), "avg_ms": sum(durs) / len(durs) / 1e6 if durs else None,
+           "min_ms": min(durs) / 1e6 if durs else None, "max_ms": max(durs) / 1e6 if durs else None,
+           "source": path}
+    print(json.dumps(out))
+    if len(sys.argv) > 2:
+        with open(sys.argv[2], "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+"""SAGE teacher at the ogbl-collab shape (N=235,868, E=2,358,104 directed,
+F=128 -> 256 -> 256 -> 256): CSR mean-aggregate bandwidth (forward and the
+transposed backward) against the 8 TB/s HBM roofline, and one full teacher
+train() step.  Algorithmic bytes per aggregate:
+    E*F*s (neighbour rows) + 4E (col) + 4(N+1) (rowptr) + N*F*s (write)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
+
+import torch  # noqa: E402
+
+import llp_data  # noqa: E402
+import llp_hip as K  # noqa: E402
+import llp_sage  # noqa: E402
+import llp_teacher  # noqa: E402
+import models  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=5)
+    opt = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    dt = torch.float32 if opt.dtype == "fp32" else torch.bfloat16
+    data = llp_data.synthetic_collab(seed=0, with_eval=False)
+    N = data.N
+    g = llp_sage.Graph(data.edge_index, N, dev)
+    E = g.num_edges
+    es = 4 if dt == torch.float32 else 2
+    res = {"N": N, "E": E, "dtype": opt.dtype, "aggregate": []}
+    for F_ in (128, 256):
+        x = torch.randn(N, F_, device=dev).to(dt)
+        out = torch.empty(N, F_, device=dev, dtype=dt)
+        for mode, (rp, cl, w) in (("fwd", (g.rowptr, g.col, None)), ("bwd", (g.rowptr_t, g.col_t, g.inv_deg))):
+            for _ in range(3):
+                K.csr_aggregate(N, F_, rp, cl, x, w, 0 if mode == "fwd" else 1, out)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(opt.iters):
+                K.csr_aggregate(N, F_, rp, cl, x, w, 0 if mode == "fwd" else 1, out)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / opt.iters
+            nbytes = E * F_ * es + 4 * E + 4 * (N + 1) + N * F_ * es + (4 * E if mode == "bwd" else 0)
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            res["aggregate"].append({"F": F_, "mode": mode, "ms": ms, "GB/s": gbs, "frac_hbm": gbs / 8000.0,
+                                     "bytes": nbytes})
+    # full teacher step: SAGE 128 -> 256 x3 (collab teacher: --num_layers=3), predictor 256/2 layers
+    torch.manual_seed(0)
+    model = models.SAGE("collab", data.F, 256, 256, 3, 0.5, llp_sage.SAGEConv).to(dev)
+    pred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.5).to(dev)
+    optim = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=0.005)
+    eng = llp_teacher.TeacherEngine(model, pred, data.x.to(dev), data.edge_index, N, optim, dtype=opt.dtype)
+    pairs = data.train_pairs.to(torch.int32).to(dev).contiguous()
+    P = 64 * 1024
+    perm = torch.randperm(pairs.shape[0], device=dev).to(torch.int32)
+    for i in range(2):
+        eng.step(perm[i * P:(i + 1) * P], pairs, dense_negatives=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(opt.steps):
+        eng.step(perm[i * P:(i + 1) * P], pairs, dense_negatives=False)
+    torch.cuda.synchronize()
+    dt_s = (time.perf_counter() - t0) / opt.steps
+    res["teacher_step_ms"] = dt_s * 1e3
+    res["teacher_edges_per_s"] = P / dt_s
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
