@@ -195,12 +195,14 @@ int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_n
 int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
                       const int64_t* step_ctr, int64_t stream_offset, int32_t* out, void* stream);
 
-/* Per-step index build for the minibatch layout (src/main.py:78,86-95):
- * pos edges = pairs[perm[*step_ctr*P_stride + i]] (i < P), neg edges = neg[2,P];
- * target (node id per h row) = [samples.flatten(), src(2P), dst(2P)]. */
+/* Per-step index build for the minibatch layout (src/main.py:78,81-95):
+ * pos edges = pairs[perm[*step_ctr*P_stride + i]] (i < P), neg edges =
+ * neg[2, ld_neg] columns [0, n_neg) (randint: n_neg = P; PyG dense: may be fewer);
+ * target (node id per h row) = [samples.flatten(), src(P+n_neg), dst(P+n_neg)]. */
 int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
                       const int32_t* perm, const int64_t* step_ctr, int64_t perm_stride,
-                      int64_t P, const int32_t* neg, int32_t* target, void* stream);
+                      int64_t P, const int32_t* neg, int64_t n_neg, int64_t ld_neg, int32_t* target,
+                      void* stream);
 
 /* Teacher / predictor pair indices from samples: ia[b*C+c] = samples[b,0],
  * ib[b*C+c] = samples[b,1+c]  (src/main.py:104,106). */

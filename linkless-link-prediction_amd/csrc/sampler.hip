@@ -63,23 +63,25 @@ __global__ void randint_pairs_kernel(int64_t num_nodes, int64_t n, int64_t n_tot
 __global__ void build_targets_kernel(int64_t BC1, const int32_t* __restrict__ samples,
                                      const int32_t* __restrict__ pairs, const int32_t* __restrict__ perm,
                                      const int64_t* __restrict__ step_ctr, int64_t perm_stride, int64_t P,
-                                     const int32_t* __restrict__ neg, int32_t* __restrict__ target) {
+                                     const int32_t* __restrict__ neg, int64_t n_neg, int64_t ld_neg,
+                                     int32_t* __restrict__ target) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t total = BC1 + 4 * P;
+  const int64_t n_lab = P + n_neg;     // train_edges columns (main.py:86)
+  const int64_t total = BC1 + 2 * n_lab;
   if (t >= total) return;
   if (t < BC1) {
     target[t] = samples[t];
     return;
   }
-  const int64_t u = t - BC1;           // [0, 4P): src(2P) then dst(2P)
-  const int64_t side = u / (2 * P);    // 0 = src (train_edges[0]), 1 = dst
-  const int64_t i = u % (2 * P);
+  const int64_t u = t - BC1;           // [0, 2 n_lab): src(n_lab) then dst(n_lab)
+  const int64_t side = u / n_lab;      // 0 = src (train_edges[0]), 1 = dst
+  const int64_t i = u % n_lab;
   int32_t v;
   if (i < P) {
     const int64_t e = perm[(step_ctr ? *step_ctr : 0) * perm_stride + i];
     v = pairs[2 * e + side];           // pos_train_edge[link_perm].t() (main.py:78)
   } else {
-    v = neg[side * P + (i - P)];       // neg_edge[side] (main.py:84)
+    v = neg[side * ld_neg + (i - P)];  // neg_edge[side] (main.py:81-84)
   }
   target[t] = v;
 }
@@ -133,12 +135,13 @@ extern "C" int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, 
 
 extern "C" int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
                                  const int32_t* perm, const int64_t* step_ctr, int64_t perm_stride, int64_t P,
-                                 const int32_t* neg, int32_t* target, void* stream) {
-  LLP_CHECK_ARG(samples && pairs && perm && neg && target, "llp_build_targets: null pointer");
-  const int64_t total = B * C1 + 4 * P;
+                                 const int32_t* neg, int64_t n_neg, int64_t ld_neg, int32_t* target, void* stream) {
+  LLP_CHECK_ARG(samples && pairs && perm && target && (neg || n_neg == 0), "llp_build_targets: null pointer");
+  LLP_CHECK_ARG(n_neg >= 0 && ld_neg >= n_neg, "llp_build_targets: bad negative layout");
+  const int64_t total = B * C1 + 2 * (P + n_neg);
   if (total == 0) return LLP_OK;
   hipLaunchKernelGGL(build_targets_kernel, dim3(ceil_div_u(total, 256)), dim3(256), 0, (hipStream_t)stream,
-                     B * C1, samples, pairs, perm, step_ctr, perm_stride, P, neg, target);
+                     B * C1, samples, pairs, perm, step_ctr, perm_stride, P, neg, n_neg, ld_neg, target);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

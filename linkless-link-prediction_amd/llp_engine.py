@@ -403,14 +403,16 @@ class DistillEngine(EngineBase):
 
     # ------------------------------------------------------------------ the step
     def step_minibatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
-                       samples=None, neg=None, kernel_events=None):
+                       samples=None, neg=None, kernel_events=None, dense_negatives=False):
         """One link batch of train_minibatch (src/main.py:73-143).
 
         anchors  int32[B]   this rank's slice of node_perm (src/main.py:76)
         link_ids int32[P]   this rank's slice of link_perm (src/main.py:73,78)
         pairs    int32[E,2] pos_train_edge (src/main.py:55)
-        samples / neg: optional injected samples int32[B, 1+C] / negatives int32[2, P]
-        (parity tests); otherwise drawn on the device.
+        samples / neg: optional injected samples int32[B, 1+C] / negatives int32[2, n]
+        (parity tests); otherwise drawn on the device: randint (collab,
+        src/main.py:83-84) or, with dense_negatives, PyG dense sampling
+        (non-collab, src/main.py:80-82; one host read of its count).
         Returns nothing; the loss terms stay on the device (self.terms).
         """
         a = self.args
@@ -423,28 +425,24 @@ class DistillEngine(EngineBase):
         C1 = C + 1
         H = self.stu[-1].out_f
         dt, dc = self.dtype, self.dc
-        R1 = B * C1 + 4 * P
-        R2 = B * C + 2 * P
-        P2 = 2 * P
 
-        # ---- a1-a3: samples and negatives (src/main.py:84,93)
+        # ---- a1-a3: negatives and samples (src/main.py:80-84,93)
+        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+        n_lab = P + n_neg                  # train_edges columns (src/main.py:86)
+        R1 = B * C1 + 2 * n_lab
+        R2 = B * C + n_lab
         samp = self._buf("samples", (B, C1), torch.int32)
         if samples is not None:
             samp.copy_(samples.to(torch.int32))
         else:
             K.context_sampler(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                               self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
-        negb = self._buf("neg", (2, P), torch.int32)
-        if neg is not None:
-            negb.copy_(neg.to(torch.int32))
-        else:
-            K.randint_pairs(self.N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)
         target = self._buf("target", (R1,), torch.int32)
-        K.build_targets(B, C1, samp, pairs, link_ids, None, 0, P, negb, target)
+        K.build_targets(B, C1, samp, pairs, link_ids, None, 0, P, negb, target, n_neg=n_neg)
         t_ia = self._buf("t_ia", (B * C,), torch.int32)
         t_ib = self._buf("t_ib", (B * C,), torch.int32)
         K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
-        ia, ib = self._rows_index(B, C, P2)
+        ia, ib = self._rows_index(B, C, n_lab)
 
         # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
         acts = []
@@ -480,17 +478,17 @@ class DistillEngine(EngineBase):
             raise UnboundLocalError("train_minibatch: loss is only defined when LLP_D or LLP_R is set "
                                     "(src/main.py:129-130)")
         dlogit = self._buf("dlogit", (R2,), torch.float32)
-        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(B, P2))
-        K.llp_loss(B, C, logit, t_r, P2, P, logit[B * C:], B_total, 2 * P_total, float(a.margin), 1.0,
+        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(B, n_lab))
+        K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin), 1.0,
                    float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms, ws)
 
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
         dh = self._buf("gS0", (R1, H), dt)
         if self.predictor_kind == "mlp":
-            K.hadamard_bwd_blocks(B, C, P2, H, dZ0, h, dh)
+            K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0, h, dh)
         else:
-            K.hadamard_bwd_blocks(B, C, P2, H, None, h, dh, drow=dlogit)
+            K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh, drow=dlogit)
         self._student_backward(dh, R1, target, acts, p_drop)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)

@@ -66,7 +66,8 @@ _SIGS = {
     "llp_context_sampler": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
                                     c_i64, c_vp, c_vp]),
     "llp_randint_pairs": (c_int, [c_i64, c_i64, c_i64, c_i64, c_u64, c_vp, c_i64, c_vp, c_vp]),
-    "llp_build_targets": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "llp_build_targets": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                  c_vp]),
     "llp_pair_index_from_samples": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_neg_sample_dense_workspace_bytes": (c_i64, [c_i64]),
     "llp_neg_sample_dense": (c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp, c_i64, c_vp,
@@ -272,10 +273,13 @@ def randint_pairs(num_nodes, n, seed, step_ctr, stream_offset, out, n_total=None
                               out.data_ptr(), stream_ptr()), "llp_randint_pairs")
 
 
-def build_targets(B, C1, samples, pairs, perm, step_ctr, perm_stride, P, neg, target):
+def build_targets(B, C1, samples, pairs, perm, step_ctr, perm_stride, P, neg, target, n_neg=None):
+    """neg: int32[2, ld] view whose first n_neg (default P) columns are used."""
     L = lib()
+    n_neg = P if n_neg is None else int(n_neg)
     check(L.llp_build_targets(B, C1, samples.data_ptr(), pairs.data_ptr(), perm.data_ptr(), ptr(step_ctr),
-                              perm_stride, P, neg.data_ptr(), target.data_ptr(), stream_ptr()), "llp_build_targets")
+                              perm_stride, P, ptr(neg), n_neg, neg.stride(0) if neg is not None else 0,
+                              target.data_ptr(), stream_ptr()), "llp_build_targets")
 
 
 def pair_index_from_samples(B, Cc, samples, ia, ib):
