@@ -179,8 +179,11 @@ def train_teacher(model, predictor, data, split_edge, optimizer, batch_size, enc
     else:
         mp_edges = data.edge_index
         pos_train_edge = data.edge_index.t()
+    if encoder_name == "mlp":
+        return _train_teacher_mlp(model, predictor, data, pos_train_edge, mp_edges, optimizer, batch_size, dataset,
+                                  dtype)
     if encoder_name != "sage":
-        raise NotImplementedError("teacher encoder other than 'sage' (SURVEY §8f: GCN / MLP teachers are next)")
+        raise NotImplementedError("teacher encoder 'gcn' (SURVEY §8f4: next)")
     model.train()
     predictor.train()
     eng = _teacher_engine(model, predictor, data, optimizer, mp_edges, dtype)
@@ -191,6 +194,39 @@ def train_teacher(model, predictor, data, split_edge, optimizer, batch_size, enc
     eng.begin_epoch()
     for s in range(0, E, batch_size):
         eng.step(perm[s:s + batch_size], pairs, dense_negatives=(dataset != "collab"))
+    return eng.end_epoch(E)
+
+
+def _train_teacher_mlp(model, predictor, data, pos_train_edge, mp_edges, optimizer, batch_size, dataset, dtype):
+    """The supervised MLP baseline of src/train_teacher_gnn.py:36-37: BCE on
+    (pos, neg) with h = model(x) over all nodes — the full-batch distillation
+    step with every distillation weight zero."""
+    import types
+    import models
+    key = ("mlp-teacher", id(model), id(predictor), id(optimizer), id(data))
+    eng = _ENGINES.get(key)
+    if eng is None:
+        for k in [k for k in _ENGINES if k[0] == "mlp-teacher" and k[1:3] == key[1:3]]:
+            del _ENGINES[k]
+        a = types.SimpleNamespace(rw_step=1, hops=1, ns_rate=0, ps_method="nb", dropout=float(model.dropout.p),
+                                  margin=0.0, LLP_D=0.0, LLP_R=0.0, True_label=1.0, KD_RM=0.0, KD_LM=0.0,
+                                  predictor=predictor.predictor)
+        dummy = models.LinkPredictor("mlp", 16, 16, 1, 2, 0.0)
+        N = data.x.size(0)
+        eng = DistillEngine(model, predictor, dummy, data.x, torch.zeros(N, 16), mp_edges[0].cpu().numpy(),
+                            mp_edges[1].cpu().numpy(), N, a, optimizer, dtype=dtype, seed=_epoch_seed(),
+                            device=torch.device("cuda", torch.cuda.current_device()))
+        _ENGINES[key] = eng
+    model.train()
+    predictor.train()
+    dev = eng.dev
+    pairs = _as_pairs(pos_train_edge, dev)
+    E = pairs.shape[0]
+    perm = _device_perm(E, _epoch_seed(), dev)
+    none = torch.zeros(0, dtype=torch.int32, device=dev)
+    eng.begin_epoch()
+    for s in range(0, E, batch_size):
+        eng.step_fullbatch(none, perm[s:s + batch_size], pairs, dense_negatives=(dataset != "collab"))
     return eng.end_epoch(E)
 
 

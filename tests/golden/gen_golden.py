@@ -557,8 +557,35 @@ def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, 
     print(name, "steps:", out["nsteps"], "epoch losses:", losses)
 
 
+def run_logger_case(name):
+    """src/logger.py printed output for fixed result tables (the CLI's outputs
+    must stay byte-identical)."""
+    import contextlib
+    import io
+    import json
+    mod = types.ModuleType("ref_logger")
+    p = os.path.join(REF, "logger.py")
+    exec(compile(_compile_file(p), p, "exec"), mod.__dict__)
+    cases = []
+    for cls, width in (("Logger", 2), ("ProductionLogger", 5)):
+        table = [[[float(v) for v in torch.rand(width, generator=torch.Generator().manual_seed(run * 10 + ep))]
+                  for ep in range(4)] for run in range(3)]
+        L = getattr(mod, cls)(3)
+        for run, rows in enumerate(table):
+            for r in rows:
+                L.add_result(run, tuple(r))
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            L.print_statistics(1)
+            L.print_statistics()
+        cases.append({"cls": cls, "table": table, "stdout": buf.getvalue()})
+    with open(os.path.join(HERE, name + ".json"), "w") as f:
+        json.dump(cases, f, indent=1)
+
+
 def main():
     ref_models = load_reference_models()
+    run_logger_case("logger_output")
     run_teacher_case("teacher_sage_small", N=110, F_=24, H=64, L=2, E_und=400, bs=160, updated=False,
                      transductive="transductive", seed=7)
     run_teacher_case("teacher_sage3_collab_small", N=130, F_=16, H=32, L=3, E_und=500, bs=200, updated=False,
