@@ -94,6 +94,15 @@ int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, cons
 int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit,
                     float* prob, void* stream);
 
+/* Main-loop variant of the large-tile bf16 NT kernel (a tuning knob, process
+ * wide, for A/B measurements in one process): K64 quadrant phases with
+ * 128-B DMA lines (default), ping-pong wave groups with a 5-stage / 3-ahead or
+ * 4-stage / 2-ahead ring of 64-B lines, or the lockstep 4-stage ring.  All
+ * variants give bit-identical results.  Returns the previous variant (or an
+ * error code). */
+enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 2, LLP_GEMM_Q64 = 3 };
+int llp_set_gemm_variant(int variant);
+
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
  * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then
  * reduced in a fixed order: deterministic.  C is f32 with leading dim ldc.

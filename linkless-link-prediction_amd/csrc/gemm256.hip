@@ -289,6 +289,381 @@ __device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
+// Shared epilogue of the 256x256 kernels: alpha, bias, ReLU, dropout, fused
+// Linear(N,1) head partials, LDS-staged coalesced store (+ReLU-bwd mask).
+// smem must hold SMEM_U4_EPI uint4 + 4 KiB at smem + head_off_u4.
+__device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
+                                             int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  uint4* stg = smem;
+  float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn) {
+    const int nl = wn * 64 + jn * 16 + g * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    float hw[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? p.bias[n0 + nl + r] : 0.f;
+    }
+    if (p.head_w) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hw[r] = (n0 + nl + r < p.N) ? p.head_w[n0 + nl + r] : 0.f;
+    }
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int ml = wm * 128 + im * 16 + li;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = p.alpha * acc[jn][im][r] + bv[r];
+        if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (p.drop_p > 0.f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)((m0 + ml) * p.N + n0 + nl + r));
+          v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
+        }
+      }
+      hp[im] += v[0] * hw[0] + v[1] * hw[1] + v[2] * hw[2] + v[3] * hw[3];
+      const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
+      *dst = make_uint2(lo, hi);
+    }
+  }
+  if (p.head_w) {
+    float* part = reinterpret_cast<float*>(smem + head_off_u4);   // [4 wn][256 rows]
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      float v = hp[im];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) part[wn * 256 + wm * 128 + im * 16 + li] = v;
+    }
+  }
+  __syncthreads();
+  if (p.head_w && tid < TM && m0 + tid < p.M) {
+    const float* part = reinterpret_cast<const float*>(smem + head_off_u4);
+    const float s = part[tid] + part[256 + tid] + part[512 + tid] + part[768 + tid];
+    p.head_part[(n0 / TN) * p.M + m0 + tid] = s;
+  }
+  if (!p.C) return;
+  const int chunks_per_row = TN / 8;
+#pragma unroll 4
+  for (int q = tid; q < TM * chunks_per_row; q += NT2) {
+    const int rl = q / chunks_per_row, c = q % chunks_per_row;
+    const int64_t row = m0 + rl, col = n0 + c * 8;
+    if (row >= p.M || col >= p.N) continue;
+    uint4 v = stg[rl * EPI_ROW_U4 + c];
+    if (p.act == LLP_ACT_RELU_BWD) {
+      const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
+      const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
+        const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
+        vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+      }
+      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong variant (cdna_hip_programming.md §5 "The 256² 8-phase template":
+// wave groups staggered by one barrier).  Waves 0-3 (rows 0-127 of the tile)
+// and 4-7 (rows 128-255) alternate: while one group runs its 32 MFMAs of a
+// k-step, the other group (the second wave on every SIMD) issues its 12
+// ds_read_b128 fragment reads and the next stages' LDS-DMA, so LDS latency
+// and DMA issue hide under the partner's MFMAs instead of stalling both.
+//   per k-step s:  [R_s: ds_read stage s, DMA stage s+D] bar [M_s: 32 MFMA] bar
+// group 1 runs one barrier behind group 0.  RAW: every wave waits (counted
+// vmcnt) for its part of stage s+1 in the segment that ends at the barrier
+// before group 0's R_{s+1}.  WAR: the DMA into stage s+D's buffer (last read
+// as stage s+D-NS) is issued >= 2 barriers after those reads drained, which
+// needs NS >= D + 2.
+template <int NS, int D>
+__global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp(P256 p) {
+  static_assert(NS >= D + 2, "ring too short for the prefetch distance");
+  constexpr int LOOP_U4 = NS * PSTAGE_U4;
+  constexpr int SM_U4 = LOOP_U4 > SMEM_U4_EPI + 256 ? LOOP_U4 : SMEM_U4_EPI + 256;
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TM - 1) / TM;
+  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
+  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+
+  const bf16_t* ga[2];
+  const bf16_t* gb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 32 * w + 16 * i + (lane >> 2);
+    const int lc = (lane & 3) ^ swz64(r);
+    int64_t m = m0 + r;
+    m = m < p.M ? m : p.M - 1;
+    ga[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
+    int64_t n = n0 + r;
+    n = n < p.N ? n : p.N - 1;
+    gb[i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
+  }
+  const uint32_t lds0 = lds_u32(smem);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto issue = [&](int64_t kt) {
+    const uint32_t sA = lds0 + (uint32_t)((kt % NS) * PSTAGE_U4 * 16);
+    const uint32_t sB = sA + TM * 4 * 16;
+    const int64_t koff = kt * PK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t off = (uint32_t)((32 * wu + 16 * i) * 4 * 16);
+      glds16(ga[i] + koff, __builtin_amdgcn_readfirstlane(sA + off));
+      glds16(gb[i] + koff, __builtin_amdgcn_readfirstlane(sB + off));
+    }
+  };
+
+  const int wm = w >> 2, wn = w & 3;
+  const bool grp1 = __builtin_amdgcn_readfirstlane(wm) == 1;
+  float4_t acc[4][8];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = p.K / PK;
+  for (int64_t s = 0; s < D && s < nk; ++s) issue(s);
+  // stage 0 landed (this wave's part), then visible to all
+  vm_wait_stages<NS>(min((int64_t)D, nk) - 1);
+  __builtin_amdgcn_s_barrier();
+  if (grp1) __builtin_amdgcn_s_barrier();   // stagger: group 1 one barrier behind
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    // ---- R: fragments of stage kt, DMA of stage kt + D
+    const uint4* sA = smem + (int)(kt % NS) * PSTAGE_U4;
+    const uint4* sB = sA + TM * 4;
+    short8 fw[4], fx[8];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      const int r = wn * 64 + jn * 16 + li;
+      uint4 v = sB[r * 4 + (g ^ swz64(r))];
+      fw[jn] = *reinterpret_cast<short8*>(&v);
+    }
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int r = wm * 128 + im * 16 + li;
+      uint4 v = sA[r * 4 + (g ^ swz64(r))];
+      fx[im] = *reinterpret_cast<short8*>(&v);
+    }
+#ifndef LLP_ABLATE_NOLOAD
+    if (kt + D < nk) issue(kt + D);
+#endif
+    const int64_t ahead = min(nk - 1, kt + D) - (kt + 1);   // stages issued beyond kt+1
+    if (grp1 && kt + 1 < nk) vm_wait_stages<NS>(ahead);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- M: 32 MFMAs on the fragments
+#ifndef LLP_ABLATE_NOMFMA
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+      for (int im = 0; im < 8; ++im)
+        acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#else
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
+#pragma unroll
+    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
+#endif
+    if (!grp1 && kt + 1 < nk) vm_wait_stages<NS>(ahead);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (!grp1) __builtin_amdgcn_s_barrier();   // group 0 matches group 1's barrier count
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_256(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
+}
+
+// ---------------------------------------------------------------------------
+// K64 quadrant-phase variant: full 128-byte lines per DMA piece.
+// A K-tile of 64 (A and B images [256 rows][128 B], 64 KiB) is consumed in 4
+// phases; phase p computes one quadrant (m-half mh, n-half nh) of every wave's
+// 128 x 64 output over K = 64 (16 MFMAs), in the order (0,0) (0,1) (1,1) (1,0)
+// so each phase re-reads only one operand half.  The DMA of the next K-tile is
+// cut into the same halves — chunk 0 = A rows with row%128 < 64, 1 = B rows
+// with row%64 < 32, 2 = B rows with row%64 >= 32, 3 = the other A rows — and
+// chunk j of tile t+1 is issued in phase j of tile t (2 x 1 KiB pieces per
+// wave, 8 rows x 128 B each).  Two K-tile buffers.  RAW: before the barrier of
+// the phase that first reads a chunk (phases 0, 0, 1, 2), a counted vmcnt
+// leaves exactly the younger pieces in flight.  WAR: chunk j is re-filled 2-4
+// phases after its last read (drained by lgkmcnt inside that phase).
+__device__ __forceinline__ int q64_row(int chunk, int cr) {
+  // chunk-row cr in [0,128) -> tile row
+  switch (chunk) {
+    case 0: return (cr & 63) + 128 * (cr >> 6);
+    case 3: return (cr & 63) + 128 * (cr >> 6) + 64;
+    case 1: return (cr & 31) + 64 * (cr >> 5);
+    default: return (cr & 31) + 64 * (cr >> 5) + 32;
+  }
+}
+
+__global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
+  constexpr int IMG_U4 = 256 * 8;                  // one operand image [256][8 chunks]
+  constexpr int TILE_U4 = 2 * IMG_U4;              // A then B: 64 KiB
+  constexpr int SM_U4 = 2 * TILE_U4 > SMEM_U4_EPI + 256 ? 2 * TILE_U4 : SMEM_U4_EPI + 256;
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TM - 1) / TM;
+  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
+  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+
+  // per (chunk, piece): this lane's source pointer (k-tile 0) and the piece's
+  // wave-uniform LDS row offset
+  const bf16_t* src[4][2];
+  int dst_row[4][2];
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row0 = q64_row(j, 16 * wu + 8 * i);       // 8 consecutive rows per piece
+      dst_row[j][i] = row0;
+      const int r = row0 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);                 // source swizzle: image chunk lane&7 holds lc
+      if (j == 0 || j == 3) {
+        int64_t m = m0 + r;
+        m = m < p.M ? m : p.M - 1;
+        src[j][i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
+      } else {
+        int64_t n = n0 + r;
+        n = n < p.N ? n : p.N - 1;
+        src[j][i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
+      }
+    }
+  const uint32_t lds0 = lds_u32(smem);
+  auto issue_chunk = [&](int j, int64_t kt) {
+    const uint32_t base = lds0 + (uint32_t)((kt & 1) * TILE_U4 * 16) + ((j == 0 || j == 3) ? 0u : IMG_U4 * 16u);
+    const int64_t koff = kt * TK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(src[j][i] + koff, __builtin_amdgcn_readfirstlane(base + (uint32_t)(dst_row[j][i] * 128)));
+  };
+
+  const int wm = w >> 2, wn = w & 3;
+  float4_t acc[4][8];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = p.K / TK;
+  short8 fa[2][4];        // [k32 half][im] for the current m-half
+  short8 fb[2][2][2];     // [n-half][k32 half][jn]
+  auto read_a = [&](const uint4* sA, int mh) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int im = 0; im < 4; ++im) {
+        const int r = wm * 128 + mh * 64 + im * 16 + li;
+        uint4 v = sA[r * 8 + ((kh * 4 + g) ^ (r & 7))];
+        fa[kh][im] = *reinterpret_cast<short8*>(&v);
+      }
+  };
+  auto read_b = [&](const uint4* sB, int nh) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) {
+        const int r = wn * 64 + nh * 32 + jn * 16 + li;
+        uint4 v = sB[r * 8 + ((kh * 4 + g) ^ (r & 7))];
+        fb[nh][kh][jn] = *reinterpret_cast<short8*>(&v);
+      }
+  };
+  auto mfma_q = [&](int mh, int nh) {
+#ifndef LLP_ABLATE_NOMFMA
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int im = 0; im < 4; ++im)
+          acc[nh * 2 + jn][mh * 4 + im] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][kh][jn], fa[kh][im], acc[nh * 2 + jn][mh * 4 + im], 0,
+                                                      0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#else
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int im = 0; im < 4; ++im) asm volatile("" ::"v"(fa[kh][im]));
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) asm volatile("" ::"v"(fb[nh][kh][jn]));
+    }
+#endif
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: the whole of K-tile 0
+#pragma unroll
+  for (int j = 0; j < 4; ++j) issue_chunk(j, 0);
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
+    const uint4* sB = sA + IMG_U4;
+    // phase 0: quadrant (0,0) needs chunks 0, 1 of this tile; younger: chunks 2, 3
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    barrier();
+#ifndef LLP_ABLATE_NOLOAD
+    if (more) issue_chunk(0, kt + 1);
+#endif
+    read_a(sA, 0);
+    read_b(sB, 0);
+    mfma_q(0, 0);
+    // phase 1: (0,1) needs chunk 2; younger: chunk 3 (+ chunk 0 of the next tile)
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    barrier();
+#ifndef LLP_ABLATE_NOLOAD
+    if (more) issue_chunk(1, kt + 1);
+#endif
+    read_b(sB, 1);
+    mfma_q(0, 1);
+    // phase 2: (1,1) needs chunk 3; younger: chunks 0, 1 of the next tile
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+#ifndef LLP_ABLATE_NOLOAD
+    if (more) issue_chunk(2, kt + 1);
+#endif
+    read_a(sA, 1);
+    mfma_q(1, 1);
+    // phase 3: (1,0), everything resident
+    barrier();
+#ifndef LLP_ABLATE_NOLOAD
+    if (more) issue_chunk(3, kt + 1);
+#endif
+    read_b(sB, 0);
+    mfma_q(1, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_256(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
+}
+
 template <int NS>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   constexpr int LOOP_U4 = NS * PSTAGE_U4;
@@ -459,7 +834,26 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   }
 }
 
+int g_gemm_variant = -1;
+
 }  // namespace
+
+// NT main-loop variant for the large-tile bf16 path (tuning / A-B in one
+// process): LLP_GEMM_PP53 (default), LLP_GEMM_PP42, LLP_GEMM_PIPE (the
+// lockstep NS-stage ring).  Env LLP_GEMM_VARIANT sets the initial value.
+int llp_gemm_variant() {
+  if (g_gemm_variant < 0) {
+    const char* e = getenv("LLP_GEMM_VARIANT");
+    g_gemm_variant = e ? atoi(e) : LLP_GEMM_Q64;
+  }
+  return g_gemm_variant;
+}
+extern "C" int llp_set_gemm_variant(int v) {
+  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_Q64, "llp_set_gemm_variant: %d", v);
+  const int old = llp_gemm_variant();
+  g_gemm_variant = v;
+  return old;
+}
 
 // Called from llp_gemm_nt when the shapes allow it (gemm.hip).
 int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
@@ -482,8 +876,15 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   const int64_t tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   static const int pipe_env = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
   const int pipe = ((head_w || !C) && (pipe_env < 3 || pipe_env > 5)) ? 4 : pipe_env;
+  const int variant = llp_gemm_variant();
   if (A->ptr2)
     hipLaunchKernelGGL(gemm_nt_bf16_256<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_PP53)
+    hipLaunchKernelGGL((gemm_nt_bf16_pp<5, 3>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_PP42)
+    hipLaunchKernelGGL((gemm_nt_bf16_pp<4, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_Q64)
+    hipLaunchKernelGGL(gemm_nt_bf16_q64, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (pipe == 4 || pipe == 5)
     hipLaunchKernelGGL(gemm_nt_bf16_256p<4>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (pipe == 3)

@@ -10,6 +10,11 @@
 
 #include "../linkless-link-prediction_amd/csrc/gemm256.hip"
 
+namespace llp {
+thread_local char g_err[512];
+int set_error(int code, const char*, ...) { return code; }
+}  // namespace llp
+
 #define CK(x) do { hipError_t err_ = (x); if (err_ != hipSuccess) { printf("%s\n", hipGetErrorString(err_)); exit(1); } } while (0)
 
 int main(int argc, char** argv) {
@@ -34,11 +39,11 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&s));
   CK(hipEventCreate(&e));
   for (int i = 0; i < 3; ++i)
-    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, 0);
+    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, nullptr, nullptr, 0);
   CK(hipEventRecord(s, 0));
   const int it = 20;
   for (int i = 0; i < it; ++i)
-    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, 0);
+    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, nullptr, nullptr, 0);
   CK(hipEventRecord(e, 0));
   CK(hipEventSynchronize(e));
   float ms;

@@ -1,0 +1,99 @@
+"""A/B of the large-tile bf16 NT main-loop variants (llp_set_gemm_variant) in
+one process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24), on
+random data at the collab step shapes.  Also checks that every variant gives
+bit-identical outputs (same per-accumulator k order) and matches torch.
+
+    python tools/gemm_variants.py [--rounds 5] [--iters 10]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
+
+import torch  # noqa: E402
+
+import llp_hip as K  # noqa: E402
+
+VARIANTS = (0, 1, 3)
+NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    opt = ap.parse_args()
+    L = K.lib()
+    dev = "cuda"
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    R1, R2, N0 = 747_214, 603_032, 235_868
+    x = torch.randn(N0, 128, device=dev, dtype=bf, generator=g)
+    idx = torch.randint(0, N0, (R1,), device=dev, dtype=torch.int32, generator=g)
+    h = torch.randn(R1, 1024, device=dev, dtype=bf, generator=g)
+    W = (torch.randn(1024, 1024, device=dev, generator=g) * 0.03).to(bf)
+    W1 = (torch.randn(1024, 128, device=dev, generator=g) * 0.1).to(bf)
+    Wt = (torch.randn(256, 512, device=dev, generator=g) * 0.05).to(bf)
+    xa = torch.randn(N0, 512, device=dev, dtype=bf, generator=g)
+    bias = torch.randn(1024, device=dev, generator=g)
+    aux = torch.randn(R1, 1024, device=dev, dtype=bf, generator=g)
+    out = torch.empty(R1, 1024, device=dev, dtype=bf)
+    outs = torch.empty(N0, 256, device=dev, dtype=bf)
+    cases = {
+        "L1 fwd gather 747214x1024x128": (lambda: K.gemm_nt(K.operand(x, idx), K.operand(W1), R1, 1024, 128, out, 1,
+                                                            bias=bias, act=K.ACT_RELU), 2 * R1 * 1024 * 128, out),
+        "L2 fwd 747214x1024x1024": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1, bias=bias,
+                                                      act=K.ACT_RELU), 2 * R1 * 1024 * 1024, out),
+        "L2 dgrad relu-bwd 747214x1024x1024": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1,
+                                                                 act=K.ACT_RELU_BWD, aux=aux), 2 * R1 * 1024 * 1024,
+                                               out),
+        "P fwd 603032x1024x1024": (lambda: K.gemm_nt(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024, out[:R2], 1,
+                                                     bias=bias, act=K.ACT_RELU), 2 * R2 * 1024 * 1024, out),
+        "SAGE 235868x256x512": (lambda: K.gemm_nt(K.operand(xa), K.operand(Wt), N0, 256, 512, outs, 1, bias=bias[:256],
+                                                  act=K.ACT_RELU), 2 * N0 * 256 * 512, outs),
+    }
+    # bit-identity across variants + a torch spot check
+    for name, (fn, flop, o) in cases.items():
+        res = []
+        for v in VARIANTS:
+            L.llp_set_gemm_variant(v)
+            o.zero_()
+            fn()
+            torch.cuda.synchronize()
+            res.append(o.clone())
+        same = all(torch.equal(res[0], r) for r in res[1:])
+        print(f"{name}: variants bit-identical: {same}", flush=True)
+    if True:   # torch check of the L2 fwd on 4096 rows
+        L.llp_set_gemm_variant(2)
+        cases["L2 fwd 747214x1024x1024"][0]()
+        torch.cuda.synchronize()
+        ref = torch.relu(h[:4096].float() @ W.float().t() + bias)
+        err = (out[:4096].float() - ref).abs().max().item()
+        print(f"L2 fwd vs torch fp32 (4096 rows): max abs err {err:.4f} (ref max {ref.abs().max().item():.2f})")
+    times = {(n, v): [] for n in cases for v in VARIANTS}
+    for r in range(opt.rounds):
+        for name, (fn, flop, o) in cases.items():
+            for v in VARIANTS:
+                L.llp_set_gemm_variant(v)
+                fn()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(opt.iters):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                times[(name, v)].append(s.elapsed_time(e) / opt.iters)
+    for name, (fn, flop, o) in cases.items():
+        row = []
+        for v in VARIANTS:
+            t = sorted(times[(name, v)])
+            med = t[len(t) // 2]
+            row.append(f"{NAMES[v]} {med:.3f} ms {flop / med / 1e9:.0f} TF")
+        print(f"{name:38s} | " + " | ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
