@@ -49,9 +49,11 @@ def collab_args():
                                  transductive="transductive", minibatch=True)
 
 
-def step_flops(B, C, P, F, H, L):
-    """Algorithmic FLOP of one distillation step."""
-    rows_mlp = B * (C + 1) + 4 * P
+def step_flops(B, C, P, F, H, L, rows_student=None):
+    """Algorithmic FLOP of one distillation step; rows_student
+    replaces the reference's B(C+1)+4P student rows by the rows executed (the
+    engine runs the dropout-free student on unique nodes)."""
+    rows_mlp = B * (C + 1) + 4 * P if rows_student is None else rows_student
     rows_pred = B * C + 2 * P
     fwd_mlp = 2 * rows_mlp * (F * H + (L - 1) * H * H)
     fwd_pred = 2 * rows_pred * ((L - 1) * H * H + H)
@@ -107,12 +109,13 @@ def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, 
                        P_total=P_full)
     lin = eng.stu[1]
     A = eng._bufs["H0"]
-    R1 = (b1 - b0) * (eng.args.rw_step * eng.args.hops * (1 + eng.args.ns_rate) + 1) + 4 * (p1 - p0)
+    R1 = eng.last_student_rows
     out = eng._buf("H1", (R1, lin.out_f), eng.dtype)
     a_op = K.operand(A[:R1 * lin.in_f].view(R1, lin.in_f))
     for _ in range(n):
         K.gemm_nt(a_op, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, eng.dc, bias=lin.b, act=K.ACT_RELU)
     torch.cuda.synchronize()
+    print(json.dumps({"dominant_rows": R1, "H": lin.out_f, "launches": n}), flush=True)
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_dominant.json")
@@ -128,9 +131,13 @@ def pmc_traffic(rows, H, dtype):
             p = json.load(f)
     except (OSError, ValueError):
         return None
-    if p.get("rows") != rows or p.get("H") != H or p.get("dtype") != dtype:
+    if p.get("H") != H or p.get("dtype") != dtype or not p.get("rows"):
         return None
-    return p.get("traffic_bytes_per_launch")
+    # the unique-node count varies a little from step to step: scale the measured
+    # launch linearly in M (the A panel and C are M x H, W is fixed) within 5 %
+    if abs(rows - p["rows"]) > 0.05 * p["rows"]:
+        return None
+    return p.get("traffic_bytes_per_launch") * rows / p["rows"]
 
 
 def evaluate(model, pred, data, dev):
@@ -293,18 +300,24 @@ def main():
         return
     loss = eng.end_epoch(opt.steps * P_full)
 
-    # dominant kernel: student layer-2 forward GEMM (rows_mlp x 1024 x 1024, bf16 MFMA)
-    rows_mlp = (b1 - b0) * (C + 1) + 4 * (p1 - p0)
+    # dominant kernel: student layer-2 forward GEMM (rows_exec x 1024 x 1024, bf16 MFMA);
+    # rows_exec = unique nodes of this rank's x[this_target] rows (rows_ref)
+    rows_ref = (b1 - b0) * (C + 1) + 4 * (p1 - p0)
+    rows_exec = eng.last_student_rows or rows_ref
+    rows_all = torch.tensor([float(rows_exec)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(rows_all)
     if not kern_ev:   # graph mode: time the dominant kernel in a few eager steps after the timed region
         for s in range(3):
             one_step(opt.warmup + opt.steps + s, True)
         torch.cuda.synchronize()
     kt = [s.elapsed_time(e) for s, e in kern_ev]
     k_ms = float(np.mean(kt)) if kt else float("nan")
-    k_flop = 2.0 * rows_mlp * H * H
+    k_flop = 2.0 * rows_exec * H * H
     peak = PEAK_BF16_TFLOPS if opt.dtype == "bf16" else PEAK_F32_TFLOPS
     achieved = k_flop / (k_ms * 1e-3) / 1e12
     flop_step = step_flops(B_full, C, P_full, F, H, L)
+    flop_exec = step_flops(B_full, C, P_full, F, H, L, rows_student=float(rows_all.item()))
 
     res = None
     if rank == 0:
@@ -318,12 +331,14 @@ def main():
             "config": {"workload": "ogbl-collab transductive LLP distillation (train_minibatch)", "N": N, "F": F,
                        "hidden": H, "num_layers": L, "anchors_per_step": B_full, "contexts_per_anchor": C,
                        "edges_per_step": P_full, "global_batch": P_full, "parallelism": f"dp{world}",
-                       "step_tflop": flop_step / 1e12, "mfma_util_step": flop_step / (dt / opt.steps) / 1e12 / peak
-                       / world},
-            "roofline": {"bound": "mfma", "kernel": "gemm_nt_bf16_256p student layer-2 forward "
-                         f"({rows_mlp}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": pmc_traffic(rows_mlp, H, opt.dtype),
-                         "algorithmic_bytes": 2.0 * rows_mlp * H * 2 + 2.0 * H * H, "kernel_ms": k_ms},
+                       "step_tflop_reference": flop_step / 1e12, "step_tflop_executed": flop_exec / 1e12,
+                       "student_rows_per_step": {"reference": B_full * (C + 1) + 4 * P_full,
+                                                 "unique_nodes": int(rows_all.item())},
+                       "mfma_util_step": flop_exec / (dt / opt.steps) / 1e12 / peak / world},
+            "roofline": {"bound": "mfma", "kernel": "gemm_nt_bf16_q64 student layer-2 forward "
+                         f"({rows_exec}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": pmc_traffic(rows_exec, H, opt.dtype),
+                         "algorithmic_bytes": 2.0 * rows_exec * H * 2 + 2.0 * H * H, "kernel_ms": k_ms},
             "loss": loss,
             "hipgraph": bool(graph is not None),
         }

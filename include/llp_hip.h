@@ -171,9 +171,28 @@ int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a, const int3
  * pairs).  Deterministic: every dh row is written exactly once.
  *   dh[anchor b]      = sum_c dZ[b*C+c] * h[ctx(b,c)]
  *   dh[ctx(b,c)]      = dZ[b*C+c] * h[anchor b]
- *   dh[src i]         = dZ[B*C+i] * h[dst i],  dh[dst i] = dZ[B*C+i] * h[src i] */
+ *   dh[src i]         = dZ[B*C+i] * h[dst i],  dh[dst i] = dZ[B*C+i] * h[src i]
+ * hidx (may be NULL): h holds unique nodes only, target-layout row r reads h[hidx[r]]
+ * (dh stays in the target layout). */
 int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t H,
-                            const void* dZ, const float* drow, const void* h, void* dh, void* stream);
+                            const void* dZ, const float* drow, const void* h, const int32_t* hidx, void* dh,
+                            void* stream);
+
+/* ---------------------------------------------------------------- unique-node compaction
+ * The student MLP of train_minibatch runs on data.x[this_target] (src/main.py:95-96);
+ * without dropout duplicate rows give identical activations, so the engine runs it
+ * on the unique nodes.  llp_dedup_rows: uniq[0..U) = sorted distinct values of
+ * target[0..R) (U -> *n_unique, device), pos[r] = slot of target[r]; seg_rows =
+ * rows grouped by slot in row order (stable sort), seg_ptr[0..U] = group bounds.
+ * llp_segment_sum_rows: out[u] = sum of src rows of group u (f32 accumulate,
+ * fixed order: deterministic).  llp_gather_i32: out[i] = src[idx[i]]. */
+int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R);
+int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
+                   int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
+                   int64_t workspace_bytes, void* stream);
+int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
+                         const void* src, int64_t ld_src, void* out, int64_t ld_out, void* stream);
+int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
 
 /* Generic scatter form (full-batch train(), src/main.py:173-214, where rows of
  * h repeat): dh[ia[r]] += dZ[r]*h2[ib[r]],  dh[ib[r]] += dZ[r]*h1[ia[r]]

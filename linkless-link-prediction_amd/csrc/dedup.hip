@@ -1,0 +1,206 @@
+// Unique-node compaction of the student's gathered rows (minibatch path).
+//
+// train_minibatch evaluates the student on data.x[this_target] (src/main.py:95-96):
+// ~747k rows per collab step drawn from ~225k distinct nodes (anchors, walk
+// contexts, random negatives and edge endpoints repeat).  Without dropout the
+// MLP is a row-wise function, so duplicate rows produce bit-identical
+// activations: the engine runs the student on the unique nodes and reduces
+// each node's row gradients (a deterministic segmented sum over its rows, in
+// row order) before the student backward.
+#include "llp_common.h"
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+namespace {
+
+__global__ void mark_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ mark) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < R) mark[target[r]] = 1;
+}
+
+// after the exclusive scan: uidx[v] = slot of node v (valid where mark[v] was 1)
+__global__ void compact_kernel(int64_t N, const int32_t* __restrict__ mark, const int32_t* __restrict__ uidx,
+                               int32_t* __restrict__ uniq, int32_t* __restrict__ n_unique) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v < N && mark[v]) uniq[uidx[v]] = (int32_t)v;
+  if (v == N - 1) *n_unique = uidx[v] + mark[v];
+}
+
+__global__ void pos_kernel(int64_t R, const int32_t* __restrict__ target, const int32_t* __restrict__ uidx,
+                           int32_t* __restrict__ pos, int32_t* __restrict__ rows) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < R) {
+    pos[r] = uidx[target[r]];
+    rows[r] = (int32_t)r;
+  }
+}
+
+// seg_ptr[u] = first position of key u in the sorted keys (keys are dense 0..U-1)
+__global__ void seg_ptr_kernel(int64_t R, const int32_t* __restrict__ skeys, int32_t* __restrict__ seg_ptr,
+                               const int32_t* __restrict__ n_unique) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < R && (i == 0 || skeys[i] != skeys[i - 1])) seg_ptr[skeys[i]] = (int32_t)i;
+  if (i == 0) seg_ptr[*n_unique] = (int32_t)R;
+}
+
+template <typename T>
+struct V8;
+template <>
+struct V8<bf16_t> {
+  static constexpr int E = 8;
+  __device__ static void add(float* a, uint4 v) {
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[2 * i] += __uint_as_float(u[i] << 16);
+      a[2 * i + 1] += __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  }
+  __device__ static uint4 pack(const float* a) {
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = (uint32_t)f2bf(a[2 * i]) | ((uint32_t)f2bf(a[2 * i + 1]) << 16);
+    return make_uint4(u[0], u[1], u[2], u[3]);
+  }
+};
+template <>
+struct V8<float> {
+  static constexpr int E = 4;
+  __device__ static void add(float* a, uint4 v) {
+    a[0] += __uint_as_float(v.x); a[1] += __uint_as_float(v.y);
+    a[2] += __uint_as_float(v.z); a[3] += __uint_as_float(v.w);
+  }
+  __device__ static uint4 pack(const float* a) {
+    return make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3]));
+  }
+};
+
+// out[u] = sum over k in [seg_ptr[u], seg_ptr[u+1]) of src[rows[k]] (f32 accumulate,
+// row order): one thread per 16-B column chunk, a block covers 256/cpr segments.
+template <typename T>
+__global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, const int32_t* __restrict__ seg_ptr,
+                                                          const int32_t* __restrict__ rows,
+                                                          const T* __restrict__ src, int64_t lds_,
+                                                          T* __restrict__ out, int64_t ldo) {
+  constexpr int E = V8<T>::E;
+  const int cpr = (int)(H / E);
+  const int spb = 256 / cpr;
+  const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
+  const int64_t u = (int64_t)blockIdx.x * spb + slot;
+  if (slot >= spb || u >= U) return;
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  const int beg = seg_ptr[u], end = seg_ptr[u + 1];
+  int k = beg;
+  for (; k + 1 < end; k += 2) {   // two rows in flight
+    const uint4 v0 = *reinterpret_cast<const uint4*>(src + (int64_t)rows[k] * lds_ + c * E);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(src + (int64_t)rows[k + 1] * lds_ + c * E);
+    V8<T>::add(acc, v0);
+    V8<T>::add(acc, v1);
+  }
+  if (k < end) V8<T>::add(acc, *reinterpret_cast<const uint4*>(src + (int64_t)rows[k] * lds_ + c * E));
+  *reinterpret_cast<uint4*>(out + u * ldo + c * E) = V8<T>::pack(acc);
+}
+
+__global__ void gather_i32_kernel(int64_t n, const int32_t* __restrict__ idx, const int32_t* __restrict__ src,
+                                  int32_t* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+
+size_t scan_bytes(int64_t N) {
+  size_t b = 0;
+  rocprim::exclusive_scan(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)N,
+                          rocprim::plus<int32_t>());
+  return b;
+}
+size_t sort_bytes(int64_t R) {
+  size_t b = 0;
+  rocprim::radix_sort_pairs(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
+                            (int32_t*)nullptr, (unsigned int)R);
+  return b;
+}
+int64_t al256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+}  // namespace
+
+extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) {
+  return 2 * al256((num_nodes + 1) * 4) + 3 * al256(R * 4) + al256((int64_t)scan_bytes(num_nodes)) +
+         al256((int64_t)sort_bytes(R)) + 512;
+}
+
+extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
+                              int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
+                              int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(target && uniq && pos && n_unique && seg_ptr && seg_rows && workspace, "llp_dedup_rows: null");
+  LLP_CHECK_ARG(num_nodes > 0 && num_nodes < (1ll << 31) && R > 0 && R < (1ll << 31), "llp_dedup_rows: sizes");
+  LLP_CHECK_ARG(workspace_bytes >= llp_dedup_rows_workspace_bytes(num_nodes, R), "llp_dedup_rows: workspace");
+  hipStream_t s = (hipStream_t)stream;
+  char* w = reinterpret_cast<char*>(workspace);
+  int32_t* mark = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  int32_t* uidx = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  int32_t* keys_out = reinterpret_cast<int32_t*>(w);
+  w += al256(R * 4);
+  int32_t* rows_in = reinterpret_cast<int32_t*>(w);
+  w += al256(R * 4);
+  w += al256(R * 4);   // spare
+  void* scan_tmp = w;
+  size_t scan_b = scan_bytes(num_nodes);
+  w += al256((int64_t)scan_b);
+  void* sort_tmp = w;
+  size_t sort_b = sort_bytes(R);
+
+  hipError_t e = hipMemsetAsync(mark, 0, (size_t)num_nodes * 4, s);
+  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
+  hipLaunchKernelGGL(mark_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, mark);
+  LLP_LAUNCH_CHECK();
+  e = rocprim::exclusive_scan(scan_tmp, scan_b, mark, uidx, 0, (size_t)num_nodes, rocprim::plus<int32_t>(), s);
+  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: scan");
+  hipLaunchKernelGGL(compact_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, mark, uidx, uniq,
+                     n_unique);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pos_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, pos, rows_in);
+  LLP_LAUNCH_CHECK();
+  // stable sort of the rows by their unique slot: each node's rows stay in row order
+  int bits = 1;
+  while ((1ll << bits) < num_nodes) ++bits;
+  e = rocprim::radix_sort_pairs(sort_tmp, sort_b, pos, keys_out, rows_in, seg_rows, (unsigned int)R, 0, bits, s);
+  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: sort");
+  hipLaunchKernelGGL(seg_ptr_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, keys_out, seg_ptr, n_unique);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
+                                    const void* src, int64_t ld_src, void* out, int64_t ld_out, void* stream) {
+  LLP_CHECK_ARG(seg_ptr && rows && src && out, "llp_segment_sum_rows: null");
+  const int E = dtype == LLP_BF16 ? 8 : 4;
+  const int es = dtype == LLP_BF16 ? 2 : 4;
+  LLP_CHECK_ARG(H % E == 0 && H / E <= 256 && (ld_src * es) % 16 == 0 && (ld_out * es) % 16 == 0 &&
+                    (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0,
+                "llp_segment_sum_rows: rows must be 16-B aligned, H <= 256 chunks");
+  if (U == 0) return LLP_OK;
+  const int64_t cpr = H / E, spb = 256 / cpr;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(segment_sum_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
+                       (const bf16_t*)src, ld_src, (bf16_t*)out, ld_out);
+  else
+    hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
+                       (const float*)src, ld_src, (float*)out, ld_out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream) {
+  LLP_CHECK_ARG(idx && src && out, "llp_gather_i32: null");
+  if (n == 0) return LLP_OK;
+  hipLaunchKernelGGL(gather_i32_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, idx, src,
+                     out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}

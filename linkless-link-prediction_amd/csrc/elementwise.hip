@@ -101,10 +101,14 @@ __global__ __launch_bounds__(256) void hadamard_bwd_blocks_vec_kernel(int64_t B,
                                                                        int64_t anchor_blocks,
                                                                        const T* __restrict__ dZ,
                                                                        const float* __restrict__ drow,
-                                                                       const T* __restrict__ h, T* __restrict__ dh) {
+                                                                       const T* __restrict__ h,
+                                                                       const int32_t* __restrict__ hidx,
+                                                                       T* __restrict__ dh) {
   constexpr int E = 16 / sizeof(T);
   const int cpr = (int)(H / E);
   const int64_t C1 = C + 1;
+  // h row of target-layout row r: r itself, or hidx[r] when h holds unique nodes only
+  auto hrow = [&](int64_t r) -> int64_t { return hidx ? (int64_t)hidx[r] : r; };
   if ((int64_t)blockIdx.x < anchor_blocks) {
     const int apb = 256 / cpr;
     const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(256) void hadamard_bwd_blocks_vec_kernel(int64_t B,
     if (slot >= apb || b >= B) return;
     const int64_t col = (int64_t)c * E;
     Chunk<T> ha;
-    ha.load(h + (b * C1) * H + col);
+    ha.load(h + hrow(b * C1) * H + col);
     float acc[E];
 #pragma unroll
     for (int i = 0; i < E; ++i) acc[i] = 0.f;
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(256) void hadamard_bwd_blocks_vec_kernel(int64_t B,
       const int64_t r = b * C + cc;
       Chunk<T> d, hc;
       if (drow) d.fill(drow[r]); else d.load(dZ + r * H + col);
-      hc.load(h + (b * C1 + 1 + cc) * H + col);
+      hc.load(h + hrow(b * C1 + 1 + cc) * H + col);
       float o[E];
 #pragma unroll
       for (int i = 0; i < E; ++i) {
@@ -139,8 +143,8 @@ __global__ __launch_bounds__(256) void hadamard_bwd_blocks_vec_kernel(int64_t B,
     const int64_t r = B * C + i;
     Chunk<T> d, hs, hd;
     if (drow) d.fill(drow[r]); else d.load(dZ + r * H + col);
-    hs.load(h + (base + i) * H + col);
-    hd.load(h + (base + L2 + i) * H + col);
+    hs.load(h + hrow(base + i) * H + col);
+    hd.load(h + hrow(base + L2 + i) * H + col);
     float o1[E], o2[E];
 #pragma unroll
     for (int k = 0; k < E; ++k) {
@@ -392,7 +396,8 @@ int64_t max_chunks_of(int64_t max_numel) { return (max_numel + OPT_CHUNK - 1) / 
 }  // namespace
 
 extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t H, const void* dZ,
-                                       const float* drow, const void* h, void* dh, void* stream) {
+                                       const float* drow, const void* h, const int32_t* hidx, void* dh,
+                                       void* stream) {
   LLP_CHECK_ARG((dZ || drow) && h && dh, "llp_hadamard_bwd_blocks: null pointer");
   const int64_t nblk = B + (L2 + 63) / 64;
   if (nblk == 0) return LLP_OK;
@@ -402,6 +407,7 @@ extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t 
     const int64_t cpr = H * es / 16;
     const bool vec = (H * es) % 16 == 0 && cpr <= 256 && (uintptr_t)h % 16 == 0 && (uintptr_t)dh % 16 == 0 &&
                      (!dZ || (uintptr_t)dZ % 16 == 0);
+    LLP_CHECK_ARG(vec || !hidx, "llp_hadamard_bwd_blocks: hidx needs 16-B aligned rows");
     if (vec) {
       const int64_t apb = 256 / cpr;
       const int64_t ab = (B + apb - 1) / apb;
@@ -409,10 +415,10 @@ extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t 
       if (ab + lb == 0) return LLP_OK;
       if (dtype == LLP_BF16)
         hipLaunchKernelGGL(hadamard_bwd_blocks_vec_kernel<bf16_t>, dim3((unsigned)(ab + lb)), dim3(256), 0, s, B, C,
-                           L2, H, ab, (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh);
+                           L2, H, ab, (const bf16_t*)dZ, drow, (const bf16_t*)h, hidx, (bf16_t*)dh);
       else
         hipLaunchKernelGGL(hadamard_bwd_blocks_vec_kernel<float>, dim3((unsigned)(ab + lb)), dim3(256), 0, s, B, C,
-                           L2, H, ab, (const float*)dZ, drow, (const float*)h, (float*)dh);
+                           L2, H, ab, (const float*)dZ, drow, (const float*)h, hidx, (float*)dh);
       LLP_LAUNCH_CHECK();
       return LLP_OK;
     }

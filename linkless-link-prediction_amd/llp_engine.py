@@ -346,8 +346,13 @@ class DistillEngine(EngineBase):
     """
 
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
-                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None):
+                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
+        # run the dropout-free student on unique nodes (step_minibatch); off inside
+        # hipGraph capture, which cannot take the host read of the unique count
+        self.dedup = bool(dedup)
+        self._capturing = False
+        self.last_student_rows = 0
         self.args = args
         self.N = int(num_nodes)
 
@@ -443,19 +448,41 @@ class DistillEngine(EngineBase):
         t_ib = self._buf("t_ib", (B * C,), torch.int32)
         K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
         ia, ib = self._rows_index(B, C, n_lab)
+        p_drop = float(a.dropout)
+
+        # ---- unique-node compaction: without dropout the student is a row-wise
+        # function, so duplicate rows of x[this_target] give identical activations;
+        # run it on the U distinct nodes and sum each node's row gradients.
+        dedup = self.dedup and p_drop == 0.0 and not self._capturing
+        if dedup:
+            uniq = self._buf("uniq", (R1,), torch.int32)
+            pos = self._buf("pos", (R1,), torch.int32)
+            n_u = self._buf("n_unique", (1,), torch.int32)
+            seg_ptr = self._buf("seg_ptr", (R1 + 1,), torch.int32)
+            seg_rows = self._buf("seg_rows", (R1,), torch.int32)
+            wsd = self._buf("ws_dedup", (K.dedup_ws_bytes(self.N, R1) // 4 + 16,), torch.float32)
+            K.dedup_rows(self.N, R1, target, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
+            ia_h = self._buf("ia_u", (R2,), torch.int32)
+            ib_h = self._buf("ib_u", (R2,), torch.int32)
+            K.gather_i32(ia, pos, ia_h)
+            K.gather_i32(ib, pos, ib_h)
+            U = int(n_u.item())                 # one host read: the student GEMMs are sized by it
+            rows_s, gather_s = U, uniq[:U]
+        else:
+            rows_s, gather_s, ia_h, ib_h = R1, target, ia, ib
+        self.last_student_rows = rows_s
 
         # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
         acts = []
-        A = K.operand(self.x, target)
-        p_drop = float(a.dropout)
+        A = K.operand(self.x, gather_s)
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
-            out = self._buf(f"H{l}", (R1, lin.out_f), dt)
+            out = self._buf(f"H{l}", (rows_s, lin.out_f), dt)
             timed = kernel_events is not None and l == 1
             if timed:   # the dominant MFMA kernel, timed on the launch stream (bench.py roofline)
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            K.gemm_nt(A, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, dc, bias=lin.b,
+            K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.in_f, out, dc, bias=lin.b,
                       act=K.ACT_NONE if last else K.ACT_RELU,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             if timed:
@@ -467,7 +494,7 @@ class DistillEngine(EngineBase):
 
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
         logit = self._buf("logit", (R2,), torch.float32)
-        A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop)
+        A0, zacts = self._predictor_forward(h, ia_h, ib_h, R2, logit, p_drop)
 
         # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
         t_r = self._buf("t_r", (B * C,), torch.float32)
@@ -484,12 +511,18 @@ class DistillEngine(EngineBase):
 
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
-        dh = self._buf("gS0", (R1, H), dt)
+        dh_rows = self._buf("dh_rows" if dedup else "gS0", (R1, H), dt)
+        hidx = pos if dedup else None
         if self.predictor_kind == "mlp":
-            K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0, h, dh)
+            K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0, h, dh_rows, hidx=hidx)
         else:
-            K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh, drow=dlogit)
-        self._student_backward(dh, R1, target, acts, p_drop)
+            K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh_rows, drow=dlogit, hidx=hidx)
+        if dedup:
+            dh = self._buf("gS0", (rows_s, H), dt)
+            K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh)
+        else:
+            dh = dh_rows
+        self._student_backward(dh, rows_s, gather_s, acts, p_drop)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
@@ -616,8 +649,12 @@ class DistillEngine(EngineBase):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.graph(g, stream=s):
-            self.step_minibatch(anchors, link_ids, pairs, **kw)
+        self._capturing = True
+        try:
+            with torch.cuda.graph(g, stream=s):
+                self.step_minibatch(anchors, link_ids, pairs, **kw)
+        finally:
+            self._capturing = False
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g
 

@@ -62,7 +62,11 @@ _SIGS = {
     "llp_llp_loss_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_llp_loss": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32,
                              c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_vp]),
-    "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_dedup_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "llp_gather_i32": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_hadamard_bwd_scatter": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_context_sampler": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
                                     c_i64, c_vp, c_vp]),
@@ -240,10 +244,34 @@ def llp_loss(B, Cc, s_logit, t_prob, n_lab, n_pos, out_logit, B_total, n_lab_tot
                          ws.numel() * ws.element_size(), stream_ptr()), "llp_llp_loss")
 
 
-def hadamard_bwd_blocks(B, Cc, L2, H, dZ, h, dh, drow=None):
+def hadamard_bwd_blocks(B, Cc, L2, H, dZ, h, dh, drow=None, hidx=None):
     L = lib()
-    check(L.llp_hadamard_bwd_blocks(dtype_code(h.dtype), B, Cc, L2, H, ptr(dZ), ptr(drow), h.data_ptr(),
+    check(L.llp_hadamard_bwd_blocks(dtype_code(h.dtype), B, Cc, L2, H, ptr(dZ), ptr(drow), h.data_ptr(), ptr(hidx),
                                     dh.data_ptr(), stream_ptr()), "llp_hadamard_bwd_blocks")
+
+
+def dedup_ws_bytes(num_nodes, R):
+    return load().llp_dedup_rows_workspace_bytes(num_nodes, R)
+
+
+def dedup_rows(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, ws):
+    L = lib()
+    check(L.llp_dedup_rows(num_nodes, R, target.data_ptr(), uniq.data_ptr(), pos.data_ptr(), n_unique.data_ptr(),
+                           seg_ptr.data_ptr(), seg_rows.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
+                           stream_ptr()), "llp_dedup_rows")
+
+
+def segment_sum_rows(U, seg_ptr, rows, src, out):
+    L = lib()
+    check(L.llp_segment_sum_rows(dtype_code(src.dtype), U, src.shape[1], seg_ptr.data_ptr(), rows.data_ptr(),
+                                 src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), stream_ptr()),
+          "llp_segment_sum_rows")
+
+
+def gather_i32(idx, src, out):
+    L = lib()
+    check(L.llp_gather_i32(idx.numel(), idx.data_ptr(), src.data_ptr(), out.data_ptr(), stream_ptr()),
+          "llp_gather_i32")
 
 
 def hadamard_rows(a, ia, b, ib, out):

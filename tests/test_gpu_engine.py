@@ -121,3 +121,40 @@ def test_engine_replays_reference_minibatch(name):
         d = (p.detach().cpu() - ref).abs()
         assert (d <= 1e-4).float().mean().item() > 0.99, (name, tuple(p.shape), d.max().item())
         assert d.max().item() <= 2 * lr * len(case.steps), (name, tuple(p.shape), d.max().item())
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_engine_unique_node_student_matches_rowwise(dtype):
+    """The dropout-free student run on unique nodes (default) gives the same loss
+    terms (forward rows are identical) and the same gradients up to summation
+    order as the row-wise student on x[this_target]."""
+    import types
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, F_, H, L = 3000, 128, 256, 3
+    args = types.SimpleNamespace(rw_step=3, hops=3, ns_rate=3, ps_method="nb", dropout=0.0, margin=0.01,
+                                 LLP_D=1.0, LLP_R=1.0, True_label=1.0, predictor="mlp", lr=0.001)
+    g = torch.Generator().manual_seed(0)
+    u = torch.randint(0, N, (20000,), generator=g)
+    v = torch.randint(0, N, (20000,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
+    x = torch.randn(N, F_, generator=g) * 0.3
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    res = {}
+    for dd in (False, True):
+        eng, model, pred = _make_engine(dtype, N, F_, H, L, 3, args, x, t_h, ei)
+        eng.dedup = dd
+        anchors = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:300].to(torch.int32).to(DEV)
+        link = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(2))[:2048]
+        eng.step_minibatch(anchors, link.to(torch.int32).to(DEV), pairs.to(torch.int32).to(DEV))
+        torch.cuda.synchronize()
+        res[dd] = (eng.terms.cpu().clone(), [p.grad.detach().cpu().clone() for p in
+                                             list(model.parameters()) + list(pred.parameters())],
+                   eng.last_student_rows)
+    assert res[True][2] < res[False][2]
+    assert torch.equal(res[True][0][:4], res[False][0][:4])     # identical forward
+    for a, b in zip(res[True][1], res[False][1]):
+        tol = 1e-4 if dtype == "fp32" else 3e-2
+        assert (a - b).abs().max().item() <= tol * max(b.abs().max().item(), 1e-6), (tuple(a.shape),)

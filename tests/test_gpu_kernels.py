@@ -394,3 +394,39 @@ def test_clip_and_adam_match_oracle():
     assert step.item() == 3
     for a, b in zip(dp, cur):
         assert torch.allclose(a.cpu(), b, rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------ unique-node compaction
+@pytest.mark.parametrize("N,R", [(50, 1000), (235868, 20000), (7, 7)])
+def test_dedup_rows_and_segment_sum(N, R):
+    k = K()
+    g = torch.Generator().manual_seed(R)
+    target = torch.randint(0, N, (R,), generator=g, dtype=torch.int32)
+    tg = target.to(DEV)
+    uniq = torch.empty(R, dtype=torch.int32, device=DEV)
+    pos = torch.empty(R, dtype=torch.int32, device=DEV)
+    nu = torch.empty(1, dtype=torch.int32, device=DEV)
+    segp = torch.empty(R + 1, dtype=torch.int32, device=DEV)
+    segr = torch.empty(R, dtype=torch.int32, device=DEV)
+    ws = torch.empty(k.dedup_ws_bytes(N, R) // 4 + 16, device=DEV)
+    k.dedup_rows(N, R, tg, uniq, pos, nu, segp, segr, ws)
+    torch.cuda.synchronize()
+    u_ref, inv = np.unique(target.numpy(), return_inverse=True)
+    U = int(nu.item())
+    assert U == u_ref.size
+    assert np.array_equal(uniq[:U].cpu().numpy(), u_ref)
+    assert np.array_equal(pos.cpu().numpy(), inv)
+    rows_ref = np.argsort(inv, kind="stable")          # rows grouped by slot, in row order
+    assert np.array_equal(segr.cpu().numpy(), rows_ref)
+    assert np.array_equal(segp[:U + 1].cpu().numpy(), np.concatenate([[0], np.cumsum(np.bincount(inv))]))
+    for dt in (torch.float32, torch.bfloat16):
+        src = torch.randn(R, 64, generator=g).to(DEV, dt)
+        out = torch.empty(U, 64, device=DEV, dtype=dt)
+        k.segment_sum_rows(U, segp, segr, src, out)
+        ref = torch.zeros(U, 64).index_add_(0, torch.from_numpy(inv).long(), src.float().cpu())
+        tol = 1e-5 if dt == torch.float32 else 2e-2
+        assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * max(1.0, ref.abs().max().item()))
+    idx = torch.randint(0, R, (333,), generator=g, dtype=torch.int32)
+    o = torch.empty(333, dtype=torch.int32, device=DEV)
+    k.gather_i32(idx.to(DEV), pos, o)
+    assert np.array_equal(o.cpu().numpy(), inv[idx.numpy()])

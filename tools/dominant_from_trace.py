@@ -8,6 +8,8 @@ import csv
 import json
 import sys
 
+KERNEL = "gemm_nt_bf16_q64"
+
 
 def main():
     path = sys.argv[1]
@@ -22,11 +24,11 @@ def main():
         if "context_walk_kernel" in name:
             k = 0
             continue
-        if k is not None and "gemm_nt_bf16_256p" in name:
+        if k is not None and KERNEL in name:
             k += 1
             if k == 2:
                 durs.append(e - s)
-    out = {"kernel": "gemm_nt_bf16_256p (student layer-2 forward, 2nd NT launch of each step)",
+    out = {"kernel": KERNEL + " (student layer-2 forward, 2nd NT launch of each step)",
            "launches": len(durs), "avg_ms": sum(durs) / len(durs) / 1e6 if durs else None,
            "min_ms": min(durs) / 1e6 if durs else None, "max_ms": max(durs) / 1e6 if durs else None,
            "source": path}
