@@ -1,0 +1,49 @@
+"""Reference point: torch.mm (hipBLASLt) vs the hand-written NT/TN kernels at
+the step's GEMM shapes, same random bf16 data, interleaved rounds."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
+import torch  # noqa: E402
+
+import llp_hip as K  # noqa: E402
+
+
+def t(fn, it=10):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it
+
+
+def main():
+    dev = "cuda"
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    for M in (603_032, 225_384):
+        A = torch.randn(M, 1024, device=dev, dtype=bf, generator=g)
+        W = (torch.randn(1024, 1024, device=dev, generator=g) * 0.03).to(bf)
+        out = torch.empty(M, 1024, device=dev, dtype=bf)
+        Wt = W.t().contiguous()
+        ws = torch.empty(K.gemm_tn_ws_bytes(1, M, 1024, 1024) // 4 + 16, device=dev)
+        gW = torch.empty(1024, 1024, device=dev)
+        f = 2 * M * 1024 * 1024
+        res = {}
+        for r in range(3):
+            for name, fn in (("ours NT", lambda: K.gemm_nt(K.operand(A), K.operand(W), M, 1024, 1024, out, 1)),
+                             ("torch mm NT", lambda: torch.mm(A, Wt, out=out)),
+                             ("ours TN", lambda: K.gemm_tn(K.operand(A), K.operand(A), M, 1024, 1024, gW, 1, ws)),
+                             ("torch mm TN", lambda: torch.mm(A.t(), A))):
+                res.setdefault(name, []).append(t(fn))
+        for name, v in res.items():
+            ms = sorted(v)[1]
+            print(f"M={M:7d} {name:12s} {ms:.3f} ms {f / ms / 1e9:.0f} TF", flush=True)
+
+
+if __name__ == "__main__":
+    main()
