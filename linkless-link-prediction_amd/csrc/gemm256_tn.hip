@@ -200,7 +200,11 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
 
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  int64_t splits = (768 + tiles - 1) / tiles;
+  static const int64_t target = [] {
+    const char* e = getenv("LLP_TN_BLOCKS");   // tuning knob: blocks per launch
+    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)256;
+  }();
+  int64_t splits = (target + tiles - 1) / tiles;
   const int64_t maxs = (M + TKM * 16 - 1) / (TKM * 16);   // >= 16 m-steps per split
   if (splits > maxs) splits = maxs;
   return splits < 1 ? 1 : splits;

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, con
 // write fused in.  Vector form: a row is cpr 16-byte chunks; 256 threads
 // cover rpp = 256 / cpr rows per pass and a block walks HB_ROWS rows; the rpp
 // partial rows are combined in LDS and one slab row [blk][H] is written.
-constexpr int HB_ROWS = 2048;
+constexpr int HB_ROWS = 512;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
                                                          const float* __restrict__ weight,
@@ -253,41 +253,50 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
   float wv[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) wv[i] = (w && active) ? alpha * w[c * CH + i] : alpha;
-  if (active) {
-    for (int64_t r = r0 + rl; r < r1; r += rpp) {
-      const uint4 raw = *reinterpret_cast<const uint4*>(Z + r * ldz + (int64_t)c * CH);
-      float z[CH];
-      if constexpr (sizeof(T) == 2) {
-        const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
+  // four rows in flight per lane: issue the loads, then consume them in order
+  auto consume = [&](int64_t r, const uint4 raw) {
+    float z[CH];
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          z[2 * i] = __uint_as_float(u[i] << 16);
-          z[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
-        }
-      } else {
-        z[0] = __uint_as_float(raw.x); z[1] = __uint_as_float(raw.y);
-        z[2] = __uint_as_float(raw.z); z[3] = __uint_as_float(raw.w);
+      for (int i = 0; i < 4; ++i) {
+        z[2 * i] = __uint_as_float(u[i] << 16);
+        z[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
       }
-      const float g = weight ? weight[r] : 1.f;
-      accb += g;
-#pragma unroll
-      for (int i = 0; i < CH; ++i) acc[i] += g * z[i];
-      if (dZ) {
-        float d[CH];
-#pragma unroll
-        for (int i = 0; i < CH; ++i) d[i] = (relu_mask && !(z[i] > 0.f)) ? 0.f : g * wv[i];
-        uint4 o;
-        if constexpr (sizeof(T) == 2) {
-          o.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
-          o.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
-          o.z = (uint32_t)f2bf(d[4]) | ((uint32_t)f2bf(d[5]) << 16);
-          o.w = (uint32_t)f2bf(d[6]) | ((uint32_t)f2bf(d[7]) << 16);
-        } else {
-          o = make_uint4(__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3]));
-        }
-        *reinterpret_cast<uint4*>(dZ + r * lddz + (int64_t)c * CH) = o;
-      }
+    } else {
+      z[0] = __uint_as_float(raw.x); z[1] = __uint_as_float(raw.y);
+      z[2] = __uint_as_float(raw.z); z[3] = __uint_as_float(raw.w);
     }
+    const float g = weight ? weight[r] : 1.f;
+    accb += g;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) acc[i] += g * z[i];
+    if (dZ) {
+      float d[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) d[i] = (relu_mask && !(z[i] > 0.f)) ? 0.f : g * wv[i];
+      uint4 o;
+      if constexpr (sizeof(T) == 2) {
+        o.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
+        o.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
+        o.z = (uint32_t)f2bf(d[4]) | ((uint32_t)f2bf(d[5]) << 16);
+        o.w = (uint32_t)f2bf(d[6]) | ((uint32_t)f2bf(d[7]) << 16);
+      } else {
+        o = make_uint4(__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3]));
+      }
+      *reinterpret_cast<uint4*>(dZ + r * lddz + (int64_t)c * CH) = o;
+    }
+  };
+  if (active) {
+    int64_t r = r0 + rl;
+    for (; r + 3 * rpp < r1; r += 4 * rpp) {
+      uint4 raw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) raw[j] = *reinterpret_cast<const uint4*>(Z + (r + j * rpp) * ldz + (int64_t)c * CH);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) consume(r + j * rpp, raw[j]);
+    }
+    for (; r < r1; r += rpp) consume(r, *reinterpret_cast<const uint4*>(Z + r * ldz + (int64_t)c * CH));
   }
   // combine the rpp row-lanes (fixed order -> deterministic)
   if (active)
@@ -340,19 +349,21 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const
   }
 }
 
-// out[n] (+)= sum_i slab[i][n]: 64 columns x 4 slab-lanes per block, fixed order.
+// out[n] (+)= sum_i slab[i][n]: 16 columns x 16 slab-lanes per block, fixed order.
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int64_t nslab, int64_t H,
                                                        float* __restrict__ out, int accumulate) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int64_t n = (int64_t)blockIdx.x * 64 + cl;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t n = (int64_t)blockIdx.x * 16 + cl;
   float s = 0.f;
   if (n < H)
-    for (int64_t i = sl; i < nslab; i += 4) s += slab[i * H + n];
+    for (int64_t i = sl; i < nslab; i += 16) s += slab[i * H + n];
   red[sl][cl] = s;
   __syncthreads();
   if (sl == 0 && n < H) {
-    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][cl];
     out[n] = accumulate ? out[n] + v : v;
   }
 }
@@ -449,7 +460,7 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
     LLP_LAUNCH_CHECK();
   }
   if (dw) {
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, 64)), dim3(256), 0, s, slab, ns, H, dw, accumulate);
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, 16)), dim3(256), 0, s, slab, ns, H, dw, accumulate);
     LLP_LAUNCH_CHECK();
   }
   if (db) {
