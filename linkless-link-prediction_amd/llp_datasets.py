@@ -90,6 +90,36 @@ def synthetic_transductive(name: str, seed: int = 0):
     return data, split_edge
 
 
+def _coalesce(edge_index: torch.Tensor, N: int) -> torch.Tensor:
+    """Sorted by (row, col), duplicates removed — the layout PyG datasets ship."""
+    key = torch.unique(edge_index[0].long() * N + edge_index[1].long())
+    return torch.stack([key // N, key % N], 0)
+
+
+def load_graph(name: str, dataset_dir: str, synthetic: bool, seed: int = 0):
+    """The whole graph (``get_dataset(...)[0]`` of src/utils.py:31-53) as a
+    llp_split.GraphData(x, edge_index) with both directions of every edge —
+    the input of the production split.  From ``<dataset_dir>/<ds>.pt``
+    ('edge_index', else train+valid+test edges) or ``--synthetic``."""
+    import llp_split
+    path = os.path.join(dataset_dir, name + ".pt")
+    if os.path.exists(path):
+        b = torch.load(path, weights_only=True)
+        x = b["x"].float()
+        if "edge_index" in b:
+            ei = b["edge_index"].long()
+        else:
+            se = b["split_edge"]
+            und = torch.cat([se[s]["edge"] for s in ("train", "valid", "test")], 0).long().t()
+            ei = torch.cat([und, und.flip([0])], -1)
+    elif synthetic:
+        data, _ = synthetic_transductive(name, seed)
+        x, ei = data.x, data.edge_index.long()
+    else:
+        raise FileNotFoundError(f"{path} not found (or pass --synthetic)")
+    return llp_split.GraphData(x, _coalesce(ei, x.size(0)))
+
+
 def load_transductive(name: str, dataset_dir: str, synthetic: bool, seed: int = 0):
     path = os.path.join(dataset_dir, name + ".pt")
     if os.path.exists(path):

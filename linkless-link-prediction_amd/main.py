@@ -20,8 +20,9 @@ import numpy as np
 import torch
 
 import llp_datasets
+import llp_split
 import llp_train
-from logger import Logger
+from logger import Logger, ProductionLogger
 from models import MLP, LinkPredictor
 
 
@@ -107,6 +108,30 @@ def _write_summary(path, loggers, transductive):
                     f.write(f'{n}: {b[:, i].mean():.2f} ± {b[:, i].std():.2f}' + ('\n' if i == 4 else ''))
 
 
+def print_epoch(results, run, epoch, loss, transductive):
+    """Per-epoch lines of src/main.py:435-456 (train_teacher_gnn.py:463-487)."""
+    for key, result in results.items():
+        print(key)
+        if transductive:
+            valid_hits, test_hits = result
+            print(f'Run: {run + 1:02d}, '
+                  f'Epoch: {epoch:02d}, '
+                  f'Loss: {loss:.4f}, '
+                  f'Valid: {100 * valid_hits:.2f}%, '
+                  f'Test: {100 * test_hits:.2f}%')
+        else:
+            valid_hits, test_hits, old_old, old_new, new_new = result
+            print(f'Run: {run + 1:02d}, '
+                  f'Epoch: {epoch:02d}, '
+                  f'Loss: {loss:.4f}, '
+                  f'valid: {100 * valid_hits:.2f}%, '
+                  f'test: {100 * test_hits:.2f}%, '
+                  f'old_old: {100 * old_old:.2f}%, '
+                  f'old_new: {100 * old_new:.2f}%, '
+                  f'new_new: {100 * new_new:.2f}%')
+    print('---')
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     print(args)
@@ -121,15 +146,25 @@ def main(argv=None):
     device = torch.device(f'cuda:{args.device}')
     torch.cuda.set_device(device)
 
-    if args.transductive != "transductive":
-        raise NotImplementedError("production split needs ../data/<ds>_production.pkl of PyG Data objects, which "
-                                  "cannot be loaded without torch_geometric (SURVEY §8f2-3: next)")
-    data, split_edge = llp_datasets.load_transductive(args.datasets, args.dataset_dir, args.synthetic)
-    args.metric = 'Hits@50' if args.datasets == "collab" else 'Hits@20'
-    input_size = data.x.size(1)
-    if not args.minibatch:
-        data.x = data.x.to(device)
-    args.node_batch_size = int(data.x.size(0) / (split_edge['train']['edge'].size(0) / args.link_batch_size))
+    transductive = args.transductive == "transductive"
+    if transductive:
+        data, split_edge = llp_datasets.load_transductive(args.datasets, args.dataset_dir, args.synthetic)
+        args.metric = 'Hits@50' if args.datasets == "collab" else 'Hits@20'
+        input_size = data.x.size(1)
+        if not args.minibatch:
+            data.x = data.x.to(device)
+        args.node_batch_size = int(data.x.size(0) / (split_edge['train']['edge'].size(0) / args.link_batch_size))
+    else:
+        # src/main.py:337-346: the split train_teacher_gnn.py cached (made here when absent)
+        training_data, val_data, inference_data, data, test_edge_bundle, negative_samples = \
+            llp_split.production_split(args.datasets, args.dataset_dir, args.synthetic)
+        input_size = training_data.x.size(1)
+        if not args.minibatch:
+            training_data.to(device)
+        val_data.to(device)
+        inference_data.to(device)
+        args.node_batch_size = int(training_data.x.size(0) /
+                                   (training_data.edge_index.size(1) / args.link_batch_size))
 
     model = MLP(args.num_layers, input_size, args.hidden_channels, args.hidden_channels, args.dropout).to(device)
     predictor = LinkPredictor(args.predictor, args.hidden_channels, args.hidden_channels, 1, args.num_layers,
@@ -143,9 +178,12 @@ def main(argv=None):
     for p in teacher_predictor.parameters():
         p.requires_grad = False
 
-    Ks = ('Hits@10', 'Hits@50', 'Hits@100') if args.datasets == "collab" else \
-        ('Hits@10', 'Hits@20', 'Hits@30', 'Hits@50')
-    loggers = {k: Logger(args.runs, args) for k in Ks + ('AUC',)}
+    if not transductive:
+        loggers = {k: ProductionLogger(args.runs, args) for k in ('Hits@10', 'Hits@20', 'Hits@30', 'Hits@50', 'AUC')}
+    else:
+        Ks = ('Hits@10', 'Hits@50', 'Hits@100') if args.datasets == "collab" else \
+            ('Hits@10', 'Hits@20', 'Hits@30', 'Hits@50')
+        loggers = {k: Logger(args.runs, args) for k in Ks + ('AUC',)}
 
     for run in range(args.runs):
         seed_everything(run + 1)
@@ -155,10 +193,17 @@ def main(argv=None):
         cnt_wait = 0
         best_val = 0.0
         for epoch in range(1, 1 + args.epochs):
-            fn = llp_train.train_minibatch if args.minibatch else llp_train.train
-            loss = fn(model, predictor, t_h, teacher_predictor, data, split_edge, optimizer, args, device)
-            results, h = llp_train.test_transductive(model, predictor, data, split_edge, None, args.link_batch_size,
-                                                     'mlp', args.datasets, args)
+            if transductive:
+                fn = llp_train.train_minibatch if args.minibatch else llp_train.train
+                loss = fn(model, predictor, t_h, teacher_predictor, data, split_edge, optimizer, args, device)
+                results, h = llp_train.test_transductive(model, predictor, data, split_edge, None,
+                                                         args.link_batch_size, 'mlp', args.datasets, args)
+            else:   # src/main.py:420-423: full-batch train() in the production setting
+                loss = llp_train.train(model, predictor, t_h, teacher_predictor, training_data, None, optimizer,
+                                       args, device)
+                results, h = llp_train.test_production(model, predictor, val_data, inference_data,
+                                                       test_edge_bundle, negative_samples, None,
+                                                       args.link_batch_size, 'mlp', args.datasets)
             if results[args.metric][0] >= best_val:
                 best_val = results[args.metric][0]
                 cnt_wait = 0
@@ -167,22 +212,14 @@ def main(argv=None):
             for key, result in results.items():
                 loggers[key].add_result(run, result)
             if epoch % args.log_steps == 0:
-                for key, result in results.items():
-                    valid_hits, test_hits = result
-                    print(key)
-                    print(f'Run: {run + 1:02d}, '
-                          f'Epoch: {epoch:02d}, '
-                          f'Loss: {loss:.4f}, '
-                          f'Valid: {100 * valid_hits:.2f}%, '
-                          f'Test: {100 * test_hits:.2f}%')
-                print('---')
+                print_epoch(results, run, epoch, loss, transductive)
             if cnt_wait >= args.patience:
                 break
         for key in loggers.keys():
             print(key)
             loggers[key].print_statistics(run)
 
-    _write_summary(logger_file, loggers, True)
+    _write_summary(logger_file, loggers, transductive)
 
 
 if __name__ == "__main__":

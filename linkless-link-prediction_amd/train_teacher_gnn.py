@@ -15,10 +15,11 @@ import os
 import torch
 
 import llp_datasets
+import llp_split
 import llp_train
 from llp_sage import SAGEConv, SAGEConv_updated
-from logger import Logger
-from main import seed_everything, _write_summary
+from logger import Logger, ProductionLogger
+from main import print_epoch, seed_everything, _write_summary
 from models import MLP, SAGE, LinkPredictor
 
 
@@ -62,14 +63,21 @@ def main(argv=None):
         raise RuntimeError("the LLP trainer runs on an MI355X (HIP device) only — no CPU fallback")
     device = torch.device(f'cuda:{args.device}')
     torch.cuda.set_device(device)
-    if args.transductive != "transductive":
-        raise NotImplementedError("production split needs ../data/<ds>_production.pkl of PyG Data objects, which "
-                                  "cannot be loaded without torch_geometric (SURVEY §8f2-3: next)")
-
-    data, split_edge = llp_datasets.load_transductive(args.datasets, args.dataset_dir, args.synthetic)
-    args.metric = 'Hits@50' if args.datasets == "collab" else 'Hits@20'
-    data.x = data.x.to(device)
-    input_size = data.x.size(1)
+    transductive = args.transductive == "transductive"
+    if transductive:
+        data, split_edge = llp_datasets.load_transductive(args.datasets, args.dataset_dir, args.synthetic)
+        args.metric = 'Hits@50' if args.datasets == "collab" else 'Hits@20'
+        data.x = data.x.to(device)
+        input_size = data.x.size(1)
+    else:
+        # src/train_teacher_gnn.py:340-369: load the cached split or make it (seed 234)
+        training_data, val_data, inference_data, _, test_edge_bundle, negative_samples = \
+            llp_split.production_split(args.datasets, args.dataset_dir, args.synthetic)
+        input_size = training_data.x.size(1)
+        args.metric = 'Hits@20'
+        training_data.to(device)
+        val_data.to(device)
+        inference_data.to(device)
 
     if args.encoder == 'sage':
         conv = SAGEConv_updated if args.datasets == "coauthor-physics" else SAGEConv
@@ -82,9 +90,12 @@ def main(argv=None):
     predictor = LinkPredictor(args.predictor, args.hidden_channels, args.hidden_channels, 1, 2,
                               args.dropout).to(device)
 
-    Ks = ('Hits@10', 'Hits@50', 'Hits@100') if args.datasets == "collab" else \
-        ('Hits@10', 'Hits@20', 'Hits@30', 'Hits@50')
-    loggers = {k: Logger(args.runs, args) for k in Ks + ('AUC',)}
+    if not transductive:
+        loggers = {k: ProductionLogger(args.runs, args) for k in ('Hits@10', 'Hits@20', 'Hits@30', 'Hits@50', 'AUC')}
+    else:
+        Ks = ('Hits@10', 'Hits@50', 'Hits@100') if args.datasets == "collab" else \
+            ('Hits@10', 'Hits@20', 'Hits@30', 'Hits@50')
+        loggers = {k: Logger(args.runs, args) for k in Ks + ('AUC',)}
     tag = args.datasets + "-" + args.encoder + "_" + args.transductive + ".pkl"
     val_max = 0.0
     for run in range(args.runs):
@@ -95,10 +106,17 @@ def main(argv=None):
         cnt_wait = 0
         best_val = 0.0
         for epoch in range(1, 1 + args.epochs):
-            loss = llp_train.train_teacher(model, predictor, data, split_edge, optimizer, args.batch_size,
-                                           args.encoder, args.datasets, args.transductive, dtype=args.dtype)
-            results, h = llp_train.test_transductive(model, predictor, data, split_edge, None, args.batch_size,
-                                                     args.encoder, args.datasets, args)
+            if transductive:
+                loss = llp_train.train_teacher(model, predictor, data, split_edge, optimizer, args.batch_size,
+                                               args.encoder, args.datasets, args.transductive, dtype=args.dtype)
+                results, h = llp_train.test_transductive(model, predictor, data, split_edge, None, args.batch_size,
+                                                         args.encoder, args.datasets, args)
+            else:
+                loss = llp_train.train_teacher(model, predictor, training_data, None, optimizer, args.batch_size,
+                                               args.encoder, args.datasets, args.transductive, dtype=args.dtype)
+                results, h = llp_train.test_production(model, predictor, val_data, inference_data,
+                                                       test_edge_bundle, negative_samples, None, args.batch_size,
+                                                       args.encoder, args.datasets)
             if results[args.metric][0] > val_max:
                 val_max = results[args.metric][0]
                 if args.encoder != 'mlp':
@@ -115,21 +133,13 @@ def main(argv=None):
             for key, result in results.items():
                 loggers[key].add_result(run, result)
             if epoch % args.log_steps == 0:
-                for key, result in results.items():
-                    valid_hits, test_hits = result
-                    print(key)
-                    print(f'Run: {run + 1:02d}, '
-                          f'Epoch: {epoch:02d}, '
-                          f'Loss: {loss:.4f}, '
-                          f'Valid: {100 * valid_hits:.2f}%, '
-                          f'Test: {100 * test_hits:.2f}%')
-                print('---')
+                print_epoch(results, run, epoch, loss, transductive)
             if cnt_wait >= args.patience:
                 break
         for key in loggers.keys():
             print(key)
             loggers[key].print_statistics(run)
-    _write_summary(logger_file, loggers, True)
+    _write_summary(logger_file, loggers, transductive)
 
 
 if __name__ == "__main__":

@@ -557,6 +557,187 @@ def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, 
     print(name, "steps:", out["nsteps"], "epoch losses:", losses)
 
 
+class _PygData:
+    """torch_geometric.data.Data stand-in for the production-split stubs."""
+
+    def __init__(self, x=None, edge_index=None, **kw):
+        self.x, self.edge_index = x, edge_index
+        self.__dict__.update(kw)
+
+    @property
+    def num_nodes(self):
+        return self.x.size(0)
+
+    def clone(self):
+        return _PygData(**{k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.__dict__.items()})
+
+
+def _pyg_sample(population, k):
+    if population <= k:
+        return torch.arange(population)
+    return torch.tensor(random.sample(range(population), k))
+
+
+def _pyg_negative_sampling(edge_index, num_nodes=None, num_neg_samples=None, method="sparse",
+                           force_undirected=False):
+    """PyG 2.2.0 torch_geometric.utils.negative_sampling, sparse method."""
+    assert method == "sparse"
+    n = num_nodes
+    row, col = edge_index
+    if force_undirected:
+        m = row < col
+        r, c = row[m], col[m]
+        idx = r * n + c - torch.arange(1, n).cumsum(0)[r]
+        population = n * (n + 1) // 2 - n
+    else:
+        m = row != col
+        r, c = row[m], col[m].clone()
+        c[r < c] -= 1
+        idx = r * (n - 1) + c
+        population = n * n - n
+    if idx.numel() >= population:
+        return edge_index.new_empty((2, 0))
+    if num_neg_samples is None:
+        num_neg_samples = edge_index.size(1)
+    if force_undirected:
+        num_neg_samples = num_neg_samples // 2
+    sample_size = int(1.1 * num_neg_samples / (1.0 - idx.numel() / population))
+    neg = None
+    for _ in range(3):
+        rnd = _pyg_sample(population, sample_size)
+        bad = np.isin(rnd, idx)
+        if neg is not None:
+            bad |= np.isin(rnd, neg)
+        rnd = rnd[~torch.from_numpy(bad).to(torch.bool)]
+        neg = rnd if neg is None else torch.cat([neg, rnd])
+        if neg.numel() >= num_neg_samples:
+            neg = neg[:num_neg_samples]
+            break
+    if force_undirected:
+        off = torch.arange(1, n).cumsum(0)
+        end = torch.arange(n, n * n, n).sub_(off)
+        r = torch.bucketize(neg, end, right=True)
+        c = off[r].add_(neg) % n
+        return torch.stack([torch.cat([r, c]), torch.cat([c, r])], 0)
+    r = torch.div(neg, n - 1, rounding_mode="floor")
+    c = neg % (n - 1)
+    c[r <= c] += 1
+    return torch.stack([r, c], 0)
+
+
+class _PygRandomNodeSplit:
+    def __init__(self, split="train_rest", num_splits=1, num_train_per_class=20, num_val=500, num_test=1000,
+                 key="y"):
+        assert split == "train_rest" and num_splits == 1
+        self.num_val, self.num_test = num_val, num_test
+
+    def __call__(self, data):
+        out = data.clone()
+        n = out.num_nodes
+        masks = [torch.zeros(n, dtype=torch.bool) for _ in range(3)]
+        nv = round(n * self.num_val) if isinstance(self.num_val, float) else self.num_val
+        nt = round(n * self.num_test) if isinstance(self.num_test, float) else self.num_test
+        perm = torch.randperm(n)
+        masks[1][perm[:nv]] = True
+        masks[2][perm[nv:nv + nt]] = True
+        masks[0][perm[nv + nt:]] = True
+        out.train_mask, out.val_mask, out.test_mask = masks
+        return out
+
+
+class _PygRandomLinkSplit:
+    def __init__(self, num_val=0.1, num_test=0.2, is_undirected=False, key="edge_label", split_labels=False,
+                 add_negative_train_samples=True, neg_sampling_ratio=1.0, disjoint_train_ratio=0.0):
+        assert is_undirected and not split_labels and add_negative_train_samples and disjoint_train_ratio == 0
+        self.num_val, self.num_test, self.ratio = num_val, num_test, neg_sampling_ratio
+
+    def __call__(self, data):
+        ei = data.edge_index
+        perm = (ei[0] <= ei[1]).nonzero(as_tuple=False).view(-1)
+        perm = perm[torch.randperm(perm.size(0), device=perm.device)]
+        nv = int(self.num_val * perm.numel())
+        nt = int(self.num_test * perm.numel())
+        ntr = perm.numel() - nv - nt
+        tr, va, te, trva = perm[:ntr], perm[ntr:ntr + nv], perm[ntr + nv:], perm[:ntr + nv]
+        n_tr, n_va, n_te = int(ntr * self.ratio), int(nv * self.ratio), int(nt * self.ratio)
+        neg = _pyg_negative_sampling(ei, data.num_nodes, num_neg_samples=n_tr + n_va + n_te, method="sparse")
+        assert neg.size(1) == n_tr + n_va + n_te
+
+        def make(mp, lab_idx, negs):
+            e = ei[:, mp]
+            out = _PygData(data.x, torch.cat([e, e.flip([0])], dim=-1))
+            out.edge_label = torch.cat([torch.ones(lab_idx.numel()), torch.zeros(negs.size(1))], dim=0)
+            out.edge_label_index = torch.cat([ei[:, lab_idx], negs], dim=-1)
+            return out
+        return (make(tr, tr, neg[:, n_va + n_te:]), make(tr, va, neg[:, :n_va]),
+                make(trva, te, neg[:, n_va:n_va + n_te]))
+
+
+def _pyg_subgraph(subset, edge_index, relabel_nodes=False):
+    assert subset.dtype == torch.bool and relabel_nodes
+    node_idx = torch.zeros(subset.numel(), dtype=torch.long)
+    node_idx[subset] = torch.arange(int(subset.sum()))
+    keep = subset[edge_index[0]] & subset[edge_index[1]]
+    return node_idx[edge_index[:, keep]], None
+
+
+def load_reference_production_split():
+    """Exec src/generate_production_split.py over the PyG stubs above."""
+    pyg = types.ModuleType("torch_geometric")
+    pd = types.ModuleType("torch_geometric.data")
+    pd.Data, pd.Dataset = _PygData, list
+    pt = types.ModuleType("torch_geometric.transforms")
+    pt.RandomLinkSplit, pt.RandomNodeSplit = _PygRandomLinkSplit, _PygRandomNodeSplit
+    pu = types.ModuleType("torch_geometric.utils")
+    pu.negative_sampling, pu.subgraph = _pyg_negative_sampling, _pyg_subgraph
+    pu.add_self_loops = pu.train_test_split_edges = pu.to_networkx = None
+    ogb = types.ModuleType("ogb")
+    ogl = types.ModuleType("ogb.linkproppred")
+    ogl.PygLinkPropPredDataset = None
+    stubs = {"torch_geometric": pyg, "torch_geometric.data": pd, "torch_geometric.transforms": pt,
+             "torch_geometric.utils": pu, "ogb": ogb, "ogb.linkproppred": ogl}
+    saved = {k: sys.modules.get(k) for k in stubs}
+    sys.modules.update(stubs)
+    try:
+        mod = types.ModuleType("ref_generate_production_split")
+        p = os.path.join(REF, "generate_production_split.py")
+        exec(compile(_compile_file(p), p, "exec"), mod.__dict__)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return mod
+
+
+def run_production_split_case(name, N, F_, E_und, ratios, seed):
+    """src/generate_production_split.py:32-95 on a coalesced synthetic graph."""
+    import contextlib
+    import io
+    mod = load_reference_production_split()
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randint(0, N, (E_und,), generator=g)
+    v = torch.randint(0, N, (E_und,), generator=g)
+    keep = u != v
+    und = torch.stack([u[keep], v[keep]])
+    key = torch.unique(torch.cat([und, und.flip([0])], -1)[0] * N + torch.cat([und, und.flip([0])], -1)[1])
+    ei = torch.stack([key // N, key % N])
+    x = torch.randn(N, F_, generator=g)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        tr, va, inf, _, bundle, neg = mod.do_production_edge_split([_PygData(x, ei)], name, *ratios)
+    out = dict(N=np.int64(N), x=x.numpy(), edge_index=ei.numpy(), ratios=np.array(ratios, np.float64),
+               train_x=tr.x.numpy(), train_edge_index=tr.edge_index.numpy(),
+               train_edge_label=tr.edge_label.numpy(), train_edge_label_index=tr.edge_label_index.numpy(),
+               val_edge_index=va.edge_index.numpy(), val_edge_label=va.edge_label.numpy(),
+               val_edge_label_index=va.edge_label_index.numpy(), inference_edge_index=inf.edge_index.numpy(),
+               old_old=bundle[0].numpy(), old_new=bundle[1].numpy(), new_new=bundle[2].numpy(),
+               test=bundle[3].numpy(), negative_samples=neg.numpy(),
+               stdout=np.frombuffer(buf.getvalue().encode(), np.uint8))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
 def run_logger_case(name):
     """src/logger.py printed output for fixed result tables (the CLI's outputs
     must stay byte-identical)."""
@@ -585,6 +766,12 @@ def run_logger_case(name):
 
 def main():
     ref_models = load_reference_models()
+    run_production_split_case("production_split_cora_small", N=300, F_=8, E_und=900, ratios=(0.3, 0.3, 0.3, 0.1),
+                              seed=12)
+    run_production_split_case("production_split_small", N=500, F_=4, E_und=2500, ratios=(0.1, 0.1, 0.1, 0.1),
+                              seed=13)
+    if os.environ.get("GOLDEN_ONLY") == "production_split":
+        return
     run_logger_case("logger_output")
     run_teacher_case("teacher_sage_small", N=110, F_=24, H=64, L=2, E_und=400, bs=160, updated=False,
                      transductive="transductive", seed=7)

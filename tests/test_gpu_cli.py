@@ -56,3 +56,32 @@ def test_teacher_then_student_cli(workdir):
                              "--minibatch", "--LLP_D=1", "--LLP_R=1", "--True_label=1", "--dropout=0.0",
                              "--hops=2", "--rw_step=2", "--ns_rate=2", "--dtype=bf16", "--link_batch_size=1024"])
     assert "Run: 01, Epoch: 02" in out
+
+
+def test_production_cli(workdir):
+    """Production (inductive) setting end to end: the teacher CLI makes and
+    caches the split (src/train_teacher_gnn.py:341-365), trains on the
+    old-node graph and reports old_old / old_new / new_new; the student CLI
+    reads the same split and the teacher's artefacts (src/main.py:337-346)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import main as student_cli
+    import train_teacher_gnn as teacher_cli
+    out = _run(teacher_cli, ["--datasets=cora", "--encoder=sage", "--runs=1", "--epochs=2", "--synthetic",
+                             "--transductive=production"])
+    assert "splitting the datasets now..." in out and "#Old Nodes:\t1896" in out
+    line = [l for l in out.splitlines() if l.startswith("Run: 01, Epoch: 02")][0]
+    for k in ("valid: ", "test: ", "old_old: ", "old_new: ", "new_new: "):
+        assert k in line, line
+    assert os.path.exists(workdir / "data" / "cora_production.pt")
+    tag = "cora-sage_production.pkl"
+    feats = torch.load(workdir / "saved-features" / tag, weights_only=True)["features"]
+    assert feats.shape == (1896, 256) and torch.isfinite(feats).all()
+    out = _run(student_cli, ["--datasets=cora", "--encoder=sage", "--runs=1", "--epochs=2", "--synthetic",
+                             "--transductive=production", "--LLP_D=1", "--LLP_R=1", "--True_label=0.1",
+                             "--dropout=0.0", "--hops=1", "--rw_step=3", "--ns_rate=1"])
+    assert "splitting the datasets now..." not in out          # the cached split is reused
+    lines = [l for l in out.splitlines() if l.startswith("Run: 01, Epoch: 02")]
+    assert len(lines) == 5 and "new_new: " in lines[0], out
+    txt = open(workdir / "results" / "cora_KD_production.txt").read()
+    assert "Final old_new" in txt
