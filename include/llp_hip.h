@@ -298,6 +298,16 @@ int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowpt
                       const void* x, int64_t ldx, const float* inv_deg, int mode,
                       void* out, int64_t ldo, int accumulate, void* stream);
 
+/* GCN propagation, replaces torch_geometric 2.2.0 GCNConv.propagate after
+ * gcn_norm (GCNConv(cached=True) at src/models.py:60-64, GCN.forward :72-78):
+ *   out[i] = dinv[i] * sum_{e in row i} dinv[col[e]] * x[col[e]]  (+ bias)
+ * over the CSR-by-destination of the graph with its self-loops replaced by
+ * one loop per node (dinv = deg^-1/2 of that graph).  Over the transposed CSR
+ * with bias = NULL it is the backward dX of the same propagation. */
+int llp_gcn_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
+                      const void* x, int64_t ldx, const float* dinv, const float* bias, void* out, int64_t ldo,
+                      int accumulate, void* stream);
+
 /* ---------------------------------------------------------------- optimiser tail
  * Multi-tensor clip_grad_norm_(group, max_norm) per group (Q9) + Adam
  * (torch.optim.Adam defaults, src/main.py:134-138,400-402).  Descriptor tables

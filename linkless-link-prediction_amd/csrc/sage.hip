@@ -50,7 +50,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_t F, const int32_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col, const T* __restrict__ x,
                                                           int64_t ldx, const float* __restrict__ inv_deg, int mode,
-                                                          T* __restrict__ out, int64_t ldo, int accumulate) {
+                                                          const float* __restrict__ bias, T* __restrict__ out,
+                                                          int64_t ldo, int accumulate) {
   constexpr int E = V16<T>::E;
   __shared__ float red[4][64 * E];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -109,9 +110,12 @@ __global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_
       __builtin_amdgcn_wave_barrier();
     }
     if (grp == 0 && active) {
-      const float sc = mode ? 1.f : 1.f / (float)max(end - beg, (int64_t)1);
+      const float sc = mode == 0 ? 1.f / (float)max(end - beg, (int64_t)1) : (mode == 2 ? inv_deg[row] : 1.f);
 #pragma unroll
       for (int i = 0; i < E; ++i) acc[i] *= sc;
+      if (bias)
+#pragma unroll
+        for (int i = 0; i < E; ++i) acc[i] += bias[(c0 + gl) * E + i];
       uint4* dst = reinterpret_cast<uint4*>(out + row * ldo + (c0 + gl) * E);
       if (accumulate) {
         float prev[E];
@@ -132,12 +136,13 @@ __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int
                                                              const int32_t* __restrict__ rowptr,
                                                              const int32_t* __restrict__ col, const T* __restrict__ x,
                                                              int64_t ldx, const float* __restrict__ inv_deg, int mode,
-                                                             T* __restrict__ out, int64_t ldo, int accumulate) {
+                                                             const float* __restrict__ bias, T* __restrict__ out,
+                                                             int64_t ldo, int accumulate) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_rows) return;
   const int64_t beg = rowptr[row], end = rowptr[row + 1];
-  const float sc = mode ? 1.f : 1.f / (float)max(end - beg, (int64_t)1);
+  const float sc = mode == 0 ? 1.f / (float)max(end - beg, (int64_t)1) : (mode == 2 ? inv_deg[row] : 1.f);
   for (int64_t f = lane; f < F; f += 64) {
     float acc = 0.f;
     for (int64_t e = beg; e < end; ++e) {
@@ -147,6 +152,7 @@ __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int
       acc += (mode ? inv_deg[j] : 1.f) * v;
     }
     acc *= sc;
+    if (bias) acc += bias[f];
     T* d = out + row * ldo + f;
     if constexpr (sizeof(T) == 2) {
       if (accumulate) acc += bf2f(*d);
@@ -160,13 +166,10 @@ __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int
 
 }  // namespace
 
-extern "C" int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
-                                 const void* x, int64_t ldx, const float* inv_deg, int mode, void* out, int64_t ldo,
-                                 int accumulate, void* stream) {
-  LLP_CHECK_ARG(rowptr && x && out, "llp_csr_aggregate: null pointer");
-  LLP_CHECK_ARG(mode == 0 || (mode == 1 && inv_deg), "llp_csr_aggregate: mode 1 needs inv_deg");
+static int csr_aggregate_launch(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
+                                const void* x, int64_t ldx, const float* inv_deg, int mode, const float* bias,
+                                void* out, int64_t ldo, int accumulate, hipStream_t s) {
   if (n_rows == 0 || F == 0) return LLP_OK;
-  hipStream_t s = (hipStream_t)stream;
   const int es = dtype == LLP_BF16 ? 2 : 4;
   const int E = 16 / es;
   const bool vec = (F % E == 0) && (ldx % E == 0) && (ldo % E == 0) && ((uintptr_t)x % 16 == 0) &&
@@ -175,18 +178,38 @@ extern "C" int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int
   if (dtype == LLP_BF16) {
     if (vec)
       hipLaunchKernelGGL(csr_agg_vec_kernel<bf16_t>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const bf16_t*)x,
-                         ldx, inv_deg, mode, (bf16_t*)out, ldo, accumulate);
+                         ldx, inv_deg, mode, bias, (bf16_t*)out, ldo, accumulate);
     else
       hipLaunchKernelGGL(csr_agg_scalar_kernel<bf16_t>, grid, dim3(256), 0, s, n_rows, F, rowptr, col,
-                         (const bf16_t*)x, ldx, inv_deg, mode, (bf16_t*)out, ldo, accumulate);
+                         (const bf16_t*)x, ldx, inv_deg, mode, bias, (bf16_t*)out, ldo, accumulate);
   } else {
     if (vec)
       hipLaunchKernelGGL(csr_agg_vec_kernel<float>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const float*)x, ldx,
-                         inv_deg, mode, (float*)out, ldo, accumulate);
+                         inv_deg, mode, bias, (float*)out, ldo, accumulate);
     else
       hipLaunchKernelGGL(csr_agg_scalar_kernel<float>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const float*)x,
-                         ldx, inv_deg, mode, (float*)out, ldo, accumulate);
+                         ldx, inv_deg, mode, bias, (float*)out, ldo, accumulate);
   }
   LLP_LAUNCH_CHECK();
   return LLP_OK;
+}
+
+extern "C" int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
+                                 const void* x, int64_t ldx, const float* inv_deg, int mode, void* out, int64_t ldo,
+                                 int accumulate, void* stream) {
+  LLP_CHECK_ARG(rowptr && x && out, "llp_csr_aggregate: null pointer");
+  LLP_CHECK_ARG(mode == 0 || (mode == 1 && inv_deg), "llp_csr_aggregate: mode 1 needs inv_deg");
+  return csr_aggregate_launch(dtype, n_rows, F, rowptr, col, x, ldx, inv_deg, mode, nullptr, out, ldo, accumulate,
+                              (hipStream_t)stream);
+}
+
+// GCN propagation (PyG GCNConv after gcn_norm): out[i] = dinv[i] * sum_{j in row i} dinv[j] * x[j] (+ bias).
+// With the self-loop CSR by destination this is the forward; with the transposed CSR and no bias, the
+// backward dX of the same propagation.
+extern "C" int llp_gcn_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
+                                 const void* x, int64_t ldx, const float* dinv, const float* bias, void* out,
+                                 int64_t ldo, int accumulate, void* stream) {
+  LLP_CHECK_ARG(rowptr && col && x && out && dinv, "llp_gcn_aggregate: null pointer");
+  return csr_aggregate_launch(dtype, n_rows, F, rowptr, col, x, ldx, dinv, 2, bias, out, ldo, accumulate,
+                              (hipStream_t)stream);
 }

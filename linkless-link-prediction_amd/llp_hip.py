@@ -85,6 +85,7 @@ _SIGS = {
     "llp_auc_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_auc": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "llp_csr_aggregate": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_int, c_vp]),
+    "llp_gcn_aggregate": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
     "llp_grad_sumsq_workspace_bytes": (c_i64, [c_int, c_i64]),
     "llp_grad_sumsq": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
     "llp_adam_step": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
@@ -399,6 +400,14 @@ def csr_aggregate(n_rows, F, rowptr, col, x, inv_deg, mode, out, accumulate=Fals
     check(L.llp_csr_aggregate(dtype_code(x.dtype), n_rows, F, rowptr.data_ptr(), col.data_ptr(), x.data_ptr(),
                               x.stride(0), ptr(inv_deg), mode, out.data_ptr(), out.stride(0), int(accumulate),
                               stream_ptr()), "llp_csr_aggregate")
+
+
+def gcn_aggregate(n_rows, F, rowptr, col, x, dinv, out, bias=None, accumulate=False):
+    """out[i] = dinv[i] * sum_j dinv[j] x[j] (+ bias) over the CSR rows (llp_gcn_aggregate)."""
+    L = lib()
+    check(L.llp_gcn_aggregate(dtype_code(x.dtype), n_rows, F, rowptr.data_ptr(), col.data_ptr(), x.data_ptr(),
+                              x.stride(0), dinv.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0),
+                              int(accumulate), stream_ptr()), "llp_gcn_aggregate")
 
 
 def grad_sumsq_ws_bytes(n, max_numel):

@@ -207,3 +207,35 @@ class _MeanAgg(torch.autograd.Function):
 def mean_aggregate(x, graph):
     _require_cuda(x)
     return _MeanAgg.apply(x, graph)
+
+
+class _GCNAgg(torch.autograd.Function):
+    """GCN propagation D^-1/2 A D^-1/2 y (+ bias) over the self-loop CSR (llp_gcn_aggregate)."""
+
+    @staticmethod
+    def forward(ctx, y, bias, graph):
+        out = torch.empty(graph.num_dst, y.shape[1], dtype=y.dtype, device=y.device)
+        K.gcn_aggregate(graph.num_dst, y.shape[1], graph.rowptr, graph.col, y.contiguous(), graph.dinv, out,
+                        bias=None if bias is None else bias.detach().float().contiguous())
+        ctx.graph = graph
+        ctx.n_src = y.shape[0]
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        g = ctx.graph
+        gout = gout.contiguous()
+        gy = torch.empty(ctx.n_src, gout.shape[1], dtype=gout.dtype, device=gout.device)
+        K.gcn_aggregate(ctx.n_src, gout.shape[1], g.rowptr_t, g.col_t, gout, g.dinv, gy)
+        gb = None
+        if ctx.has_bias and ctx.needs_input_grad[1]:
+            gb = torch.empty(gout.shape[1], dtype=torch.float32, device=gout.device)
+            ws = torch.empty(K.colsum_ws_bytes(gout.shape[0], gout.shape[1]), dtype=torch.uint8, device=gout.device)
+            K.colsum(gout, gout.shape[0], gout.shape[1], gb, ws)
+        return gy, gb, None
+
+
+def gcn_aggregate(y, graph, bias=None):
+    _require_cuda(y)
+    return _GCNAgg.apply(y, bias, graph)

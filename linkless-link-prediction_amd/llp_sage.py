@@ -7,9 +7,14 @@ layers used by the reference's SAGE encoder (src/models.py:82-119).
                       root (used at src/train_teacher_gnn.py:381-383).
   SAGEConv_updated  — src/sageconv_updated.py:9-93: lin_l FIRST, then the
                       mean, then + lin_r(x) (used for coauthor-physics).
+  GCNConv           — torch_geometric 2.2.0 GCNConv(cached=True) (restated):
+                      lin (no bias), symmetric-normalised propagation over the
+                      graph with one self-loop per node, + bias (the GCN
+                      encoder, src/models.py:56-80).
 
-State-dict keys (``lin_l.weight``, ``lin_l.bias``, ``lin_r.weight``) match
-PyG's, so the reference's saved teacher weights load here.
+State-dict keys (``lin_l.weight``, ``lin_l.bias``, ``lin_r.weight``; GCN:
+``bias``, ``lin.weight``) match PyG's, so the reference's saved teacher
+weights load here.
 """
 from __future__ import annotations
 
@@ -23,13 +28,22 @@ import llp_ops as ops
 class Graph:
     """edge_index (2, E) as CSR by destination (PyG flow source_to_target):
     row i lists the sources of the edges into i, duplicates kept.
-    Also the transposed CSR (by source) and 1/deg for the backward."""
+    Also the transposed CSR (by source) and 1/deg for the backward.
 
-    def __init__(self, edge_index, num_nodes: int, device):
+    ``gcn=True``: the graph GCNConv propagates over (PyG 2.2.0 gcn_norm with
+    add_remaining_self_loops): input self-loops dropped, one loop per node
+    added; ``dinv`` = deg^-1/2 with deg counted at the destination."""
+
+    def __init__(self, edge_index, num_nodes: int, device, gcn: bool = False):
         ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
         src = ei[0].astype(np.int64)
         dst = ei[1].astype(np.int64)
         N = int(num_nodes)
+        if gcn:
+            keep = src != dst
+            loops = np.arange(N, dtype=np.int64)
+            src = np.concatenate([src[keep], loops])
+            dst = np.concatenate([dst[keep], loops])
         assert src.size < 2 ** 31
         order = np.argsort(dst, kind="stable")
         deg = np.bincount(dst, minlength=N)
@@ -47,20 +61,24 @@ class Graph:
         self.rowptr_t = torch.from_numpy(rowptr_t.astype(np.int32)).to(dev)
         self.col_t = torch.from_numpy(dst[order_t].astype(np.int32)).to(dev)
         self.inv_deg = torch.from_numpy((1.0 / np.maximum(deg, 1)).astype(np.float32)).to(dev)
+        self.gcn = gcn
+        if gcn:
+            self.dinv = torch.from_numpy((1.0 / np.sqrt(deg.astype(np.float64))).astype(np.float32)).to(dev)
 
 
 _GRAPH_CACHE = {}
 
 
-def as_graph(edge_index, num_nodes, device):
+def as_graph(edge_index, num_nodes, device, gcn=False):
     """Cache the CSR per edge_index tensor (the reference re-passes the same
-    data.adj_t every step, src/train_teacher_gnn.py:43)."""
+    data.adj_t every step, src/train_teacher_gnn.py:43; GCNConv(cached=True)
+    caches its normalised graph likewise)."""
     if isinstance(edge_index, Graph):
         return edge_index
-    key = (id(edge_index), int(num_nodes), str(device))
+    key = (id(edge_index), int(num_nodes), str(device), bool(gcn))
     g = _GRAPH_CACHE.get(key)
     if g is None or g[0] is not edge_index:
-        g = (edge_index, Graph(edge_index, num_nodes, device))
+        g = (edge_index, Graph(edge_index, num_nodes, device, gcn=gcn))
         _GRAPH_CACHE[key] = g
     return g[1]
 
@@ -103,3 +121,32 @@ class SAGEConv_updated(SAGEConv):
         if self.root_weight:
             out = out + ops.linear(x, self.lin_r.weight, None)
         return out
+
+
+class GCNConv(nn.Module):
+    """GCNConv(in, out, cached=True) with PyG 2.2.0 defaults (normalize,
+    add_self_loops, improved=False, bias): out = D^-1/2 (A - loops + I) D^-1/2 (x W^T) + b."""
+
+    def __init__(self, in_channels, out_channels, cached=False, bias=True, improved=False, add_self_loops=True,
+                 normalize=True, **kwargs):
+        super().__init__()
+        if improved or not add_self_loops or not normalize:
+            raise NotImplementedError("GCNConv options other than the reference's (src/models.py:60-64)")
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.cached = cached
+        self.lin = nn.Linear(in_channels, out_channels, bias=False)
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.lin.weight)       # PyG 'glorot'
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def forward(self, x, edge_index):
+        g = as_graph(edge_index, x.shape[0], x.device, gcn=True)
+        return ops.gcn_aggregate(ops.linear(x, self.lin.weight, None), g, self.bias)
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"

@@ -16,7 +16,15 @@ Encoder layer l (in F, out O), both conv flavours the reference uses:
       ONE GEMM against Wst = [W_l ; W_r] (2O x F) gives [U | R] (N x 2O); the
       aggregate of U accumulates into R in place.
 
-Backward (both flavours): with dOut the layer's output gradient and
+  GCNConv (PyG 2.2.0, cached=True; the GCN encoder, src/models.py:56-80)
+      out = D^-1/2 (A - loops + I) D^-1/2 (x W^T) + b
+      ONE GEMM Y = x W^T, then the normalised aggregate of Y over the
+      self-loop CSR with the bias fused (llp_gcn_aggregate); ReLU/dropout by
+      act_2d.  Backward: db = colsum(dZ), dY = the same aggregate over the
+      transposed CSR, dW = dY^T x (TN), dX = dY W with the previous layer's
+      mask in the GEMM epilogue.
+
+Backward (SAGE flavours): with dOut the layer's output gradient and
 G = mean-backward(dOut) over the transposed CSR, dX = [G | dOut] . [W_l^T | W_r^T]
 is ONE K-concatenated GEMM whose epilogue applies the previous layer's
 ReLU/dropout mask; weight gradients are TN GEMMs with the bias gradient fused.
@@ -33,12 +41,12 @@ import torch
 
 import llp_hip as K
 from llp_engine import EngineBase
-from llp_sage import Graph, SAGEConv_updated
+from llp_sage import GCNConv, Graph, SAGEConv_updated
 
 
 class TeacherEngine(EngineBase):
     """``model``: models.SAGE (convs of SAGEConv or SAGEConv_updated, root_weight,
-    norm_type 'none'); ``predictor``: LinkPredictor; ``x``: node features;
+    norm_type 'none') or models.GCN (GCNConv with bias); ``predictor``: LinkPredictor; ``x``: node features;
     ``edge_index``: the message-passing graph (data.adj_t / data.edge_index,
     src/train_teacher_gnn.py:23-27,43-46); ``optimizer``: Adam over
     model.parameters() + predictor.parameters()."""
@@ -53,18 +61,30 @@ class TeacherEngine(EngineBase):
         if getattr(model, "norm_type", "none") != "none":
             raise NotImplementedError("SAGE norm_type other than 'none' (not used by the reference scripts)")
         self.convs = list(model.convs)
+        self.gcn = isinstance(self.convs[0], GCNConv)
         self.updated = isinstance(self.convs[0], SAGEConv_updated)
-        if any(isinstance(c, SAGEConv_updated) != self.updated or not c.root_weight for c in self.convs):
+        if self.gcn:
+            if any(not isinstance(c, GCNConv) or c.bias is None for c in self.convs):
+                raise NotImplementedError("all convs GCNConv with bias")
+        elif any(isinstance(c, SAGEConv_updated) != self.updated or not c.root_weight for c in self.convs):
             raise NotImplementedError("all convs of one flavour, with root_weight")
         self.p_drop = float(model.dropout)
         ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
-        self.graph = Graph(ei, N, self.dev)
+        self.graph = Graph(ei, N, self.dev, gcn=self.gcn)
         self._neg_rc = (ei[0], ei[1])        # row, col = data.adj_t (src/train_teacher_gnn.py:23)
         self.num_edges = int(ei.shape[1])
 
         # ---------------- per-layer weights and shadows
         self.layers = []
         for l, conv in enumerate(self.convs):
+            if self.gcn:
+                W = conv.lin.weight
+                O, F = W.shape
+                Wc = torch.empty(O, F, dtype=dt, device=self.dev)
+                WT = torch.empty(F, O, dtype=dt, device=self.dev)
+                self._set_shadow(W, Wc, WT)
+                self.layers.append(dict(F=F, O=O, conv=conv, Wf=Wc, WT=WT, bias=conv.bias.data))
+                continue
             Wl, bl, Wr = conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight
             O, F = Wl.shape
             L = dict(F=F, O=O, conv=conv)
@@ -93,6 +113,10 @@ class TeacherEngine(EngineBase):
         x = x.to(self.dev)
         for l, L in enumerate(self.layers):
             F, O = L["F"], L["O"]
+            if self.gcn:
+                L["X"] = x.to(dt).contiguous() if l == 0 else torch.empty(N, F, dtype=dt, device=self.dev)
+                L["G"] = torch.empty(N, O, dtype=dt, device=self.dev)          # dZ of the layer
+                continue
             if self.updated:
                 L["X"] = x.to(dt).contiguous() if l == 0 else torch.empty(N, F, dtype=dt, device=self.dev)
                 L["YY"] = torch.empty(N, 2 * O, dtype=dt, device=self.dev)
@@ -120,7 +144,16 @@ class TeacherEngine(EngineBase):
             drop = None if (last or not training) else self._dropout(self.p_drop, 1 + l)
             act = K.ACT_NONE if last else K.ACT_RELU
             nxt = None if last else self.layers[l + 1]
-            if self.updated:
+            if self.gcn:
+                Y = self._buf("gcn_Y", (N, O), self.dtype)
+                K.gemm_nt(K.operand(L["X"]), K.operand(L["Wf"]), N, O, F, Y, dc)
+                if last:
+                    K.gcn_aggregate(N, O, g.rowptr, g.col, Y, g.dinv, self.h, bias=L["bias"])
+                else:
+                    Z = self._buf("gcn_Z", (N, O), self.dtype)
+                    K.gcn_aggregate(N, O, g.rowptr, g.col, Y, g.dinv, Z, bias=L["bias"])
+                    K.act_2d(Z, nxt["X"], act=act, dropout=drop)
+            elif self.updated:
                 YY = L["YY"]
                 K.gemm_nt(K.operand(L["X"]), K.operand(L["Wf"]), N, 2 * O, F, YY, dc, bias=L["bias"])
                 K.csr_aggregate(N, O, g.rowptr, g.col, YY[:, :O], None, 0, YY[:, O:], accumulate=True)
@@ -142,6 +175,8 @@ class TeacherEngine(EngineBase):
         nl = len(self.layers)
         last = self.layers[-1]
         O = last["O"]
+        if self.gcn:
+            return self._gcn_backward(dh32, alpha)
         Gl = last["G"]
         if dt == torch.float32:
             K.act_2d(dh32, Gl[:, O:], act=K.ACT_NONE)
@@ -174,6 +209,29 @@ class TeacherEngine(EngineBase):
                 prev = self.layers[l - 1]
                 K.gemm_nt(K.operand(G), K.operand(L["WT"]), N, F, 2 * O, prev["G"][:, prev["O"]:], dc,
                           act=K.ACT_RELU_BWD, aux=L["X"], alpha=alpha)
+
+    def _gcn_backward(self, dh32, alpha):
+        g = self.graph
+        dt, dc = self.dtype, self.dc
+        N = self.N
+        last = self.layers[-1]
+        if dt == torch.float32:
+            K.act_2d(dh32, last["G"], act=K.ACT_NONE)
+        else:
+            K.convert(dh32, last["G"])
+        for l in range(len(self.layers) - 1, -1, -1):
+            L = self.layers[l]
+            F, O = L["F"], L["O"]
+            dZ, conv = L["G"], L["conv"]
+            K.colsum(dZ, N, O, conv.bias.grad, self._ws("ws_colsum", K.colsum_ws_bytes(N, O)))
+            dY = self._buf("gcn_dY", (N, O), dt)
+            K.gcn_aggregate(N, O, g.rowptr_t, g.col_t, dZ, g.dinv, dY)
+            ws = self._ws("ws_tn", K.gemm_tn_ws_bytes(dc, N, O, F))
+            K.gemm_tn(K.operand(dY), K.operand(L["X"]), N, O, F, conv.lin.weight.grad, dc, ws)
+            if l > 0:
+                prev = self.layers[l - 1]
+                K.gemm_nt(K.operand(dY), K.operand(L["WT"]), N, F, O, prev["G"], dc, act=K.ACT_RELU_BWD,
+                          aux=L["X"], alpha=alpha)
 
     # ------------------------------------------------------------------ the step
     def step(self, link_ids, pairs, p_offset=0, P_total=None, neg=None, dense_negatives=True):

@@ -170,9 +170,9 @@ def _teacher_engine(model, predictor, data, optimizer, edge_index, dtype):
 
 def train_teacher(model, predictor, data, split_edge, optimizer, batch_size, encoder_name, dataset, transductive,
                   dtype="fp32"):
-    """src/train_teacher_gnn.py:21-73 for encoder_name 'sage' (TeacherEngine)
-    and 'mlp' (the DistillEngine machinery is not needed: the MLP teacher runs
-    through the module ops)."""
+    """src/train_teacher_gnn.py:21-73 for encoder_name 'sage' / 'gcn'
+    (TeacherEngine) and 'mlp' (the full-batch DistillEngine with every
+    distillation weight zero)."""
     if transductive == "transductive":
         mp_edges = data.adj_t
         pos_train_edge = split_edge["train"]["edge"]
@@ -182,8 +182,8 @@ def train_teacher(model, predictor, data, split_edge, optimizer, batch_size, enc
     if encoder_name == "mlp":
         return _train_teacher_mlp(model, predictor, data, pos_train_edge, mp_edges, optimizer, batch_size, dataset,
                                   dtype)
-    if encoder_name != "sage":
-        raise NotImplementedError("teacher encoder 'gcn' (SURVEY §8f4: next)")
+    if encoder_name not in ("sage", "gcn"):
+        raise ValueError(f"unknown encoder {encoder_name!r}")
     model.train()
     predictor.train()
     eng = _teacher_engine(model, predictor, data, optimizer, mp_edges, dtype)

@@ -2,14 +2,15 @@
 (src/models.py), computing on MI355X through libllp_hip (llp_ops.py).
 
   MLP(num_layers, input_dim, hidden_dim, output_dim, dropout_ratio, norm_type='none')   src/models.py:6-54
+  GCN(in, hidden, out, num_layers, dropout)                                             src/models.py:56-80
   SAGE(data_name, in, hidden, out, num_layers, dropout, conv_layer, norm_type='none')   src/models.py:82-119
   LinkPredictor(predictor, in, hidden, out, num_layers, dropout)                        src/models.py:121-150
 
 State-dict keys match (``layers.{i}.weight``, ``lins.{i}.weight``,
 ``convs.{i}.lin_l.weight`` ...), so teacher/student checkpoints written by the
 reference load here and vice versa.  Forward/backward run as HIP kernels; a CPU
-tensor raises (no fallback).  norm_type 'batch'/'layer' and the GCN encoder are
-out of scope.
+tensor raises (no fallback).  norm_type 'batch'/'layer' (never set by the
+reference's scripts or CLIs) is not implemented.
 """
 import torch
 import torch.nn as nn
@@ -48,6 +49,31 @@ class MLP(nn.Module):
             h = ops.linear(h, layer.weight, layer.bias, relu=not last,
                            dropout=0.0 if last else self.dropout.p, training=self.training)
         return h
+
+
+class GCN(nn.Module):
+    """src/models.py:56-80: GCNConv(cached=True) layers (llp_sage.GCNConv),
+    ReLU + dropout between them.  Trained by llp_teacher.TeacherEngine."""
+
+    def __init__(self, in_channels, hidden_channels, out_channels, num_layers, dropout):
+        super().__init__()
+        from llp_sage import GCNConv
+        self.convs = nn.ModuleList()
+        self.convs.append(GCNConv(in_channels, hidden_channels, cached=True))
+        for _ in range(num_layers - 2):
+            self.convs.append(GCNConv(hidden_channels, hidden_channels, cached=True))
+        self.convs.append(GCNConv(hidden_channels, out_channels, cached=True))
+        self.dropout = dropout
+
+    def reset_parameters(self):
+        for conv in self.convs:
+            conv.reset_parameters()
+
+    def forward(self, x, adj_t):
+        for conv in self.convs[:-1]:
+            x = conv(x, adj_t)
+            x = ops.relu_dropout(x, self.dropout, self.training)
+        return self.convs[-1](x, adj_t)
 
 
 class SAGE(nn.Module):

@@ -6,7 +6,8 @@ the best-validation teacher writes ``../saved-features/<ds>-<enc>_<mode>.pkl``
 main.py (and the reference's main.py) read.
 
 Encoders: 'sage' (SAGEConv; SAGEConv_updated for coauthor-physics, :376-383)
-on llp_teacher.TeacherEngine, 'mlp' on the full-batch engine.  Additive
+and 'gcn' (:384-387) on llp_teacher.TeacherEngine, 'mlp' on the full-batch
+engine.  Additive
 flags: --dtype {fp32,bf16}, --synthetic (see main.py).
 """
 import argparse
@@ -20,7 +21,7 @@ import llp_train
 from llp_sage import SAGEConv, SAGEConv_updated
 from logger import Logger, ProductionLogger
 from main import print_epoch, seed_everything, _write_summary
-from models import MLP, SAGE, LinkPredictor
+from models import GCN, MLP, SAGE, LinkPredictor
 
 
 def build_parser():
@@ -83,10 +84,12 @@ def main(argv=None):
         conv = SAGEConv_updated if args.datasets == "coauthor-physics" else SAGEConv
         model = SAGE(args.datasets, input_size, args.hidden_channels, args.hidden_channels, args.num_layers,
                      args.dropout, conv).to(device)
+    elif args.encoder == 'gcn':
+        model = GCN(input_size, args.hidden_channels, args.hidden_channels, args.num_layers, args.dropout).to(device)
     elif args.encoder == 'mlp':
         model = MLP(args.num_layers, input_size, args.hidden_channels, args.hidden_channels, args.dropout).to(device)
     else:
-        raise NotImplementedError("encoder 'gcn' (SURVEY §8f4: next)")
+        raise ValueError(f"unknown encoder {args.encoder!r}")
     predictor = LinkPredictor(args.predictor, args.hidden_channels, args.hidden_channels, 1, 2,
                               args.dropout).to(device)
 

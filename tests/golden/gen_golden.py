@@ -406,6 +406,22 @@ class _RestatedSAGEConv(nn.Module):
         return O.sage_conv(x, edge_index, self.lin_l.weight, self.lin_l.bias, self.lin_r.weight)
 
 
+class _RestatedGCNConv(nn.Module):
+    """PyG 2.2.0 GCNConv(cached=True) parameters: ``bias`` then ``lin.weight``."""
+
+    def __init__(self, in_channels, out_channels, cached=False, bias=True, **kw):
+        super().__init__()
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+        self.lin = nn.Linear(in_channels, out_channels, bias=False)
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.lin.weight)
+        nn.init.zeros_(self.bias)
+
+    def forward(self, x, edge_index):
+        return O.gcn_conv(x, edge_index, self.lin.weight, self.bias)
+
+
 class _MessagePassing(nn.Module):
     def __init__(self, aggr="mean", **kw):
         super().__init__()
@@ -423,9 +439,10 @@ def load_reference_sage():
     stubs = {}
     pyg = types.ModuleType("torch_geometric")
     pyg_nn = types.ModuleType("torch_geometric.nn")
-    for n in ("GCNConv", "GATConv", "APPNP"):
+    for n in ("GATConv", "APPNP"):
         setattr(pyg_nn, n, type(n, (), {}))
     pyg_nn.SAGEConv = _RestatedSAGEConv
+    pyg_nn.GCNConv = _RestatedGCNConv
     conv = types.ModuleType("torch_geometric.nn.conv")
     conv.MessagePassing = _MessagePassing
     dense = types.ModuleType("torch_geometric.nn.dense")
@@ -512,15 +529,25 @@ def load_reference_teacher_train(rec: Recorder, neg_seed: int):
     return ns["train"]
 
 
-def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, dataset="cora", epochs=2):
+def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, dataset="cora", epochs=2,
+                     encoder="sage", self_loops=0):
     rec = Recorder()
     ref_mods, ref_updated = load_reference_sage()
     train = load_reference_teacher_train(rec, neg_seed=seed + 31)
     torch.manual_seed(seed)
     pairs, ei = synth_graph(N, E_und, seed, interleave=False)
+    if self_loops:       # GCN's gcn_norm drops input self-loops before adding its own
+        loops = torch.arange(0, N, max(1, N // self_loops))[:self_loops]
+        pairs = torch.cat([pairs, torch.stack([loops, loops], 1)], 0)
+        ei = torch.cat([pairs, pairs.flip(1)], 0).t().contiguous()
     x = torch.randn(N, F_) * 0.5
-    conv_layer = ref_updated if updated else ref_mods.SAGE.__init__.__globals__["SAGEConv"]
-    model = ref_mods.SAGE(dataset, F_, H, H, L, 0.0, conv_layer)
+    if encoder == "gcn":
+        model = ref_mods.GCN(F_, H, H, L, 0.0)
+        for c in model.convs:     # non-zero biases so the bias path is exercised
+            nn.init.uniform_(c.bias, -0.1, 0.1)
+    else:
+        conv_layer = ref_updated if updated else ref_mods.SAGE.__init__.__globals__["SAGEConv"]
+        model = ref_mods.SAGE(dataset, F_, H, H, L, 0.0, conv_layer)
     predictor = ref_mods.LinkPredictor("mlp", H, H, 1, 2, 0.0)
     init_enc = {k: v.clone() for k, v in model.state_dict().items()}
     init_pred = {k: v.clone() for k, v in predictor.state_dict().items()}
@@ -532,12 +559,12 @@ def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, 
     else:
         data = types.SimpleNamespace(x=x, edge_index=ei)
         split_edge = None
-    losses = [train(model, predictor, data, split_edge, opt, bs, "sage", dataset, transductive)
+    losses = [train(model, predictor, data, split_edge, opt, bs, encoder, dataset, transductive)
               for _ in range(epochs)]
     mp_edges = data.adj_t if transductive == "transductive" else ei
     out = dict(N=N, F=F_, H=H, L=L, x=x.numpy(), edge_index=mp_edges.numpy(), train_pairs=pairs.numpy(),
                epoch_losses=np.array(losses, np.float64), updated=np.array(int(updated)), batch_size=np.array(bs),
-               transductive=np.array(transductive), dataset=np.array(dataset))
+               transductive=np.array(transductive), dataset=np.array(dataset), encoder=np.array(encoder))
     for k, v in init_enc.items():
         out[f"init/enc/{k}"] = v.numpy()
     for k, v in init_pred.items():
@@ -771,6 +798,14 @@ def main():
     run_production_split_case("production_split_small", N=500, F_=4, E_und=2500, ratios=(0.1, 0.1, 0.1, 0.1),
                               seed=13)
     if os.environ.get("GOLDEN_ONLY") == "production_split":
+        return
+    # GCN teacher (src/models.py:56-80): directed transductive graph (one-direction
+    # adj_t, self-loops in the input) and a symmetric production graph, 3 layers
+    run_teacher_case("teacher_gcn_small", N=110, F_=24, H=64, L=2, E_und=400, bs=160, updated=False,
+                     transductive="transductive", seed=21, encoder="gcn", self_loops=6)
+    run_teacher_case("teacher_gcn3_production_small", N=120, F_=40, H=32, L=3, E_und=380, bs=256,
+                     updated=False, transductive="production", seed=22, encoder="gcn")
+    if os.environ.get("GOLDEN_ONLY") == "gcn":
         return
     run_logger_case("logger_output")
     run_teacher_case("teacher_sage_small", N=110, F_=24, H=64, L=2, E_und=400, bs=160, updated=False,

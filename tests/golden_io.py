@@ -112,7 +112,8 @@ def load_teacher_case(name):
         train_pairs=torch.from_numpy(z["train_pairs"].copy()), epoch_losses=z["epoch_losses"],
         enc0=_params(z, "init/enc", enc_keys), pred0=_params(z, "init/pred", pred_keys),
         enc_final=_params(z, "final/enc", enc_keys), pred_final=_params(z, "final/pred", pred_keys),
-        h_eval=torch.from_numpy(z["h_eval"].copy()), steps=[])
+        h_eval=torch.from_numpy(z["h_eval"].copy()), steps=[],
+        encoder=str(z["encoder"]) if "encoder" in z.files else "sage")
     c.pos_train_edge = c.train_pairs if c.transductive == "transductive" else c.edge_index.t()
     ng = len(c.enc0) + len(c.pred0)
     for s in range(int(z["nsteps"])):
@@ -129,6 +130,7 @@ def load_teacher_case(name):
     return c
 
 
-TEACHER_CASES = ["teacher_sage_small", "teacher_sage3_collab_small", "teacher_updated_production_small"]
+TEACHER_CASES = ["teacher_sage_small", "teacher_sage3_collab_small", "teacher_updated_production_small",
+                 "teacher_gcn_small", "teacher_gcn3_production_small"]
 MINIBATCH_CASES = ["minibatch_collab_small", "minibatch_rw_small"]
 FULLBATCH_CASES = ["fullbatch_cora_small", "fullbatch_production_small"]

@@ -85,3 +85,15 @@ def test_production_cli(workdir):
     assert len(lines) == 5 and "new_new: " in lines[0], out
     txt = open(workdir / "results" / "cora_KD_production.txt").read()
     assert "Final old_new" in txt
+
+
+def test_gcn_teacher_cli(workdir):
+    """--encoder=gcn (src/train_teacher_gnn.py:384-387) writes the artefacts the
+    student CLI reads under the gcn tag."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import train_teacher_gnn as teacher_cli
+    out = _run(teacher_cli, ["--datasets=cora", "--encoder=gcn", "--runs=1", "--epochs=2", "--synthetic"])
+    assert "Run: 01, Epoch: 02" in out
+    sd = torch.load(workdir / "saved-models" / "cora-gcn_transductive.pkl", weights_only=True)
+    assert "convs.0.lin.weight" in sd["gnn"] and "convs.0.bias" in sd["gnn"]

@@ -22,8 +22,11 @@ def _build(c, dtype="fp32", dropout=0.0):
     import llp_sage
     import llp_teacher
     import models
-    conv = llp_sage.SAGEConv_updated if c.updated else llp_sage.SAGEConv
-    model = models.SAGE(c.dataset, c.F, c.H, c.H, c.L, dropout, conv).to(DEV)
+    if c.encoder == "gcn":
+        model = models.GCN(c.F, c.H, c.H, c.L, dropout).to(DEV)
+    else:
+        conv = llp_sage.SAGEConv_updated if c.updated else llp_sage.SAGEConv
+        model = models.SAGE(c.dataset, c.F, c.H, c.H, c.L, dropout, conv).to(DEV)
     pred = models.LinkPredictor("mlp", c.H, c.H, 1, 2, dropout).to(DEV)
     with torch.no_grad():
         for p, v in zip(list(model.parameters()) + list(pred.parameters()), c.enc0 + c.pred0):
@@ -68,7 +71,7 @@ def test_teacher_engine_replays_reference(name):
         (h - c.h_eval).abs().max()
 
 
-@pytest.mark.parametrize("name", ["teacher_sage_small", "teacher_updated_production_small"])
+@pytest.mark.parametrize("name", ["teacher_sage_small", "teacher_updated_production_small", "teacher_gcn_small"])
 def test_teacher_engine_bf16_and_dropout_run(name):
     """bf16 engine tracks fp32 on the first step; dropout + device negatives run."""
     _need_gpu()
@@ -120,3 +123,33 @@ def test_sage_module_forward_backward(updated):
     for c, (wl, bl, wr) in zip(model.convs, convs):
         assert torch.allclose(c.lin_l.weight.grad.cpu(), wl.grad, rtol=1e-3, atol=1e-4)
         assert torch.allclose(c.lin_r.weight.grad.cpu(), wr.grad, rtol=1e-3, atol=1e-4)
+
+
+def test_gcn_module_forward_backward():
+    """models.GCN through the autograd ops (GCNConv: lin, normalised propagation
+    with self-loops, bias) vs the oracle, on a directed graph with self-loops."""
+    _need_gpu()
+    import models
+    torch.manual_seed(1)
+    N, F_, H = 160, 48, 64
+    ei = torch.randint(0, N, (2, 800))
+    ei[:, :10] = torch.arange(10).repeat(2, 1)          # input self-loops (dropped by gcn_norm)
+    model = models.GCN(F_, H, H, 3, 0.0).to(DEV)
+    with torch.no_grad():
+        for c in model.convs:
+            c.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(N, F_)
+    xd = x.to(DEV).requires_grad_()
+    h = model(xd, ei.to(DEV))
+    gh = torch.randn_like(h)
+    h.backward(gh)
+    convs = [(c.lin.weight.detach().cpu().requires_grad_(), c.bias.detach().cpu().requires_grad_())
+             for c in model.convs]
+    xr = x.clone().requires_grad_()
+    href = O.gcn_forward(xr, ei, convs, 0.0)
+    href.backward(gh.cpu())
+    assert torch.allclose(h.detach().cpu(), href.detach(), rtol=1e-4, atol=1e-4)
+    assert torch.allclose(xd.grad.cpu(), xr.grad, rtol=1e-3, atol=1e-4)
+    for c, (w, b) in zip(model.convs, convs):
+        assert torch.allclose(c.lin.weight.grad.cpu(), w.grad, rtol=1e-3, atol=1e-4)
+        assert torch.allclose(c.bias.grad.cpu(), b.grad, rtol=1e-3, atol=1e-4)

@@ -91,6 +91,14 @@ def test_oracle_replays_reference_steps(name):
             tot, n, ep = 0.0, 0, ep + 1
 
 
+def _oracle_encoder(c, enc, training):
+    if c.encoder == "gcn":   # per conv: bias, lin.weight (PyG GCNConv parameter order)
+        convs = [(enc[2 * i + 1], enc[2 * i]) for i in range(c.L)]
+        return O.gcn_forward(c.x, c.edge_index, convs, 0.0, training=training)
+    convs = [tuple(enc[3 * i:3 * i + 3]) for i in range(c.L)]
+    return O.sage_forward(c.x, c.edge_index, convs, 0.0, training=training, updated=c.updated)
+
+
 def _oracle_teacher_replay(c):
     """Oracle restatement of the teacher's train() on the recorded permutations
     and negatives: SAGE forward, LinkPredictor, BCE, clip per module, Adam."""
@@ -99,8 +107,7 @@ def _oracle_teacher_replay(c):
     adam = O.AdamState(enc + pred, lr=0.005)
     recs = []
     for st in c.steps:
-        convs = [tuple(enc[3 * i:3 * i + 3]) for i in range(c.L)]
-        h = O.sage_forward(c.x, c.edge_index, convs, 0.0, updated=c.updated)
+        h = _oracle_encoder(c, enc, True)
         tr = torch.cat([st.edge, st.neg_edge], 1)
         out = O.link_predictor_forward(h[tr[0]], h[tr[1]], pred[0::2], pred[1::2]).squeeze(-1)
         label = torch.cat([torch.ones(st.edge.size(1)), torch.zeros(st.neg_edge.size(1))])
@@ -122,7 +129,5 @@ def test_oracle_replays_reference_teacher(name):
             assert torch.allclose(g, ref, rtol=1e-4, atol=1e-6), (name, (g - ref).abs().max())
     for p, ref in zip(enc + pred, c.enc_final + c.pred_final):
         assert torch.allclose(p.detach(), ref, rtol=1e-4, atol=1e-5), (name, (p - ref).abs().max())
-    convs = [tuple(enc[3 * i:3 * i + 3]) for i in range(c.L)]
-    h = O.sage_forward(c.x, c.edge_index, [tuple(t.detach() for t in cv) for cv in convs], 0.0, training=False,
-                       updated=c.updated)
+    h = _oracle_encoder(c, [p.detach() for p in enc], False)
     assert torch.allclose(h, c.h_eval, rtol=1e-4, atol=1e-5)
