@@ -1,12 +1,19 @@
-"""Production (inductive) edge split — drop-in for the reference's
-``do_production_edge_split`` (src/generate_production_split.py:32-95) and the
-``../data/<ds>_production.pkl`` cache that train_teacher_gnn.py writes and
-main.py reads (src/train_teacher_gnn.py:341-365, src/main.py:338).
+"""Edge splits of the reference, restated on its own random streams:
+
+  do_edge_split              src/utils.py:62-105 (the SEAL transductive split,
+                             cached by the reference as ``../data/<ds>.pkl``,
+                             src/main.py:296-301, src/train_teacher_gnn.py:310-315)
+  do_production_edge_split   src/generate_production_split.py:32-95 (the
+                             inductive split, cached as ``<ds>_production.pkl``,
+                             src/train_teacher_gnn.py:341-365, src/main.py:338)
 
 The reference builds the split from torch_geometric 2.2.0 pieces; those are
 restated here on the SAME random streams the reference draws from, so a given
 graph and seed split into the same node / edge sets:
 
+  train_test_split_edges(data, val, test)   ``torch.randperm`` over row<col edges,
+                                            train edges made undirected, negatives
+                                            from a dense N x N upper-triangle mask
   negative_sampling(..., method='sparse')   Python ``random.sample`` over the
                                             edge-vector population, ``np.isin``
                                             filtering, <= 3 rounds
@@ -28,6 +35,7 @@ tensors, read back with ``torch.load(weights_only=True)``.
 """
 from __future__ import annotations
 
+import math
 import os
 import random
 
@@ -138,6 +146,79 @@ def negative_sampling(edge_index: torch.Tensor, num_nodes: int, num_neg_samples:
             neg_idx = neg_idx[:num_neg_samples]
             break
     return _vector_to_edge_index(neg_idx, N, force_undirected)
+
+
+# --- transductive (SEAL) split ---
+
+def coalesce(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
+    """Sorted by (row, col), duplicates removed (torch_geometric.utils.coalesce)."""
+    key = torch.unique(edge_index[0].long() * num_nodes + edge_index[1].long())
+    return torch.stack([key.div(num_nodes, rounding_mode="floor"), key % num_nodes], 0)
+
+
+def to_undirected(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
+    return coalesce(torch.cat([edge_index, edge_index.flip([0])], 1), num_nodes)
+
+
+def add_self_loops(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
+    loops = torch.arange(num_nodes, dtype=edge_index.dtype).unsqueeze(0).repeat(2, 1)
+    return torch.cat([edge_index, loops], 1)
+
+
+def train_test_split_edges(edge_index: torch.Tensor, num_nodes: int, val_ratio: float = 0.05,
+                           test_ratio: float = 0.1) -> dict:
+    """PyG 2.2.0 train_test_split_edges: shuffled row<col edges cut into
+    val / test / train (train returned in both directions, coalesced); val and
+    test negatives drawn from the upper triangle minus every positive edge."""
+    row, col = edge_index
+    mask = row < col
+    row, col = row[mask], col[mask]
+    n_v = int(math.floor(val_ratio * row.size(0)))
+    n_t = int(math.floor(test_ratio * row.size(0)))
+    perm = torch.randperm(row.size(0))
+    row, col = row[perm], col[perm]
+    out = {"val_pos": torch.stack([row[:n_v], col[:n_v]]),
+           "test_pos": torch.stack([row[n_v:n_v + n_t], col[n_v:n_v + n_t]]),
+           "train_pos": to_undirected(torch.stack([row[n_v + n_t:], col[n_v + n_t:]]), num_nodes)}
+    neg_mask = torch.ones(num_nodes, num_nodes, dtype=torch.uint8).triu(diagonal=1).to(torch.bool)
+    neg_mask[row, col] = 0
+    neg_row, neg_col = neg_mask.nonzero(as_tuple=False).t()
+    del neg_mask
+    sel = torch.randperm(neg_row.size(0))[:n_v + n_t]
+    neg_row, neg_col = neg_row[sel], neg_col[sel]
+    out["val_neg"] = torch.stack([neg_row[:n_v], neg_col[:n_v]])
+    out["test_neg"] = torch.stack([neg_row[n_v:n_v + n_t], neg_col[n_v:n_v + n_t]])
+    return out
+
+
+def do_edge_split(data: GraphData, fast_split: bool = False, val_ratio: float = 0.05, test_ratio: float = 0.1,
+                  split_seed: int = 234) -> dict:
+    """src/utils.py:62-105 -> split_edge {'train','valid','test'} x {'edge','edge_neg'}
+    with edges as [E, 2] int64 (the dict the reference torch.saves)."""
+    random.seed(split_seed)
+    torch.manual_seed(split_seed)
+    ei = data.edge_index.cpu().long()
+    N = data.num_nodes
+    if not fast_split:
+        s = train_test_split_edges(ei, N, val_ratio, test_ratio)
+        s["train_neg"] = negative_sampling(add_self_loops(s["train_pos"], N), N,
+                                           num_neg_samples=s["train_pos"].size(1))
+    else:
+        row, col = ei
+        mask = row < col
+        row, col = row[mask], col[mask]
+        n_v = int(math.floor(val_ratio * row.size(0)))
+        n_t = int(math.floor(test_ratio * row.size(0)))
+        perm = torch.randperm(row.size(0))
+        row, col = row[perm], col[perm]
+        s = {"val_pos": torch.stack([row[:n_v], col[:n_v]]),
+             "test_pos": torch.stack([row[n_v:n_v + n_t], col[n_v:n_v + n_t]]),
+             "train_pos": torch.stack([row[n_v + n_t:], col[n_v + n_t:]])}
+        neg = negative_sampling(ei, N, num_neg_samples=row.size(0))
+        s["val_neg"], s["test_neg"], s["train_neg"] = neg[:, :n_v], neg[:, n_v:n_v + n_t], neg[:, n_v + n_t:]
+    return {"train": {"edge": s["train_pos"].t(), "edge_neg": s["train_neg"].t()},
+            "valid": {"edge": s["val_pos"].t(), "edge_neg": s["val_neg"].t()},
+            "test": {"edge": s["test_pos"].t(), "edge_neg": s["test_neg"].t()}}
 
 
 # --- transforms ---
@@ -297,6 +378,7 @@ def production_split(data_name: str, dataset_dir: str, synthetic: bool):
     return split
 
 
-__all__ = ["GraphData", "negative_sampling", "random_node_split", "split_edges", "subgraph_relabel",
+__all__ = ["GraphData", "coalesce", "to_undirected", "add_self_loops", "train_test_split_edges", "do_edge_split",
+           "negative_sampling", "random_node_split", "split_edges", "subgraph_relabel",
            "random_link_split", "production_ratios", "do_production_edge_split", "save_production_split",
            "load_production_split", "production_split"]

@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import ast
 import itertools
+import math
 import os
 import random
 import sys
@@ -765,6 +766,89 @@ def run_production_split_case(name, N, F_, E_und, ratios, seed):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
+
+def _pyg_coalesce_und(ei, n):
+    e = torch.cat([ei, ei.flip([0])], 1)
+    key = torch.unique(e[0] * n + e[1])
+    return torch.stack([key // n, key % n])
+
+
+def _pyg_train_test_split_edges(data, val_ratio=0.05, test_ratio=0.1):
+    """PyG 2.2.0 torch_geometric.utils.train_test_split_edges (no edge_attr)."""
+    n = data.num_nodes
+    row, col = data.edge_index
+    data.edge_index = None
+    m = row < col
+    row, col = row[m], col[m]
+    n_v = int(math.floor(val_ratio * row.size(0)))
+    n_t = int(math.floor(test_ratio * row.size(0)))
+    perm = torch.randperm(row.size(0))
+    row, col = row[perm], col[perm]
+    data.val_pos_edge_index = torch.stack([row[:n_v], col[:n_v]], dim=0)
+    data.test_pos_edge_index = torch.stack([row[n_v:n_v + n_t], col[n_v:n_v + n_t]], dim=0)
+    data.train_pos_edge_index = _pyg_coalesce_und(torch.stack([row[n_v + n_t:], col[n_v + n_t:]], dim=0), n)
+    neg_adj_mask = torch.ones(n, n, dtype=torch.uint8).triu(diagonal=1).to(torch.bool)
+    neg_adj_mask[row, col] = 0
+    neg_row, neg_col = neg_adj_mask.nonzero(as_tuple=False).t()
+    perm = torch.randperm(neg_row.size(0))[:n_v + n_t]
+    neg_row, neg_col = neg_row[perm], neg_col[perm]
+    data.val_neg_edge_index = torch.stack([neg_row[:n_v], neg_col[:n_v]], dim=0)
+    data.test_neg_edge_index = torch.stack([neg_row[n_v:n_v + n_t], neg_col[n_v:n_v + n_t]], dim=0)
+    return data
+
+
+def _pyg_add_self_loops(edge_index, edge_attr=None, num_nodes=None):
+    n = num_nodes if num_nodes is not None else int(edge_index.max()) + 1
+    loops = torch.arange(n).unsqueeze(0).repeat(2, 1)
+    return torch.cat([edge_index, loops], dim=1), None
+
+
+def load_reference_utils():
+    """Exec src/utils.py (get_dataset / do_edge_split) over restated PyG stubs."""
+    pyg = types.ModuleType("torch_geometric")
+    pyg.datasets = types.ModuleType("torch_geometric.datasets")
+    pd = types.ModuleType("torch_geometric.data")
+    pd.Data, pd.Dataset = _PygData, list
+    pu = types.ModuleType("torch_geometric.utils")
+    pu.negative_sampling, pu.add_self_loops = _pyg_negative_sampling, _pyg_add_self_loops
+    pu.train_test_split_edges = _pyg_train_test_split_edges
+    pt = types.ModuleType("torch_geometric.transforms")
+    for n in ("NormalizeFeatures", "Compose", "BaseTransform", "ToDevice", "RandomLinkSplit"):
+        setattr(pt, n, None)
+    stubs = {"torch_geometric": pyg, "torch_geometric.datasets": pyg.datasets, "torch_geometric.data": pd,
+             "torch_geometric.utils": pu, "torch_geometric.transforms": pt}
+    saved = {k: sys.modules.get(k) for k in stubs}
+    sys.modules.update(stubs)
+    try:
+        mod = types.ModuleType("ref_utils")
+        p = os.path.join(REF, "utils.py")
+        exec(compile(_compile_file(p), p, "exec"), mod.__dict__)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return mod
+
+
+def run_edge_split_case(name, N, E_und, seed, fast_split=False):
+    """src/utils.py:62-105 (the SEAL split the reference caches as ../data/<ds>.pkl)."""
+    mod = load_reference_utils()
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randint(0, N, (E_und,), generator=g)
+    v = torch.randint(0, N, (E_und,), generator=g)
+    keep = u != v
+    ei = _pyg_coalesce_und(torch.stack([u[keep], v[keep]]), N)
+    x = torch.randn(N, 4, generator=g)
+    se = mod.do_edge_split([_PygData(x, ei)], fast_split=fast_split)
+    out = dict(N=np.int64(N), x=x.numpy(), edge_index=ei.numpy(), fast_split=np.array(int(fast_split)))
+    for s in ("train", "valid", "test"):
+        for k in ("edge", "edge_neg"):
+            out[f"{s}/{k}"] = se[s][k].numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
 def run_logger_case(name):
     """src/logger.py printed output for fixed result tables (the CLI's outputs
     must stay byte-identical)."""
@@ -793,6 +877,10 @@ def run_logger_case(name):
 
 def main():
     ref_models = load_reference_models()
+    run_edge_split_case("edge_split_small", N=200, E_und=700, seed=14)
+    run_edge_split_case("edge_split_fast_small", N=150, E_und=500, seed=15, fast_split=True)
+    if os.environ.get("GOLDEN_ONLY") == "edge_split":
+        return
     run_production_split_case("production_split_cora_small", N=300, F_=8, E_und=900, ratios=(0.3, 0.3, 0.3, 0.1),
                               seed=12)
     run_production_split_case("production_split_small", N=500, F_=4, E_und=2500, ratios=(0.1, 0.1, 0.1, 0.1),

@@ -94,3 +94,20 @@ def test_undirected_vector_round_trip():
     idx2, pop2 = llp_split._edge_index_to_vector(back[:, :pop].flip([0]), N, False)
     back2 = llp_split._vector_to_edge_index(idx2, N, False)
     assert torch.equal(back2, back[:, :pop].flip([0]))
+
+
+@pytest.mark.parametrize("case", ["edge_split_small", "edge_split_fast_small"])
+def test_edge_split_matches_reference(case):
+    """do_edge_split (src/utils.py:62-105, the transductive SEAL split the
+    reference caches as ../data/<ds>.pkl): same edges, same order."""
+    g = np.load(os.path.join(HERE, "golden", case + ".npz"))
+    data = llp_split.GraphData(torch.from_numpy(g["x"]), torch.from_numpy(g["edge_index"]))
+    se = llp_split.do_edge_split(data, fast_split=bool(int(g["fast_split"])))
+    for s in ("train", "valid", "test"):
+        for k in ("edge", "edge_neg"):
+            np.testing.assert_array_equal(se[s][k].numpy(), g[f"{s}/{k}"], err_msg=f"{s}/{k}")
+    if not int(g["fast_split"]):
+        # train positives come back in both directions (to_undirected), the others once
+        tr = se["train"]["edge"]
+        assert set(map(tuple, tr.tolist())) == set(map(tuple, tr.flip(1).tolist()))
+        assert bool((se["valid"]["edge"][:, 0] < se["valid"]["edge"][:, 1]).all())
