@@ -100,7 +100,7 @@ int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b,
  * 4-stage / 2-ahead ring of 64-B lines, or the lockstep 4-stage ring.  All
  * variants give bit-identical results.  Returns the previous variant (or an
  * error code). */
-enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 2, LLP_GEMM_Q64 = 3 };
+enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 2, LLP_GEMM_Q64 = 3, LLP_GEMM_Q64L = 4 };
 int llp_set_gemm_variant(int variant);
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
@@ -193,6 +193,15 @@ int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t*
 int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
                          const void* src, int64_t ld_src, void* out, int64_t ld_out, void* stream);
 int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
+/* Backward of the predictor input h[i] * h[j] (src/main.py:102-103,126) reduced
+ * straight onto the unique nodes: dh[u] = sum over the target rows of node u
+ * (seg_ptr / rows from llp_dedup_rows, row order) of each row's Hadamard
+ * gradient, f32 accumulation, one write per node.  Row layouts as
+ * llp_hadamard_bwd_blocks; h is the unique-node table [U, H], pos maps target
+ * rows to it; drow (dZ = NULL) is the 'inner' predictor's per-pair scalar. */
+int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
+                              const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos, const void* dZ,
+                              const float* drow, const void* h, void* dh, int64_t ld_dh, void* stream);
 
 /* Generic scatter form (full-batch train(), src/main.py:173-214, where rows of
  * h repeat): dh[ia[r]] += dZ[r]*h2[ib[r]],  dh[ib[r]] += dZ[r]*h1[ia[r]]

@@ -104,6 +104,83 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, 
   *reinterpret_cast<uint4*>(out + u * ldo + c * E) = V8<T>::pack(acc);
 }
 
+// Fused Hadamard backward + per-node reduction (the unique-node student path).
+// The predictor input of pair row z is h[a_z] * h[b_z]; its gradient dZ[z]
+// reaches a_z as dZ[z] * h[b_z] and b_z as dZ[z] * h[a_z].  Target rows (the
+// student's gathered layout, src/main.py:95) are [B anchors x (1 + C)] then
+// [L2 sources | L2 destinations]; pair rows are [B x C anchor-context] then
+// [L2 links].  For unique node u this sums, over its target rows in row order,
+//   anchor row b*C1      : sum_cc dZ[b*C+cc] * h[pos[b*C1+1+cc]]
+//   context row b*C1+1+cc: dZ[b*C+cc] * h[pos[b*C1]]
+//   source row base+i    : dZ[B*C+i] * h[pos[base+L2+i]]
+//   dest row base+L2+i   : dZ[B*C+i] * h[pos[base+i]]
+// in f32 registers and writes dh[u] once (drow: 'inner' predictor, dZ[z] = drow[z]
+// broadcast).  One thread per 16-B column chunk, 256/cpr nodes per block.
+template <typename T>
+__device__ __forceinline__ void load16(const T* p, float* v) {
+  const uint4 r = *reinterpret_cast<const uint4*>(p);
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t u[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  } else {
+    v[0] = __uint_as_float(r.x); v[1] = __uint_as_float(r.y); v[2] = __uint_as_float(r.z); v[3] = __uint_as_float(r.w);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
+    int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ pos, const T* __restrict__ dZ,
+    const float* __restrict__ drow, const T* __restrict__ h, T* __restrict__ dh, int64_t ldo) {
+  constexpr int E = V8<T>::E;
+  const int cpr = (int)(H / E);
+  const int spb = 256 / cpr;
+  const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
+  const int64_t u = (int64_t)blockIdx.x * spb + slot;
+  if (slot >= spb || u >= U) return;
+  const int64_t C1 = C + 1, base = B * C1, col = (int64_t)c * E;
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  auto add_pair = [&](int64_t z, int64_t hr) {
+    float d[E], hv[E];
+    if (drow) {
+      const float s = drow[z];
+#pragma unroll
+      for (int i = 0; i < E; ++i) d[i] = s;
+    } else {
+      load16<T>(dZ + z * H + col, d);
+    }
+    load16<T>(h + hr * H + col, hv);
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += d[i] * hv[i];
+  };
+  const int beg = seg_ptr[u], end = seg_ptr[u + 1];
+  for (int k = beg; k < end; ++k) {
+    const int64_t r = rows[k];
+    if (r < base) {
+      const int64_t b = r / C1, j = r - b * C1;
+      if (j == 0) {
+        const int32_t* pc = pos + b * C1 + 1;
+        const int64_t z0 = b * C;
+#pragma unroll 4
+        for (int64_t cc = 0; cc < C; ++cc) add_pair(z0 + cc, pc[cc]);
+      } else {
+        add_pair(b * C + j - 1, pos[b * C1]);
+      }
+    } else {
+      const int64_t i = r - base;
+      if (i < L2) add_pair(B * C + i, pos[base + L2 + i]);
+      else add_pair(B * C + (i - L2), pos[base + (i - L2)]);
+    }
+  }
+  *reinterpret_cast<uint4*>(dh + u * ldo + col) = V8<T>::pack(acc);
+}
+
 __global__ void gather_i32_kernel(int64_t n, const int32_t* __restrict__ idx, const int32_t* __restrict__ src,
                                   int32_t* __restrict__ out) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -201,6 +278,29 @@ extern "C" int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src,
   if (n == 0) return LLP_OK;
   hipLaunchKernelGGL(gather_i32_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, idx, src,
                      out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
+                                         const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos,
+                                         const void* dZ, const float* drow, const void* h, void* dh, int64_t ld_dh,
+                                         void* stream) {
+  LLP_CHECK_ARG(seg_ptr && rows && pos && h && dh && (dZ || drow), "llp_hadamard_bwd_segments: null");
+  const int E = dtype == LLP_BF16 ? 8 : 4;
+  const int es = dtype == LLP_BF16 ? 2 : 4;
+  LLP_CHECK_ARG(H % E == 0 && H / E <= 256 && (ld_dh * es) % 16 == 0 && (uintptr_t)h % 16 == 0 &&
+                    (uintptr_t)dh % 16 == 0 && (!dZ || (uintptr_t)dZ % 16 == 0),
+                "llp_hadamard_bwd_segments: rows must be 16-B aligned, H <= 256 chunks");
+  if (U == 0) return LLP_OK;
+  const int64_t cpr = H / E, spb = 256 / cpr;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LLP_BF16)
+    hipLaunchKernelGGL(hadamard_bwd_segments_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
+                       H, seg_ptr, rows, pos, (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh, ld_dh);
+  else
+    hipLaunchKernelGGL(hadamard_bwd_segments_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
+                       H, seg_ptr, rows, pos, (const float*)dZ, drow, (const float*)h, (float*)dh, ld_dh);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

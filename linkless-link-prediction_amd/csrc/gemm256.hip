@@ -514,6 +514,11 @@ __device__ __forceinline__ int q64_row(int chunk, int cr) {
   }
 }
 
+// LEAN: phase 3 keeps B-half 0 in registers from phase 0 (no re-read) and
+// drops its barrier — its operands were published by the barriers of phases 0
+// and 2, and chunk 3's refill target (A-half 1 of the other buffer) was last
+// read three barriers earlier.
+template <bool LEAN>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
   constexpr int IMG_U4 = 256 * 8;                  // one operand image [256][8 chunks]
   constexpr int TILE_U4 = 2 * IMG_U4;              // A then B: 64 KiB
@@ -652,11 +657,12 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
     read_a(sA, 1);
     mfma_q(1, 1);
     // phase 3: (1,0), everything resident
-    barrier();
+    if (!LEAN) barrier();
+    else __builtin_amdgcn_sched_barrier(0);
 #ifndef LLP_ABLATE_NOLOAD
     if (more) issue_chunk(3, kt + 1);
 #endif
-    read_b(sB, 0);
+    if (!LEAN) read_b(sB, 0);
     mfma_q(1, 0);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -844,12 +850,12 @@ int g_gemm_variant = -1;
 int llp_gemm_variant() {
   if (g_gemm_variant < 0) {
     const char* e = getenv("LLP_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : LLP_GEMM_Q64;
+    g_gemm_variant = e ? atoi(e) : LLP_GEMM_Q64L;
   }
   return g_gemm_variant;
 }
 extern "C" int llp_set_gemm_variant(int v) {
-  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_Q64, "llp_set_gemm_variant: %d", v);
+  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_Q64L, "llp_set_gemm_variant: %d", v);
   const int old = llp_gemm_variant();
   g_gemm_variant = v;
   return old;
@@ -884,7 +890,9 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   else if (variant == LLP_GEMM_PP42)
     hipLaunchKernelGGL((gemm_nt_bf16_pp<4, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (variant == LLP_GEMM_Q64)
-    hipLaunchKernelGGL(gemm_nt_bf16_q64, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    hipLaunchKernelGGL(gemm_nt_bf16_q64<false>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_Q64L)
+    hipLaunchKernelGGL(gemm_nt_bf16_q64<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (pipe == 4 || pipe == 5)
     hipLaunchKernelGGL(gemm_nt_bf16_256p<4>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (pipe == 3)

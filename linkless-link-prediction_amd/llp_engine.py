@@ -20,12 +20,19 @@ transposed copy, refreshed by the Adam kernel.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 import llp_hip as K
+
+# unique-node path: LLP_SEGMENT_FUSED=1 reduces the Hadamard backward straight onto the unique nodes
+# (llp_hadamard_bwd_segments, f32 accumulation, no [R1, H] row gradients).  It reads every pair row's
+# gradient twice (once per endpoint) and measured 14.99 vs 14.83 ms/step on the collab bench against
+# the default two-kernel path (row gradients in pair-block order + segment sum), so it is opt-in.
+_SEGMENT_FUSED = os.environ.get("LLP_SEGMENT_FUSED", "0") == "1"
 
 _DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
 
@@ -511,17 +518,24 @@ class DistillEngine(EngineBase):
 
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
-        dh_rows = self._buf("dh_rows" if dedup else "gS0", (R1, H), dt)
-        hidx = pos if dedup else None
-        if self.predictor_kind == "mlp":
-            K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0, h, dh_rows, hidx=hidx)
-        else:
-            K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh_rows, drow=dlogit, hidx=hidx)
-        if dedup:
+        mlp = self.predictor_kind == "mlp"
+        if dedup and _SEGMENT_FUSED:
+            # Hadamard backward reduced straight onto the unique nodes (no [R1, H] row gradients)
             dh = self._buf("gS0", (rows_s, H), dt)
-            K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh)
+            K.hadamard_bwd_segments(rows_s, B, C, n_lab, H, seg_ptr, seg_rows, pos, dZ0 if mlp else None, h, dh,
+                                    drow=None if mlp else dlogit)
         else:
-            dh = dh_rows
+            dh_rows = self._buf("dh_rows" if dedup else "gS0", (R1, H), dt)
+            hidx = pos if dedup else None
+            if mlp:
+                K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0, h, dh_rows, hidx=hidx)
+            else:
+                K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh_rows, drow=dlogit, hidx=hidx)
+            if dedup:
+                dh = self._buf("gS0", (rows_s, H), dt)
+                K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh)
+            else:
+                dh = dh_rows
         self._student_backward(dh, rows_s, gather_s, acts, p_drop)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)

@@ -430,3 +430,50 @@ def test_dedup_rows_and_segment_sum(N, R):
     o = torch.empty(333, dtype=torch.int32, device=DEV)
     k.gather_i32(idx.to(DEV), pos, o)
     assert np.array_equal(o.cpu().numpy(), inv[idx.numpy()])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("inner", [False, True])
+def test_hadamard_bwd_segments(dtype, inner):
+    """Fused Hadamard backward reduced onto unique nodes == per-row gradients
+    (anchor rows sum their C contexts) index-added by node, f32."""
+    k = K()
+    g = torch.Generator().manual_seed(5)
+    N, B, C, L2, H = 400, 37, 6, 53, 256
+    R1 = B * (C + 1) + 2 * L2
+    R2 = B * C + L2
+    target = torch.randint(0, N, (R1,), generator=g, dtype=torch.int32)
+    tg = target.to(DEV)
+    uniq = torch.empty(R1, dtype=torch.int32, device=DEV)
+    pos = torch.empty(R1, dtype=torch.int32, device=DEV)
+    nu = torch.empty(1, dtype=torch.int32, device=DEV)
+    segp = torch.empty(R1 + 1, dtype=torch.int32, device=DEV)
+    segr = torch.empty(R1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(k.dedup_ws_bytes(N, R1) // 4 + 16, device=DEV)
+    k.dedup_rows(N, R1, tg, uniq, pos, nu, segp, segr, ws)
+    U = int(nu.item())
+    h = torch.randn(U, H, generator=g).to(DEV, dtype)
+    dZ = torch.randn(R2, H, generator=g).to(DEV, dtype)
+    drow = torch.randn(R2, generator=g).to(DEV)
+    out = torch.empty(U, H, device=DEV, dtype=dtype)
+    k.hadamard_bwd_segments(U, B, C, L2, H, segp, segr, pos, None if inner else dZ, h, out,
+                            drow=drow if inner else None)
+    torch.cuda.synchronize()
+    hr = h.float().cpu()[pos.cpu().long()]                              # [R1, H] rows of h per target row
+    d = drow.cpu().unsqueeze(1).expand(R2, H) if inner else dZ.float().cpu()
+    C1 = C + 1
+    rows = torch.zeros(R1, H)
+    for b in range(B):
+        a = b * C1
+        for cc in range(C):
+            z = b * C + cc
+            rows[a] += d[z] * hr[a + 1 + cc]
+            rows[a + 1 + cc] = d[z] * hr[a]
+    base = B * C1
+    for i in range(L2):
+        z = B * C + i
+        rows[base + i] = d[z] * hr[base + L2 + i]
+        rows[base + L2 + i] = d[z] * hr[base + i]
+    ref = torch.zeros(U, H).index_add_(0, pos.cpu().long(), rows)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * ref.abs().max().item())

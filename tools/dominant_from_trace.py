@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-KERNEL = "gemm_nt_bf16_q64"
+KERNEL = "gemm_nt_bf16_q64<true>"
 
 
 def main():

@@ -16,8 +16,8 @@ import torch  # noqa: E402
 
 import llp_hip as K  # noqa: E402
 
-VARIANTS = (0, 1, 3)
-NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64"}
+VARIANTS = (3, 4)
+NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean"}
 
 
 def main():
