@@ -110,6 +110,11 @@ class EngineBase:
         for p in self.all_params:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
+        # group 0 (student / encoder) first, then the predictor: the predictor's
+        # gradients are the tail of flat_grad, final once its backward is done
+        assert self.param_groups_of == sorted(self.param_groups_of)
+        self._tail_off = sum(p.numel() for p, gr in zip(self.all_params, self.param_groups_of) if gr == 0)
+        self._pending = None
         self.optimizer = optimizer
         self._init_optimizer_state()
 
@@ -291,6 +296,7 @@ class EngineBase:
     def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop):
         dt, dc = self.dtype, self.dc
         if self.predictor_kind != "mlp":
+            self._allreduce_tail_begin()
             return None
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
         Zl = zacts[-1]
@@ -307,6 +313,8 @@ class EngineBase:
             wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
             K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
                       colsum_a=lin.lin.bias.grad)
+            if l == 0:
+                self._allreduce_tail_begin()      # every predictor gradient is final here
             gnext = self._buf(nxt, (R2, lin.in_f), dt)
             if l > 0:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
@@ -316,9 +324,23 @@ class EngineBase:
             cur, nxt = nxt, cur
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
+    def _allreduce_tail_begin(self):
+        """Start the SUM all-reduce of the predictor's gradients on RCCL's stream
+        (async; it waits for the kernels already queued) so it overlaps the
+        Hadamard / student (encoder) backward."""
+        if self.world > 1 and self._pending is None and self._tail_off < self.flat_grad.numel():
+            self._pending = dist.all_reduce(self.flat_grad[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
+                                            async_op=True)
+
     def _allreduce_and_update(self):
         if self.world > 1:
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+            if self._pending is not None:
+                if self._tail_off > 0:
+                    dist.all_reduce(self.flat_grad[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
+                self._pending.wait()            # stream-ordered: no host block on RCCL
+                self._pending = None
+            else:
+                dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
         g = self.optimizer.param_groups[0]
         K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq)
         b1, b2 = g["betas"]
