@@ -24,7 +24,11 @@ extern "C" {
 #define LLP_E_ARG 10001
 #define LLP_E_WORKSPACE 10002
 
-enum llp_dtype { LLP_F32 = 0, LLP_BF16 = 1 };
+enum llp_dtype { LLP_F32 = 0, LLP_BF16 = 1,
+                 /* aux of llp_gemm_nt only: a ReLU bit mask, bit c%8 of byte c/8 of row r at
+                  * aux + r*ld_aux (bytes) -- written by an act=RELU GEMM (bit = bf16 output > 0),
+                  * read by act=RELU_BWD in place of the bf16 activations (16x less traffic) */
+                 LLP_MASK = 2 };
 
 enum llp_act {
   LLP_ACT_NONE = 0,      /* y = alpha*acc + bias                          */
@@ -60,7 +64,8 @@ int llp_device_count(void);
  * and the data-gradient dX = dY . W with B = W^T.  dtype LLP_F32 runs the exact
  * f32 MFMA (v_mfma_f32_16x16x4_f32); LLP_BF16 runs v_mfma_f32_16x16x32_bf16
  * with f32 accumulation.  c_dtype / aux_dtype select the output / aux element
- * type.  bias (f32[N]) may be NULL. */
+ * type (aux_dtype LLP_MASK: aux is a ReLU bit mask, see enum llp_dtype; bf16
+ * 256-tile path only).  bias (f32[N]) may be NULL. */
 /* Optional inverted dropout after the activation (F.dropout / nn.Dropout after
  * ReLU, src/models.py:52-53,144-145): element (m, n) is kept iff
  * u >= p with u = uniform draw #(m*N + n) of Philox stream

@@ -21,7 +21,7 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
                          int64_t ldc, const float* bias, int act, const void* aux, int64_t ld_aux, float alpha,
                          float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
                          const int64_t* drop_ctr, int64_t drop_stream, const float* head_w, float* head_part,
-                         hipStream_t s);
+                         uint8_t* mask_out, const uint8_t* mask_in, int64_t ld_mask, hipStream_t s);
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q);
 int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
                          float* ws_colsum, int64_t splits, hipStream_t s);
@@ -517,6 +517,9 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   LLP_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "llp_gemm_nt: negative size");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_nt: bad dtype %d", dtype);
   LLP_CHECK_ARG(act != LLP_ACT_RELU_BWD || aux, "llp_gemm_nt: RELU_BWD needs aux");
+  const bool mask = aux && aux_dtype == LLP_MASK;
+  LLP_CHECK_ARG(!mask || act == LLP_ACT_RELU || act == LLP_ACT_RELU_BWD,
+                "llp_gemm_nt: a bit-mask aux goes with RELU (written) or RELU_BWD (read)");
   if (M == 0 || N == 0) return LLP_OK;
   NTParams p;
   p.A = to_op(A);
@@ -548,13 +551,18 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
   if (!force_v1 && dtype == LLP_BF16 && c_dtype == LLP_BF16 && K > 0 && K % 64 == 0 && N % 8 == 0 && !B->ptr2 &&
       a16(A->ptr, A->ld) && (!A->ptr2 || a16(A->ptr2, A->ld2)) && a16(B->ptr, B->ld) && a16(C, ldc) &&
-      (act != LLP_ACT_RELU_BWD || (aux_dtype == LLP_BF16 && a16(aux, ld_aux)))) {
-    const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, aux, ld_aux, alpha, p.drop_p,
-                                        p.drop_thresh, p.drop_scale, p.drop_seed, p.drop_ctr, p.drop_stream,
-                                        nullptr, nullptr, s);
+      (act != LLP_ACT_RELU_BWD || mask || (aux_dtype == LLP_BF16 && a16(aux, ld_aux))) &&
+      (!mask || (N % 32 == 0 && ld_aux % 4 == 0 && (uintptr_t)aux % 4 == 0))) {
+    uint8_t* mask_out = mask && act == LLP_ACT_RELU ? (uint8_t*)aux : nullptr;
+    const uint8_t* mask_in = mask && act == LLP_ACT_RELU_BWD ? (const uint8_t*)aux : nullptr;
+    const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, mask ? nullptr : aux, ld_aux, alpha,
+                                        p.drop_p, p.drop_thresh, p.drop_scale, p.drop_seed, p.drop_ctr,
+                                        p.drop_stream, nullptr, nullptr, mask_out, mask_in, ld_aux, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_nt (256 tile): %s", hipGetErrorString((hipError_t)rc));
     return LLP_OK;
   }
+  LLP_CHECK_ARG(!mask, "llp_gemm_nt: bit-mask aux needs the bf16 256-tile path (bf16 in/out, K %% 64 == 0, "
+                       "N %% 32 == 0, 16-byte aligned operands)");
   const int es = dtype == LLP_BF16 ? 2 : 4;
   const bool vec = aligned_op(A, es, K) && aligned_op(B, es, K);
   dim3 grid((unsigned)tiles);
@@ -608,7 +616,7 @@ extern "C" int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_opera
     dstr = dropout->stream_offset;
   }
   const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, nullptr, 0, alpha, dp, dth, ds, dseed, dctr,
-                                      dstr, head_w, head_part, (hipStream_t)stream);
+                                      dstr, head_w, head_part, nullptr, nullptr, 0, (hipStream_t)stream);
   if (rc != 0) return llp::set_error(rc, "llp_gemm_nt_head: %s", hipGetErrorString((hipError_t)rc));
   return LLP_OK;
 }

@@ -42,6 +42,11 @@ struct P256 {
   // head_part[tn][m] = sum over this tile's columns of y[m, n] * head_w[n]
   const float* head_w;
   float* head_part;
+  // ReLU mask as bits (bit c%8 of byte c/8 of row r at +r*ld_mask): written by a
+  // RELU forward (mask_out), read by RELU_BWD instead of the bf16 aux (mask_in)
+  uint8_t* mask_out;
+  const uint8_t* mask_in;
+  int64_t ld_mask;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -355,21 +360,42 @@ __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8
   for (int q = tid; q < TM * chunks_per_row; q += NT2) {
     const int rl = q / chunks_per_row, c = q % chunks_per_row;
     const int64_t row = m0 + rl, col = n0 + c * 8;
-    if (row >= p.M || col >= p.N) continue;
+    const bool ok = row < p.M && col < p.N;
     uint4 v = stg[rl * EPI_ROW_U4 + c];
     if (p.act == LLP_ACT_RELU_BWD) {
-      const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
-      const uint32_t av[4] = {a.x, a.y, a.z, a.w};
       uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      if (p.mask_in) {
+        const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
-        const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
-        vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+        for (int e = 0; e < 4; ++e)
+          vv[e] = ((bits >> (2 * e)) & 1u ? (vv[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (vv[e] & 0xFFFF0000u) : 0u);
+      } else if (ok) {
+        const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
+        const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
+          const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
+          vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+        }
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
-    *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+    if (ok) *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+    if (p.mask_out) {
+      // bit e of this chunk's byte = (bf16 output e > 0), the test RELU_BWD applies;
+      // four consecutive lanes (one row, 32 columns) pack one 32-bit word
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+      uint32_t byte = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        byte |= (__uint_as_float(vw[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
+        byte |= (__uint_as_float(vw[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
+      }
+      const uint32_t b1 = __shfl_down(byte, 1, 64), b2 = __shfl_down(byte, 2, 64), b3 = __shfl_down(byte, 3, 64);
+      if ((q & 3) == 0 && ok)
+        *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    }
   }
 }
 
@@ -822,21 +848,42 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   for (int q = tid; q < TM * chunks_per_row; q += NT2) {
     const int rl = q / chunks_per_row, c = q % chunks_per_row;
     const int64_t row = m0 + rl, col = n0 + c * 8;
-    if (row >= p.M || col >= p.N) continue;
+    const bool ok = row < p.M && col < p.N;
     uint4 v = stg[rl * EPI_ROW_U4 + c];
     if (p.act == LLP_ACT_RELU_BWD) {
-      const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
-      const uint32_t av[4] = {a.x, a.y, a.z, a.w};
       uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      if (p.mask_in) {
+        const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
-        const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
-        vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+        for (int e = 0; e < 4; ++e)
+          vv[e] = ((bits >> (2 * e)) & 1u ? (vv[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (vv[e] & 0xFFFF0000u) : 0u);
+      } else if (ok) {
+        const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
+        const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
+          const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
+          vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
+        }
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
-    *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+    if (ok) *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+    if (p.mask_out) {
+      // bit e of this chunk's byte = (bf16 output e > 0), the test RELU_BWD applies;
+      // four consecutive lanes (one row, 32 columns) pack one 32-bit word
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+      uint32_t byte = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        byte |= (__uint_as_float(vw[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
+        byte |= (__uint_as_float(vw[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
+      }
+      const uint32_t b1 = __shfl_down(byte, 1, 64), b2 = __shfl_down(byte, 2, 64), b3 = __shfl_down(byte, 3, 64);
+      if ((q & 3) == 0 && ok)
+        *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    }
   }
 }
 
@@ -866,10 +913,13 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
                          int64_t ldc, const float* bias, int act, const void* aux, int64_t ld_aux, float alpha,
                          float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
                          const int64_t* drop_ctr, int64_t drop_stream, const float* head_w, float* head_part,
-                         hipStream_t s) {
+                         uint8_t* mask_out, const uint8_t* mask_in, int64_t ld_mask, hipStream_t s) {
   P256 p;
   p.head_w = head_w;
   p.head_part = head_part;
+  p.mask_out = mask_out;
+  p.mask_in = mask_in;
+  p.ld_mask = ld_mask;
   if ((head_w || !C) && A->ptr2) return (int)hipErrorInvalidValue;   // fused head: pipelined kernel only
   p.A = (const bf16_t*)A->ptr; p.ia = A->idx; p.A2 = (const bf16_t*)A->ptr2; p.ia2 = A->idx2;
   p.lda = A->ld; p.lda2 = A->ptr2 ? A->ld2 : 0;

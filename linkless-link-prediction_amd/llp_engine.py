@@ -98,6 +98,7 @@ class EngineBase:
         self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self._bufs = {}
         self._shadows = {}
+        self._act_mask = {}     # id(activation buffer) -> its ReLU bit mask (or None)
 
     def _init_params(self, all_params, groups, optimizer):
         """``groups[i]``: clip group of all_params[i] (clip_grad_norm_ per module, Q9)."""
@@ -187,6 +188,15 @@ class EngineBase:
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.dev)
             self._bufs[name] = b
         return b[:numel].view(*shape)
+
+    def _mask(self, name, rows, cols, k_fwd, k_bwd):
+        """ReLU bit mask [rows, cols/8] (bf16 engine): the forward GEMM (inner
+        dimension k_fwd) writes it, the ReLU-backward GEMM (inner dimension k_bwd)
+        reads it instead of the bf16 activations.  Both must run on the 256-tile
+        path (K % 64, N % 32), else None (the bf16 activations serve as before)."""
+        if self.dtype != torch.bfloat16 or cols % 32 != 0 or k_fwd % 64 != 0 or k_bwd % 64 != 0:
+            return None
+        return self._buf(name, (rows, cols // 8), torch.uint8)
 
     def _ws(self, name, nbytes):
         return self._buf(name, (nbytes // 4 + 16,), torch.float32)
@@ -284,8 +294,10 @@ class EngineBase:
                 K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
                 fused = True
             else:
+                zm = self._mask(f"Zm{l}", R2, lin.out_f, lin.in_f, self.prd[l + 1].out_f) if not last else None
                 K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
-                          dropout=self._dropout(p_drop, 5 + l))
+                          aux=zm, dropout=self._dropout(p_drop, 5 + l))
+                self._act_mask[id(out)] = zm
             zacts.append(out)
             A = K.operand(out)
         if not fused:
@@ -318,11 +330,17 @@ class EngineBase:
             gnext = self._buf(nxt, (R2, lin.in_f), dt)
             if l > 0:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
-                          act=K.ACT_RELU_BWD, aux=zacts[l - 1], alpha=alpha)
+                          act=K.ACT_RELU_BWD, aux=self._relu_aux(zacts[l - 1]), alpha=alpha)
             else:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
             cur, nxt = nxt, cur
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
+
+    def _relu_aux(self, act):
+        """What the ReLU-backward GEMM reads for activation ``act``: its bit mask when
+        the forward wrote one, else the activations themselves."""
+        m = self._act_mask.get(id(act))
+        return m if m is not None else act
 
     def _allreduce_tail_begin(self):
         """Start the SUM all-reduce of the predictor's gradients on RCCL's stream
@@ -449,6 +467,7 @@ class DistillEngine(EngineBase):
         (non-collab, src/main.py:80-82; one host read of its count).
         Returns nothing; the loss terms stay on the device (self.terms).
         """
+        self._act_mask.clear()
         a = self.args
         B = int(anchors.numel())
         P = int(link_ids.numel())
@@ -511,8 +530,10 @@ class DistillEngine(EngineBase):
             if timed:   # the dominant MFMA kernel, timed on the launch stream (bench.py roofline)
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
+            hm = None if last else self._mask(f"Hm{l}", rows_s, lin.out_f, lin.in_f, self.stu[l + 1].out_f)
+            self._act_mask[id(out)] = hm
             K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.in_f, out, dc, bias=lin.b,
-                      act=K.ACT_NONE if last else K.ACT_RELU,
+                      act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             if timed:
                 ev[1].record()
@@ -578,6 +599,7 @@ class DistillEngine(EngineBase):
         neg      optional injected negatives int32[2, n_neg] (parity tests).
         Returns the number of negatives used (host int; the dense sampler's count
         is read back, one sync, as the reference's shapes are host-known)."""
+        self._act_mask.clear()
         a = self.args
         B = int(anchors.numel())
         P = int(link_ids.numel())
@@ -618,8 +640,10 @@ class DistillEngine(EngineBase):
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (N, lin.out_f), dt)
+            hm = None if last else self._mask(f"Hm{l}", N, lin.out_f, lin.in_f, self.stu[l + 1].out_f)
+            self._act_mask[id(out)] = hm
             K.gemm_nt(A, K.operand(lin.Wcomp), N, lin.out_f, lin.in_f, out, dc, bias=lin.b,
-                      act=K.ACT_NONE if last else K.ACT_RELU,
+                      act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             acts.append(out)
             A = K.operand(out)
@@ -737,5 +761,5 @@ class DistillEngine(EngineBase):
             if l > 0:
                 gnext = self._buf(nxt, (R1, lin.in_f), dt)
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
-                          act=K.ACT_RELU_BWD, aux=acts[l - 1], alpha=alpha)
+                          act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)
                 cur, nxt = nxt, cur

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libllp_hip.so")
 
-LLP_F32, LLP_BF16 = 0, 1
+LLP_F32, LLP_BF16, LLP_MASK = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_RELU_BWD = 0, 1, 2
 
 c_i64 = C.c_int64
@@ -170,9 +170,11 @@ def operand(t, idx=None, t2=None, idx2=None) -> Operand:
 def gemm_nt(A: Operand, B: Operand, M, N, K, C_out, dtype, bias=None, act=ACT_NONE, aux=None, alpha=1.0,
             dropout: Dropout | None = None):
     L = lib()
+    # a uint8 aux is a ReLU bit mask [M, N/8]: written by act=RELU, read by act=RELU_BWD
+    aux_code = 0 if aux is None else (LLP_MASK if aux.dtype == torch.uint8 else dtype_code(aux.dtype))
     check(L.llp_gemm_nt(dtype, M, N, K, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0),
                         dtype_code(C_out.dtype), ptr(bias), act, ptr(aux), aux.stride(0) if aux is not None else 0,
-                        dtype_code(aux.dtype) if aux is not None else 0, alpha,
+                        aux_code, alpha,
                         C.byref(dropout) if dropout is not None else None, stream_ptr()), "llp_gemm_nt")
 
 

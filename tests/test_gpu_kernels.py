@@ -477,3 +477,35 @@ def test_hadamard_bwd_segments(dtype, inner):
     ref = torch.zeros(U, H).index_add_(0, pos.cpu().long(), rows)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1000, 1024, 128), (517, 96, 256), (300, 288, 64)])
+def test_gemm_relu_bit_mask(M, N, Kd):
+    """act=RELU with a uint8 aux writes bit c%8 of byte c/8 = (bf16 output > 0);
+    act=RELU_BWD reading that mask equals RELU_BWD reading the bf16 activations."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    mask = torch.full((M, N // 8), 0xAB, dtype=torch.uint8, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)          # kept alive: the kernel reads it
+    drop = k.Dropout(0.25, 77, ctr.data_ptr(), 3)
+    k.gemm_nt(k.operand(x), k.operand(w), M, N, Kd, y, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=mask, dropout=drop)
+    y2 = torch.empty_like(y)
+    k.gemm_nt(k.operand(x), k.operand(w), M, N, Kd, y2, k.LLP_BF16, bias=b, act=k.ACT_RELU, dropout=drop)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)                                      # writing the mask changes nothing else
+    pos = (y.float() > 0).cpu().numpy()
+    bits = np.unpackbits(mask.cpu().numpy(), axis=1, bitorder="little")
+    assert np.array_equal(bits.astype(bool), pos)
+    gy = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    # any [M, N] product exercises the RELU_BWD epilogue: C = gy . w^T (B = w, [N, Kd])
+    assert w.shape == (N, Kd)
+    d_aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    d_msk = torch.empty_like(d_aux)
+    k.gemm_nt(k.operand(gy), k.operand(w), M, N, Kd, d_aux, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=y, alpha=1.5)
+    k.gemm_nt(k.operand(gy), k.operand(w), M, N, Kd, d_msk, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=mask, alpha=1.5)
+    torch.cuda.synchronize()
+    assert torch.equal(d_aux, d_msk)

@@ -39,11 +39,11 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&s));
   CK(hipEventCreate(&e));
   for (int i = 0; i < 3; ++i)
-    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, nullptr, nullptr, 0);
+    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0);
   CK(hipEventRecord(s, 0));
   const int it = 20;
   for (int i = 0; i < it; ++i)
-    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, nullptr, nullptr, 0);
+    llp_gemm_nt_bf16_256(&a, &b, M, N, K, C, N, nullptr, 0, nullptr, 0, 1.f, 0.f, 0, 1.f, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0);
   CK(hipEventRecord(e, 0));
   CK(hipEventSynchronize(e));
   float ms;
