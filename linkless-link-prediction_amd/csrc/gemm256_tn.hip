@@ -84,10 +84,33 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
   const bf16_t* zrow = reinterpret_cast<const bf16_t*>(g_zero_row);
   const uint32_t lds0 = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)smem);
 
+  // full stages (every row < mend, plain operands): per-lane pointers advanced
+  // by a uniform stride, no per-stage address arithmetic beside the MFMAs
+  const int64_t nfull = (p.ia || p.ib) ? 0 : (mend - mbeg) / TKM;
+  const bf16_t* pa[2];
+  const bf16_t* pb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = rbase + 2 * i;
+    const int lc8 = (pc ^ swz(r)) * 8;
+    pa[i] = p.A + (mbeg + r) * p.lda + p0 + min(lc8, capA);
+    pb[i] = p.B + (mbeg + r) * p.ldb + q0 + min(lc8, capB);
+  }
+  const int64_t strideA = (int64_t)TKM * p.lda, strideB = (int64_t)TKM * p.ldb;
   auto issue = [&](int64_t st) {
     const int64_t mt = mbeg + st * TKM;
     const uint32_t sA = lds0 + (uint32_t)((st % NS) * STAGE_T * 16);
     const uint32_t sB = sA + IMG_U4 * 16;
+    if (st < nfull) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t off = (uint32_t)((4 * wu + 2 * i) * 32 * 16);
+        glds16(pa[i] + st * strideA, __builtin_amdgcn_readfirstlane(sA + off));
+        glds16(pb[i] + st * strideB, __builtin_amdgcn_readfirstlane(sB + off));
+      }
+      return;
+    }
+    // ragged last stage or gathered rows: rows past the split's end read zeros
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r = rbase + 2 * i;
