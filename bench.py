@@ -202,6 +202,9 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph (N=1)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="single GPU: run only rank 0's shard of an R-rank job (no collective) and report "
+                         "its per-step time, to see the per-rank fixed costs of strong scaling")
     opt = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,8 +247,9 @@ def main():
     node_perm = torch.randperm(N, generator=g, device=dev).to(torch.int32)
     n_full = min(E_train // P_full, N // B_full)
     # this rank's shard of every global batch
-    b0, b1 = rank * B_full // world, (rank + 1) * B_full // world
-    p0, p1 = rank * P_full // world, (rank + 1) * P_full // world
+    shards = opt.emulate_ranks if (opt.emulate_ranks and world == 1) else world
+    b0, b1 = rank * B_full // shards, (rank + 1) * B_full // shards
+    p0, p1 = rank * P_full // shards, (rank + 1) * P_full // shards
 
     kern_ev = []
 
@@ -297,6 +301,11 @@ def main():
     if opt.profile_kernels:
         if world > 1:
             dist.destroy_process_group()
+        return
+    if opt.emulate_ranks and world == 1:
+        print(json.dumps({"emulated_ranks": shards, "rank0_ms_per_step": dt / opt.steps * 1e3,
+                          "anchors": b1 - b0, "edges": p1 - p0,
+                          "student_rows": eng.last_student_rows}), flush=True)
         return
     loss = eng.end_epoch(opt.steps * P_full)
 

@@ -225,11 +225,20 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, con
   }
 }
 
+constexpr int HB_ROWS = 512;        // rows per block at large R (see colsum_rows)
+
+// rows per colsum block: HB_ROWS at large R, fewer (>= 64) so that a small R
+// still spreads over >= ~1024 blocks (every CU busy)
+__host__ __device__ inline int64_t colsum_rows(int64_t R) {
+  int64_t hb = (R + 1023) / 1024;
+  hb = hb < 64 ? 64 : (hb > HB_ROWS ? HB_ROWS : hb);
+  return hb;
+}
+
 // Column sums (weighted: sum_r weight[r] * Z[r, n]) with the head backward's dZ
 // write fused in.  Vector form: a row is cpr 16-byte chunks; 256 threads
 // cover rpp = 256 / cpr rows per pass and a block walks HB_ROWS rows; the rpp
 // partial rows are combined in LDS and one slab row [blk][H] is written.
-constexpr int HB_ROWS = 512;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
                                                          const float* __restrict__ weight,
@@ -244,8 +253,9 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
   const int t = threadIdx.x;
   const int c = t % cpr, rl = t / cpr;
   const bool active = rl < rpp;
-  const int64_t r0 = (int64_t)blockIdx.x * HB_ROWS;
-  const int64_t r1 = min(R, r0 + HB_ROWS);
+  const int64_t hb = colsum_rows(R);
+  const int64_t r0 = (int64_t)blockIdx.x * hb;
+  const int64_t r1 = min(R, r0 + hb);
   float acc[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) acc[i] = 0.f;
@@ -322,8 +332,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const
                                                      const float* __restrict__ weight, const float* __restrict__ w,
                                                      int relu_mask, float alpha, T* __restrict__ dZ, int64_t lddz,
                                                      float* __restrict__ slab, float* __restrict__ slab_b) {
-  const int64_t r0 = (int64_t)blockIdx.x * HB_ROWS;
-  const int64_t r1 = min(R, r0 + HB_ROWS);
+  const int64_t hb = colsum_rows(R);
+  const int64_t r0 = (int64_t)blockIdx.x * hb;
+  const int64_t r1 = min(R, r0 + hb);
   for (int64_t n = threadIdx.x; n < H; n += blockDim.x) {
     const float wn = w ? w[n] : 1.f;
     float acc = 0.f;
@@ -422,7 +433,7 @@ extern "C" int llp_head_fwd(int dtype, int64_t R, int64_t H, const void* Z, int6
   return LLP_OK;
 }
 
-static int64_t colsum_slabs(int64_t R) { return (R + HB_ROWS - 1) / HB_ROWS; }
+static int64_t colsum_slabs(int64_t R) { return (R + colsum_rows(R) - 1) / colsum_rows(R); }
 
 extern "C" int64_t llp_head_bwd_workspace_bytes(int64_t R, int64_t H) {
   return colsum_slabs(R) * (H + 1) * (int64_t)sizeof(float);

@@ -397,7 +397,7 @@ class DistillEngine(EngineBase):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
         # run the dropout-free student on unique nodes (step_minibatch); off inside
         # hipGraph capture, which cannot take the host read of the unique count
-        self.dedup = bool(dedup)
+        self.dedup = bool(dedup) and os.environ.get("LLP_DEDUP", "1") != "0"
         self._capturing = False
         self.last_student_rows = 0
         self.args = args
