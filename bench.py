@@ -187,6 +187,33 @@ def sage_aggregate(data, dev):
             "note": "x (121 MB) stays resident in the 256 MiB Infinity Cache across the ~10 neighbour re-reads"}
 
 
+def sage_teacher_step(data, dev, dtype, steps=5):
+    """One teacher train() batch (src/train_teacher_gnn.py:33-71, §8 a11-a13) at
+    the collab shape: 3-layer SAGE 128 -> 256 over the full graph, predictor
+    256/2, 65,536 positives + randint negatives, bf16 TeacherEngine."""
+    import llp_sage
+    import llp_teacher
+    import models
+    torch.manual_seed(0)
+    model = models.SAGE("collab", data.F, 256, 256, 3, 0.0, llp_sage.SAGEConv).to(dev)
+    pred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
+    optim = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=0.005)
+    eng = llp_teacher.TeacherEngine(model, pred, data.x.to(dev), data.edge_index, data.N, optim, dtype=dtype)
+    pairs = data.train_pairs.to(torch.int32).to(dev).contiguous()
+    P = 64 * 1024
+    perm = torch.randperm(pairs.shape[0], device=dev).to(torch.int32)
+    for i in range(2):
+        eng.step(perm[i * P:(i + 1) * P], pairs, dense_negatives=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        eng.step(perm[i * P:(i + 1) * P], pairs, dense_negatives=False)
+    torch.cuda.synchronize()
+    dt_s = (time.perf_counter() - t0) / steps
+    return {"ms_per_step": dt_s * 1e3, "edges_per_s": P / dt_s, "dtype": dtype,
+            "config": "SAGE 3x(128->256) over N=235,868 / E=2,358,104, LinkPredictor 256x2, 65,536 positives"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -355,6 +382,7 @@ def main():
             res.update(evaluate(model, pred, data, dev))
         if not opt.no_sage:
             res["sage_aggregate"] = sage_aggregate(data, dev)
+            res["sage_teacher_step"] = sage_teacher_step(data, dev, opt.dtype)
         if world == 1 and not opt.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, a, t_h, init, B_full, P_full, sample_P=opt.cpu_sample_edges)
         print(json.dumps(res), flush=True)
