@@ -226,7 +226,8 @@ def main():
     ap.add_argument("--profile-kernels", action="store_true", help="exit right after the timed region")
     ap.add_argument("--dominant-only", type=int, default=0,
                     help="run only the dominant kernel this many times (rocprofv3 --pmc passes) and exit")
-    ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph (N=1)")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay the step from a captured hipGraph (N=1; --no-graph: eager launches)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
     ap.add_argument("--emulate-ranks", type=int, default=0,

@@ -51,6 +51,12 @@ typedef struct llp_operand {
   const int32_t* idx2;
   int64_t ld;
   int64_t ld2;
+  /* Optional device-resident row count (int32, may be NULL).  When set, the
+   * GEMM runs on min(M, *rows_dev) rows (llp_gemm_nt: of A and C; llp_gemm_tn:
+   * the contraction rows of A and B) while its grid stays sized by the host M,
+   * so a data-dependent row count (the unique-node student, *n_unique of
+   * llp_dedup_rows) needs no host read and the launch is hipGraph-capturable. */
+  const int32_t* rows_dev;
 } llp_operand;
 
 int llp_version(void);
@@ -190,13 +196,16 @@ int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t
  * target[0..R) (U -> *n_unique, device), pos[r] = slot of target[r]; seg_rows =
  * rows grouped by slot in row order (stable sort), seg_ptr[0..U] = group bounds.
  * llp_segment_sum_rows: out[u] = sum of src rows of group u (f32 accumulate,
- * fixed order: deterministic).  llp_gather_i32: out[i] = src[idx[i]]. */
+ * fixed order: deterministic); u_dev (may be NULL): device count, the call
+ * covers min(U, *u_dev) groups (grid sized by U: capturable).
+ * llp_gather_i32: out[i] = src[idx[i]]. */
 int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R);
 int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
                    int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
                    int64_t workspace_bytes, void* stream);
 int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
-                         const void* src, int64_t ld_src, void* out, int64_t ld_out, void* stream);
+                         const void* src, int64_t ld_src, void* out, int64_t ld_out,
+                         const int32_t* u_dev, void* stream);
 int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
 /* Backward of the predictor input h[i] * h[j] (src/main.py:102-103,126) reduced
  * straight onto the unique nodes: dh[u] = sum over the target rows of node u
@@ -206,7 +215,8 @@ int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* o
  * rows to it; drow (dZ = NULL) is the 'inner' predictor's per-pair scalar. */
 int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
                               const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos, const void* dZ,
-                              const float* drow, const void* h, void* dh, int64_t ld_dh, void* stream);
+                              const float* drow, const void* h, void* dh, int64_t ld_dh, const int32_t* u_dev,
+                              void* stream);
 
 /* Generic scatter form (full-batch train(), src/main.py:173-214, where rows of
  * h repeat): dh[ia[r]] += dZ[r]*h2[ib[r]],  dh[ib[r]] += dZ[r]*h1[ia[r]]

@@ -82,12 +82,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, const int32_t* __restrict__ seg_ptr,
                                                           const int32_t* __restrict__ rows,
                                                           const T* __restrict__ src, int64_t lds_,
-                                                          T* __restrict__ out, int64_t ldo) {
+                                                          T* __restrict__ out, int64_t ldo,
+                                                          const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
   const int cpr = (int)(H / E);
   const int spb = 256 / cpr;
   const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
   const int64_t u = (int64_t)blockIdx.x * spb + slot;
+  if (u_dev && (int64_t)*u_dev < U) U = *u_dev;
   if (slot >= spb || u >= U) return;
   float acc[E];
 #pragma unroll
@@ -135,12 +137,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
     int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ rows, const int32_t* __restrict__ pos, const T* __restrict__ dZ,
-    const float* __restrict__ drow, const T* __restrict__ h, T* __restrict__ dh, int64_t ldo) {
+    const float* __restrict__ drow, const T* __restrict__ h, T* __restrict__ dh, int64_t ldo,
+    const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
   const int cpr = (int)(H / E);
   const int spb = 256 / cpr;
   const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
   const int64_t u = (int64_t)blockIdx.x * spb + slot;
+  if (u_dev && (int64_t)*u_dev < U) U = *u_dev;
   if (slot >= spb || u >= U) return;
   const int64_t C1 = C + 1, base = B * C1, col = (int64_t)c * E;
   float acc[E];
@@ -253,7 +257,8 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
 }
 
 extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
-                                    const void* src, int64_t ld_src, void* out, int64_t ld_out, void* stream) {
+                                    const void* src, int64_t ld_src, void* out, int64_t ld_out,
+                                    const int32_t* u_dev, void* stream) {
   LLP_CHECK_ARG(seg_ptr && rows && src && out, "llp_segment_sum_rows: null");
   const int E = dtype == LLP_BF16 ? 8 : 4;
   const int es = dtype == LLP_BF16 ? 2 : 4;
@@ -265,10 +270,10 @@ extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32
   hipStream_t s = (hipStream_t)stream;
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(segment_sum_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
-                       (const bf16_t*)src, ld_src, (bf16_t*)out, ld_out);
+                       (const bf16_t*)src, ld_src, (bf16_t*)out, ld_out, u_dev);
   else
     hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
-                       (const float*)src, ld_src, (float*)out, ld_out);
+                       (const float*)src, ld_src, (float*)out, ld_out, u_dev);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
@@ -285,7 +290,7 @@ extern "C" int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src,
 extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
                                          const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos,
                                          const void* dZ, const float* drow, const void* h, void* dh, int64_t ld_dh,
-                                         void* stream) {
+                                         const int32_t* u_dev, void* stream) {
   LLP_CHECK_ARG(seg_ptr && rows && pos && h && dh && (dZ || drow), "llp_hadamard_bwd_segments: null");
   const int E = dtype == LLP_BF16 ? 8 : 4;
   const int es = dtype == LLP_BF16 ? 2 : 4;
@@ -297,10 +302,10 @@ extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_
   hipStream_t s = (hipStream_t)stream;
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(hadamard_bwd_segments_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
-                       H, seg_ptr, rows, pos, (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh, ld_dh);
+                       H, seg_ptr, rows, pos, (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh, ld_dh, u_dev);
   else
     hipLaunchKernelGGL(hadamard_bwd_segments_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
-                       H, seg_ptr, rows, pos, (const float*)dZ, drow, (const float*)h, (float*)dh, ld_dh);
+                       H, seg_ptr, rows, pos, (const float*)dZ, drow, (const float*)h, (float*)dh, ld_dh, u_dev);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -59,6 +59,7 @@ struct NTParams {
   uint64_t drop_seed;
   const int64_t* drop_ctr;
   int64_t drop_stream;
+  const int32_t* m_dev;  // device row count (llp_operand.rows_dev) or NULL
 };
 
 struct TNParams {
@@ -67,7 +68,15 @@ struct TNParams {
   int64_t mchunk;
   int64_t splits;
   float* ws;  // [splits][P][Q]
+  const int32_t* m_dev;  // device row count: M and mchunk are re-derived from it
 };
+
+// min(M, *m_dev) (M when m_dev is NULL)
+__device__ __forceinline__ int64_t rows_live(int64_t M, const int32_t* m_dev) {
+  if (!m_dev) return M;
+  const int64_t c = *m_dev;
+  return c < M ? (c > 0 ? c : 0) : M;
+}
 
 template <typename T>
 struct Traits;
@@ -167,8 +176,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  p.M = rows_live(p.M, p.m_dev);
   const int64_t tilesN = (p.N + BN - 1) / BN;
   const int64_t tilesM = (p.M + BM - 1) / BM;
+  if ((int64_t)blockIdx.x >= tilesM * tilesN) return;
   const int64_t lt = xcd_remap(blockIdx.x, tilesM * tilesN);
   const int64_t tm = lt / tilesN, tn = lt % tilesN;
   const int64_t m0 = tm * BM, n0 = tn * BN;
@@ -340,6 +351,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
   const int64_t tile = lt / splits, z = lt % splits;
   const int64_t tp = tile / tilesQ, tq = tile % tilesQ;
   const int64_t p0 = tp * BM, q0 = tq * BN;
+  if (p.m_dev) {   // live rows from the device count; the grid (splits) is the host M's
+    p.M = rows_live(p.M, p.m_dev);
+    const int64_t mc = (p.M + splits - 1) / splits;
+    p.mchunk = mc > 0 ? (mc + BKM - 1) / BKM * BKM : BKM;
+  }
   const int64_t mbeg = z * p.mchunk;
   const int64_t mend = min(p.M, mbeg + p.mchunk);
 
@@ -525,6 +541,7 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   p.A = to_op(A);
   p.B = to_op(B);
   p.M = M; p.N = N; p.K = K;
+  p.m_dev = A->rows_dev;
   p.C = C; p.ldc = ldc; p.c_bf16 = c_dtype == LLP_BF16;
   p.bias = bias; p.act = act; p.aux = aux; p.ld_aux = ld_aux; p.aux_bf16 = aux_dtype == LLP_BF16;
   p.alpha = alpha;
@@ -634,12 +651,21 @@ extern "C" int llp_head_finish(int64_t parts, int64_t M, const float* part, cons
 extern "C" int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N);
 extern "C" int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
                           void* workspace, int64_t workspace_bytes, void* stream);
+namespace llp {
+int colsum_rows_dev(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
+                    void* workspace, int64_t workspace_bytes, const int32_t* m_dev, void* stream);
+}
 
 // workspace = [weight slabs: splits*P*Q f32][column-sum region]
 static int64_t tn_colsum_region(int dtype, int64_t M, int64_t P) {
   int64_t r = llp_colsum_workspace_bytes(M, P);
   if (dtype == LLP_BF16) r = std::max(r, llp_gemm_tn_256_splits(M, P, 256) * P * (int64_t)sizeof(float));
   return r;
+}
+
+// the contraction rows' device count: A's, else B's
+static const int32_t* tn_rows_dev(const llp_operand* A, const llp_operand* B) {
+  return A->rows_dev ? A->rows_dev : B->rows_dev;
 }
 
 extern "C" int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q) {
@@ -684,14 +710,15 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
   const int64_t splits = tn_splits(dtype, M, P, Q);
   if (colsum_a) {
     char* region = reinterpret_cast<char*>(workspace) + splits * P * Q * (int64_t)sizeof(float);
-    const int rc = llp_colsum(dtype, M, P, A->ptr, A->ld, colsum_a, accumulate, region,
-                              tn_colsum_region(dtype, M, P), stream);
+    const int rc = llp::colsum_rows_dev(dtype, M, P, A->ptr, A->ld, colsum_a, accumulate, region,
+                                        tn_colsum_region(dtype, M, P), tn_rows_dev(A, B), stream);
     if (rc != 0) return rc;
   }
   TNParams p;
   p.A = to_op(A);
   p.B = to_op(B);
   p.M = M; p.P = P; p.Q = Q;
+  p.m_dev = tn_rows_dev(A, B);
   const int64_t bkm = dtype == LLP_BF16 ? 64 : 32;
   int64_t mchunk = (M + splits - 1) / splits;
   mchunk = (mchunk + bkm - 1) / bkm * bkm;

@@ -47,6 +47,10 @@ struct P256 {
   uint8_t* mask_out;
   const uint8_t* mask_in;
   int64_t ld_mask;
+  // device row count (llp_operand.rows_dev): M = min(M, *m_dev) at run time;
+  // the grid and head_part's row stride (head_ld) stay the host M
+  const int32_t* m_dev;
+  int64_t head_ld;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -56,6 +60,42 @@ __device__ __forceinline__ int64_t xcd_remap2(int64_t bid, int64_t nwg) {
   const int64_t q = nwg / 8, r = nwg % 8;
   const int64_t xcd = bid % 8, loc = bid / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// This block's output tile.  Applies the device row count first (p.M shrinks to
+// min(M, *m_dev)); the grid is sized for the host M, and blocks past the live
+// tiles return before touching memory.  The live tiles are remapped as a
+// contiguous range per XCD, as without a count.
+__device__ __forceinline__ bool tile_256(P256& p, int64_t& m0, int64_t& n0) {
+  if (p.m_dev) {
+    const int64_t c = *p.m_dev;
+    p.M = c < p.M ? (c > 0 ? c : 0) : p.M;
+  }
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TM - 1) / TM;
+  const int64_t nt = tilesM * tilesN;
+  if ((int64_t)blockIdx.x >= nt) return false;
+  const int64_t lt = xcd_remap2(blockIdx.x, nt);
+  m0 = (lt / tilesN) * TM;
+  n0 = (lt % tilesN) * TN;
+  return true;
+}
+
+// Tile of this block on the HOST grid when the row count is device-resident
+// (q64 kernel): m-tiles are dealt to XCDs round-robin (XCD x = blockIdx % 8
+// takes m-tiles x, x+8, ..., each with its tilesN n-tiles in consecutive
+// blocks), so the tiles past the live row count, which are the highest
+// m-tiles, are spread over all eight XCDs instead of idling the last one.
+// Needs no device value: the prologue is issued before the count is waited on.
+// The grid is ceil(tilesM / 8) * 8 * tilesN blocks (llp_gemm_nt_bf16_256).
+__device__ __forceinline__ bool tile_256_host_interleaved(const P256& p, int64_t& m0, int64_t& n0) {
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TM - 1) / TM;
+  const int64_t xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+  const int64_t mt = (loc / tilesN) * 8 + xcd;
+  m0 = mt * TM;
+  n0 = (loc % tilesN) * TN;
+  return mt < tilesM;
 }
 
 __device__ __forceinline__ uint32_t mulbf2(uint32_t a, uint32_t b) {
@@ -69,10 +109,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[SMEM_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int64_t tilesN = (p.N + TN - 1) / TN;
-  const int64_t tilesM = (p.M + TM - 1) / TM;
-  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
-  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+  int64_t m0, n0;
+  if (!tile_256(p, m0, n0)) return;
 
   // ---------------- staging addresses
   // glds: wave w stages rows [32w, 32w+32) of A and of B: 4 instructions each,
@@ -352,7 +390,7 @@ __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8
   if (p.head_w && tid < TM && m0 + tid < p.M) {
     const float* part = reinterpret_cast<const float*>(smem + head_off_u4);
     const float s = part[tid] + part[256 + tid] + part[512 + tid] + part[768 + tid];
-    p.head_part[(n0 / TN) * p.M + m0 + tid] = s;
+    p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = s;
   }
   if (!p.C) return;
   const int chunks_per_row = TN / 8;
@@ -420,10 +458,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp(P256 p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int64_t tilesN = (p.N + TN - 1) / TN;
-  const int64_t tilesM = (p.M + TM - 1) / TM;
-  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
-  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+  int64_t m0, n0;
+  if (!tile_256(p, m0, n0)) return;
 
   const bf16_t* ga[2];
   const bf16_t* gb[2];
@@ -552,10 +588,12 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int64_t tilesN = (p.N + TN - 1) / TN;
-  const int64_t tilesM = (p.M + TM - 1) / TM;
-  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
-  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+  int64_t m0, n0;
+  // device row count: load it now, wait for it only after the K-tile-0 DMA is
+  // issued (rows up to the host M are addressable: stale, never stored)
+  const bool dyn = p.m_dev != nullptr;
+  const int32_t mlive = dyn ? *p.m_dev : 0;
+  if (dyn ? !tile_256_host_interleaved(p, m0, n0) : !tile_256(p, m0, n0)) return;
 
   // per (chunk, piece): this lane's source pointer (k-tile 0) and the piece's
   // wave-uniform LDS row offset
@@ -651,6 +689,13 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
   // prologue: the whole of K-tile 0
 #pragma unroll
   for (int j = 0; j < 4; ++j) issue_chunk(j, 0);
+  if (dyn) {
+    p.M = mlive < p.M ? (mlive > 0 ? mlive : 0) : p.M;
+    if (m0 >= p.M) {   // a tile past the live rows: drain its DMA and leave
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
   for (int64_t kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
@@ -703,10 +748,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4 + 256];   // + 4 KiB head partials
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int64_t tilesN = (p.N + TN - 1) / TN;
-  const int64_t tilesM = (p.M + TM - 1) / TM;
-  const int64_t lt = xcd_remap2(blockIdx.x, tilesM * tilesN);
-  const int64_t m0 = (lt / tilesN) * TM, n0 = (lt % tilesN) * TN;
+  int64_t m0, n0;
+  if (!tile_256(p, m0, n0)) return;
 
   // glds: wave w stages rows [32w, 32w+32): 2 instructions per operand, each 16
   // rows x 64 B; lane -> row 32w + 16i + (lane>>2), physical chunk lane & 3.
@@ -840,7 +883,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   if (p.head_w && tid < TM && m0 + tid < p.M) {
     const float* part = reinterpret_cast<const float*>(smem + SM_U4);
     const float s = part[tid] + part[256 + tid] + part[512 + tid] + part[768 + tid];
-    p.head_part[(n0 / TN) * p.M + m0 + tid] = s;
+    p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = s;
   }
   if (!p.C) return;
   const int chunks_per_row = TN / 8;
@@ -925,11 +968,16 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.lda = A->ld; p.lda2 = A->ptr2 ? A->ld2 : 0;
   p.B = (const bf16_t*)B->ptr; p.ib = B->idx; p.ldb = B->ld;
   p.M = M; p.N = N; p.K = K;
+  p.m_dev = A->rows_dev;
+  p.head_ld = M;
   p.C = (bf16_t*)C; p.ldc = ldc;
   p.bias = bias; p.act = act; p.aux = (const bf16_t*)aux; p.ld_aux = ld_aux; p.alpha = alpha;
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
   p.drop_ctr = drop_ctr; p.drop_stream = drop_stream;
-  const int64_t tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  // with a device row count the q64 kernel maps the host grid interleaved over
+  // the XCDs (tile_256_host_interleaved): m-tiles padded to a multiple of 8;
+  // the other variants map the live tiles and let the surplus blocks exit
+  const int64_t tiles = (A->rows_dev ? ((M + 8 * TM - 1) / (8 * TM)) * 8 : (M + TM - 1) / TM) * ((N + TN - 1) / TN);
   static const int pipe_env = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
   const int pipe = ((head_w || !C) && (pipe_env < 3 || pipe_env > 5)) ? 4 : pipe_env;
   const int variant = llp_gemm_variant();

@@ -33,6 +33,7 @@ struct PTN {
   int64_t M, P, Q, mchunk, splits;
   float* ws;
   float* ws_colsum;   // [splits][P] column sums of A (bias gradient), or NULL
+  const int32_t* m_dev;   // device row count (llp_operand.rows_dev) or NULL
 };
 
 typedef __attribute__((address_space(3))) short4_t lds_s4;
@@ -71,6 +72,12 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
   const int64_t lt = xcd_remap3(blockIdx.x, tilesP * tilesQ * p.splits);
   const int64_t tile = lt / p.splits, z = lt % p.splits;
   const int64_t p0 = (tile / tilesQ) * TP, q0 = (tile % tilesQ) * TQ;
+  if (p.m_dev) {   // live rows from the device count; the grid (splits) is the host M's
+    const int64_t c = *p.m_dev;
+    p.M = c < p.M ? (c > 0 ? c : 0) : p.M;
+    const int64_t mc = (p.M + p.splits - 1) / p.splits;
+    p.mchunk = mc > 0 ? (mc + TKM - 1) / TKM * TKM : TKM;
+  }
   const int64_t mbeg = z * p.mchunk;
   const int64_t mend = min(p.M, mbeg + p.mchunk);
 
@@ -240,6 +247,7 @@ int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.A = (const bf16_t*)A->ptr; p.ia = A->idx; p.lda = A->ld;
   p.B = (const bf16_t*)B->ptr; p.ib = B->idx; p.ldb = B->ld;
   p.M = M; p.P = P; p.Q = Q;
+  p.m_dev = A->rows_dev ? A->rows_dev : B->rows_dev;
   int64_t mchunk = (M + splits - 1) / splits;
   mchunk = (mchunk + TKM - 1) / TKM * TKM;
   p.mchunk = mchunk > 0 ? mchunk : TKM;

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
                                                          const float* __restrict__ weight,
                                                          const float* __restrict__ w, int relu_mask, float alpha,
                                                          T* __restrict__ dZ, int64_t lddz, float* __restrict__ slab,
-                                                         float* __restrict__ slab_b) {
+                                                         float* __restrict__ slab_b, const int32_t* __restrict__ r_dev) {
   constexpr int CH = 16 / sizeof(T);
   __shared__ float part[256 * CH];
   __shared__ float partb[256];
@@ -253,9 +253,9 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
   const int t = threadIdx.x;
   const int c = t % cpr, rl = t / cpr;
   const bool active = rl < rpp;
-  const int64_t hb = colsum_rows(R);
+  const int64_t hb = colsum_rows(R);   // the grid's split (host R); rows past *r_dev are not live
   const int64_t r0 = (int64_t)blockIdx.x * hb;
-  const int64_t r1 = min(R, r0 + hb);
+  const int64_t r1 = min(r_dev ? min(R, (int64_t)*r_dev) : R, r0 + hb);
   float acc[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) acc[i] = 0.f;
@@ -331,10 +331,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
                                                      const float* __restrict__ weight, const float* __restrict__ w,
                                                      int relu_mask, float alpha, T* __restrict__ dZ, int64_t lddz,
-                                                     float* __restrict__ slab, float* __restrict__ slab_b) {
-  const int64_t hb = colsum_rows(R);
+                                                     float* __restrict__ slab, float* __restrict__ slab_b,
+                                                     const int32_t* __restrict__ r_dev) {
+  const int64_t hb = colsum_rows(R);   // the grid's split (host R); rows past *r_dev are not live
   const int64_t r0 = (int64_t)blockIdx.x * hb;
-  const int64_t r1 = min(R, r0 + hb);
+  const int64_t r1 = min(r_dev ? min(R, (int64_t)*r_dev) : R, r0 + hb);
   for (int64_t n = threadIdx.x; n < H; n += blockDim.x) {
     const float wn = w ? w[n] : 1.f;
     float acc = 0.f;
@@ -443,7 +444,7 @@ extern "C" int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N) { return llp
 static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t ldz, const float* weight,
                          const float* w, int relu_mask, float alpha, void* dZ, int64_t lddz, float* dw, float* db,
                          int accumulate,
-                         void* workspace, int64_t workspace_bytes, hipStream_t s) {
+                         void* workspace, int64_t workspace_bytes, hipStream_t s, const int32_t* r_dev = nullptr) {
   LLP_CHECK_ARG(workspace_bytes >= llp_head_bwd_workspace_bytes(R, H), "colsum: workspace too small");
   const int64_t ns = colsum_slabs(R);
   float* slab = reinterpret_cast<float*>(workspace);
@@ -456,17 +457,17 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
     if (dtype == LLP_BF16) {
       if (vec)
         hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z,
-                           ldz, weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr);
+                           ldz, weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
       else
         hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz,
-                           weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr);
+                           weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
     } else {
       if (vec)
         hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
-                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr);
+                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
       else
         hipLaunchKernelGGL(colsum_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
-                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr);
+                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
     }
     LLP_LAUNCH_CHECK();
   }
@@ -496,3 +497,14 @@ extern "C" int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_
   return colsum_launch(dtype, M, N, Y, ldy, nullptr, nullptr, 0, 1.f, nullptr, 0, out, nullptr, accumulate, workspace,
                        workspace_bytes, (hipStream_t)stream);
 }
+
+// llp_colsum over min(M, *m_dev) live rows (grid sized by M): the bias
+// gradient of a GEMM whose row count is device-resident (gemm.hip).
+namespace llp {
+int colsum_rows_dev(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
+                    void* workspace, int64_t workspace_bytes, const int32_t* m_dev, void* stream) {
+  LLP_CHECK_ARG(Y && out, "llp_colsum: null input");
+  return colsum_launch(dtype, M, N, Y, ldy, nullptr, nullptr, 0, 1.f, nullptr, 0, out, nullptr, accumulate, workspace,
+                       workspace_bytes, (hipStream_t)stream, m_dev);
+}
+}  // namespace llp

@@ -33,6 +33,9 @@ import llp_hip as K
 # gradient twice (once per endpoint) and measured 14.99 vs 14.83 ms/step on the collab bench against
 # the default two-kernel path (row gradients in pair-block order + segment sum), so it is opt-in.
 _SEGMENT_FUSED = os.environ.get("LLP_SEGMENT_FUSED", "0") == "1"
+# unique-node path: the unique count stays on the device (GEMM grids sized by the bound min(R1, N));
+# LLP_DEVICE_COUNT=0 reads it on the host instead (a sync per step, not capturable; A/B knob)
+_DEVICE_COUNT = os.environ.get("LLP_DEVICE_COUNT", "1") != "0"
 
 _DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
 
@@ -395,11 +398,11 @@ class DistillEngine(EngineBase):
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
                  dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
-        # run the dropout-free student on unique nodes (step_minibatch); off inside
-        # hipGraph capture, which cannot take the host read of the unique count
+        # run the dropout-free student on unique nodes (step_minibatch); the unique
+        # count stays on the device, so this path is hipGraph-capturable too
         self.dedup = bool(dedup) and os.environ.get("LLP_DEDUP", "1") != "0"
-        self._capturing = False
-        self.last_student_rows = 0
+        self._rows_dev = None      # int32 device count of the unique-node student (last step), or None
+        self._rows_host = 0
         self.args = args
         self.N = int(num_nodes)
 
@@ -436,6 +439,14 @@ class DistillEngine(EngineBase):
         self._build_descs()
 
     # ------------------------------------------------------------------ helpers
+    @property
+    def last_student_rows(self):
+        """Student rows of the last minibatch step: the unique-node count (a
+        device read, so it synchronises) or the row-wise R1."""
+        if self._rows_dev is not None:
+            return int(self._rows_dev.item())
+        return self._rows_host
+
     def _rows_index(self, B, C, P2):
         """Predictor-row -> h-row index for the minibatch layout (static per shape)."""
         key = ("rows", B, C, P2)
@@ -501,9 +512,13 @@ class DistillEngine(EngineBase):
         # ---- unique-node compaction: without dropout the student is a row-wise
         # function, so duplicate rows of x[this_target] give identical activations;
         # run it on the U distinct nodes and sum each node's row gradients.
-        dedup = self.dedup and p_drop == 0.0 and not self._capturing
+        dedup = self.dedup and p_drop == 0.0
+        n_u = None
         if dedup:
+            fresh = "uniq" not in self._bufs or self._bufs["uniq"].numel() < R1
             uniq = self._buf("uniq", (R1,), torch.int32)
+            if fresh:   # slots past the live count are read (never used) by the q64 GEMM prologue: keep them ids
+                uniq.zero_()
             pos = self._buf("pos", (R1,), torch.int32)
             n_u = self._buf("n_unique", (1,), torch.int32)
             seg_ptr = self._buf("seg_ptr", (R1 + 1,), torch.int32)
@@ -514,15 +529,23 @@ class DistillEngine(EngineBase):
             ib_h = self._buf("ib_u", (R2,), torch.int32)
             K.gather_i32(ia, pos, ia_h)
             K.gather_i32(ib, pos, ib_h)
-            U = int(n_u.item())                 # one host read: the student GEMMs are sized by it
-            rows_s, gather_s = U, uniq[:U]
+            # No host read of U: the student kernels are launched for the bound
+            # min(R1, N) and run on the *n_unique live rows (llp_operand.rows_dev),
+            # so the step stays asynchronous and hipGraph-capturable.
+            # (LLP_DEVICE_COUNT=0: read U on the host and size the launches by it.)
+            if _DEVICE_COUNT:
+                rows_s, gather_s = min(R1, self.N), uniq
+            else:
+                rows_s = int(n_u.item())
+                gather_s, n_u = uniq[:rows_s], None
         else:
             rows_s, gather_s, ia_h, ib_h = R1, target, ia, ib
-        self.last_student_rows = rows_s
+        self._rows_dev = n_u
+        self._rows_host = rows_s
 
         # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
         acts = []
-        A = K.operand(self.x, gather_s)
+        A = K.operand(self.x, gather_s, count=n_u)
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (rows_s, lin.out_f), dt)
@@ -539,7 +562,7 @@ class DistillEngine(EngineBase):
                 ev[1].record()
                 kernel_events.append(ev)
             acts.append(out)
-            A = K.operand(out)
+            A = K.operand(out, count=n_u)
         h = acts[-1]
 
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
@@ -566,7 +589,7 @@ class DistillEngine(EngineBase):
             # Hadamard backward reduced straight onto the unique nodes (no [R1, H] row gradients)
             dh = self._buf("gS0", (rows_s, H), dt)
             K.hadamard_bwd_segments(rows_s, B, C, n_lab, H, seg_ptr, seg_rows, pos, dZ0 if mlp else None, h, dh,
-                                    drow=None if mlp else dlogit)
+                                    drow=None if mlp else dlogit, count=n_u)
         else:
             dh_rows = self._buf("dh_rows" if dedup else "gS0", (R1, H), dt)
             hidx = pos if dedup else None
@@ -576,10 +599,10 @@ class DistillEngine(EngineBase):
                 K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh_rows, drow=dlogit, hidx=hidx)
             if dedup:
                 dh = self._buf("gS0", (rows_s, H), dt)
-                K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh)
+                K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh, count=n_u)
             else:
                 dh = dh_rows
-        self._student_backward(dh, rows_s, gather_s, acts, p_drop)
+        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
@@ -646,7 +669,7 @@ class DistillEngine(EngineBase):
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             acts.append(out)
-            A = K.operand(out)
+            A = K.operand(out, count=n_u)
         h = acts[-1]
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
@@ -709,12 +732,8 @@ class DistillEngine(EngineBase):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        self._capturing = True
-        try:
-            with torch.cuda.graph(g, stream=s):
-                self.step_minibatch(anchors, link_ids, pairs, **kw)
-        finally:
-            self._capturing = False
+        with torch.cuda.graph(g, stream=s):
+            self.step_minibatch(anchors, link_ids, pairs, **kw)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g
 
@@ -747,19 +766,20 @@ class DistillEngine(EngineBase):
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _student_backward(self, dh, R1, target, acts, p_drop):
+    def _student_backward(self, dh, R1, target, acts, p_drop, count=None):
+        """count: int32 device row count (unique-node student) or None."""
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
         cur, nxt = "gS0", "gS1"
         for l in range(len(self.stu) - 1, -1, -1):
             lin = self.stu[l]
             gcur = self._buf(cur, (R1, lin.out_f), dt)
-            A_in = K.operand(acts[l - 1]) if l > 0 else K.operand(self.x, target)
+            A_in = K.operand(acts[l - 1], count=count) if l > 0 else K.operand(self.x, target, count=count)
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.in_f)
-            K.gemm_tn(K.operand(gcur), A_in, R1, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
-                      colsum_a=lin.lin.bias.grad)
+            K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
+                      self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
             if l > 0:
                 gnext = self._buf(nxt, (R1, lin.in_f), dt)
-                K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
+                K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
                           act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)
                 cur, nxt = nxt, cur

@@ -26,7 +26,8 @@ c_u64 = C.c_uint64
 
 
 class Operand(C.Structure):
-    _fields_ = [("ptr", c_vp), ("idx", c_vp), ("ptr2", c_vp), ("idx2", c_vp), ("ld", c_i64), ("ld2", c_i64)]
+    _fields_ = [("ptr", c_vp), ("idx", c_vp), ("ptr2", c_vp), ("idx2", c_vp), ("ld", c_i64), ("ld2", c_i64),
+                ("rows_dev", c_vp)]
 
 
 class Dropout(C.Structure):
@@ -65,9 +66,9 @@ _SIGS = {
     "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_dedup_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "llp_hadamard_bwd_segments": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                          c_vp, c_i64, c_vp]),
+                                          c_vp, c_i64, c_vp, c_vp]),
     "llp_gather_i32": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_hadamard_bwd_scatter": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_context_sampler": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
@@ -155,14 +156,19 @@ def dtype_code(t: torch.dtype) -> int:
     raise TypeError(f"unsupported dtype {t}")
 
 
-def operand(t, idx=None, t2=None, idx2=None) -> Operand:
+def operand(t, idx=None, t2=None, idx2=None, count=None) -> Operand:
     """Operand over the row-major 2-D tensor ``t`` (rows optionally gathered by
-    int32 ``idx``), optionally times ``t2[idx2]`` elementwise."""
+    int32 ``idx``), optionally times ``t2[idx2]`` elementwise.  ``count``: an
+    int32 device scalar; the GEMM then runs on min(M, count) rows without a
+    host read (llp_operand.rows_dev)."""
     assert t.dim() == 2 and t.stride(1) == 1
     if idx is not None:
         assert idx.dtype == torch.int32 and idx.is_contiguous()
-    o = Operand(t.data_ptr(), ptr(idx), ptr(t2), ptr(idx2), t.stride(0), t2.stride(0) if t2 is not None else 0)
-    o._keep = (t, idx, t2, idx2)   # the struct holds raw pointers: keep the tensors alive with it
+    if count is not None:
+        assert count.dtype == torch.int32 and count.device == t.device
+    o = Operand(t.data_ptr(), ptr(idx), ptr(t2), ptr(idx2), t.stride(0), t2.stride(0) if t2 is not None else 0,
+                ptr(count))
+    o._keep = (t, idx, t2, idx2, count)   # the struct holds raw pointers: keep the tensors alive with it
     return o
 
 
@@ -266,20 +272,22 @@ def dedup_rows(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, ws)
                            stream_ptr()), "llp_dedup_rows")
 
 
-def segment_sum_rows(U, seg_ptr, rows, src, out):
+def segment_sum_rows(U, seg_ptr, rows, src, out, count=None):
+    """out[u] = sum of src[rows[seg_ptr[u]:seg_ptr[u+1]]] for u < U (u < min(U, count) with an
+    int32 device ``count``)."""
     L = lib()
     check(L.llp_segment_sum_rows(dtype_code(src.dtype), U, src.shape[1], seg_ptr.data_ptr(), rows.data_ptr(),
-                                 src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), stream_ptr()),
-          "llp_segment_sum_rows")
+                                 src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), ptr(count),
+                                 stream_ptr()), "llp_segment_sum_rows")
 
 
-def hadamard_bwd_segments(U, B, C, L2, H, seg_ptr, rows, pos, dZ, h, dh, drow=None):
+def hadamard_bwd_segments(U, B, C, L2, H, seg_ptr, rows, pos, dZ, h, dh, drow=None, count=None):
     """dh[u] (U x H) = per-node sum of the Hadamard-backward rows (llp_hadamard_bwd_segments)."""
     L = lib()
     t = dZ if dZ is not None else h
     check(L.llp_hadamard_bwd_segments(dtype_code(t.dtype), U, B, C, L2, H, seg_ptr.data_ptr(), rows.data_ptr(),
                                       pos.data_ptr(), ptr(dZ), ptr(drow), h.data_ptr(), dh.data_ptr(), dh.stride(0),
-                                      stream_ptr()), "llp_hadamard_bwd_segments")
+                                      ptr(count), stream_ptr()), "llp_hadamard_bwd_segments")
 
 
 def gather_i32(idx, src, out):

@@ -158,3 +158,55 @@ def test_engine_unique_node_student_matches_rowwise(dtype):
     for a, b in zip(res[True][1], res[False][1]):
         tol = 1e-4 if dtype == "fp32" else 3e-2
         assert (a - b).abs().max().item() <= tol * max(b.abs().max().item(), 1e-6), (tuple(a.shape),)
+
+
+def test_engine_unique_node_step_graph_replay_matches_eager():
+    """The unique-node minibatch step (device-resident unique count, no host
+    read) captured once into a hipGraph and replayed on fresh batches gives
+    bit-identical loss terms and parameters to the same steps run eagerly
+    (BASELINE configs[4]: hipGraph-captured distillation step)."""
+    import types
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, F_, H, L = 3000, 128, 256, 3
+    args = types.SimpleNamespace(rw_step=3, hops=3, ns_rate=3, ps_method="nb", dropout=0.0, margin=0.01,
+                                 LLP_D=1.0, LLP_R=1.0, True_label=1.0, predictor="mlp", lr=0.001)
+    g = torch.Generator().manual_seed(0)
+    u = torch.randint(0, N, (20000,), generator=g)
+    v = torch.randint(0, N, (20000,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
+    x = torch.randn(N, F_, generator=g) * 0.3
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    pairs_d = pairs.to(torch.int32).to(DEV)
+    batches = []
+    for i in range(4):
+        a = torch.randperm(N, generator=torch.Generator().manual_seed(10 + i))[:300].to(torch.int32).to(DEV)
+        lk = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(20 + i))[:2048].to(torch.int32)
+        batches.append((a, lk.to(DEV)))
+    res = {}
+    for mode in ("eager", "graph"):
+        eng, model, pred = _make_engine("bf16", N, F_, H, L, 3, args, x, t_h, ei)
+        assert eng.dedup
+        anchors = torch.empty(300, dtype=torch.int32, device=DEV)
+        links = torch.empty(2048, dtype=torch.int32, device=DEV)
+        anchors.copy_(batches[0][0])
+        links.copy_(batches[0][1])
+        eng.step_minibatch(anchors, links, pairs_d)
+        graph = eng.capture_minibatch(anchors, links, pairs_d) if mode == "graph" else None
+        for a, lk in batches[1:]:
+            anchors.copy_(a)
+            links.copy_(lk)
+            if graph is not None:
+                graph.replay()
+            else:
+                eng.step_minibatch(anchors, links, pairs_d)
+        torch.cuda.synchronize()
+        res[mode] = (eng.terms.cpu().clone(), [p.detach().cpu().clone() for p in
+                                               list(model.parameters()) + list(pred.parameters())],
+                     eng.last_student_rows)
+    assert torch.equal(res["graph"][0], res["eager"][0])
+    for a, b in zip(res["graph"][1], res["eager"][1]):
+        assert torch.equal(a, b)
+    assert 0 < res["graph"][2] == res["eager"][2] < 300 * 37 + 4 * 2048

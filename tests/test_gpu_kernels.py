@@ -509,3 +509,56 @@ def test_gemm_relu_bit_mask(M, N, Kd):
     k.gemm_nt(k.operand(gy), k.operand(w), M, N, Kd, d_msk, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=mask, alpha=1.5)
     torch.cuda.synchronize()
     assert torch.equal(d_aux, d_msk)
+
+
+# ------------------------------------------------------------------ device row count (llp_operand.rows_dev)
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("Mmax,Mlive", [(3000, 2311), (1000, 0), (700, 700), (257, 1)])
+def test_gemm_device_row_count(dt, Mmax, Mlive):
+    """A GEMM launched for Mmax rows with rows_dev = Mlive: rows < Mlive are
+    bit-identical to a launch for exactly Mlive rows, rows past it untouched
+    (NT: C rows; TN and its fused bias gradient: only live rows contract).
+    This is the unique-node student's sync-free path (no host read of U)."""
+    k = K()
+    g = torch.Generator().manual_seed(Mmax + Mlive)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    code = k.dtype_code(tdt)
+    N0, Kd, N = 4000, 128, 256
+    X = torch.randn(N0, Kd, generator=g).to(DEV, tdt)
+    idx = torch.randint(0, N0, (Mmax,), generator=g, dtype=torch.int32).to(DEV)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, tdt)
+    b = torch.randn(N, generator=g).to(DEV)
+    cnt = torch.tensor([Mlive], dtype=torch.int32, device=DEV)
+    sentinel = torch.full((Mmax, N), 7.0, device=DEV, dtype=tdt)
+    out = sentinel.clone()
+    k.gemm_nt(k.operand(X, idx, count=cnt), k.operand(W), Mmax, N, Kd, out, code, bias=b, act=k.ACT_RELU)
+    ref = sentinel.clone()
+    if Mlive:
+        k.gemm_nt(k.operand(X, idx[:Mlive]), k.operand(W), Mlive, N, Kd, ref[:Mlive], code, bias=b, act=k.ACT_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # TN with the bias gradient fused: dW = A^T X[idx], db = colsum(A)
+    A = torch.randn(Mmax, N, generator=g).to(DEV, tdt)
+    ws = torch.empty(k.gemm_tn_ws_bytes(code, Mmax, N, Kd) // 4 + 16, device=DEV)
+    dW = torch.empty(N, Kd, device=DEV)
+    db = torch.empty(N, device=DEV)
+    k.gemm_tn(k.operand(A, count=cnt), k.operand(X, idx, count=cnt), Mmax, N, Kd, dW, code, ws, colsum_a=db)
+    torch.cuda.synchronize()
+    Ar, Xr = A[:Mlive].double().cpu(), X[idx[:Mlive].long()].double().cpu()
+    refW = Ar.t() @ Xr
+    refb = Ar.sum(0)
+    tol = 1e-4 if dt == "fp32" else 2e-3
+    assert (dW.cpu().double() - refW).abs().max().item() <= tol * (1 + refW.abs().max().item())
+    assert (db.cpu().double() - refb).abs().max().item() <= tol * (1 + refb.abs().max().item())
+    # segment sum over min(U, count) groups
+    R = 2 * Mmax + 1
+    segp = torch.arange(0, R + 1, 2, dtype=torch.int32, device=DEV)[:Mmax + 1].contiguous()
+    segr = torch.arange(R, dtype=torch.int32, device=DEV)
+    src = torch.randn(R, 64, generator=g).to(DEV, tdt)
+    o = torch.full((Mmax, 64), 7.0, device=DEV, dtype=tdt)
+    k.segment_sum_rows(Mmax, segp, segr, src, o, count=cnt)
+    torch.cuda.synchronize()
+    exp = src.float().cpu()[:2 * Mmax].view(Mmax, 2, 64).sum(1)
+    got = o.float().cpu()
+    assert torch.allclose(got[:Mlive], exp[:Mlive], rtol=1e-2, atol=1e-2)
+    assert bool((got[Mlive:] == 7.0).all())
