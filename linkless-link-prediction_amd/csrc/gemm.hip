@@ -493,6 +493,69 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, int64_t splits,
   }
 }
 
+// Vector form: C[p][q..q+3] (+)= sum_z ws[z][p][q..q+3] for Q % 4 == 0.  A block
+// is 64 float4 columns x 4 slab groups (group g sums z in [g*S/4, (g+1)*S/4)
+// with 8 loads in flight per thread); the group sums are added in group order
+// through LDS: a fixed order, so the result is deterministic.  The scalar
+// kernel above keeps one load in flight per thread and is latency-bound at
+// large S (the teacher's TN splits, S = 128).
+constexpr int SR_G = 4, SR_L = 256 / SR_G;
+__global__ __launch_bounds__(256) void slab_reduce_v4_kernel(const float4* __restrict__ ws, int64_t S, int64_t n4,
+                                                             int64_t Q4, float* __restrict__ C, int64_t ldc,
+                                                             int accumulate) {
+  __shared__ float4 part[SR_G][SR_L];
+  const int lane = threadIdx.x % SR_L, g = threadIdx.x / SR_L;
+  const int64_t e4 = (int64_t)blockIdx.x * SR_L + lane;
+  const int64_t z1 = (g + 1) * S / SR_G;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e4 < n4) {
+    int64_t z = g * S / SR_G;
+    for (; z + 8 <= z1; z += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ws[(z + k) * n4 + e4];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+      }
+    }
+    for (; z < z1; ++z) {
+      const float4 v = ws[z * n4 + e4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  part[g][lane] = acc;
+  __syncthreads();
+  if (g != 0 || e4 >= n4) return;
+  float4 t = part[0][lane];
+#pragma unroll
+  for (int k = 1; k < SR_G; ++k) {
+    const float4 v = part[k][lane];
+    t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+  }
+  float4* dst = reinterpret_cast<float4*>(C + (e4 / Q4) * ldc + (e4 % Q4) * 4);
+  if (accumulate) {
+    const float4 o = *dst;
+    t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
+  }
+  *dst = t;
+}
+
+// C (+)= sum of the S slabs [S][P][Q] (f32), deterministic.
+void slab_reduce(const float* ws, int64_t S, int64_t P, int64_t Q, float* C, int64_t ldc, int accumulate,
+                 hipStream_t s) {
+  const int64_t n = P * Q;
+  if (n == 0) return;
+  if (Q % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)ws % 16 == 0) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(slab_reduce_v4_kernel, dim3(ceil_div_u(n4, SR_L)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(ws), S, n4, Q / 4, C, ldc, accumulate);
+  } else {
+    const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, ws, S, P, Q, C, ldc, accumulate);
+  }
+}
+
 Op to_op(const llp_operand* o) {
   Op r;
   r.ptr = reinterpret_cast<const char*>(o->ptr);
@@ -695,14 +758,10 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     float* wcs = colsum_a ? ws + sp * P * Q : nullptr;
     const int rc = llp_gemm_tn_bf16_256(A, B, M, P, Q, ws, wcs, sp, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (256 tile): %s", hipGetErrorString((hipError_t)rc));
-    const int64_t n = P * Q;
-    unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, (const float*)ws, sp, P, Q, C, ldc,
-                       accumulate);
+    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s);
     LLP_LAUNCH_CHECK();
-    if (colsum_a) {
-      hipLaunchKernelGGL(slab_reduce_kernel, dim3(ceil_div_u(P, 256)), dim3(256), 0, s, (const float*)wcs, sp, P,
-                         (int64_t)1, colsum_a, (int64_t)1, accumulate);
+    if (colsum_a) {   // [sp][P] column-sum slabs: P rows of one column
+      slab_reduce(wcs, sp, (int64_t)1, P, colsum_a, P, accumulate, s);
       LLP_LAUNCH_CHECK();
     }
     return LLP_OK;
@@ -738,10 +797,7 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     else hipLaunchKernelGGL((gemm_tn_kernel<float, false>), g2, dim3(NTHREADS), 0, s, pp);
   }
   LLP_LAUNCH_CHECK();
-  const int64_t n = P * Q;
-  unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, (const float*)workspace, splits, P, Q, C, ldc,
-                     accumulate);
+  slab_reduce(reinterpret_cast<const float*>(workspace), splits, P, Q, C, ldc, accumulate, s);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
