@@ -196,15 +196,17 @@ int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t
  * target[0..R) (U -> *n_unique, device), pos[r] = slot of target[r]; seg_rows =
  * rows grouped by slot in row order (stable sort), seg_ptr[0..U] = group bounds.
  * llp_segment_sum_rows: out[u] = sum of src rows of group u (f32 accumulate,
- * fixed order: deterministic); u_dev (may be NULL): device count, the call
- * covers min(U, *u_dev) groups (grid sized by U: capturable).
+ * fixed order: deterministic); out_rows (may be NULL): group u is written to
+ * out row out_rows[u] (uniq: a scatter onto node rows, e.g. the teacher's
+ * dh[N, H], src/train_teacher_gnn.py:62); u_dev (may be NULL): device count,
+ * the call covers min(U, *u_dev) groups (grid sized by U: capturable).
  * llp_gather_i32: out[i] = src[idx[i]]. */
 int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R);
 int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
                    int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
                    int64_t workspace_bytes, void* stream);
 int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
-                         const void* src, int64_t ld_src, void* out, int64_t ld_out,
+                         const void* src, int64_t ld_src, void* out, int64_t ld_out, const int32_t* out_rows,
                          const int32_t* u_dev, void* stream);
 int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
 /* Backward of the predictor input h[i] * h[j] (src/main.py:102-103,126) reduced

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, 
                                                           const int32_t* __restrict__ rows,
                                                           const T* __restrict__ src, int64_t lds_,
                                                           T* __restrict__ out, int64_t ldo,
+                                                          const int32_t* __restrict__ out_rows,
                                                           const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
   const int cpr = (int)(H / E);
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, 
     V8<T>::add(acc, v1);
   }
   if (k < end) V8<T>::add(acc, *reinterpret_cast<const uint4*>(src + (int64_t)rows[k] * lds_ + c * E));
-  *reinterpret_cast<uint4*>(out + u * ldo + c * E) = V8<T>::pack(acc);
+  const int64_t orow = out_rows ? (int64_t)out_rows[u] : u;
+  *reinterpret_cast<uint4*>(out + orow * ldo + c * E) = V8<T>::pack(acc);
 }
 
 // Fused Hadamard backward + per-node reduction (the unique-node student path).
@@ -258,7 +260,7 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
 
 extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
                                     const void* src, int64_t ld_src, void* out, int64_t ld_out,
-                                    const int32_t* u_dev, void* stream) {
+                                    const int32_t* out_rows, const int32_t* u_dev, void* stream) {
   LLP_CHECK_ARG(seg_ptr && rows && src && out, "llp_segment_sum_rows: null");
   const int E = dtype == LLP_BF16 ? 8 : 4;
   const int es = dtype == LLP_BF16 ? 2 : 4;
@@ -270,10 +272,10 @@ extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32
   hipStream_t s = (hipStream_t)stream;
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(segment_sum_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
-                       (const bf16_t*)src, ld_src, (bf16_t*)out, ld_out, u_dev);
+                       (const bf16_t*)src, ld_src, (bf16_t*)out, ld_out, out_rows, u_dev);
   else
     hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
-                       (const float*)src, ld_src, (float*)out, ld_out, u_dev);
+                       (const float*)src, ld_src, (float*)out, ld_out, out_rows, u_dev);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

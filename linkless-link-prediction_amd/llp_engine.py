@@ -669,7 +669,7 @@ class DistillEngine(EngineBase):
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             acts.append(out)
-            A = K.operand(out, count=n_u)
+            A = K.operand(out)
         h = acts[-1]
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)

@@ -166,24 +166,41 @@ class TeacherEngine(EngineBase):
                           dropout=drop)
         return self.h
 
-    def _encode_backward(self, dh32):
-        """Backward of _encode from d(loss)/dh (f32 [N, O])."""
+    def _dh_slot(self):
+        """The last layer's output-gradient slot [N, O] (compute dtype): d(loss)/dh lands here."""
+        last = self.layers[-1]
+        return last["G"] if self.gcn else last["G"][:, last["O"]:]
+
+    def _hadamard_bwd_nodes(self, R, tgt, dZ0, drow, h):
+        """d(loss)/dh of the predictor input h[ia] * h[ib] (src/train_teacher_gnn.py:41,61-62),
+        written into _dh_slot() deterministically: the 2R endpoint rows tgt = [ia | ib] are
+        grouped by node (llp_dedup_rows), each row's gradient dZ[r] * h[partner] is formed once
+        (llp_hadamard_bwd_blocks, label-row layout) and every node's rows are summed in row
+        order (f32) straight into its row of the slot; the other rows are zero."""
+        N, O = self.N, self.out_dim
+        R2 = 2 * R
+        uniq = self._buf("hb_uniq", (R2,), torch.int32)
+        pos = self._buf("hb_pos", (R2,), torch.int32)
+        n_u = self._buf("hb_nu", (1,), torch.int32)
+        seg_ptr = self._buf("hb_segp", (R2 + 1,), torch.int32)
+        seg_rows = self._buf("hb_segr", (R2,), torch.int32)
+        wsd = self._buf("hb_ws", (K.dedup_ws_bytes(N, R2) // 4 + 16,), torch.float32)
+        K.dedup_rows(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
+        dh_rows = self._buf("hb_rows", (R2, O), self.dtype)
+        K.hadamard_bwd_blocks(0, 1, R, O, dZ0, h, dh_rows, drow=drow, hidx=tgt)
+        slot = self._dh_slot()
+        slot.zero_()
+        K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, slot, count=n_u, out_rows=uniq)
+
+    def _encode_backward(self):
+        """Backward of _encode from d(loss)/dh, already in _dh_slot()."""
         g = self.graph
         dt, dc = self.dtype, self.dc
         N = self.N
         alpha = 1.0 / (1.0 - self.p_drop) if self.p_drop > 0 else 1.0
         nl = len(self.layers)
-        last = self.layers[-1]
-        O = last["O"]
         if self.gcn:
-            return self._gcn_backward(dh32, alpha)
-        Gl = last["G"]
-        if dt == torch.float32:
-            K.act_2d(dh32, Gl[:, O:], act=K.ACT_NONE)
-        else:
-            dh = self._buf("dh_c", (N, O), dt)
-            K.convert(dh32, dh)
-            K.act_2d(dh, Gl[:, O:], act=K.ACT_NONE)
+            return self._gcn_backward(alpha)
         for l in range(nl - 1, -1, -1):
             L = self.layers[l]
             F, O = L["F"], L["O"]
@@ -210,15 +227,10 @@ class TeacherEngine(EngineBase):
                 K.gemm_nt(K.operand(G), K.operand(L["WT"]), N, F, 2 * O, prev["G"][:, prev["O"]:], dc,
                           act=K.ACT_RELU_BWD, aux=L["X"], alpha=alpha)
 
-    def _gcn_backward(self, dh32, alpha):
+    def _gcn_backward(self, alpha):
         g = self.graph
         dt, dc = self.dtype, self.dc
         N = self.N
-        last = self.layers[-1]
-        if dt == torch.float32:
-            K.act_2d(dh32, last["G"], act=K.ACT_NONE)
-        else:
-            K.convert(dh32, last["G"])
         for l in range(len(self.layers) - 1, -1, -1):
             L = self.layers[l]
             F, O = L["F"], L["O"]
@@ -247,8 +259,8 @@ class TeacherEngine(EngineBase):
         h = self._encode(training=True)
         negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
         R = P + n_neg
-        ia = self._buf("t_ia", (max(R, 1),), torch.int32)[:R]
-        ib = self._buf("t_ib", (max(R, 1),), torch.int32)[:R]
+        tgt = self._buf("t_tgt", (max(2 * R, 1),), torch.int32)[:2 * R]   # [ia | ib]: endpoint rows
+        ia, ib = tgt[:R], tgt[R:]
         K.fullbatch_pairs(0, 0, None, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
         logit = self._buf("logit", (R,), torch.float32)
         A0, zacts = self._predictor_forward(h, ia, ib, R, logit, self.pred_drop)
@@ -257,14 +269,12 @@ class TeacherEngine(EngineBase):
         # BCE only (src/train_teacher_gnn.py:56-58)
         K.llp_loss(0, 1, None, None, R, P, logit, 1, P_total + n_neg_total, 0.0, 1.0, 1.0, 0.0, 0.0, None, dlogit,
                    self.terms, ws)
-        dh32 = self._buf("dh32", (N, O), torch.float32)
-        dh32.zero_()
         dZ0 = self._predictor_backward(dlogit, R, A0, zacts, self.pred_drop)
         if self.predictor_kind == "mlp":
-            K.hadamard_bwd_scatter(R, O, dZ0, ia, ib, h, dh32)
+            self._hadamard_bwd_nodes(R, tgt, dZ0, None, h)
         else:
-            K.hadamard_bwd_scatter(R, O, None, ia, ib, h, dh32, drow=dlogit)
-        self._encode_backward(dh32)
+            self._hadamard_bwd_nodes(R, tgt, None, dlogit, h)
+        self._encode_backward()
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)

@@ -153,3 +153,23 @@ def test_gcn_module_forward_backward():
     for c, (w, b) in zip(model.convs, convs):
         assert torch.allclose(c.lin.weight.grad.cpu(), w.grad, rtol=1e-3, atol=1e-4)
         assert torch.allclose(c.bias.grad.cpu(), b.grad, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_teacher_step_is_deterministic(dtype):
+    """Two runs of the same teacher steps give bit-identical gradients and
+    weights: the predictor-input backward is a fixed-order per-node sum
+    (no float atomics), the TN splits reduce in a fixed order."""
+    _need_gpu()
+    c = G.load_teacher_case(G.TEACHER_CASES[0])
+    pairs = c.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+    runs = []
+    for _ in range(2):
+        eng, model, pred = _build(c, dtype=dtype)
+        for st in c.steps[:3]:
+            eng.step(st.link_perm.to(torch.int32).to(DEV), pairs, neg=st.neg_edge.to(DEV))
+        torch.cuda.synchronize()
+        ps = list(model.parameters()) + list(pred.parameters())
+        runs.append([p.detach().cpu().clone() for p in ps] + [p.grad.detach().cpu().clone() for p in ps])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
