@@ -72,25 +72,25 @@ __global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_
     for (int i = 0; i < E; ++i) acc[i] = 0.f;
     if (active) {
       const int64_t ch = c0 + gl;
-      int64_t e = beg + grp;
-      // 4 neighbours in flight per group
-      for (; e + 3 * G < end; e += 4 * G) {
-        const int32_t j0 = col[e], j1 = col[e + G], j2 = col[e + 2 * G], j3 = col[e + 3 * G];
-        const uint4 v0 = *reinterpret_cast<const uint4*>(x + (int64_t)j0 * ldx + ch * E);
-        const uint4 v1 = *reinterpret_cast<const uint4*>(x + (int64_t)j1 * ldx + ch * E);
-        const uint4 v2 = *reinterpret_cast<const uint4*>(x + (int64_t)j2 * ldx + ch * E);
-        const uint4 v3 = *reinterpret_cast<const uint4*>(x + (int64_t)j3 * ldx + ch * E);
-        const float w0 = mode ? inv_deg[j0] : 1.f, w1 = mode ? inv_deg[j1] : 1.f;
-        const float w2 = mode ? inv_deg[j2] : 1.f, w3 = mode ? inv_deg[j3] : 1.f;
-        V16<T>::add(acc, v0, w0);
-        V16<T>::add(acc, v1, w1);
-        V16<T>::add(acc, v2, w2);
-        V16<T>::add(acc, v3, w3);
-      }
-      for (; e < end; e += G) {
-        const int32_t j = col[e];
-        const uint4 v = *reinterpret_cast<const uint4*>(x + (int64_t)j * ldx + ch * E);
-        V16<T>::add(acc, v, mode ? inv_deg[j] : 1.f);
+      // 4 neighbours in flight per group, the last round predicated: at the
+      // collab degree (~10) a group sees 2-3 neighbours, which the unpredicated
+      // tail walked one dependent load at a time.  Accumulation order per group
+      // is unchanged (e, e+G, e+2G, ...).
+      for (int64_t e = beg + grp; e < end; e += 4 * G) {
+        int32_t j[4];
+        bool v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k] = e + k * G < end;
+          j[k] = v[k] ? col[e + k * G] : 0;
+        }
+        uint4 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          r[k] = v[k] ? *reinterpret_cast<const uint4*>(x + (int64_t)j[k] * ldx + ch * E) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (v[k]) V16<T>::add(acc, r[k], mode ? inv_deg[j[k]] : 1.f);
       }
     }
     if (G > 1) {
