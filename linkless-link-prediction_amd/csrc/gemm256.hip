@@ -258,11 +258,12 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
         if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
       }
       if (p.drop_p > 0.f) {
+        // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
+        // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
+        const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
+        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)((m0 + ml) * p.N + n0 + nl + r));
-          v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
       }
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -335,8 +336,9 @@ __device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
 // Shared epilogue of the 256x256 kernels: alpha, bias, ReLU, dropout, fused
 // Linear(N,1) head partials, LDS-staged coalesced store (+ReLU-bwd mask).
 // smem must hold SMEM_U4_EPI uint4 + 4 KiB at smem + head_off_u4.
-__device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
-                                             int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
+template <int TMv, int NTHR>
+__device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
+                                           int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
   const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
   uint4* stg = smem;
   float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -363,11 +365,12 @@ __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8
         if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
       }
       if (p.drop_p > 0.f) {
+        // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
+        // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
+        const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
+        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)((m0 + ml) * p.N + n0 + nl + r));
-          v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
       }
       hp[im] += v[0] * hw[0] + v[1] * hw[1] + v[2] * hw[2] + v[3] * hw[3];
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -377,25 +380,25 @@ __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8
     }
   }
   if (p.head_w) {
-    float* part = reinterpret_cast<float*>(smem + head_off_u4);   // [4 wn][256 rows]
+    float* part = reinterpret_cast<float*>(smem + head_off_u4);   // [4 wn][TMv rows]
 #pragma unroll
     for (int im = 0; im < 8; ++im) {
       float v = hp[im];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (g == 0) part[wn * 256 + wm * 128 + im * 16 + li] = v;
+      if (g == 0) part[wn * TMv + wm * 128 + im * 16 + li] = v;
     }
   }
   __syncthreads();
-  if (p.head_w && tid < TM && m0 + tid < p.M) {
+  if (p.head_w && tid < TMv && m0 + tid < p.M) {
     const float* part = reinterpret_cast<const float*>(smem + head_off_u4);
-    const float s = part[tid] + part[256 + tid] + part[512 + tid] + part[768 + tid];
+    const float s = part[tid] + part[TMv + tid] + part[2 * TMv + tid] + part[3 * TMv + tid];
     p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = s;
   }
   if (!p.C) return;
   const int chunks_per_row = TN / 8;
 #pragma unroll 4
-  for (int q = tid; q < TM * chunks_per_row; q += NT2) {
+  for (int q = tid; q < TMv * chunks_per_row; q += NTHR) {
     const int rl = q / chunks_per_row, c = q % chunks_per_row;
     const int64_t row = m0 + rl, col = n0 + c * 8;
     const bool ok = row < p.M && col < p.N;
@@ -435,6 +438,11 @@ __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8
         *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
     }
   }
+}
+
+__device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
+                                             int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
+  epilogue_t<TM, NT2>(p, acc, smem, head_off_u4, m0, n0, tid, wm, wn, g, li);
 }
 
 // ---------------------------------------------------------------------------
@@ -855,11 +863,12 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
         if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
       }
       if (p.drop_p > 0.f) {
+        // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
+        // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
+        const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
+        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)((m0 + ml) * p.N + n0 + nl + r));
-          v[r] = (x >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
       }
       hp[im] += v[0] * hw[0] + v[1] * hw[1] + v[2] * hw[2] + v[3] * hw[3];
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -930,6 +939,159 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Half-height tiles, two workgroups per CU (LLP_GEMM_H128): 128 (m) x 256 (n)
+// per 256-thread workgroup; wave w owns columns [64w, 64w+64) of all 128 rows
+// (the 128 x 64 wave tile of the 256 kernels, same MFMA roles and epilogue).
+// K32 stages of 64-B lines (the pp images and swizzle) in a 3-stage ring,
+// two stages in flight, one barrier per stage: 24 KiB per stage, 72 KiB per
+// workgroup, so two workgroups share a CU (<= 256 VGPRs at two waves per SIMD).
+// They run unsynchronised: one workgroup's epilogue store issue and prologue
+// overlap the other's MFMA main loop -- the per-tile constant that the 256 x
+// 256 kernels (one workgroup per CU) serialise.  Row tiles of 128 also halve
+// the last-wave tail at the teacher's N = 256.
+constexpr int HTM = 128;
+constexpr int HNT = 256;
+constexpr int HNS = 3;
+constexpr int HSTAGE_U4 = (HTM + TN) * 4;     // 24 KiB: A [128][64 B] then B [256][64 B]
+constexpr int HEPI_U4 = HTM * EPI_ROW_U4;     // staged C tile, 66 KiB
+
+template <int TMv>
+__device__ __forceinline__ bool tile_live(P256& p, int64_t& m0, int64_t& n0) {
+  if (p.m_dev) {
+    const int64_t c = *p.m_dev;
+    p.M = c < p.M ? (c > 0 ? c : 0) : p.M;
+  }
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TMv - 1) / TMv;
+  const int64_t nt = tilesM * tilesN;
+  if ((int64_t)blockIdx.x >= nt) return false;
+  const int64_t lt = xcd_remap2(blockIdx.x, nt);
+  m0 = (lt / tilesN) * TMv;
+  n0 = (lt % tilesN) * TN;
+  return true;
+}
+
+template <int TMv>
+__device__ __forceinline__ bool tile_host_interleaved(const P256& p, int64_t& m0, int64_t& n0) {
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM = (p.M + TMv - 1) / TMv;
+  const int64_t xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+  const int64_t mt = (loc / tilesN) * 8 + xcd;
+  m0 = mt * TMv;
+  n0 = (loc % tilesN) * TN;
+  return mt < tilesM;
+}
+
+__global__ __launch_bounds__(HNT, 2) void gemm_nt_bf16_h128(P256 p) {
+  constexpr int LOOP_U4 = HNS * HSTAGE_U4;
+  constexpr int SM_U4 = LOOP_U4 > HEPI_U4 + 128 ? LOOP_U4 : HEPI_U4 + 128;   // + 2 KiB head partials
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  int64_t m0, n0;
+  const bool dyn = p.m_dev != nullptr;
+  const int32_t mlive = dyn ? *p.m_dev : 0;
+  if (dyn ? !tile_host_interleaved<HTM>(p, m0, n0) : !tile_live<HTM>(p, m0, n0)) return;
+
+  // DMA pieces (1 KiB = 16 rows x 64 B): A rows 32w + 16i + (lane>>2), i < 2;
+  // B rows 64w + 16i + (lane>>2), i < 4; physical chunk lane & 3
+  const bf16_t* ga[2];
+  const bf16_t* gb[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 32 * w + 16 * i + (lane >> 2);
+    const int lc = (lane & 3) ^ swz64(r);
+    int64_t m = m0 + r;
+    m = m < p.M ? m : p.M - 1;
+    ga[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 64 * w + 16 * i + (lane >> 2);
+    const int lc = (lane & 3) ^ swz64(r);
+    int64_t n = n0 + r;
+    n = n < p.N ? n : p.N - 1;
+    gb[i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
+  }
+  const uint32_t lds0 = lds_u32(smem);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto issue = [&](int64_t kt) {   // 6 LDS-DMA pieces per wave per stage
+    const uint32_t sA = lds0 + (uint32_t)((kt % HNS) * HSTAGE_U4 * 16);
+    const uint32_t sB = sA + HTM * 4 * 16;
+    const int64_t koff = kt * PK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(ga[i] + koff, __builtin_amdgcn_readfirstlane(sA + (uint32_t)((32 * wu + 16 * i) * 4 * 16)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16(gb[i] + koff, __builtin_amdgcn_readfirstlane(sB + (uint32_t)((64 * wu + 16 * i) * 4 * 16)));
+  };
+
+  float4_t acc[4][8];   // [n-tile jn][m-tile im]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = p.K / PK;
+  issue(0);
+  if (nk > 1) issue(1);
+  if (dyn) {   // the device row count, waited on only now (rows up to the host M are addressable)
+    p.M = mlive < p.M ? (mlive > 0 ? mlive : 0) : p.M;
+    if (m0 >= p.M) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    // RAW: this wave's pieces of stage kt landed (stage kt+1's 6 may still fly), then visible to all.
+    // WAR: the barrier also orders the refill of stage kt+2's buffer (= stage kt-1's) after every
+    // wave's fragment reads of stage kt-1 (consumed by its MFMAs before it got here).
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#ifndef LLP_ABLATE_NOLOAD
+    if (kt + 2 < nk) issue(kt + 2);
+#endif
+    const uint4* sA = smem + (int)(kt % HNS) * HSTAGE_U4;
+    const uint4* sB = sA + HTM * 4;
+    short8 fw[4], fx[8];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      const int r = w * 64 + jn * 16 + li;
+      uint4 v = sB[r * 4 + (g ^ swz64(r))];
+      fw[jn] = *reinterpret_cast<short8*>(&v);
+    }
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int r = im * 16 + li;
+      uint4 v = sA[r * 4 + (g ^ swz64(r))];
+      fx[im] = *reinterpret_cast<short8*>(&v);
+    }
+#ifndef LLP_ABLATE_NOMFMA
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+      for (int im = 0; im < 8; ++im)
+        acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#else
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
+#pragma unroll
+    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
+#endif
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_t<HTM, HNT>(p, acc, smem, HEPI_U4, m0, n0, tid, 0, w, g, li);
+}
+
 int g_gemm_variant = -1;
 
 }  // namespace
@@ -945,7 +1107,7 @@ int llp_gemm_variant() {
   return g_gemm_variant;
 }
 extern "C" int llp_set_gemm_variant(int v) {
-  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_Q64L, "llp_set_gemm_variant: %d", v);
+  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_H128, "llp_set_gemm_variant: %d", v);
   const int old = llp_gemm_variant();
   g_gemm_variant = v;
   return old;
@@ -977,10 +1139,11 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   // with a device row count the q64 kernel maps the host grid interleaved over
   // the XCDs (tile_256_host_interleaved): m-tiles padded to a multiple of 8;
   // the other variants map the live tiles and let the surplus blocks exit
-  const int64_t tiles = (A->rows_dev ? ((M + 8 * TM - 1) / (8 * TM)) * 8 : (M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  const int variant = llp_gemm_variant();
+  const int64_t tmr = (variant == LLP_GEMM_H128 && !A->ptr2) ? HTM : TM;   // rows per tile
+  const int64_t tiles = (A->rows_dev ? ((M + 8 * tmr - 1) / (8 * tmr)) * 8 : (M + tmr - 1) / tmr) * ((N + TN - 1) / TN);
   static const int pipe_env = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
   const int pipe = ((head_w || !C) && (pipe_env < 3 || pipe_env > 5)) ? 4 : pipe_env;
-  const int variant = llp_gemm_variant();
   if (A->ptr2)
     hipLaunchKernelGGL(gemm_nt_bf16_256<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (variant == LLP_GEMM_PP53)
@@ -991,6 +1154,8 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
     hipLaunchKernelGGL(gemm_nt_bf16_q64<false>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (variant == LLP_GEMM_Q64L)
     hipLaunchKernelGGL(gemm_nt_bf16_q64<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_H128)
+    hipLaunchKernelGGL(gemm_nt_bf16_h128, dim3((unsigned)tiles), dim3(HNT), 0, s, p);
   else if (pipe == 4 || pipe == 5)
     hipLaunchKernelGGL(gemm_nt_bf16_256p<4>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (pipe == 3)

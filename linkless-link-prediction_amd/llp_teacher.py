@@ -127,6 +127,14 @@ class TeacherEngine(EngineBase):
                 L["XA"] = XA
                 L["X"] = XA[:, F:]
             L["G"] = torch.empty(N, 2 * O, dtype=dt, device=self.dev)        # [mean-bwd(dOut) | dOut]
+        # ReLU(+dropout) bit masks of the SAGEConv layer inputs (bf16): layer l-1's forward GEMM
+        # writes bit (output > 0) of layer l's input, layer l's data-gradient GEMM reads it in
+        # place of the bf16 activations (16x less epilogue traffic); both on the 256-tile path
+        if not (self.gcn or self.updated) and dt == torch.bfloat16:
+            for l in range(1, len(self.layers)):
+                P_, L = self.layers[l - 1], self.layers[l]
+                if L["F"] % 32 == 0 and (2 * P_["F"]) % 64 == 0 and (2 * L["O"]) % 64 == 0:
+                    L["M"] = torch.empty(N, L["F"] // 8, dtype=torch.uint8, device=self.dev)
         self.out_dim = self.layers[-1]["O"]
         self.h = torch.empty(N, self.out_dim, dtype=dt, device=self.dev)
         self._build_descs()
@@ -163,7 +171,7 @@ class TeacherEngine(EngineBase):
                 K.csr_aggregate(N, F, g.rowptr, g.col, XA[:, F:], None, 0, XA[:, :F])
                 out = self.h if last else nxt["X"]
                 K.gemm_nt(K.operand(XA), K.operand(L["Wf"]), N, O, 2 * F, out, dc, bias=L["bias"], act=act,
-                          dropout=drop)
+                          aux=None if last else nxt.get("M"), dropout=drop)
         return self.h
 
     def _dh_slot(self):
@@ -224,8 +232,9 @@ class TeacherEngine(EngineBase):
                 # dX = [G | dOut] . [W_l^T | W_r^T]^T, ReLU/dropout mask of layer l-1 in the epilogue,
                 # written straight into layer l-1's output-gradient slot
                 prev = self.layers[l - 1]
+                mask = L.get("M")
                 K.gemm_nt(K.operand(G), K.operand(L["WT"]), N, F, 2 * O, prev["G"][:, prev["O"]:], dc,
-                          act=K.ACT_RELU_BWD, aux=L["X"], alpha=alpha)
+                          act=K.ACT_RELU_BWD, aux=L["X"] if mask is None else mask, alpha=alpha)
 
     def _gcn_backward(self, alpha):
         g = self.graph

@@ -173,3 +173,27 @@ def test_teacher_step_is_deterministic(dtype):
         runs.append([p.detach().cpu().clone() for p in ps] + [p.grad.detach().cpu().clone() for p in ps])
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+def test_teacher_bf16_relu_bit_masks_match_activation_masks():
+    """bf16 SAGE teacher with dropout: the ReLU/dropout bit masks written by the
+    forward GEMMs give bit-identical gradients and weights to the data-gradient
+    GEMMs masking on the stored bf16 activations."""
+    _need_gpu()
+    c = G.load_teacher_case("teacher_sage3_collab_small")   # H = 32, 3 layers: layer 2 takes a mask
+    pairs = c.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+    runs = []
+    for use_mask in (True, False):
+        eng, model, pred = _build(c, dtype="bf16", dropout=0.5)
+        if not use_mask:
+            for L in eng.layers:
+                L.pop("M", None)
+        else:
+            assert "M" in eng.layers[2]
+        for st in c.steps[:3]:
+            eng.step(st.link_perm.to(torch.int32).to(DEV), pairs, neg=st.neg_edge.to(DEV))
+        torch.cuda.synchronize()
+        ps = list(model.parameters()) + list(pred.parameters())
+        runs.append([p.detach().cpu().clone() for p in ps])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

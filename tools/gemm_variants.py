@@ -16,8 +16,8 @@ import torch  # noqa: E402
 
 import llp_hip as K  # noqa: E402
 
-VARIANTS = (3, 4)
-NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean"}
+VARIANTS = (4, 5)
+NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean", 5: "h128"}
 
 
 def main():
@@ -52,6 +52,12 @@ def main():
                                                out),
         "P fwd 603032x1024x1024": (lambda: K.gemm_nt(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024, out[:R2], 1,
                                                      bias=bias, act=K.ACT_RELU), 2 * R2 * 1024 * 1024, out),
+        "U fwd 225334x1024x1024": (lambda: K.gemm_nt(K.operand(h[:225334]), K.operand(W), 225334, 1024, 1024,
+                                                     out[:225334], 1, bias=bias, act=K.ACT_RELU),
+                                   2 * 225334 * 1024 * 1024, out),
+        "SAGE L0 235868x256x256": (lambda: K.gemm_nt(K.operand(xa[:, :256]), K.operand(Wt[:, :256]), N0, 256, 256,
+                                                     outs, 1, bias=bias[:256], act=K.ACT_RELU),
+                                   2 * N0 * 256 * 256, outs),
         "SAGE 235868x256x512": (lambda: K.gemm_nt(K.operand(xa), K.operand(Wt), N0, 256, 512, outs, 1, bias=bias[:256],
                                                   act=K.ACT_RELU), 2 * N0 * 256 * 512, outs),
     }
@@ -67,7 +73,7 @@ def main():
         same = all(torch.equal(res[0], r) for r in res[1:])
         print(f"{name}: variants bit-identical: {same}", flush=True)
     if True:   # torch check of the L2 fwd on 4096 rows
-        L.llp_set_gemm_variant(2)
+        L.llp_set_gemm_variant(5)
         cases["L2 fwd 747214x1024x1024"][0]()
         torch.cuda.synchronize()
         ref = torch.relu(h[:4096].float() @ W.float().t() + bias)
