@@ -65,6 +65,7 @@ class _Linear:
         self.W = lin.weight.data
         self.b = lin.bias.data
         self.out_f, self.in_f = self.W.shape
+        self.k_in = self.in_f      # GEMM inner dimension (the first student layer may run on zero-padded K)
         self.Wc = None
         self.Wt = None
         if need_c and dtype != torch.float32:
@@ -339,6 +340,26 @@ class EngineBase:
             cur, nxt = nxt, cur
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
+    def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
+        """d(loss)/dh of the predictor input h[ia] * h[ib] into ``out`` [N, H] (compute dtype),
+        deterministically: the 2R endpoint rows tgt = [ia | ib] are grouped by node
+        (llp_dedup_rows), each row's gradient dZ[r] * h[partner] is formed once
+        (llp_hadamard_bwd_blocks, label-row layout; drow: the 'inner' predictor's scalar) and
+        every node's rows are summed in row order (f32) into its row of ``out``; other rows are 0."""
+        N, H = self.N, h.shape[1]
+        R2 = 2 * R
+        uniq = self._buf("hb_uniq", (R2,), torch.int32)
+        pos = self._buf("hb_pos", (R2,), torch.int32)
+        n_u = self._buf("hb_nu", (1,), torch.int32)
+        seg_ptr = self._buf("hb_segp", (R2 + 1,), torch.int32)
+        seg_rows = self._buf("hb_segr", (R2,), torch.int32)
+        wsd = self._buf("hb_ws", (K.dedup_ws_bytes(N, R2) // 4 + 16,), torch.float32)
+        K.dedup_rows(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
+        dh_rows = self._buf("hb_rows", (R2, H), h.dtype)
+        K.hadamard_bwd_blocks(0, 1, R, H, dZ, h, dh_rows, drow=drow, hidx=tgt)
+        out.zero_()
+        K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, out, count=n_u, out_rows=uniq)
+
     def _relu_aux(self, act):
         """What the ReLU-backward GEMM reads for activation ``act``: its bit mask when
         the forward wrote one, else the activations themselves."""
@@ -410,8 +431,17 @@ class DistillEngine(EngineBase):
         self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
         stu = list(model.layers)
         self.stu = [_Linear(l, self.dtype, need_t=(i > 0), need_c=True) for i, l in enumerate(stu)]
+        # bf16: the input width is zero-padded to a multiple of 64 (x and the first layer's compute
+        # copy) so that the first layer runs on the 256-tile MFMA kernels (cora 1,433 -> 1,472,
+        # coauthor-physics 8,415 -> 8,448, ...); padded columns are 0 in both, the products exact
+        F_in = self.stu[0].in_f
+        self.F_pad = -(-F_in // 64) * 64 if (self.dtype == torch.bfloat16 and F_in % 64) else F_in
+        if self.F_pad != F_in:
+            l0 = self.stu[0]
+            l0.Wc = torch.zeros(l0.out_f, self.F_pad, dtype=self.dtype, device=l0.W.device)
+            l0.k_in = self.F_pad
         for l in self.stu:
-            self._set_shadow(l.lin.weight, l.Wc, l.Wt)
+            self._set_shadow(l.lin.weight, l.Wc, l.Wt, l.k_in if l.Wc is not None else 0)
         stu_params = [p for l in stu for p in (l.weight, l.bias)]
         prd_params = self._setup_predictor(predictor, args.predictor)
         self._init_params(stu_params + prd_params, [0] * len(stu_params) + [1] * len(prd_params), optimizer)
@@ -428,7 +458,11 @@ class DistillEngine(EngineBase):
         self.t_dropout = float(getattr(teacher_predictor, "dropout", 0.0)) if teacher_predictor.training else 0.0
 
         # ---------------- data
-        self.x = x.to(self.dev).to(self.dtype).contiguous()
+        if self.F_pad != F_in:
+            self.x = torch.zeros(self.N, self.F_pad, dtype=self.dtype, device=self.dev)
+            self.x[:, :F_in].copy_(x.to(self.dev))
+        else:
+            self.x = x.to(self.dev).to(self.dtype).contiguous()
         self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
         self._neg_rc = (np.asarray(row), np.asarray(col))
         self._neg_keys = None
@@ -553,9 +587,9 @@ class DistillEngine(EngineBase):
             if timed:   # the dominant MFMA kernel, timed on the launch stream (bench.py roofline)
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            hm = None if last else self._mask(f"Hm{l}", rows_s, lin.out_f, lin.in_f, self.stu[l + 1].out_f)
+            hm = None if last else self._mask(f"Hm{l}", rows_s, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
             self._act_mask[id(out)] = hm
-            K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.in_f, out, dc, bias=lin.b,
+            K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.k_in, out, dc, bias=lin.b,
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             if timed:
@@ -653,8 +687,8 @@ class DistillEngine(EngineBase):
         n_lab_total = P_total + n_neg_total
         BC = Bc * C
         R2 = BC + n_lab
-        ia = self._buf("fb_ia", (max(R2, 1),), torch.int32)[:R2]
-        ib = self._buf("fb_ib", (max(R2, 1),), torch.int32)[:R2]
+        ia_ib = self._buf("fb_iab", (max(2 * R2, 1),), torch.int32)[:2 * R2]   # [ia | ib]: endpoint rows
+        ia, ib = ia_ib[:R2], ia_ib[R2:]
         K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
 
         # ---- a4: student MLP over all nodes (src/main.py:173)
@@ -663,9 +697,9 @@ class DistillEngine(EngineBase):
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (N, lin.out_f), dt)
-            hm = None if last else self._mask(f"Hm{l}", N, lin.out_f, lin.in_f, self.stu[l + 1].out_f)
+            hm = None if last else self._mask(f"Hm{l}", N, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
             self._act_mask[id(out)] = hm
-            K.gemm_nt(A, K.operand(lin.Wcomp), N, lin.out_f, lin.in_f, out, dc, bias=lin.b,
+            K.gemm_nt(A, K.operand(lin.Wcomp), N, lin.out_f, lin.k_in, out, dc, bias=lin.b,
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, 1 + l))
             acts.append(out)
@@ -688,11 +722,14 @@ class DistillEngine(EngineBase):
         K.llp_loss(Bc, C, logit, t_r, n_lab, P, logit[BC:], B_total if use_llp else 1, n_lab_total,
                    float(a.margin), 1.0, float(a.True_label), float(a.LLP_D) if use_llp else 0.0,
                    float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws)
-        # d(loss)/dh accumulates in f32 (scatter-add over the gathered rows); in
-        # fp32 mode it IS the student backward's first gradient buffer
-        dh32 = self._buf("gS0" if dt == torch.float32 else "dh32", (N, H), torch.float32)
-        dh32.zero_()
         w_rm, w_lm = float(a.KD_RM), float(a.KD_LM)
+        # d(loss)/dh: without KD_RM, the pair rows' Hadamard gradients are grouped by node and
+        # summed in row order (deterministic, straight into the compute-dtype buffer); with KD_RM
+        # (which adds at the anchors) they accumulate by f32 scatter-add, then convert
+        grouped = w_rm == 0.0
+        if not grouped:   # in fp32 mode dh32 IS the student backward's first gradient buffer
+            dh32 = self._buf("gS0" if dt == torch.float32 else "dh32", (N, H), torch.float32)
+            dh32.zero_()
         if w_rm != 0.0 or w_lm != 0.0:
             if w_rm != 0.0 and self.t_h.shape[1] != H:
                 raise ValueError("KD_RM needs the student width to equal the teacher's (src/main.py:218)")
@@ -700,21 +737,26 @@ class DistillEngine(EngineBase):
             K.kd_terms(self.terms, wsk, n_lab=n_lab if w_lm != 0.0 else 0, out_logit=logit[BC:],
                        t_prob_lab=t_r[BC:R2] if w_lm != 0.0 else None, n_lab_total=n_lab_total, w_lm=w_lm,
                        dlogit_lab=dlogit[BC:], B_rm=B if w_rm != 0.0 else 0, h=h, t_h=self.t_h, idx_rm=anchors,
-                       B_rm_total=B_total, w_rm=w_rm, dh=dh32)
+                       B_rm_total=B_total, w_rm=w_rm, dh=None if grouped else dh32)
         else:
             self.terms[4:6].zero_()
 
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
-        if self.predictor_kind == "mlp":
-            K.hadamard_bwd_scatter(R2, H, dZ0, ia, ib, h, dh32)
-        else:
-            K.hadamard_bwd_scatter(R2, H, None, ia, ib, h, dh32, drow=dlogit)
-        if dt == torch.float32:
-            dh = dh32
-        else:
+        mlp = self.predictor_kind == "mlp"
+        if grouped:
             dh = self._buf("gS0", (N, H), dt)
-            K.convert(dh32, dh)
+            self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh)
+        else:
+            if mlp:
+                K.hadamard_bwd_scatter(R2, H, dZ0, ia, ib, h, dh32)
+            else:
+                K.hadamard_bwd_scatter(R2, H, None, ia, ib, h, dh32, drow=dlogit)
+            if dt == torch.float32:
+                dh = dh32
+            else:
+                dh = self._buf("gS0", (N, H), dt)
+                K.convert(dh32, dh)
         self._student_backward(dh, N, None, acts, p_drop)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
@@ -775,9 +817,13 @@ class DistillEngine(EngineBase):
             lin = self.stu[l]
             gcur = self._buf(cur, (R1, lin.out_f), dt)
             A_in = K.operand(acts[l - 1], count=count) if l > 0 else K.operand(self.x, target, count=count)
-            wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.in_f)
-            K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
+            wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
+            padded = lin.k_in != lin.in_f
+            dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad
+            K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc,
                       self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+            if padded:   # the zero-padded input columns' gradient is dropped
+                lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
             if l > 0:
                 gnext = self._buf(nxt, (R1, lin.in_f), dt)
                 K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,

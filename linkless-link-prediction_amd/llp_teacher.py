@@ -179,27 +179,6 @@ class TeacherEngine(EngineBase):
         last = self.layers[-1]
         return last["G"] if self.gcn else last["G"][:, last["O"]:]
 
-    def _hadamard_bwd_nodes(self, R, tgt, dZ0, drow, h):
-        """d(loss)/dh of the predictor input h[ia] * h[ib] (src/train_teacher_gnn.py:41,61-62),
-        written into _dh_slot() deterministically: the 2R endpoint rows tgt = [ia | ib] are
-        grouped by node (llp_dedup_rows), each row's gradient dZ[r] * h[partner] is formed once
-        (llp_hadamard_bwd_blocks, label-row layout) and every node's rows are summed in row
-        order (f32) straight into its row of the slot; the other rows are zero."""
-        N, O = self.N, self.out_dim
-        R2 = 2 * R
-        uniq = self._buf("hb_uniq", (R2,), torch.int32)
-        pos = self._buf("hb_pos", (R2,), torch.int32)
-        n_u = self._buf("hb_nu", (1,), torch.int32)
-        seg_ptr = self._buf("hb_segp", (R2 + 1,), torch.int32)
-        seg_rows = self._buf("hb_segr", (R2,), torch.int32)
-        wsd = self._buf("hb_ws", (K.dedup_ws_bytes(N, R2) // 4 + 16,), torch.float32)
-        K.dedup_rows(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
-        dh_rows = self._buf("hb_rows", (R2, O), self.dtype)
-        K.hadamard_bwd_blocks(0, 1, R, O, dZ0, h, dh_rows, drow=drow, hidx=tgt)
-        slot = self._dh_slot()
-        slot.zero_()
-        K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, slot, count=n_u, out_rows=uniq)
-
     def _encode_backward(self):
         """Backward of _encode from d(loss)/dh, already in _dh_slot()."""
         g = self.graph
@@ -280,9 +259,9 @@ class TeacherEngine(EngineBase):
                    self.terms, ws)
         dZ0 = self._predictor_backward(dlogit, R, A0, zacts, self.pred_drop)
         if self.predictor_kind == "mlp":
-            self._hadamard_bwd_nodes(R, tgt, dZ0, None, h)
+            self._hadamard_bwd_nodes(R, tgt, dZ0, None, h, self._dh_slot())
         else:
-            self._hadamard_bwd_nodes(R, tgt, None, dlogit, h)
+            self._hadamard_bwd_nodes(R, tgt, None, dlogit, h, self._dh_slot())
         self._encode_backward()
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)

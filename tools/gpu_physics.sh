@@ -1,0 +1,7 @@
+# coauthor-physics production (BASELINE configs[3]) full-batch step: bf16/fp32 timing, rank-0 shard at R=4, kernel profile.
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python tools/physics_bench.py --steps 10 > gpurun_out/physics.log 2>&1 && \
+timeout -k 10 300 python tools/physics_bench.py --steps 10 --dtype bf16 --emulate-ranks 4 > gpurun_out/physics_r4.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_phys -o phys --output-format csv -- python tools/physics_bench.py --steps 5 --dtype bf16 > gpurun_out/prof_phys.log 2>&1
+echo rc=$?
