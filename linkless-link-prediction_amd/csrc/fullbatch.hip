@@ -76,66 +76,99 @@ __global__ void neg_candidates(int64_t M, int enumerate_all, uint64_t population
   }
 }
 
-// Ordered compaction of the valid candidates (one block): the first num_neg of
-// them in stream order, decoded as PyG does: row = idx / (N-1), col = idx %
-// (N-1), col += (row <= col).
-__global__ __launch_bounds__(1024) void neg_compact(int64_t M, int64_t num_nodes, int64_t num_neg,
-                                                    const int64_t* __restrict__ cand,
-                                                    const int32_t* __restrict__ slot,
-                                                    const int32_t* __restrict__ tmin, int32_t* __restrict__ out,
-                                                    int64_t ld_out, int32_t* __restrict__ count) {
-  __shared__ int32_t wsum[16];
-  __shared__ int32_t base_s;
+// Ordered compaction of the valid candidates: the first num_neg of them in
+// stream order, decoded as PyG does: row = idx / (N-1), col = idx % (N-1),
+// col += (row <= col).  Three passes over tiles of 1024 candidates (256
+// threads x 4): per-tile valid counts, one-block exclusive scan of the tile
+// counts (and the final count), per-tile scan + scatter.
+constexpr int NC_TILE = 1024;
+
+__device__ __forceinline__ int neg_valid(int64_t i, int64_t M, const int32_t* __restrict__ slot,
+                                         const int32_t* __restrict__ tmin) {
+  if (i >= M) return 0;
+  const int32_t s = slot[i];
+  return (s >= 0 && tmin[s] == (int32_t)i) ? 1 : 0;
+}
+
+// block-wide exclusive scan of one int per thread (256 threads); returns the exclusive
+// prefix, *total = block sum
+__device__ __forceinline__ int block_excl_scan256(int v, int* wsum, int* total) {
   const int tid = threadIdx.x;
-  if (tid == 0) base_s = 0;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if ((tid & 63) >= o) incl += y;
+  }
+  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
   __syncthreads();
-  const int64_t per = 2048;   // candidates per pass: 1024 threads x 2
-  for (int64_t p0 = 0; p0 < M; p0 += per) {
-    const int base = base_s;
-    if (base >= num_neg) break;
-    int v[2];
-    int64_t idx[2];
+  int wbase = 0;
+  for (int w = 0; w < (tid >> 6); ++w) wbase += wsum[w];
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  return wbase + incl - v;
+}
+
+__global__ __launch_bounds__(256) void neg_tile_count(int64_t M, const int32_t* __restrict__ slot,
+                                                      const int32_t* __restrict__ tmin, int32_t* __restrict__ tcount) {
+  __shared__ int wsum[4];
+  const int64_t i0 = (int64_t)blockIdx.x * NC_TILE + 4 * threadIdx.x;
+  int v = 0;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      idx[k] = p0 + 2 * tid + k;
-      v[k] = 0;
-      if (idx[k] < M) {
-        const int32_t s = slot[idx[k]];
-        v[k] = (s >= 0 && tmin[s] == (int32_t)idx[k]) ? 1 : 0;
-      }
-    }
-    int mine = v[0] + v[1];
-    // block exclusive scan of mine
-    int incl = mine;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o, 64);
-      if ((tid & 63) >= o) incl += y;
-    }
-    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+  for (int k = 0; k < 4; ++k) v += neg_valid(i0 + k, M, slot, tmin);
+  int total;
+  block_excl_scan256(v, wsum, &total);
+  if (threadIdx.x == 0) tcount[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void neg_tile_scan(int64_t ntiles, int64_t num_neg, int32_t* __restrict__ tbase,
+                                                     int32_t* __restrict__ count) {
+  __shared__ int wsum[4];
+  int64_t carry = 0;
+  for (int64_t t0 = 0; t0 < ntiles; t0 += 256) {
+    const int64_t t = t0 + threadIdx.x;
+    const int v = t < ntiles ? tbase[t] : 0;       // tile counts in, tile bases out (in place)
+    int total;
+    const int ex = block_excl_scan256(v, wsum, &total);
     __syncthreads();
-    int wbase = 0;
-    for (int w = 0; w < (tid >> 6); ++w) wbase += wsum[w];
-    int pos = base + wbase + incl - mine;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (v[k]) {
-        if (pos < num_neg) {
-          const int64_t c = cand[idx[k]];
-          const int64_t r = c / (num_nodes - 1);
-          int64_t cc = c % (num_nodes - 1);
-          if (r <= cc) cc += 1;
-          out[pos] = (int32_t)r;
-          out[ld_out + pos] = (int32_t)cc;
-        }
-        ++pos;
-      }
-    }
-    __syncthreads();
-    if (tid == 1023) base_s = min((int64_t)pos, num_neg);
+    if (t < ntiles) tbase[t] = (int32_t)min(carry + ex, (int64_t)0x7FFFFFFF);
+    carry += total;
     __syncthreads();
   }
-  if (tid == 0) *count = base_s;
+  if (threadIdx.x == 0) *count = (int32_t)min(carry, num_neg);
+}
+
+__global__ __launch_bounds__(256) void neg_tile_scatter(int64_t M, int64_t num_nodes, int64_t num_neg,
+                                                        const int64_t* __restrict__ cand,
+                                                        const int32_t* __restrict__ slot,
+                                                        const int32_t* __restrict__ tmin,
+                                                        const int32_t* __restrict__ tbase, int32_t* __restrict__ out,
+                                                        int64_t ld_out) {
+  __shared__ int wsum[4];
+  const int64_t base = tbase[blockIdx.x];
+  if (base >= num_neg) return;                      // uniform per block
+  const int64_t i0 = (int64_t)blockIdx.x * NC_TILE + 4 * threadIdx.x;
+  int v[4], mine = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = neg_valid(i0 + k, M, slot, tmin);
+    mine += v[k];
+  }
+  int total;
+  int64_t pos = base + block_excl_scan256(mine, wsum, &total);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (v[k]) {
+      if (pos < num_neg) {
+        const int64_t c = cand[i0 + k];
+        const int64_t r = c / (num_nodes - 1);
+        int64_t cc = c % (num_nodes - 1);
+        if (r <= cc) cc += 1;
+        out[pos] = (int32_t)r;
+        out[ld_out + pos] = (int32_t)cc;
+      }
+      ++pos;
+    }
+  }
 }
 
 // ia/ib for the full-batch predictor rows: B*C context pairs (anchor, context)
@@ -260,7 +293,8 @@ int64_t pow2_at_least(int64_t v) {
 
 extern "C" int64_t llp_neg_sample_dense_workspace_bytes(int64_t max_candidates) {
   const int64_t T = pow2_at_least(2 * max_candidates);
-  return T * 8 + T * 4 + max_candidates * 8 + max_candidates * 4 + 64;
+  const int64_t ntiles = (max_candidates + NC_TILE - 1) / NC_TILE;
+  return T * 8 + T * 4 + max_candidates * 8 + max_candidates * 4 + ntiles * 4 + 64;
 }
 
 extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys,
@@ -293,9 +327,19 @@ extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys,
                        step_ctr, stream_offset, edge_keys, n_keys, cand, slot, tkeys, tmin, T);
     LLP_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(neg_compact, dim3(1), dim3(1024), 0, s, M, num_nodes, num_neg, cand, slot, tmin, out, ld_out,
-                     count);
+  const int64_t ntiles = (M + NC_TILE - 1) / NC_TILE;
+  int32_t* tbase = reinterpret_cast<int32_t*>(w + T * 12 + M * 12);
+  if (ntiles > 0) {
+    hipLaunchKernelGGL(neg_tile_count, dim3((unsigned)ntiles), dim3(256), 0, s, M, slot, tmin, tbase);
+    LLP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(neg_tile_scan, dim3(1), dim3(256), 0, s, ntiles, num_neg, tbase, count);
   LLP_LAUNCH_CHECK();
+  if (ntiles > 0) {
+    hipLaunchKernelGGL(neg_tile_scatter, dim3((unsigned)ntiles), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot,
+                       tmin, tbase, out, ld_out);
+    LLP_LAUNCH_CHECK();
+  }
   return LLP_OK;
 }
 
