@@ -195,8 +195,10 @@ def sage_teacher_step(data, dev, dtype, steps=5):
     import llp_teacher
     import models
     torch.manual_seed(0)
-    model = models.SAGE("collab", data.F, 256, 256, 3, 0.0, llp_sage.SAGEConv).to(dev)
-    pred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
+    # dropout 0.5: train_teacher_gnn.py's default (src/train_teacher_gnn.py:277), live in the encoder
+    # and the predictor (fused Philox masks in the GEMM epilogues)
+    model = models.SAGE("collab", data.F, 256, 256, 3, 0.5, llp_sage.SAGEConv).to(dev)
+    pred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.5).to(dev)
     optim = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=0.005)
     eng = llp_teacher.TeacherEngine(model, pred, data.x.to(dev), data.edge_index, data.N, optim, dtype=dtype)
     pairs = data.train_pairs.to(torch.int32).to(dev).contiguous()
@@ -211,7 +213,27 @@ def sage_teacher_step(data, dev, dtype, steps=5):
     torch.cuda.synchronize()
     dt_s = (time.perf_counter() - t0) / steps
     return {"ms_per_step": dt_s * 1e3, "edges_per_s": P / dt_s, "dtype": dtype,
-            "config": "SAGE 3x(128->256) over N=235,868 / E=2,358,104, LinkPredictor 256x2, 65,536 positives"}
+            "config": "SAGE 3x(128->256) over N=235,868 / E=2,358,104, LinkPredictor 256x2, dropout 0.5, "
+                      "65,536 positives"}
+
+
+def physics_production_step(dtype):
+    """BASELINE configs[3] at one GPU: the full-batch train() step at the
+    coauthor-physics production shape (tools/physics_bench.py), plus rank 0's
+    shard of the same batch at 4 ranks (no collective)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import llp_split
+    import physics_bench
+    split = llp_split.production_split("coauthor-physics", os.path.join(tempfile.gettempdir(), "llp_physics"),
+                                       synthetic=True)
+    r1 = physics_bench.run(dtype, 10, 2, 0, split)
+    r4 = physics_bench.run(dtype, 10, 2, 4, split)
+    return {"config": "coauthor-physics production LLP (N_old=%d, F=%d, H=256, L=2, C=%d, 65,536 edges/step)"
+                      % (r1["N_old"], r1["F"], r1["contexts_per_anchor"]),
+            "dtype": dtype, "ms_per_step": r1["ms_per_step"], "edges_per_s": r1["edges_per_s"],
+            "rank0_ms_per_step_at_4_ranks": r4["ms_per_step"],
+            "note": "the full-batch student runs over all N_old nodes on every rank (src/main.py:173)"}
 
 
 def main():
@@ -230,6 +252,7 @@ def main():
                     help="replay the step from a captured hipGraph (N=1; --no-graph: eager launches)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
+    ap.add_argument("--no-physics", action="store_true")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single GPU: run only rank 0's shard of an R-rank job (no collective) and report "
                          "its per-step time, to see the per-rank fixed costs of strong scaling")
@@ -384,6 +407,8 @@ def main():
         if not opt.no_sage:
             res["sage_aggregate"] = sage_aggregate(data, dev)
             res["sage_teacher_step"] = sage_teacher_step(data, dev, opt.dtype)
+        if world == 1 and not opt.no_physics:
+            res["physics_production_step"] = physics_production_step(opt.dtype)
         if world == 1 and not opt.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, a, t_h, init, B_full, P_full, sample_P=opt.cpu_sample_edges)
         print(json.dumps(res), flush=True)
