@@ -109,9 +109,10 @@ def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, 
                        P_total=P_full)
     lin = eng.stu[1]
     A = eng._bufs["H0"]
-    R1 = eng.last_student_rows
+    cnt = eng._rows_dev                       # the step's launch: host bound, device unique count
+    R1 = A.numel() // lin.in_f if cnt is not None else eng.last_student_rows
     out = eng._buf("H1", (R1, lin.out_f), eng.dtype)
-    a_op = K.operand(A[:R1 * lin.in_f].view(R1, lin.in_f))
+    a_op = K.operand(A[:R1 * lin.in_f].view(R1, lin.in_f), count=cnt)
     for _ in range(n):
         K.gemm_nt(a_op, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, eng.dc, bias=lin.b, act=K.ACT_RELU)
     torch.cuda.synchronize()
