@@ -259,8 +259,8 @@ class EngineBase:
             ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
             K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, 14, negg, cnt, ws)
             n_neg_total = int(cnt.item())
-            lo = min(p_offset, n_neg_total)
-            hi = min(p_offset + P, n_neg_total) if self.world > 1 else n_neg_total
+            lo = min(p_offset, n_neg_total)         # this shard's columns (all of them unsharded)
+            hi = min(p_offset + P, n_neg_total)
             return negg[:, lo:hi], hi - lo, n_neg_total
         negb = self._buf("neg", (2, max(P, 1)), torch.int32)
         K.randint_pairs(N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)

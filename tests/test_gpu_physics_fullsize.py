@@ -1,0 +1,121 @@
+"""BASELINE configs[3] at full size: the full-batch train() step
+(src/main.py:147-236) at the coauthor-physics production shape (synthetic
+graph split by the reference's do_production_edge_split: 31,044 old nodes,
+8,415 binary features, 288,498 directed training edges; student 8,415 -> 256
+-> 256, C = 20 contexts, 65,536 edges, PyG-dense negatives).  The CPU oracle
+cannot run this size in a test, so the properties checked are size-independent:
+
+* determinism: the same step from the same state is bit-identical in bf16
+  (node-grouped Hadamard backward, fixed-order reductions, no atomics);
+* anchor/edge sharding (what each of R ranks computes before the gradient
+  all-reduce): the two half-batch shards' gradients sum to the whole batch's;
+* the bf16 step (first layer on zero-padded K = 8,448) tracks the fp32 step
+  on the loss terms and the gradients of the padded first layer and the head."""
+import os
+import sys
+import tempfile
+import types
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def physics():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import llp_split
+    import physics_bench
+    split = llp_split.production_split("coauthor-physics", os.path.join(tempfile.gettempdir(), "llp_physics"),
+                                       synthetic=True)
+    return split[0], physics_bench.physics_args()
+
+
+def _step(physics, dtype, b_rng=None, p_rng=None):
+    import llp_engine
+    import models
+    td, a = physics
+    N, F_ = td.x.size(0), td.x.size(1)
+    E = td.edge_index.size(1)
+    P = a.link_batch_size
+    B = int(N / (E / P))
+    torch.manual_seed(1)
+    model = models.MLP(a.num_layers, F_, a.hidden_channels, a.hidden_channels, 0.0).to(DEV)
+    pred = models.LinkPredictor("mlp", a.hidden_channels, a.hidden_channels, 1, a.num_layers, 0.0).to(DEV)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(DEV)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    t_h = torch.randn(N, 256, generator=torch.Generator().manual_seed(2)) * 0.3
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
+    row, col = td.edge_index
+    eng = llp_engine.DistillEngine(model, pred, tpred, td.x.to(DEV), t_h.to(DEV), row.numpy(), col.numpy(), N, a,
+                                   opt, dtype=dtype, seed=11)
+    g = torch.Generator().manual_seed(3)
+    anchors = torch.randperm(N, generator=g)[:B].to(torch.int32).to(DEV)
+    links = torch.randperm(E, generator=g)[:P].to(torch.int32).to(DEV)
+    b0, b1 = b_rng or (0, B)
+    p0, p1 = p_rng or (0, P)
+    pairs = td.edge_index.t().to(torch.int32).to(DEV).contiguous()
+    eng.step_fullbatch(anchors[b0:b1], links[p0:p1], pairs, b_offset=b0, p_offset=p0, B_total=B, P_total=P,
+                       dense_negatives=True)
+    torch.cuda.synchronize()
+    ps = list(model.parameters()) + list(pred.parameters())
+    out = types.SimpleNamespace(terms=eng.terms.cpu().clone(), B=B, P=P,
+                                grads=[p.grad.detach().float().cpu().clone() for p in ps])
+    del eng, model, pred, tpred, opt
+    torch.cuda.empty_cache()
+    return out
+
+
+def test_physics_fullbatch_step_is_deterministic(physics):
+    r1 = _step(physics, "bf16")
+    r2 = _step(physics, "bf16")
+    assert torch.isfinite(r1.terms[:4]).all()
+    assert torch.equal(r1.terms, r2.terms)
+    for a, b in zip(r1.grads, r2.grads):
+        assert torch.equal(a, b)
+
+
+def test_physics_fullbatch_shards_sum_to_the_batch(physics):
+    """Two ranks' shards (global normalisers, global draw indices, each rank's
+    column slice of the global dense-negative list) sum to the whole batch's
+    gradient: the all-reduce then gives every rank the single-GPU gradient."""
+    whole = _step(physics, "fp32")
+    B, P = whole.B, whole.P
+    s0 = _step(physics, "fp32", (0, B // 2), (0, P // 2))
+    s1 = _step(physics, "fp32", (B // 2, B), (P // 2, P))
+    for g, a, b in zip(whole.grads, s0.grads, s1.grads):
+        err = (a + b - g).abs().max().item()
+        assert err <= 1e-4 * max(g.abs().max().item(), 1e-6) + 1e-7, (tuple(g.shape), err)
+    # the loss terms add up as well (each rank reports its share of the global mean)
+    assert abs(float(s0.terms[0] + s1.terms[0]) - float(whole.terms[0])) <= 1e-4 * max(1.0, abs(float(whole.terms[0])))
+
+
+def test_physics_fullbatch_bf16_tracks_fp32(physics):
+    """bf16 (first layer on zero-padded K = 8,448, 256-tile MFMA kernels) vs fp32
+    (exact f32 MFMA on K = 8,415): the loss terms agree to 2e-2, and so do the
+    gradients the padded path produces directly: the first layer's weight
+    (cosine > 0.99) and the predictor head's (cosine > 0.99).  The interior
+    parameters' gradients at initialisation are differences of nearly balanced
+    positive / negative pair contributions (BCE at sigmoid(0) ~ 1/2, a constant
+    rank hinge), so bf16 rounding of the activations moves them by O(1)
+    relative (tools/debug_physics_bf16.py prints every parameter); the
+    reference has no bf16 path to hold them to."""
+    f32 = _step(physics, "fp32")
+    b16 = _step(physics, "bf16")
+    for k in range(4):
+        a, b = float(b16.terms[k]), float(f32.terms[k])
+        assert abs(a - b) <= 2e-2 * max(abs(b), 1e-3), (k, a, b)
+
+    def cos(a, b):
+        return torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
+
+    assert b16.grads[0].shape == (256, 8415)
+    assert cos(b16.grads[0], f32.grads[0]) > 0.99                 # student layer-0 weight (padded K)
+    for i in (-2, -1):                                            # predictor head weight and bias
+        assert cos(b16.grads[i], f32.grads[i]) > 0.99, i
