@@ -194,8 +194,11 @@ class TeacherEngine(EngineBase):
             G = L["G"]
             dOut = G[:, O:]
             conv = L["conv"]
-            # G = mean-backward(dOut) over the transposed CSR (scale 1/deg of the destination)
-            K.csr_aggregate(N, O, g.rowptr_t, g.col_t, dOut, g.inv_deg, 1, G[:, :O])
+            # G = mean-backward(dOut) over the transposed CSR (scale 1/deg of the destination);
+            # SAGEConv's first layer needs no input gradient, and its weight gradients read dOut
+            # and the stored forward aggregate, so G is not formed there
+            if l > 0 or self.updated:
+                K.csr_aggregate(N, O, g.rowptr_t, g.col_t, dOut, g.inv_deg, 1, G[:, :O])
             wsb = K.gemm_tn_ws_bytes(dc, N, O, F)
             ws = self._ws("ws_tn", wsb)
             if self.updated:
