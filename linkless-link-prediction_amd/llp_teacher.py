@@ -135,6 +135,7 @@ class TeacherEngine(EngineBase):
                 P_, L = self.layers[l - 1], self.layers[l]
                 if L["F"] % 32 == 0 and (2 * P_["F"]) % 64 == 0 and (2 * L["O"]) % 64 == 0:
                     L["M"] = torch.empty(N, L["F"] // 8, dtype=torch.uint8, device=self.dev)
+        self._agg0_done = False   # mean aggregate of the input features (first SAGEConv layer) formed
         self.out_dim = self.layers[-1]["O"]
         self.h = torch.empty(N, self.out_dim, dtype=dt, device=self.dev)
         self._build_descs()
@@ -168,7 +169,11 @@ class TeacherEngine(EngineBase):
                 K.act_2d(YY[:, O:], self.h if last else nxt["X"], act=act, dropout=drop)
             else:
                 XA = L["XA"]
-                K.csr_aggregate(N, F, g.rowptr, g.col, XA[:, F:], None, 0, XA[:, :F])
+                # the first layer aggregates the raw features (no dropout before it,
+                # src/models.py:113-118): the same every step, so formed once
+                if l > 0 or not self._agg0_done:
+                    K.csr_aggregate(N, F, g.rowptr, g.col, XA[:, F:], None, 0, XA[:, :F])
+                    self._agg0_done = l == 0 or self._agg0_done
                 out = self.h if last else nxt["X"]
                 K.gemm_nt(K.operand(XA), K.operand(L["Wf"]), N, O, 2 * F, out, dc, bias=L["bias"], act=act,
                           aux=None if last else nxt.get("M"), dropout=drop)
