@@ -250,7 +250,8 @@ def main():
     ap.add_argument("--dominant-only", type=int, default=0,
                     help="run only the dominant kernel this many times (rocprofv3 --pmc passes) and exit")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
-                    help="replay the step from a captured hipGraph (N=1; --no-graph: eager launches)")
+                    help="replay the step from a captured hipGraph (N>1: graph segments with the RCCL "
+                         "all-reduces between them; --no-graph: eager launches)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
     ap.add_argument("--no-physics", action="store_true")
@@ -262,10 +263,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # (rehearsal of N ranks on fewer GPUs: ranks share devices round-robin, LLP_BENCH_BACKEND=gloo)
+    local_dev = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
+    backend = os.environ.get("LLP_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     import llp_data
     import llp_engine
@@ -315,7 +319,7 @@ def main():
     if opt.dominant_only:
         dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, opt.dominant_only)
         return
-    use_graph = opt.graph and world == 1
+    use_graph = opt.graph
     for s in range(opt.warmup):
         one_step(s, False)
     graph = None

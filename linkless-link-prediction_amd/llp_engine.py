@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 import llp_hip as K
+from contextlib import nullcontext as _nullctx
 
 # unique-node path: LLP_SEGMENT_FUSED=1 reduces the Hadamard backward straight onto the unique nodes
 # (llp_hadamard_bwd_segments, f32 accumulation, no [R1, H] row gradients).  It reads every pair row's
@@ -36,6 +37,12 @@ _SEGMENT_FUSED = os.environ.get("LLP_SEGMENT_FUSED", "0") == "1"
 # unique-node path: the unique count stays on the device (GEMM grids sized by the bound min(R1, N));
 # LLP_DEVICE_COUNT=0 reads it on the host instead (a sync per step, not capturable; A/B knob)
 _DEVICE_COUNT = os.environ.get("LLP_DEVICE_COUNT", "1") != "0"
+# minibatch step: weight-gradient (TN) GEMMs and the frozen teacher predictor run on a second HIP
+# stream beside the data-gradient GEMMs / Hadamard backward / student forward of the main stream
+# (fork/join by events, hipGraph-capturable); LLP_OVERLAP=0 runs everything on one stream (A/B knob)
+# bit mask: 1 teacher predictor beside the student forward; 2 the predictor's first-layer weight
+# gradient beside the Hadamard backward; 4 every other weight gradient beside its data gradient
+_OVERLAP = int(os.environ.get("LLP_OVERLAP", "0"))
 
 _DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
 
@@ -79,6 +86,56 @@ class _Linear:
         return self.Wc if self.Wc is not None else self.W
 
 
+class _SegmentedGraph:
+    """A multi-rank step as hipGraph segments with the collectives between them.
+
+    Capture cuts the graph at every collective (``cut``); ``replay`` launches the
+    segments on the current stream and runs each collective eagerly in between,
+    so RCCL (or gloo) orders itself against the segments by the stream, exactly
+    as in an eager step.  All segments share one memory pool."""
+
+    def __init__(self, dev):
+        self.items = []
+        self.stream = torch.cuda.Stream(device=dev)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.g = None
+        self._ctx = None
+
+    def begin(self):
+        self._ctx = torch.cuda.stream(self.stream)
+        self._ctx.__enter__()
+        self._open()
+
+    def _open(self):
+        self.g = torch.cuda.CUDAGraph()
+        # thread_local: the process group's own threads may query events meanwhile
+        self.g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
+
+    def _close(self):
+        self.g.capture_end()
+        self.items.append(self.g)
+        self.g = None
+
+    def cut(self, fn):
+        self._close()
+        self.items.append(fn)
+        self._open()
+
+    def end(self):
+        try:
+            if self.g is not None:
+                self._close()
+        finally:
+            self._ctx.__exit__(None, None, None)
+
+    def replay(self):
+        for it in self.items:
+            if isinstance(it, torch.cuda.CUDAGraph):
+                it.replay()
+            else:
+                it()
+
+
 class EngineBase:
     """Device state shared by the distillation and teacher engines: the flat
     f32 gradient buffer the parameters' ``.grad`` view, Adam state in the
@@ -103,6 +160,24 @@ class EngineBase:
         self._bufs = {}
         self._shadows = {}
         self._act_mask = {}     # id(activation buffer) -> its ReLU bit mask (or None)
+        self._side = None       # second stream (created on first use) for the overlapped kernels
+        self._forked = False
+        self._seg = None        # _SegmentedGraph while a multi-rank step is being captured
+
+    def _fork(self):
+        """Context that runs the enclosed launches on the side stream, after
+        everything already queued on the current (main) stream."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        self._side.wait_stream(torch.cuda.current_stream(self.dev))
+        self._forked = True
+        return torch.cuda.stream(self._side)
+
+    def _join(self):
+        """The main stream waits for the side stream's launches."""
+        if self._forked:
+            torch.cuda.current_stream(self.dev).wait_stream(self._side)
+            self._forked = False
 
     def _init_params(self, all_params, groups, optimizer):
         """``groups[i]``: clip group of all_params[i] (clip_grad_norm_ per module, Q9)."""
@@ -120,6 +195,7 @@ class EngineBase:
         assert self.param_groups_of == sorted(self.param_groups_of)
         self._tail_off = sum(p.numel() for p, gr in zip(self.all_params, self.param_groups_of) if gr == 0)
         self._pending = None
+        self._tail_issued = False
         self.optimizer = optimizer
         self._init_optimizer_state()
 
@@ -309,7 +385,11 @@ class EngineBase:
                        logit=logit)
         return A0, zacts
 
-    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop):
+    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop, overlap=False):
+        """overlap: each weight-gradient GEMM runs on the side stream (its inputs are
+        final, its output is only flat_grad) beside the next data-gradient GEMM; the
+        data gradients then take three buffers so none is overwritten while a side
+        GEMM still reads it.  The caller joins (``_join``) before clip + Adam."""
         dt, dc = self.dtype, self.dc
         if self.predictor_kind != "mlp":
             self._allreduce_tail_begin()
@@ -321,23 +401,39 @@ class EngineBase:
         ws = self._ws("ws_col", K.head_bwd_ws_bytes(R2, max(Hh, 1)))
         K.head_bwd(dlogit, Zl, R2, Hh, self.head.weight.data.view(-1), True, g, self.head.weight.grad.view(-1),
                    self.head.bias.grad, ws, alpha=alpha)
-        cur, nxt = "gP0", "gP1"
+        names = ["gP0", "gP1", "gP2"] if overlap & 4 else ["gP0", "gP1"]
+        k = 0
         for l in range(len(self.prd) - 1, -1, -1):
             lin = self.prd[l]
-            gcur = self._buf(cur, (R2, lin.out_f), dt)
+            gcur = self._buf(names[k % len(names)], (R2, lin.out_f), dt)
             A_in = K.operand(zacts[l - 1]) if l > 0 else A0
             wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
-            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
-                      colsum_a=lin.lin.bias.grad)
-            if l == 0:
-                self._allreduce_tail_begin()      # every predictor gradient is final here
-            gnext = self._buf(nxt, (R2, lin.in_f), dt)
+            late = bool(overlap & 2) and l == 0   # forked after the data-gradient GEMM below
+            if (overlap & 4) and l > 0 or (overlap & 4) and l == 0 and not late:
+                with self._fork():
+                    K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
+                              self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                    if l == 0:
+                        self._allreduce_tail_begin()      # issued after the side stream's last predictor GEMM
+            elif late:
+                pass
+            else:
+                K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
+                          self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                if l == 0:
+                    self._allreduce_tail_begin()      # every predictor gradient is final here
+            k += 1
+            gnext = self._buf(names[k % len(names)], (R2, lin.in_f), dt)
             if l > 0:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
                           act=K.ACT_RELU_BWD, aux=self._relu_aux(zacts[l - 1]), alpha=alpha)
             else:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
-            cur, nxt = nxt, cur
+            if late:
+                with self._fork():
+                    K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
+                              self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                    self._allreduce_tail_begin()
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
     def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
@@ -370,19 +466,38 @@ class EngineBase:
         """Start the SUM all-reduce of the predictor's gradients on RCCL's stream
         (async; it waits for the kernels already queued) so it overlaps the
         Hadamard / student (encoder) backward."""
-        if self.world > 1 and self._pending is None and self._tail_off < self.flat_grad.numel():
-            self._pending = dist.all_reduce(self.flat_grad[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
-                                            async_op=True)
+        if self.world > 1 and not self._tail_issued and self._tail_off < self.flat_grad.numel():
+            self._tail_issued = True
+            self._collective(self._tail_allreduce)
+
+    def _tail_allreduce(self):
+        self._pending = dist.all_reduce(self.flat_grad[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
+                                        async_op=True)
+
+    def _finish_allreduce(self, tail_issued):
+        if tail_issued:
+            if self._tail_off > 0:
+                dist.all_reduce(self.flat_grad[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
+            self._pending.wait()            # stream-ordered: no host block on RCCL
+            self._pending = None
+        else:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+
+    def _collective(self, fn):
+        """Run the collective ``fn`` now or, while a multi-rank step is being
+        captured (``_seg``), close the current graph segment and replay ``fn``
+        eagerly between the segments (RCCL is never inside a hipGraph)."""
+        if self._seg is None:
+            fn()
+        else:
+            self._seg.cut(fn)
 
     def _allreduce_and_update(self):
+        self._join()
         if self.world > 1:
-            if self._pending is not None:
-                if self._tail_off > 0:
-                    dist.all_reduce(self.flat_grad[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
-                self._pending.wait()            # stream-ordered: no host block on RCCL
-                self._pending = None
-            else:
-                dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+            tail = self._tail_issued
+            self._tail_issued = False
+            self._collective(lambda: self._finish_allreduce(tail))
         g = self.optimizer.param_groups[0]
         K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq)
         b1, b2 = g["betas"]
@@ -417,11 +532,12 @@ class DistillEngine(EngineBase):
     """
 
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
-                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True):
+                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, overlap=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
         # run the dropout-free student on unique nodes (step_minibatch); the unique
         # count stays on the device, so this path is hipGraph-capturable too
         self.dedup = bool(dedup) and os.environ.get("LLP_DEDUP", "1") != "0"
+        self.overlap = bool(overlap)   # second stream for the TN GEMMs / teacher predictor (step_minibatch)
         self._rows_dev = None      # int32 device count of the unique-node student (last step), or None
         self._rows_host = 0
         self.args = args
@@ -542,6 +658,14 @@ class DistillEngine(EngineBase):
         K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
         ia, ib = self._rows_index(B, C, n_lab)
         p_drop = float(a.dropout)
+        overlap = _OVERLAP if (self.overlap and self._seg is None) else 0
+        side_teacher = bool(overlap & 1) and kernel_events is None   # bench's timed launch runs alone
+        if side_teacher:
+            # a6 (frozen teacher predictor, src/main.py:104,106) depends only on the
+            # samples: it runs on the side stream beside the student forward
+            t_r = self._buf("t_r", (B * C,), torch.float32)
+            with self._fork():
+                self._teacher_forward(B * C, t_ia, t_ib, t_r)
 
         # ---- unique-node compaction: without dropout the student is a row-wise
         # function, so duplicate rows of x[this_target] give identical activations;
@@ -605,7 +729,10 @@ class DistillEngine(EngineBase):
 
         # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
         t_r = self._buf("t_r", (B * C,), torch.float32)
-        self._teacher_forward(B * C, t_ia, t_ib, t_r)
+        if side_teacher:
+            self._join()
+        else:
+            self._teacher_forward(B * C, t_ia, t_ib, t_r)
 
         # ---- a7-a9: fused LLP_D + LLP_R + BCE and d(loss)/d(logit) (src/main.py:107-130)
         if not (a.LLP_D or a.LLP_R):
@@ -617,7 +744,7 @@ class DistillEngine(EngineBase):
                    float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms, ws)
 
         # ---- a10: backward
-        dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
+        dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop, overlap=overlap)
         mlp = self.predictor_kind == "mlp"
         if dedup and _SEGMENT_FUSED:
             # Hadamard backward reduced straight onto the unique nodes (no [R1, H] row gradients)
@@ -636,7 +763,7 @@ class DistillEngine(EngineBase):
                 K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh, count=n_u)
             else:
                 dh = dh_rows
-        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u)
+        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
@@ -770,7 +897,24 @@ class DistillEngine(EngineBase):
         (e.g. ``anchors.copy_(node_perm[i*B:(i+1)*B])``) before each ``replay()``.
         Every random draw is keyed by device counters (Philox stream = 16 *
         step_ctr + offset; Adam's step), so each replay is a fresh step.  Call
-        after at least one eager step (kernels and buffers already loaded)."""
+        after at least one eager step (kernels and buffers already loaded).
+        With several ranks the step is captured as segments cut at the gradient
+        all-reduces, which run eagerly between them at replay (_SegmentedGraph);
+        the returned object has the same ``replay()``."""
+        if self.world > 1:
+            # RCCL stays outside the graphs: one segment per stretch between collectives
+            torch.cuda.synchronize(self.dev)
+            seg = _SegmentedGraph(self.dev)
+            seg.stream.wait_stream(torch.cuda.current_stream(self.dev))
+            self._seg = seg
+            try:
+                seg.begin()
+                self.step_minibatch(anchors, link_ids, pairs, **kw)
+            finally:
+                self._seg = None
+                seg.end()
+            torch.cuda.current_stream(self.dev).wait_stream(seg.stream)
+            return seg
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
@@ -808,24 +952,28 @@ class DistillEngine(EngineBase):
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _student_backward(self, dh, R1, target, acts, p_drop, count=None):
-        """count: int32 device row count (unique-node student) or None."""
+    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, overlap=False):
+        """count: int32 device row count (unique-node student) or None.  dh lives in
+        buffer 'gS0'.  overlap: weight-gradient GEMMs on the side stream, as in
+        _predictor_backward (three data-gradient buffers)."""
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
-        cur, nxt = "gS0", "gS1"
+        names = ["gS0", "gS1", "gS2"] if overlap & 4 else ["gS0", "gS1"]
+        k = 0
         for l in range(len(self.stu) - 1, -1, -1):
             lin = self.stu[l]
-            gcur = self._buf(cur, (R1, lin.out_f), dt)
+            gcur = self._buf(names[k % len(names)], (R1, lin.out_f), dt)
             A_in = K.operand(acts[l - 1], count=count) if l > 0 else K.operand(self.x, target, count=count)
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
             dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad
-            K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc,
-                      self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
-            if padded:   # the zero-padded input columns' gradient is dropped
-                lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
+            with self._fork() if overlap & 4 else _nullctx():
+                K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc,
+                          self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                if padded:   # the zero-padded input columns' gradient is dropped
+                    lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
             if l > 0:
-                gnext = self._buf(nxt, (R1, lin.in_f), dt)
+                k += 1
+                gnext = self._buf(names[k % len(names)], (R1, lin.in_f), dt)
                 K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
                           act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)
-                cur, nxt = nxt, cur

@@ -84,6 +84,94 @@ def _run(rank, world, dtype, port, out):
         dist.destroy_process_group()
 
 
+def _run_graph(rank, world, port, out, use_graph):
+    """Three steps of a 2-rank job: eager, or one eager step then two replays of
+    the segmented hipGraph (capture_minibatch at world > 1)."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "linkless-link-prediction_amd"))
+    import llp_engine
+    import models
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, F_, H, L, pairs, ei, x, t_h, anchors, links, args = _problem()
+    torch.manual_seed(3)
+    model = models.MLP(L, F_, H, H, 0.0).to(dev)
+    pred = models.LinkPredictor("mlp", H, H, 1, L, 0.0).to(dev)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
+    eng = llp_engine.DistillEngine(model, pred, tpred, x.to(dev), t_h.to(dev), ei[0].numpy(), ei[1].numpy(), N, args,
+                                   opt, dtype="bf16", seed=11)
+    B, P = anchors.numel(), links.numel()
+    b0, b1 = rank * B // world, (rank + 1) * B // world
+    p0, p1 = rank * P // world, (rank + 1) * P // world
+    pr = pairs.to(torch.int32).to(dev).contiguous()
+    a_dev = anchors[b0:b1].to(dev)
+    l_dev = links[p0:p1].to(dev)
+    kw = dict(b_offset=b0, p_offset=p0, B_total=B, P_total=P)
+    eng.begin_epoch()
+    eng.step_minibatch(a_dev, l_dev, pr, **kw)
+    if use_graph:
+        g = eng.capture_minibatch(a_dev, l_dev, pr, **kw)
+        out["segments"] = sum(isinstance(it, torch.cuda.CUDAGraph) for it in g.items)
+        for _ in range(2):
+            g.replay()
+    else:
+        for _ in range(2):
+            eng.step_minibatch(a_dev, l_dev, pr, **kw)
+    loss = eng.end_epoch(3 * P)
+    torch.cuda.synchronize()
+    if rank == 0:
+        out["loss"] = loss
+        out["params"] = [p.detach().cpu().numpy().copy() for p in list(model.parameters()) + list(pred.parameters())]
+        out["grads"] = [p.grad.detach().cpu().numpy().copy() for p in
+                        list(model.parameters()) + list(pred.parameters())]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _graph_worker(rank, world, port, q, use_graph):
+    out = {}
+    _run_graph(rank, world, port, out, use_graph)
+    if rank == 0:
+        q.put(out)
+
+
+def _two_ranks(use_graph):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, q, use_graph)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+def test_two_ranks_segmented_graph_matches_eager():
+    """BASELINE configs[4]: the multi-rank step replayed from hipGraph segments (the
+    all-reduces run between them) is bit-identical to eager multi-rank steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    eager = _two_ranks(False)
+    graph = _two_ranks(True)
+    assert graph["segments"] == 3     # before the predictor all-reduce, before the student's, clip + Adam
+    assert graph["loss"] == eager["loss"], (graph["loss"], eager["loss"])
+    import numpy as np
+    for a, b in zip(graph["grads"], eager["grads"]):
+        assert np.array_equal(a, b)
+    for a, b in zip(graph["params"], eager["params"]):
+        assert np.array_equal(a, b)
+
+
 def _worker(rank, world, dtype, port, q):
     out = {}
     _run(rank, world, dtype, port, out)
