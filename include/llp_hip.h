@@ -112,7 +112,9 @@ int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b,
  * variants give bit-identical results.  Returns the previous variant (or an
  * error code). */
 enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 2, LLP_GEMM_Q64 = 3, LLP_GEMM_Q64L = 4,
-                          LLP_GEMM_H128 = 5 /* 128 x 256 tiles, two workgroups per CU */ };
+                          LLP_GEMM_H128 = 5 /* 128 x 256 tiles, two workgroups per CU */,
+                          LLP_GEMM_Q64S1 = 6 /* q64 lean, waves 4-7 staggered by one phase */,
+                          LLP_GEMM_Q64S2 = 7 /* as 6, their DMA issued after the MFMAs */ };
 int llp_set_gemm_variant(int variant);
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).

@@ -588,7 +588,13 @@ __device__ __forceinline__ int q64_row(int chunk, int cr) {
 // drops its barrier — its operands were published by the barriers of phases 0
 // and 2, and chunk 3's refill target (A-half 1 of the other buffer) was last
 // read three barriers earlier.
-template <bool LEAN>
+// STAG (waves 4-7 only; waves 0-3 run the plain order): 1 = each phase runs
+// the PREVIOUS phase's MFMAs before its own LDS reads, so on every SIMD one
+// wave computes while its partner (waves w and w+4 share a SIMD) waits on its
+// reads; 2 = as 1, and the phase's DMA chunk is issued after the MFMAs.  The
+// reads and barriers stay where they are (LDS safety unchanged) and every
+// accumulator sees its MFMAs in the same k order: outputs are bit-identical.
+template <bool LEAN, int STAG>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
   constexpr int IMG_U4 = 256 * 8;                  // one operand image [256][8 chunks]
   constexpr int TILE_U4 = 2 * IMG_U4;              // A then B: 64 KiB
@@ -704,46 +710,58 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
       return;
     }
   }
+  const bool stag = STAG > 0 && wu >= 4;
+  const bool late_dma = STAG == 2 && wu >= 4;
   for (int64_t kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
     const uint4* sB = sA + IMG_U4;
+    // (stag: the previous phase's quadrant before this phase's reads)
     // phase 0: quadrant (0,0) needs chunks 0, 1 of this tile; younger: chunks 2, 3
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     barrier();
 #ifndef LLP_ABLATE_NOLOAD
-    if (more) issue_chunk(0, kt + 1);
+    if (more && !late_dma) issue_chunk(0, kt + 1);
 #endif
+    if (stag && kt > 0) mfma_q(1, 0);
+    if (more && late_dma) issue_chunk(0, kt + 1);
     read_a(sA, 0);
     read_b(sB, 0);
-    mfma_q(0, 0);
+    if (!stag) mfma_q(0, 0);
     // phase 1: (0,1) needs chunk 2; younger: chunk 3 (+ chunk 0 of the next tile)
     if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     barrier();
 #ifndef LLP_ABLATE_NOLOAD
-    if (more) issue_chunk(1, kt + 1);
+    if (more && !late_dma) issue_chunk(1, kt + 1);
 #endif
+    if (stag) mfma_q(0, 0);
+    if (more && late_dma) issue_chunk(1, kt + 1);
     read_b(sB, 1);
-    mfma_q(0, 1);
+    if (!stag) mfma_q(0, 1);
     // phase 2: (1,1) needs chunk 3; younger: chunks 0, 1 of the next tile
     if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
 #ifndef LLP_ABLATE_NOLOAD
-    if (more) issue_chunk(2, kt + 1);
+    if (more && !late_dma) issue_chunk(2, kt + 1);
 #endif
+    if (stag) mfma_q(0, 1);
+    if (more && late_dma) issue_chunk(2, kt + 1);
     read_a(sA, 1);
-    mfma_q(1, 1);
+    if (!stag) mfma_q(1, 1);
     // phase 3: (1,0), everything resident
     if (!LEAN) barrier();
     else __builtin_amdgcn_sched_barrier(0);
 #ifndef LLP_ABLATE_NOLOAD
-    if (more) issue_chunk(3, kt + 1);
+    if (more && !late_dma) issue_chunk(3, kt + 1);
 #endif
+    if (stag) mfma_q(1, 1);
+    if (more && late_dma) issue_chunk(3, kt + 1);
     if (!LEAN) read_b(sB, 0);
-    mfma_q(1, 0);
+    if (!stag) mfma_q(1, 0);
   }
+  if (stag && nk > 0) mfma_q(1, 0);   // the staggered half's last quadrant
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   epilogue_256(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
@@ -1097,17 +1115,19 @@ int g_gemm_variant = -1;
 }  // namespace
 
 // NT main-loop variant for the large-tile bf16 path (tuning / A-B in one
-// process): LLP_GEMM_PP53 (default), LLP_GEMM_PP42, LLP_GEMM_PIPE (the
-// lockstep NS-stage ring).  Env LLP_GEMM_VARIANT sets the initial value.
+// process): LLP_GEMM_Q64S1 (default: q64 lean with waves 4-7 staggered by one
+// phase), LLP_GEMM_Q64L, LLP_GEMM_Q64, LLP_GEMM_PP53, LLP_GEMM_PP42,
+// LLP_GEMM_PIPE, LLP_GEMM_H128, LLP_GEMM_Q64S2.  Env LLP_GEMM_VARIANT sets the
+// initial value.
 int llp_gemm_variant() {
   if (g_gemm_variant < 0) {
     const char* e = getenv("LLP_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : LLP_GEMM_Q64L;
+    g_gemm_variant = e ? atoi(e) : LLP_GEMM_Q64S1;
   }
   return g_gemm_variant;
 }
 extern "C" int llp_set_gemm_variant(int v) {
-  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_H128, "llp_set_gemm_variant: %d", v);
+  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_Q64S2, "llp_set_gemm_variant: %d", v);
   const int old = llp_gemm_variant();
   g_gemm_variant = v;
   return old;
@@ -1151,9 +1171,14 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   else if (variant == LLP_GEMM_PP42)
     hipLaunchKernelGGL((gemm_nt_bf16_pp<4, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (variant == LLP_GEMM_Q64)
-    hipLaunchKernelGGL(gemm_nt_bf16_q64<false>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    hipLaunchKernelGGL((gemm_nt_bf16_q64<false, 0>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (variant == LLP_GEMM_Q64L)
-    hipLaunchKernelGGL(gemm_nt_bf16_q64<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 0>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_Q64S1)
+    hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 1>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_Q64S2)
+    hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+
   else if (variant == LLP_GEMM_H128)
     hipLaunchKernelGGL(gemm_nt_bf16_h128, dim3((unsigned)tiles), dim3(HNT), 0, s, p);
   else if (pipe == 4 || pipe == 5)

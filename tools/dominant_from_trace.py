@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-KERNEL = "gemm_nt_bf16_q64<true>"
+KERNEL = "gemm_nt_bf16_q64<true, 1>"
 
 
 def main():

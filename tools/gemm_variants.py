@@ -16,8 +16,8 @@ import torch  # noqa: E402
 
 import llp_hip as K  # noqa: E402
 
-VARIANTS = (4, 5)
-NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean", 5: "h128"}
+VARIANTS = tuple(int(v) for v in os.environ.get("LLP_AB_VARIANTS", "4,6").split(","))
+NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean", 5: "h128", 6: "q64-stag", 7: "q64-stag-late-dma"}
 
 
 def main():
@@ -41,6 +41,7 @@ def main():
     bias = torch.randn(1024, device=dev, generator=g)
     aux = torch.randn(R1, 1024, device=dev, dtype=bf, generator=g)
     out = torch.empty(R1, 1024, device=dev, dtype=bf)
+    hr = torch.relu(h[:225334])     # activation-like operand (half zeros), as in the step
     outs = torch.empty(N0, 256, device=dev, dtype=bf)
     cases = {
         "L1 fwd gather 747214x1024x128": (lambda: K.gemm_nt(K.operand(x, idx), K.operand(W1), R1, 1024, 128, out, 1,
@@ -55,6 +56,9 @@ def main():
         "U fwd 225334x1024x1024": (lambda: K.gemm_nt(K.operand(h[:225334]), K.operand(W), 225334, 1024, 1024,
                                                      out[:225334], 1, bias=bias, act=K.ACT_RELU),
                                    2 * 225334 * 1024 * 1024, out),
+        "U fwd relu-data 225334x1024x1024": (lambda: K.gemm_nt(K.operand(hr), K.operand(W), 225334, 1024, 1024,
+                                                               out[:225334], 1, bias=bias, act=K.ACT_RELU),
+                                             2 * 225334 * 1024 * 1024, out),
         "SAGE L0 235868x256x256": (lambda: K.gemm_nt(K.operand(xa[:, :256]), K.operand(Wt[:, :256]), N0, 256, 256,
                                                      outs, 1, bias=bias[:256], act=K.ACT_RELU),
                                    2 * N0 * 256 * 256, outs),
@@ -73,7 +77,7 @@ def main():
         same = all(torch.equal(res[0], r) for r in res[1:])
         print(f"{name}: variants bit-identical: {same}", flush=True)
     if True:   # torch check of the L2 fwd on 4096 rows
-        L.llp_set_gemm_variant(5)
+        L.llp_set_gemm_variant(VARIANTS[-1])
         cases["L2 fwd 747214x1024x1024"][0]()
         torch.cuda.synchronize()
         ref = torch.relu(h[:4096].float() @ W.float().t() + bias)
