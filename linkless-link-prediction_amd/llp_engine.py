@@ -194,8 +194,8 @@ class EngineBase:
         # gradients are the tail of flat_grad, final once its backward is done
         assert self.param_groups_of == sorted(self.param_groups_of)
         self._tail_off = sum(p.numel() for p, gr in zip(self.all_params, self.param_groups_of) if gr == 0)
-        self._pending = None
-        self._tail_issued = False
+        self._works = []        # async all-reduce handles of this step's gradient buckets
+        self._issued = []       # their [lo, hi) ranges in flat_grad
         self.optimizer = optimizer
         self._init_optimizer_state()
 
@@ -466,22 +466,32 @@ class EngineBase:
         """Start the SUM all-reduce of the predictor's gradients on RCCL's stream
         (async; it waits for the kernels already queued) so it overlaps the
         Hadamard / student (encoder) backward."""
-        if self.world > 1 and not self._tail_issued and self._tail_off < self.flat_grad.numel():
-            self._tail_issued = True
-            self._collective(self._tail_allreduce)
+        self._allreduce_bucket(self._tail_off, self.flat_grad.numel())
 
-    def _tail_allreduce(self):
-        self._pending = dist.all_reduce(self.flat_grad[self._tail_off:], op=dist.ReduceOp.SUM, group=self.group,
-                                        async_op=True)
+    def _allreduce_bucket(self, lo, hi):
+        """Start the async SUM all-reduce of flat_grad[lo:hi] once those gradients
+        are final (stream order); the rest of flat_grad goes in _finish_allreduce."""
+        if self.world > 1 and hi > lo and all(hi <= a or lo >= b for a, b in self._issued):
+            self._issued.append((lo, hi))
+            self._collective(lambda: self._works.append(
+                dist.all_reduce(self.flat_grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
 
-    def _finish_allreduce(self, tail_issued):
-        if tail_issued:
-            if self._tail_off > 0:
-                dist.all_reduce(self.flat_grad[:self._tail_off], op=dist.ReduceOp.SUM, group=self.group)
-            self._pending.wait()            # stream-ordered: no host block on RCCL
-            self._pending = None
-        else:
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+    def _grad_slice(self, *params):
+        """[lo, hi) of the given parameters' gradients in flat_grad (contiguous)."""
+        base = self.flat_grad.data_ptr()
+        offs = [((p.grad.data_ptr() - base) // 4, (p.grad.data_ptr() - base) // 4 + p.numel()) for p in params]
+        lo, hi = min(o[0] for o in offs), max(o[1] for o in offs)
+        assert hi - lo == sum(p.numel() for p in params)
+        return lo, hi
+
+    def _finish_allreduce(self, rest):
+        """All-reduce the ranges not yet issued (``rest``), then make the stream
+        wait for every bucket (stream-ordered: no host block on RCCL)."""
+        for lo, hi in rest:
+            dist.all_reduce(self.flat_grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
+        for w in self._works:
+            w.wait()
+        self._works = []
 
     def _collective(self, fn):
         """Run the collective ``fn`` now or, while a multi-rank step is being
@@ -495,9 +505,15 @@ class EngineBase:
     def _allreduce_and_update(self):
         self._join()
         if self.world > 1:
-            tail = self._tail_issued
-            self._tail_issued = False
-            self._collective(lambda: self._finish_allreduce(tail))
+            rest, pos = [], 0
+            for lo, hi in sorted(self._issued):
+                if lo > pos:
+                    rest.append((pos, lo))
+                pos = max(pos, hi)
+            if pos < self.flat_grad.numel():
+                rest.append((pos, self.flat_grad.numel()))
+            self._issued = []
+            self._collective(lambda: self._finish_allreduce(rest))
         g = self.optimizer.param_groups[0]
         K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq)
         b1, b2 = g["betas"]
@@ -972,6 +988,8 @@ class DistillEngine(EngineBase):
                           self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
                 if padded:   # the zero-padded input columns' gradient is dropped
                     lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
+                if l > 0:    # this layer's gradients are final: all-reduce them under the next layers' GEMMs
+                    self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))
             if l > 0:
                 k += 1
                 gnext = self._buf(names[k % len(names)], (R1, lin.in_f), dt)
