@@ -361,21 +361,37 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const
   }
 }
 
-// out[n] (+)= sum_i slab[i][n]: 16 columns x 16 slab-lanes per block, fixed order.
+// out[n] (+)= sum_i slab[i][n] in a fixed order: SUM_CB columns x (256 / SUM_CB)
+// slab-lanes per block (one column and 256 lanes when H == 1), four independent
+// partial sums per lane so four loads are in flight, then an LDS tree over the
+// lanes.  (One column chain of ~1,000 dependent loads per 16 lanes took ~20 us.)
+constexpr int SUM_CB = 4;
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int64_t nslab, int64_t H,
                                                        float* __restrict__ out, int accumulate) {
-  __shared__ float red[16][17];
-  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int64_t n = (int64_t)blockIdx.x * 16 + cl;
-  float s = 0.f;
-  if (n < H)
-    for (int64_t i = sl; i < nslab; i += 16) s += slab[i * H + n];
-  red[sl][cl] = s;
+  __shared__ float red[256];
+  const int cb = H >= SUM_CB ? SUM_CB : 1;
+  const int nl = 256 / cb;
+  const int cl = threadIdx.x % cb, sl = threadIdx.x / cb;
+  const int64_t n = (int64_t)blockIdx.x * cb + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (n < H) {
+    int64_t i = sl;
+    for (; i + 3 * nl < nslab; i += 4 * nl) {
+      s0 += slab[i * H + n];
+      s1 += slab[(i + nl) * H + n];
+      s2 += slab[(i + 2 * nl) * H + n];
+      s3 += slab[(i + 3 * nl) * H + n];
+    }
+    for (; i < nslab; i += nl) s0 += slab[i * H + n];
+  }
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
+  for (int st = nl / 2; st > 0; st >>= 1) {
+    if (sl < st) red[sl * cb + cl] += red[(sl + st) * cb + cl];
+    __syncthreads();
+  }
   if (sl == 0 && n < H) {
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v += red[k][cl];
+    const float v = red[cl];
     out[n] = accumulate ? out[n] + v : v;
   }
 }
@@ -472,7 +488,8 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
     LLP_LAUNCH_CHECK();
   }
   if (dw) {
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, 16)), dim3(256), 0, s, slab, ns, H, dw, accumulate);
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, H >= SUM_CB ? SUM_CB : 1)), dim3(256), 0, s, slab, ns, H,
+                       dw, accumulate);
     LLP_LAUNCH_CHECK();
   }
   if (db) {
