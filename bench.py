@@ -414,6 +414,22 @@ def main():
         }
         if not opt.no_eval:
             res.update(evaluate(model, pred, data, dev))
+        if world == 1:
+            # per-rank cost of strong scaling: rank 0's shard of the same global batches at
+            # 8 ranks on this GPU (eager, no collective): the 8-GPU step is this + the all-reduce
+            R8 = 8
+            s0, s1, q0, q1 = 0, B_full // R8, 0, P_full // R8
+            shard = lambda s: eng.step_minibatch(node_perm[(s % n_full) * B_full + s0:(s % n_full) * B_full + s1],
+                                                 link_perm[(s % n_full) * P_full + q0:(s % n_full) * P_full + q1],
+                                                 pairs, b_offset=s0, p_offset=q0, B_total=B_full, P_total=P_full)
+            for s in range(3):
+                shard(s)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for s in range(20):
+                shard(3 + s)
+            torch.cuda.synchronize()
+            res["rank0_ms_per_step_at_8_ranks"] = (time.perf_counter() - t1) / 20 * 1e3
         if not opt.no_sage:
             res["sage_aggregate"] = sage_aggregate(data, dev)
             res["sage_teacher_step"] = sage_teacher_step(data, dev, opt.dtype)
