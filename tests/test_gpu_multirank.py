@@ -173,6 +173,84 @@ def test_two_ranks_segmented_graph_matches_eager():
         assert np.array_equal(a, b)
 
 
+def _run_fullbatch(rank, world, port, out):
+    """Two full-batch steps (train(), src/main.py:167-235: the student over all
+    nodes, PyG-dense negatives) of this rank's shard: the BASELINE configs[3] path."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "linkless-link-prediction_amd"))
+    import llp_engine
+    import models
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, F_, H, L, pairs, ei, x, t_h, anchors, links, args = _problem()
+    args = types.SimpleNamespace(**{**vars(args), "KD_RM": 0.0, "KD_LM": 0.0, "LLP_D": 10.0, "LLP_R": 0.01,
+                                    "True_label": 0.1, "margin": 0.2})
+    torch.manual_seed(3)
+    model = models.MLP(2, F_, H, H, 0.0).to(dev)
+    pred = models.LinkPredictor("mlp", H, H, 1, 2, 0.0).to(dev)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
+    eng = llp_engine.DistillEngine(model, pred, tpred, x.to(dev), t_h.to(dev), ei[0].numpy(), ei[1].numpy(), N, args,
+                                   opt, dtype="fp32", seed=13)
+    B, P = anchors.numel(), links.numel()
+    b0, b1 = rank * B // world, (rank + 1) * B // world
+    p0, p1 = rank * P // world, (rank + 1) * P // world
+    pr = pairs.to(torch.int32).to(dev).contiguous()
+    eng.begin_epoch()
+    for _ in range(2):
+        eng.step_fullbatch(anchors[b0:b1].to(dev), links[p0:p1].to(dev), pr, b_offset=b0, p_offset=p0, B_total=B,
+                           P_total=P, dense_negatives=True)
+    loss = eng.end_epoch(2 * P)
+    torch.cuda.synchronize()
+    if rank == 0:
+        out["loss"] = loss
+        out["params"] = [p.detach().cpu().numpy().copy() for p in list(model.parameters()) + list(pred.parameters())]
+        out["grads"] = [p.grad.detach().cpu().numpy().copy() for p in
+                        list(model.parameters()) + list(pred.parameters())]
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _fullbatch_worker(rank, world, port, q):
+    out = {}
+    _run_fullbatch(rank, world, port, out)
+    if rank == 0:
+        q.put(out)
+
+
+def test_two_ranks_fullbatch_equal_one_rank():
+    """Anchor / link batches of the full-batch step sharded over 2 ranks (every rank
+    draws the same dense negatives and keeps its columns) == the whole batch on one."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    single = {}
+    _run_fullbatch(0, 1, 0, single)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fullbatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    multi = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert abs(multi["loss"] - single["loss"]) <= 1e-4 * max(1.0, abs(single["loss"])), (multi["loss"], single["loss"])
+    for a, b in zip(multi["grads"], single["grads"]):
+        err = float(abs(a - b).max())
+        assert err <= 2e-3 * max(float(abs(b).max()), 1e-6) + 1e-7, err
+    for a, b in zip(multi["params"], single["params"]):
+        assert float((abs(a - b) <= 1e-4).mean()) > 0.99
+
+
 def _worker(rank, world, dtype, port, q):
     out = {}
     _run(rank, world, dtype, port, out)
