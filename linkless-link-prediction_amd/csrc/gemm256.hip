@@ -51,6 +51,7 @@ struct P256 {
   // the grid and head_part's row stride (head_ld) stay the host M
   const int32_t* m_dev;
   int64_t head_ld;
+  int nt_store;   // epilogue stores with the non-temporal hint (default; LLP_GEMM_NT_STORE=0 turns it off)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -422,7 +423,15 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
-    if (ok) *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+    if (ok) {
+      if (p.nt_store) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 vv = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p.C + row * p.ldc + col));
+      } else {
+        *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+      }
+    }
     if (p.mask_out) {
       // bit e of this chunk's byte = (bf16 output e > 0), the test RELU_BWD applies;
       // four consecutive lanes (one row, 32 columns) pack one 32-bit word
@@ -939,7 +948,15 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
-    if (ok) *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+    if (ok) {
+      if (p.nt_store) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 vv = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p.C + row * p.ldc + col));
+      } else {
+        *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
+      }
+    }
     if (p.mask_out) {
       // bit e of this chunk's byte = (bf16 output e > 0), the test RELU_BWD applies;
       // four consecutive lanes (one row, 32 columns) pack one 32-bit word
@@ -1152,6 +1169,8 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.M = M; p.N = N; p.K = K;
   p.m_dev = A->rows_dev;
   p.head_ld = M;
+  static const int nt_store_env = getenv("LLP_GEMM_NT_STORE") ? atoi(getenv("LLP_GEMM_NT_STORE")) : 1;
+  p.nt_store = nt_store_env;
   p.C = (bf16_t*)C; p.ldc = ldc;
   p.bias = bias; p.act = act; p.aux = (const bf16_t*)aux; p.ld_aux = ld_aux; p.alpha = alpha;
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;

@@ -12,7 +12,7 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libllp_hip.so")
+LIB_PATH = os.environ.get("LLP_LIB", os.path.join(HERE, "libllp_hip.so"))   # LLP_LIB: an alternative build (A/B)
 
 LLP_F32, LLP_BF16, LLP_MASK = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_RELU_BWD = 0, 1, 2
