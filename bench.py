@@ -255,6 +255,7 @@ def main():
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
     ap.add_argument("--no-physics", action="store_true")
+    ap.add_argument("--no-shard8", action="store_true", help="skip the 8-rank per-rank shard leg")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single GPU: run only rank 0's shard of an R-rank job (no collective) and report "
                          "its per-step time, to see the per-rank fixed costs of strong scaling")
@@ -414,7 +415,7 @@ def main():
         }
         if not opt.no_eval:
             res.update(evaluate(model, pred, data, dev))
-        if world == 1:
+        if world == 1 and not opt.no_shard8 and not opt.profile_kernels:
             # per-rank cost of strong scaling: rank 0's shard of the same global batches at
             # 8 ranks on this GPU (eager, no collective): the 8-GPU step is this + the all-reduce
             R8 = 8
