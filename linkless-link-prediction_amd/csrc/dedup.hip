@@ -11,6 +11,9 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+#include <stdlib.h>
+#include <string.h>
 
 namespace {
 
@@ -207,11 +210,192 @@ size_t sort_bytes(int64_t R) {
 }
 int64_t al256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
+// ---------------------------------------------------------------- counting path
+// Same outputs as the radix path, without the sort: per-node row counts
+// (integer atomics: exact), one exclusive scan of (present, count) packed in a
+// u64 gives every node its slot and its segment start, rows are scattered to
+// their segment through an atomic cursor (any order), then every segment is
+// sorted by row id, which restores row order: bit-identical to the stable sort.
+constexpr int SHORT_SEG = 32;   // segments up to this length sort in one thread's LDS row
+constexpr int LONG_LDS = 4096;  // longer ones: one block each, ranks counted in LDS up to this length
+
+struct PackCount {
+  __host__ __device__ uint64_t operator()(int32_t c) const {
+    return (c > 0 ? (1ull << 32) : 0ull) | (uint64_t)(uint32_t)c;
+  }
+};
+
+size_t scan64_bytes(int64_t N) {
+  size_t b = 0;
+  auto it = rocprim::make_transform_iterator((const int32_t*)nullptr, PackCount());
+  rocprim::exclusive_scan(nullptr, b, it, (uint64_t*)nullptr, (uint64_t)0, (size_t)N, rocprim::plus<uint64_t>());
+  return b;
+}
+
+__global__ void count_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ cnt) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < R) atomicAdd(&cnt[target[r]], 1);
+}
+
+__global__ void compact_count_kernel(int64_t N, int64_t R, const int32_t* __restrict__ cnt,
+                                     const uint64_t* __restrict__ pre, int32_t* __restrict__ uniq,
+                                     int32_t* __restrict__ seg_ptr, int32_t* __restrict__ uidx,
+                                     int32_t* __restrict__ cursor, int32_t* __restrict__ n_unique,
+                                     int32_t* __restrict__ n_long) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v >= N) return;
+  const int32_t c = cnt[v];
+  const uint64_t q = pre[v];
+  const int32_t slot = (int32_t)(q >> 32), start = (int32_t)(q & 0xFFFFFFFFull);
+  if (c > 0) {
+    uniq[slot] = (int32_t)v;
+    seg_ptr[slot] = start;
+    uidx[v] = slot;
+    cursor[v] = start;
+  }
+  if (v == N - 1) {
+    const int32_t U = slot + (c > 0 ? 1 : 0);
+    *n_unique = U;
+    seg_ptr[U] = (int32_t)R;
+    *n_long = 0;
+  }
+}
+
+__global__ void scatter_rows_kernel(int64_t R, const int32_t* __restrict__ target, const int32_t* __restrict__ uidx,
+                                    int32_t* __restrict__ cursor, int32_t* __restrict__ pos,
+                                    int32_t* __restrict__ seg_rows) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int32_t v = target[r];
+  pos[r] = uidx[v];
+  seg_rows[atomicAdd(&cursor[v], 1)] = (int32_t)r;
+}
+
+// one thread per segment: insertion sort of up to SHORT_SEG row ids in its own
+// LDS row; longer segments are listed for segsort_long_kernel
+__global__ __launch_bounds__(256) void segsort_short_kernel(const int32_t* __restrict__ n_unique,
+                                                            const int32_t* __restrict__ seg_ptr,
+                                                            int32_t* __restrict__ seg_rows,
+                                                            int32_t* __restrict__ long_list,
+                                                            int32_t* __restrict__ n_long) {
+  __shared__ int32_t buf[256][SHORT_SEG + 1];
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s >= *n_unique) return;
+  const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
+  if (len <= 1) return;
+  if (len > SHORT_SEG) {
+    long_list[atomicAdd(n_long, 1)] = (int32_t)s;
+    return;
+  }
+  int32_t* a = buf[threadIdx.x];
+  for (int i = 0; i < len; ++i) a[i] = seg_rows[b + i];
+  for (int i = 1; i < len; ++i) {
+    const int32_t x = a[i];
+    int j = i - 1;
+    while (j >= 0 && a[j] > x) {
+      a[j + 1] = a[j];
+      --j;
+    }
+    a[j + 1] = x;
+  }
+  for (int i = 0; i < len; ++i) seg_rows[b + i] = a[i];
+}
+
+// one block per long segment (grid-strided over the list): each row id's rank
+// = the number of smaller ids in the segment (ids are distinct); the segment is
+// read from LDS, or from a copy in `scratch` past LONG_LDS rows
+__global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __restrict__ n_long,
+                                                           const int32_t* __restrict__ long_list,
+                                                           const int32_t* __restrict__ seg_ptr,
+                                                           int32_t* __restrict__ seg_rows,
+                                                           int32_t* __restrict__ scratch) {
+  __shared__ int32_t buf[LONG_LDS];
+  const int32_t nl = *n_long;
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int32_t s = long_list[i];
+    const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
+    const bool in_lds = len <= LONG_LDS;
+    const int32_t* src = in_lds ? buf : scratch + b;
+    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
+      if (in_lds) buf[k] = seg_rows[b + k];
+      else scratch[b + k] = seg_rows[b + k];
+    }
+    __syncthreads();
+    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
+      const int32_t x = src[k];
+      int32_t rank = 0;
+      for (int32_t j = 0; j < len; ++j) rank += src[j] < x ? 1 : 0;
+      seg_rows[b + rank] = x;
+    }
+    __syncthreads();
+  }
+}
+
+bool use_counting() {
+  static const bool c = [] {
+    const char* e = getenv("LLP_DEDUP_SORT");
+    return !(e && strcmp(e, "radix") == 0);
+  }();
+  return c;
+}
+
 }  // namespace
 
-extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) {
+static int64_t radix_ws_bytes(int64_t num_nodes, int64_t R) {
   return 2 * al256((num_nodes + 1) * 4) + 3 * al256(R * 4) + al256((int64_t)scan_bytes(num_nodes)) +
          al256((int64_t)sort_bytes(R)) + 512;
+}
+static int64_t counting_ws_bytes(int64_t num_nodes, int64_t R) {
+  return 3 * al256((num_nodes + 1) * 4) + al256(num_nodes * 8) + 2 * al256(R * 4) + al256(256) +
+         al256((int64_t)scan64_bytes(num_nodes)) + 512;
+}
+
+extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) {
+  const int64_t a = radix_ws_bytes(num_nodes, R), b = counting_ws_bytes(num_nodes, R);
+  return a > b ? a : b;
+}
+
+static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
+                          int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace, hipStream_t s) {
+  char* w = reinterpret_cast<char*>(workspace);
+  int32_t* cnt = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  int32_t* uidx = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  int32_t* cursor = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  uint64_t* pre = reinterpret_cast<uint64_t*>(w);
+  w += al256(num_nodes * 8);
+  int32_t* long_list = reinterpret_cast<int32_t*>(w);
+  w += al256(R * 4);
+  int32_t* scratch = reinterpret_cast<int32_t*>(w);
+  w += al256(R * 4);
+  int32_t* n_long = reinterpret_cast<int32_t*>(w);
+  w += al256(256);
+  void* scan_tmp = w;
+  size_t scan_b = scan64_bytes(num_nodes);
+
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
+  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
+  hipLaunchKernelGGL(count_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt);
+  LLP_LAUNCH_CHECK();
+  auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
+  e = rocprim::exclusive_scan(scan_tmp, scan_b, it, pre, (uint64_t)0, (size_t)num_nodes, rocprim::plus<uint64_t>(),
+                              s);
+  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: scan");
+  hipLaunchKernelGGL(compact_count_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, R, cnt, pre,
+                     uniq, seg_ptr, uidx, cursor, n_unique, n_long);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, pos,
+                     seg_rows);
+  LLP_LAUNCH_CHECK();
+  const int64_t ubound = R < num_nodes ? R : num_nodes;
+  hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
+                     seg_rows, long_list, n_long);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows, scratch);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
 }
 
 extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
@@ -221,6 +405,8 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
   LLP_CHECK_ARG(num_nodes > 0 && num_nodes < (1ll << 31) && R > 0 && R < (1ll << 31), "llp_dedup_rows: sizes");
   LLP_CHECK_ARG(workspace_bytes >= llp_dedup_rows_workspace_bytes(num_nodes, R), "llp_dedup_rows: workspace");
   hipStream_t s = (hipStream_t)stream;
+  if (use_counting())
+    return dedup_counting(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, workspace, s);
   char* w = reinterpret_cast<char*>(workspace);
   int32_t* mark = reinterpret_cast<int32_t*>(w);
   w += al256((num_nodes + 1) * 4);

@@ -397,11 +397,19 @@ def test_clip_and_adam_match_oracle():
 
 
 # ------------------------------------------------------------------ unique-node compaction
-@pytest.mark.parametrize("N,R", [(50, 1000), (235868, 20000), (7, 7)])
-def test_dedup_rows_and_segment_sum(N, R):
+@pytest.mark.parametrize("N,R,hub", [(50, 1000, 0.0), (235868, 20000, 0.0), (7, 7, 0.0), (3000, 40000, 0.3)])
+def test_dedup_rows_and_segment_sum(N, R, hub):
+    """hub > 0: that fraction of the rows on node 7 and 2 % on each of nodes 11..15, so the
+    counting path's long-segment sorts run from LDS (~800 rows) and from scratch (12k rows)."""
     k = K()
     g = torch.Generator().manual_seed(R)
     target = torch.randint(0, N, (R,), generator=g, dtype=torch.int32)
+    if hub:
+        u = torch.rand(R, generator=g)
+        target[u < hub] = 7
+        for j, v in enumerate(range(11, 16)):
+            lo = hub + 0.02 * j
+            target[(u >= lo) & (u < lo + 0.02)] = v
     tg = target.to(DEV)
     uniq = torch.empty(R, dtype=torch.int32, device=DEV)
     pos = torch.empty(R, dtype=torch.int32, device=DEV)
