@@ -63,6 +63,10 @@ __device__ __forceinline__ void vm_wait(int64_t ahead) {   // 4 glds per wave pe
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
+// STAG (default 2; A/B knob LLP_TN_STAG): 1 = waves 4-7 run each stage's MFMAs one stage
+// late (after the next barrier, before that stage's reads); 2 = as 1 with their
+// DMA issued after those MFMAs.  Bit-identical (same per-accumulator order).
+template <int STAG>
 __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE_T];   // 128 KiB
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -158,6 +162,29 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
         (lds_s4*)((lds_char*)((__attribute__((address_space(3))) uint4*)img) + off));
   };
 
+  const bool stag = STAG > 0 && wu >= 4;
+  short8 fp[4];
+  short8 fq[2][4];
+  auto mfma_cs = [&]() {
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip)
+      accb[ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fp[ip], accb[ip], 0, 0, 0);
+  };
+  auto mfma_half = [&](int jh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int ip = 0; ip < 4; ++ip)
+        acc[4 * jh + jj][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[jh][jj], fp[ip], acc[4 * jh + jj][ip], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mfma_stage = [&]() {
+    if (do_cs) mfma_cs();
+    mfma_half(0);
+    mfma_half(1);
+  };
+
   if (mbeg < mend) {
     const int64_t nsteps = (mend - mbeg + TKM - 1) / TKM;
     for (int64_t s = 0; s < NS - 1 && s < nsteps; ++s) issue(s);
@@ -165,11 +192,13 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
       vm_wait(min(nsteps - 1, st + NS - 2) - st);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (st + NS - 1 < nsteps) issue(st + NS - 1);   // into the buffer of stage st-1
+      const bool late = STAG == 2 && wu >= 4;
+      if (!late && st + NS - 1 < nsteps) issue(st + NS - 1);   // into the buffer of stage st-1
       const char* sA = reinterpret_cast<const char*>(smem + (int)(st % NS) * STAGE_T);
       const char* sB = sA + IMG_U4 * 16;
       const int row0 = 8 * g + q4;    // k rows 8g..8g+3 and 8g+4..8g+7
-      short8 fp[4];
+      if (stag && st > 0) mfma_stage();   // the previous stage's products
+      if (late && st + NS - 1 < nsteps) issue(st + NS - 1);
 #pragma unroll
       for (int ip = 0; ip < 4; ++ip) {
         const int col = wp * 64 + ip * 16 + 4 * pp;
@@ -177,31 +206,20 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { fp[ip][e] = t0[e]; fp[ip][4 + e] = t1[e]; }
       }
-      if (do_cs) {
-#pragma unroll
-        for (int ip = 0; ip < 4; ++ip)
-          accb[ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fp[ip], accb[ip], 0, 0, 0);
-      }
+      if (!stag && do_cs) mfma_cs();
 #pragma unroll
       for (int jh = 0; jh < 2; ++jh) {
-        short8 fq[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const int col = wq * 128 + (4 * jh + jj) * 16 + 4 * pp;
           const short4_t t0 = tr_read(sB, row0, col), t1 = tr_read(sB, row0 + 4, col);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { fq[jj][e] = t0[e]; fq[jj][4 + e] = t1[e]; }
+          for (int e = 0; e < 4; ++e) { fq[jh][jj][e] = t0[e]; fq[jh][jj][4 + e] = t1[e]; }
         }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-          for (int ip = 0; ip < 4; ++ip)
-            acc[4 * jh + jj][ip] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[jj], fp[ip], acc[4 * jh + jj][ip], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        if (!stag) mfma_half(jh);
       }
     }
+    if (stag) mfma_stage();   // the last stage
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (do_cs && g == 0) {   // every row of the ones-product holds the column sums: take row 0
@@ -254,6 +272,12 @@ int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.splits = splits;
   p.ws = ws;
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  hipLaunchKernelGGL(gemm_tn_bf16_256, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  static const int stag = getenv("LLP_TN_STAG") ? atoi(getenv("LLP_TN_STAG")) : 2;
+  if (stag == 1)
+    hipLaunchKernelGGL(gemm_tn_bf16_256<1>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  else if (stag == 2)
+    hipLaunchKernelGGL(gemm_tn_bf16_256<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  else
+    hipLaunchKernelGGL(gemm_tn_bf16_256<0>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   return (int)hipGetLastError();
 }
