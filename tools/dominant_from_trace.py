@@ -30,6 +30,7 @@ def main():
                 durs.append(e - s)
     out = {"kernel": KERNEL + " (student layer-2 forward, 2nd NT launch of each step)",
            "launches": len(durs), "avg_ms": sum(durs) / len(durs) / 1e6 if durs else None,
+           "median_ms": sorted(durs)[len(durs) // 2] / 1e6 if durs else None,
            "min_ms": min(durs) / 1e6 if durs else None, "max_ms": max(durs) / 1e6 if durs else None,
            "source": path}
     print(json.dumps(out))
