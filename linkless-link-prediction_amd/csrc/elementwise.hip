@@ -240,26 +240,30 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* 
 __global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors,
                                                            int64_t max_chunks, const float* __restrict__ partial,
                                                            int n_groups, float* __restrict__ sumsq) {
-  // one block; per tensor the 256 threads reduce its chunk partials in a fixed
-  // tree (deterministic), thread 0 adds the tensor total to its group.
-  __shared__ double red[4];
+  // one block, one pass: thread i sums (in double) the chunk partials i, i+256, ... of
+  // every tensor into its group's register, then a fixed LDS tree per group
+  // (deterministic; was one block-wide reduction per tensor)
+  __shared__ double red[8][256];
   double gs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int t = 0; t < n_tensors; ++t) {
+    const int gidx = descs[t].group;
     const int64_t nch = (descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK;
     double ts = 0.0;
     for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) ts += (double)partial[t * max_chunks + c];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ts += __shfl_xor(ts, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ts;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int gidx = descs[t].group;
-      if (gidx >= 0 && gidx < 8) gs[gidx] += (red[0] + red[1]) + (red[2] + red[3]);
-    }
+    for (int k = 0; k < 8; ++k)
+      if (k == gidx) gs[k] += ts;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k][threadIdx.x] = gs[k];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + st];
     __syncthreads();
   }
-  if (threadIdx.x == 0)
-    for (int gidx = 0; gidx < n_groups; ++gidx) sumsq[gidx] = (float)gs[gidx];
+  if ((int)threadIdx.x < n_groups) sumsq[threadIdx.x] = (float)red[threadIdx.x][0];
 }
 
 __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float beta1, float beta2, float eps,
@@ -339,8 +343,11 @@ __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __rest
 
 // shadow_t[c, r] = param[r, c] in the shadow dtype, 64x64 tiles through LDS so
 // both the read and the write are row-coalesced.  Grid-strided over tiles.
-__global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __restrict__ descs) {
+__global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __restrict__ descs,
+                                                       int64_t* __restrict__ step) {
   __shared__ float tile[64][65];
+  // the Adam step counter advances here (after adam_kernel read it), saving a launch
+  if (step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *step += 1;
   const llp_tensor_desc d = descs[blockIdx.y];
   if (!d.shadow_t) return;
   const int64_t rows = d.rows, cols = d.cols;
@@ -500,9 +507,7 @@ extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, sumsq, max_norm, lr,
                      beta1, beta2, eps, (const int64_t*)step);
   LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs);
-  LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(increment_kernel, dim3(1), dim3(1), 0, s, step);
+  hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, step);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
@@ -513,7 +518,7 @@ extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, 
   hipLaunchKernelGGL(shadow_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream, descs);
   LLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream,
-                     descs);
+                     descs, (int64_t*)nullptr);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
