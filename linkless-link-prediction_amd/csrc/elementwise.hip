@@ -289,7 +289,10 @@ __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __rest
   float coef = 1.f;
   if (sumsq) {
     const float total = sqrtf(sumsq[d.group]);
-    coef = fminf(max_norm / (total + 1e-6f), 1.f);   // clip_grad_norm_ (clamped coef)
+    // clip_grad_norm_: clamp(max_norm / (total + 1e-6), max=1); torch.clamp propagates a
+    // NaN norm into every gradient (fminf would drop it and leave them unclipped)
+    const float q = max_norm / (total + 1e-6f);
+    coef = (q != q) ? q : fminf(q, 1.f);
   }
   const double t = (double)(*step + 1);
   const float bc1 = (float)(1.0 - pow((double)beta1, t));

@@ -44,6 +44,10 @@ _DEVICE_COUNT = os.environ.get("LLP_DEVICE_COUNT", "1") != "0"
 # gradient beside the Hadamard backward; 4 every other weight gradient beside its data gradient
 _OVERLAP = int(os.environ.get("LLP_OVERLAP", "0"))
 
+# dropout Philox keys (EngineBase._dropout): one per module, one stream per layer and step
+DROP_ENCODER, DROP_PREDICTOR, DROP_TEACHER_PRED = 0, 1, 2
+_MAX_DROPOUT_LAYERS = 15
+
 _DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
 
 
@@ -162,6 +166,7 @@ class EngineBase:
         self._act_mask = {}     # id(activation buffer) -> its ReLU bit mask (or None)
         self._side = None       # second stream (created on first use) for the overlapped kernels
         self._forked = False
+        self._side_reads = {}   # buffer name -> event after the side-stream launches that read it
         self._seg = None        # _SegmentedGraph while a multi-rank step is being captured
 
     def _fork(self):
@@ -178,6 +183,21 @@ class EngineBase:
         if self._forked:
             torch.cuda.current_stream(self.dev).wait_stream(self._side)
             self._forked = False
+        self._side_reads.clear()
+
+    def _side_read(self, name):
+        """Record that the side-stream launches queued so far read buffer ``name``:
+        the main stream waits for them (``_before_write``) before it overwrites it."""
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        self._side_reads[name] = ev
+
+    def _before_write(self, name):
+        """The main stream is about to write buffer ``name``: wait for the side-stream
+        launches that still read it (rotated data-gradient buffers, overlap bit 4)."""
+        ev = self._side_reads.pop(name, None)
+        if ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
 
     def _init_params(self, all_params, groups, optimizer):
         """``groups[i]``: clip group of all_params[i] (clip_grad_norm_ per module, Q9)."""
@@ -265,6 +285,10 @@ class EngineBase:
         numel = int(np.prod(shape))
         b = self._bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype:
+            if b is not None and self._side is not None:
+                # a side-stream launch may still use the old storage: the allocator
+                # must not hand it out again before that stream's work is done
+                b.record_stream(self._side)
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.dev)
             self._bufs[name] = b
         return b[:numel].view(*shape)
@@ -281,10 +305,19 @@ class EngineBase:
     def _ws(self, name, nbytes):
         return self._buf(name, (nbytes // 4 + 16,), torch.float32)
 
-    def _dropout(self, p, stream_off):
+    def _dropout(self, p, module, layer):
+        """Dropout draws of ``layer`` of ``module`` (DROP_ENCODER: the student MLP / the
+        teacher's GNN, DROP_PREDICTOR: the trained LinkPredictor, DROP_TEACHER_PRED: the
+        frozen teacher predictor).  Each module has its own Philox key and each layer its
+        own stream 16 * step_ctr + 1 + layer, so no two (module, layer) pairs and no two
+        steps share draws; the other seeds' streams (sampler, negatives) never meet them."""
         if p <= 0.0:
             return None
-        return K.Dropout(float(p), self.seed ^ 0xD0D0, self.step_ctr.data_ptr(), stream_off)
+        if not 0 <= layer < _MAX_DROPOUT_LAYERS:
+            raise ValueError(f"dropout on layer {layer}: at most {_MAX_DROPOUT_LAYERS} dropout layers per module "
+                             f"(one Philox stream each per step)")
+        key = (self.seed ^ 0xD0D0 ^ (int(module) << 40)) & 0xFFFFFFFFFFFFFFFF
+        return K.Dropout(float(p), key, self.step_ctr.data_ptr(), 1 + layer)
 
     def _fusable(self, K_in, N_out):
         return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0
@@ -370,13 +403,13 @@ class EngineBase:
                 parts = K.head_parts(lin.out_f)
                 hpart = self._buf("hpart", (parts, R2), torch.float32)
                 K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, self.head.weight.data.view(-1),
-                               hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, 5 + l))
+                               hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, DROP_PREDICTOR, l))
                 K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
                 fused = True
             else:
                 zm = self._mask(f"Zm{l}", R2, lin.out_f, lin.in_f, self.prd[l + 1].out_f) if not last else None
                 K.gemm_nt(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, dc, bias=lin.b, act=K.ACT_RELU,
-                          aux=zm, dropout=self._dropout(p_drop, 5 + l))
+                          aux=zm, dropout=self._dropout(p_drop, DROP_PREDICTOR, l))
                 self._act_mask[id(out)] = zm
             zacts.append(out)
             A = K.operand(out)
@@ -411,8 +444,11 @@ class EngineBase:
             late = bool(overlap & 2) and l == 0   # forked after the data-gradient GEMM below
             if (overlap & 4) and l > 0 or (overlap & 4) and l == 0 and not late:
                 with self._fork():
+                    # side-stream TN GEMMs have a split-K workspace of their own: the main
+                    # stream's TN GEMMs (student backward) must not share it
                     K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
-                              self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                              self._ws("ws_tn_side", wsb), colsum_a=lin.lin.bias.grad)
+                    self._side_read(names[k % len(names)])
                     if l == 0:
                         self._allreduce_tail_begin()      # issued after the side stream's last predictor GEMM
             elif late:
@@ -423,6 +459,7 @@ class EngineBase:
                 if l == 0:
                     self._allreduce_tail_begin()      # every predictor gradient is final here
             k += 1
+            self._before_write(names[k % len(names)])
             gnext = self._buf(names[k % len(names)], (R2, lin.in_f), dt)
             if l > 0:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
@@ -432,7 +469,8 @@ class EngineBase:
             if late:
                 with self._fork():
                     K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
-                              self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                              self._ws("ws_tn_side", wsb), colsum_a=lin.lin.bias.grad)
+                    self._side_read(names[(k - 1) % len(names)])
                     self._allreduce_tail_begin()
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
@@ -558,6 +596,10 @@ class DistillEngine(EngineBase):
         self._rows_host = 0
         self.args = args
         self.N = int(num_nodes)
+        # Philox streams per step under self.seed: the context sampler's walks 0..rw_step-1 and its
+        # negatives rw_step, randint negatives 15 (16 * step_ctr + offset)
+        if not 1 <= int(args.rw_step) < 15:
+            raise ValueError(f"rw_step={args.rw_step}: the context sampler has streams 0..14 per step (1 <= rw_step <= 14)")
 
         # ---------------- parameters
         self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
@@ -731,7 +773,7 @@ class DistillEngine(EngineBase):
             self._act_mask[id(out)] = hm
             K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.k_in, out, dc, bias=lin.b,
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
-                      dropout=None if last else self._dropout(p_drop, 1 + l))
+                      dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
             if timed:
                 ev[1].record()
                 kernel_events.append(ev)
@@ -844,7 +886,7 @@ class DistillEngine(EngineBase):
             self._act_mask[id(out)] = hm
             K.gemm_nt(A, K.operand(lin.Wcomp), N, lin.out_f, lin.k_in, out, dc, bias=lin.b,
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
-                      dropout=None if last else self._dropout(p_drop, 1 + l))
+                      dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
             acts.append(out)
             A = K.operand(out)
         h = acts[-1]
@@ -955,7 +997,7 @@ class DistillEngine(EngineBase):
             parts = K.head_parts(W.shape[0])
             tpart = self._buf("tpart", (parts, R), torch.float32)
             K.gemm_nt_head(K.operand(tin), K.operand(W), R, W.shape[0], W.shape[1], None, w2, tpart, bias=b,
-                           act=K.ACT_RELU, dropout=self._dropout(self.t_dropout, 9))
+                           act=K.ACT_RELU, dropout=self._dropout(self.t_dropout, DROP_TEACHER_PRED, 0))
             K.head_finish(parts, R, tpart, b2, prob=t_r)
             return
         A = K.operand(self.t_h, t_ia, self.t_h, t_ib)
@@ -963,7 +1005,7 @@ class DistillEngine(EngineBase):
         for l, (W, b) in enumerate(self.t_hidden):
             out = self._buf(f"T{l}", (R, W.shape[0]), dt)
             K.gemm_nt(A, K.operand(W), R, W.shape[0], W.shape[1], out, dc, bias=b, act=K.ACT_RELU,
-                      dropout=self._dropout(self.t_dropout, 9 + l))
+                      dropout=self._dropout(self.t_dropout, DROP_TEACHER_PRED, l))
             A = K.operand(out)
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
@@ -983,15 +1025,19 @@ class DistillEngine(EngineBase):
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
             dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad
-            with self._fork() if overlap & 4 else _nullctx():
+            side = bool(overlap & 4)
+            with self._fork() if side else _nullctx():
                 K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc,
-                          self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                          self._ws("ws_tn_side" if side else "ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                if side:
+                    self._side_read(names[k % len(names)])
                 if padded:   # the zero-padded input columns' gradient is dropped
                     lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
                 if l > 0:    # this layer's gradients are final: all-reduce them under the next layers' GEMMs
                     self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))
             if l > 0:
                 k += 1
+                self._before_write(names[k % len(names)])
                 gnext = self._buf(names[k % len(names)], (R1, lin.in_f), dt)
                 K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
                           act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)

@@ -40,7 +40,7 @@ import numpy as np
 import torch
 
 import llp_hip as K
-from llp_engine import EngineBase
+from llp_engine import DROP_ENCODER, EngineBase
 from llp_sage import GCNConv, Graph, SAGEConv_updated
 
 
@@ -150,7 +150,7 @@ class TeacherEngine(EngineBase):
         for l, L in enumerate(self.layers):
             F, O = L["F"], L["O"]
             last = l == nl - 1
-            drop = None if (last or not training) else self._dropout(self.p_drop, 1 + l)
+            drop = None if (last or not training) else self._dropout(self.p_drop, DROP_ENCODER, l)
             act = K.ACT_NONE if last else K.ACT_RELU
             nxt = None if last else self.layers[l + 1]
             if self.gcn:

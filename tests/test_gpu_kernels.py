@@ -360,40 +360,87 @@ def test_csr_mean_aggregate_fwd_bwd(dt, F_):
 
 
 # ------------------------------------------------------------------ clip + Adam
-def test_clip_and_adam_match_oracle():
+# (shape, group, shadows) per tensor.  "big": one tensor of 275 chunks (> 256 finalize
+# threads, so threads sum several chunk partials), eight clip groups, bf16 shadow and
+# transposed shadow (the transpose kernel also advances the step counter).
+_ADAM_CASES = {
+    "small": [((64, 32), 0, False), ((64,), 0, False), ((1, 64), 1, False), ((1,), 1, False)],
+    "big": [((1100, 1024), 0, True), ((1024,), 0, False), ((300, 257), 1, True), ((257,), 1, False),
+            ((5000,), 2, False), ((3,), 3, False), ((70, 70), 4, True), ((9000,), 5, False), ((1,), 6, False),
+            ((129, 65), 7, True)],
+}
+
+
+@pytest.mark.parametrize("case", sorted(_ADAM_CASES))
+@pytest.mark.parametrize("nan_group", [None, 1])
+def test_clip_and_adam_match_oracle(case, nan_group):
+    """grad_sumsq (chunk partials + one-pass finalize) + clip per group + Adam
+    against the oracle's clip_grad_norm_ / Adam (src/main.py:132-138); a NaN
+    gradient turns its group's clip coefficient into NaN, as torch.clamp does."""
     k = K()
-    g = torch.Generator().manual_seed(9)
-    shapes = [(64, 32), (64,), (1, 64), (1,)]
+    spec = _ADAM_CASES[case]
+    g = torch.Generator().manual_seed(9 + len(spec))
+    shapes = [sh for sh, _, _ in spec]
+    groups = [gr for _, gr, _ in spec]
+    n_groups = max(groups) + 1
     params = [torch.randn(*s, generator=g) for s in shapes]
     grads = [torch.randn(*s, generator=g) * 3 for s in shapes]
-    groups = [0, 0, 1, 1]
+    if nan_group is not None:
+        i_nan = groups.index(nan_group)
+        grads[i_nan].view(-1)[grads[i_nan].numel() // 2] = float("nan")
     dp = [p.to(DEV).clone() for p in params]
     dg = [x.to(DEV).clone() for x in grads]
     m = [torch.zeros_like(p) for p in dp]
     v = [torch.zeros_like(p) for p in dp]
+    sh, sht = [], []
     descs = []
     for i, p in enumerate(dp):
         rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
-        descs.append(k.TensorDesc(p.data_ptr(), dg[i].data_ptr(), m[i].data_ptr(), v[i].data_ptr(), None, None,
-                                  p.numel(), rows, cols, groups[i], 0))
+        s_ = st_ = None
+        if spec[i][2]:
+            s_ = torch.zeros(rows, cols, dtype=torch.bfloat16, device=DEV)
+            st_ = torch.zeros(cols, rows, dtype=torch.bfloat16, device=DEV)
+        sh.append(s_)
+        sht.append(st_)
+        descs.append(k.TensorDesc(p.data_ptr(), dg[i].data_ptr(), m[i].data_ptr(), v[i].data_ptr(),
+                                  k.ptr(s_), k.ptr(st_), p.numel(), rows, cols, groups[i],
+                                  k.LLP_BF16 if s_ is not None else 0))
+    max_numel = max(p.numel() for p in dp)
+    assert case != "big" or -(-max_numel // 4096) > 256
     dd = k.descs_to_device(descs, DEV)
-    sumsq = torch.zeros(2, device=DEV)
-    ws = torch.empty(k.grad_sumsq_ws_bytes(4, 64 * 32) // 4 + 16, device=DEV)
+    sumsq = torch.zeros(n_groups, device=DEV)
+    ws = torch.empty(k.grad_sumsq_ws_bytes(len(dp), max_numel) // 4 + 16, device=DEV)
     step = torch.zeros(1, dtype=torch.int64, device=DEV)
     adam = O.AdamState(params, lr=0.01)
     cur = [p.clone() for p in params]
     for it in range(3):
         gs = [x * (it + 1) for x in grads]
-        for i in range(4):
+        for i in range(len(dp)):
             dg[i].copy_(gs[i].to(DEV))
-        k.grad_sumsq(dd, 4, 64 * 32, 2, sumsq, ws)
-        k.adam_step(dd, 4, 64 * 32, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step)
-        c0, _ = O.clip_grad_norm(gs[:2])
-        c1, _ = O.clip_grad_norm(gs[2:])
-        cur = adam.step(cur, c0 + c1)
-    assert step.item() == 3
-    for a, b in zip(dp, cur):
-        assert torch.allclose(a.cpu(), b, rtol=1e-5, atol=1e-6)
+        k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws)
+        k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step)
+        assert step.item() == it + 1       # one increment per adam_step
+        clipped = []
+        for gr in range(n_groups):
+            idx = [i for i in range(len(dp)) if groups[i] == gr]
+            cg, _ = O.clip_grad_norm([gs[i] for i in idx])
+            ref = sum(float((gs[i].double() ** 2).sum()) for i in idx)   # exact; torch's f32 norm is ~3e-5 off here
+            if ref == ref:
+                assert abs(sumsq[gr].item() - ref) <= 1e-5 * ref + 1e-6, (gr, sumsq[gr].item(), ref)
+            else:
+                assert sumsq[gr].item() != sumsq[gr].item()
+            clipped.append(dict(zip(idx, cg)))
+        cg_all = [clipped[groups[i]][i] for i in range(len(dp))]
+        cur = adam.step(cur, cg_all)
+    for i, (a, b) in enumerate(zip(dp, cur)):
+        if nan_group is not None and groups[i] == nan_group:
+            assert torch.isnan(a).all() and torch.isnan(b).all(), i
+            continue
+        assert torch.allclose(a.cpu(), b, rtol=1e-5, atol=1e-6), i
+        if sh[i] is not None:
+            rows, cols = sh[i].shape
+            assert torch.equal(sh[i], a.view(rows, cols).to(torch.bfloat16))
+            assert torch.equal(sht[i], a.view(rows, cols).t().to(torch.bfloat16))
 
 
 # ------------------------------------------------------------------ unique-node compaction
