@@ -106,16 +106,24 @@ int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b,
                     float* prob, void* stream);
 
 /* Main-loop variant of the large-tile bf16 NT kernel (a tuning knob, process
- * wide, for A/B measurements in one process): K64 quadrant phases with
- * 128-B DMA lines (default), ping-pong wave groups with a 5-stage / 3-ahead or
- * 4-stage / 2-ahead ring of 64-B lines, or the lockstep 4-stage ring.  All
- * variants give bit-identical results.  Returns the previous variant (or an
- * error code). */
+ * wide, for A/B measurements in one process).  Default LLP_GEMM_PP8M: K64
+ * quadrant phases with 128-B DMA lines, each phase a LOAD and an MFMA segment
+ * between barriers with waves 4-7 one barrier behind waves 0-3 (ping-pong), and
+ * the epilogue compiled per call kind.  Others: the lockstep / staggered q64
+ * loops, ping-pong rings of 64-B lines, the lockstep 4-stage ring, half-height
+ * tiles.  All variants give bit-identical results.  Returns the previous
+ * variant (or an error code); llp_gemm_variant_name() names the current one's
+ * kernel (profiles: rocprofv3 kernel names). */
 enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 2, LLP_GEMM_Q64 = 3, LLP_GEMM_Q64L = 4,
                           LLP_GEMM_H128 = 5 /* 128 x 256 tiles, two workgroups per CU */,
                           LLP_GEMM_Q64S1 = 6 /* q64 lean, waves 4-7 staggered by one phase */,
-                          LLP_GEMM_Q64S2 = 7 /* as 6, their DMA issued after the MFMAs */ };
+                          LLP_GEMM_Q64S2 = 7 /* as 6, their DMA issued after the MFMAs */,
+                          LLP_GEMM_PP8 = 8 /* q64 phases as LOAD/MFMA segments, waves 4-7 one barrier behind */,
+                          LLP_GEMM_PP8D = 9 /* as 8, register-direct epilogue (no LDS staging) */,
+                          LLP_GEMM_PP8L = 10 /* as 9, stores of whole 128-B lines */,
+                          LLP_GEMM_PP8M = 11 /* as 8, epilogue specialised per call (bias/ReLU fwd, mask bwd) */ };
 int llp_set_gemm_variant(int variant);
+const char* llp_gemm_variant_name(void);
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
  * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then

@@ -56,6 +56,12 @@ struct P256 {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// hp + v . w over four columns in a fixed fma order
+template <typename W4>
+__device__ __forceinline__ float head_dot4(float hp, const float (&v)[4], const W4& w) {
+  return fmaf(v[3], w[3], fmaf(v[2], w[2], fmaf(v[1], w[1], fmaf(v[0], w[0], hp))));
+}
+
 __device__ __forceinline__ int64_t xcd_remap2(int64_t bid, int64_t nwg) {
   if (nwg < 8) return bid;
   const int64_t q = nwg / 8, r = nwg % 8;
@@ -337,10 +343,30 @@ __device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
 // Shared epilogue of the 256x256 kernels: alpha, bias, ReLU, dropout, fused
 // Linear(N,1) head partials, LDS-staged coalesced store (+ReLU-bwd mask).
 // smem must hold SMEM_U4_EPI uint4 + 4 KiB at smem + head_off_u4.
-template <int TMv, int NTHR>
+// Epilogue specialisations (compile-time flags instead of run-time branches per element):
+// EPI_ANY reads everything from P256; EPI_FWD_RELU / EPI_FWD_NONE: alpha 1, optional bias and
+// ReLU mask out, no dropout / head / aux; EPI_BWD_MASK: ReLU backward through a bit mask, alpha,
+// no bias / dropout / head.  The host picks the mode (epi_mode_of).
+constexpr int EPI_ANY = 0, EPI_FWD_RELU = 1, EPI_FWD_NONE = 2, EPI_BWD_MASK = 3, EPI_HEAD_RELU = 4;
+
+template <int TMv, int NTHR, int MODE = EPI_ANY>
 __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
                                            int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
-  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  const bool relu = MODE == EPI_FWD_RELU || MODE == EPI_HEAD_RELU || (MODE == EPI_ANY && p.act == LLP_ACT_RELU);
+  const bool drop = MODE == EPI_ANY && p.drop_p > 0.f;
+  const bool headw = MODE == EPI_HEAD_RELU || (MODE == EPI_ANY && p.head_w);
+  const bool rbwd = MODE == EPI_BWD_MASK || (MODE == EPI_ANY && p.act == LLP_ACT_RELU_BWD);
+  const bool fwd = MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_HEAD_RELU;
+  const float alpha = fwd ? 1.f : p.alpha;
+  const float* bias = MODE == EPI_BWD_MASK ? nullptr : p.bias;
+#ifdef LLP_ABLATE_NOEPI   // tools: time the kernel without its epilogue (outputs garbage)
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(acc[jn][im]));
+  return;
+#endif
+  const uint64_t dstream = drop ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
   uint4* stg = smem;
   float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -348,11 +374,17 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
     const int nl = wn * 64 + jn * 16 + g * 4;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     float hw[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias) {
+    if (bias) {
+      if (MODE != EPI_ANY && n0 + nl + 3 < p.N && ((uintptr_t)bias & 15) == 0) {
+        const float4_t b4 = *reinterpret_cast<const float4_t*>(bias + n0 + nl);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? p.bias[n0 + nl + r] : 0.f;
+        for (int r = 0; r < 4; ++r) bv[r] = b4[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? bias[n0 + nl + r] : 0.f;
+      }
     }
-    if (p.head_w) {
+    if (headw) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) hw[r] = (n0 + nl + r < p.N) ? p.head_w[n0 + nl + r] : 0.f;
     }
@@ -362,10 +394,10 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = p.alpha * acc[jn][im][r] + bv[r];
-        if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+        v[r] = fwd ? acc[jn][im][r] + bv[r] : alpha * acc[jn][im][r] + bv[r];
+        if (relu) v[r] = fmaxf(v[r], 0.f);
       }
-      if (p.drop_p > 0.f) {
+      if (drop) {
         // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
         // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
         const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
@@ -373,14 +405,15 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
       }
-      hp[im] += v[0] * hw[0] + v[1] * hw[1] + v[2] * hw[2] + v[3] * hw[3];
+      // explicit fma order: the head partial is bit-identical across kernel variants
+      if (headw) hp[im] = head_dot4(hp[im], v, hw);
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
       *dst = make_uint2(lo, hi);
     }
   }
-  if (p.head_w) {
+  if (headw) {
     float* part = reinterpret_cast<float*>(smem + head_off_u4);   // [4 wn][TMv rows]
 #pragma unroll
     for (int im = 0; im < 8; ++im) {
@@ -391,7 +424,7 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
     }
   }
   __syncthreads();
-  if (p.head_w && tid < TMv && m0 + tid < p.M) {
+  if (headw && tid < TMv && m0 + tid < p.M) {
     const float* part = reinterpret_cast<const float*>(smem + head_off_u4);
     const float s = part[tid] + part[TMv + tid] + part[2 * TMv + tid] + part[3 * TMv + tid];
     p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = s;
@@ -404,14 +437,14 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
     const int64_t row = m0 + rl, col = n0 + c * 8;
     const bool ok = row < p.M && col < p.N;
     uint4 v = stg[rl * EPI_ROW_U4 + c];
-    if (p.act == LLP_ACT_RELU_BWD) {
+    if (rbwd) {
       uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-      if (p.mask_in) {
+      if (MODE == EPI_BWD_MASK || p.mask_in) {
         const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           vv[e] = ((bits >> (2 * e)) & 1u ? (vv[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (vv[e] & 0xFFFF0000u) : 0u);
-      } else if (ok) {
+      } else if (MODE == EPI_ANY && ok) {
         const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
         const uint32_t av[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
@@ -423,7 +456,12 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
+#ifdef LLP_ABLATE_NOSTORE   // tools: the epilogue without its global stores
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    if (false) {
+#else
     if (ok) {
+#endif
       if (p.nt_store) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 vv = {v.x, v.y, v.z, v.w};
@@ -432,7 +470,7 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
         *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
       }
     }
-    if (p.mask_out) {
+    if ((MODE == EPI_ANY || MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE) && p.mask_out) {
       // bit e of this chunk's byte = (bf16 output e > 0), the test RELU_BWD applies;
       // four consecutive lanes (one row, 32 columns) pack one 32-bit word
       const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
@@ -449,9 +487,10 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
   }
 }
 
+template <int MODE = EPI_ANY>
 __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
                                              int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
-  epilogue_t<TM, NT2>(p, acc, smem, head_off_u4, m0, n0, tid, wm, wn, g, li);
+  epilogue_t<TM, NT2, MODE>(p, acc, smem, head_off_u4, m0, n0, tid, wm, wn, g, li);
 }
 
 // ---------------------------------------------------------------------------
@@ -776,6 +815,342 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
   epilogue_256(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
 }
 
+// ---------------------------------------------------------------------------
+// Register-direct epilogue of the 256x256 kernels (no LDS staging of the C
+// tile).  After the MFMAs lane (g, li) of wave (wm, wn) holds, per (jn, im),
+// four consecutive columns 16 jn + 4 g .. +3 of row 16 im + li.  One
+// v_permlane16_swap per packed dword exchanges lane rows 1<->0 and 3<->2
+// between the jn = 2q and 2q+1 registers, so every lane then holds EIGHT
+// consecutive bf16 columns, 32 q + 16 (g & 1) + 8 (g >> 1) .. +7: one 16-B
+// store each, 16 rows x 64 contiguous bytes per wave-instruction.  Values and
+// rounding are those of epilogue_t (bit-identical); bias / head weights for the
+// lane's 16 columns come from registers loaded before the main loop (bvec).
+__device__ __forceinline__ void store_c16(const P256& p, const uint32_t (&o)[4], bool ok, int64_t row, int64_t col) {
+#ifdef LLP_ABLATE_NOSTORE
+  asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+  return;
+#endif
+  if (!ok) return;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 vv = {o[0], o[1], o[2], o[3]};
+  if (p.nt_store)
+    __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p.C + row * p.ldc + col));
+  else
+    *reinterpret_cast<u32x4*>(p.C + row * p.ldc + col) = vv;
+}
+
+__device__ __forceinline__ void load_cols16(const float* v, int64_t N, int64_t c0, float4_t (&out)[4]) {
+  // columns c0 + 16 jn + 0..3 of v (v null -> 0); c0 % 4 == 0
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn) {
+    const int64_t c = c0 + 16 * jn;
+    if (v && c + 3 < N && ((uintptr_t)v & 15) == 0) {
+      out[jn] = *reinterpret_cast<const float4_t*>(v + c);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[jn][r] = (v && c + r < N) ? v[c + r] : 0.f;
+    }
+  }
+}
+
+template <bool LINES>
+__device__ __forceinline__ void epilogue_direct(const P256& p, float4_t (&acc)[4][8], const float4_t (&bvec)[4],
+                                                uint4* smem, int head_off_u4, int64_t m0, int64_t n0, int tid,
+                                                int wm, int wn, int g, int li) {
+#ifdef LLP_ABLATE_NOEPI
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(acc[jn][im]));
+  return;
+#endif
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  const int64_t cw = n0 + wn * 64;               // first column of this wave
+  float4_t hw[4];
+  load_cols16(p.head_w, p.N, cw + g * 4, hw);
+  float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool relu = p.act == LLP_ACT_RELU;
+  const bool drop = p.drop_p > 0.f;
+  // lane's store column (relative to cw) after the swaps of pair q: 32 q + cq
+  const int cq = 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+  for (int im = 0; im < 8; ++im) {
+    const int ml = wm * 128 + im * 16 + li;
+    const int64_t row = m0 + ml;
+    uint32_t d[4][2];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = p.alpha * acc[jn][im][r] + bvec[jn][r];
+        if (relu) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (drop) {
+        const uint4 x4 = philox4((uint64_t)(row * p.N + cw + jn * 16 + g * 4) >> 2, dstream, p.drop_seed);
+        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
+      }
+      hp[im] = head_dot4(hp[im], v, hw[jn]);
+      d[jn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      d[jn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    }
+    if (!p.C) continue;
+    uint32_t oq[2][4];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      uint32_t (&o)[4] = oq[q];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(d[2 * q][e], d[2 * q + 1][e], false, false);
+        o[e] = sw[0];
+        o[2 + e] = sw[1];
+      }
+      const int64_t col = cw + 32 * q + cq;
+      const bool ok = row < p.M && col < p.N;
+      if (p.act == LLP_ACT_RELU_BWD) {
+        if (p.mask_in) {
+          const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = ((bits >> (2 * e)) & 1u ? (o[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (o[e] & 0xFFFF0000u) : 0u);
+        } else if (ok) {
+          const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
+          const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
+            const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
+            o[e] = (k0 ? (o[e] & 0xFFFFu) : 0u) | (k1 ? (o[e] & 0xFFFF0000u) : 0u);
+          }
+        }
+      }
+      if (!LINES) store_c16(p, o, ok, row, col);
+      if (p.mask_out) {
+        // bit e of the byte for columns col..col+7 = (bf16 output e > 0); the row's four
+        // lanes (g = 0..3: columns +0, +16, +8, +24 of 32 q) form one 32-bit word
+        uint32_t byte = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          byte |= (__uint_as_float(o[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
+          byte |= (__uint_as_float(o[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
+        }
+        const uint32_t b1 = __shfl(byte, li + 16, 64), b2 = __shfl(byte, li + 32, 64), b3 = __shfl(byte, li + 48, 64);
+        if (g == 0 && ok)   // bytes in column order: g0 (+0), g2 (+8), g1 (+16), g3 (+24)
+          *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + ((cw + 32 * q) >> 3)) =
+              byte | (b2 << 8) | (b1 << 16) | (b3 << 24);
+      }
+    }
+    if (LINES) {
+      // full 128-B lines: lane li^8's pair-1 chunk moves here (DPP row_ror:8), so store A
+      // writes rows 0-7 of the 16 (lanes li < 8: own pair 0, li >= 8: row li-8's pair 1)
+      // and store B rows 8-15 -- 8 rows x 128 B per wave-instruction
+      uint32_t r1[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r1[e] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)oq[1][e], 0x128, 0xF, 0xF, false);
+      const bool lo = li < 8;
+      uint32_t sa[4], sb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sa[e] = lo ? oq[0][e] : r1[e];
+        sb[e] = lo ? r1[e] : oq[0][e];
+      }
+      const int64_t rbase = m0 + wm * 128 + im * 16;
+      const int64_t ra = rbase + (lo ? li : li - 8), rb = rbase + (lo ? li + 8 : li);
+      const int64_t ca = cw + (lo ? 0 : 32) + cq, cb = cw + (lo ? 32 : 0) + cq;
+      store_c16(p, sa, ra < p.M && ca < p.N, ra, ca);
+      store_c16(p, sb, rb < p.M && cb < p.N, rb, cb);
+    }
+  }
+  if (p.head_w) {
+    float* part = reinterpret_cast<float*>(smem + head_off_u4);   // [4 wn][256 rows]
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      float v = hp[im];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) part[wn * TM + wm * 128 + im * 16 + li] = v;
+    }
+    __syncthreads();
+    if (tid < TM && m0 + tid < p.M) {
+      const float sum = part[tid] + part[TM + tid] + part[2 * TM + tid] + part[3 * TM + tid];
+      p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = sum;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong variant of the q64 loop (cdna_hip_programming.md §5 "The 256²
+// 8-phase template"): every quadrant phase is a LOAD segment (counted vmcnt,
+// the phase's ds_reads, its DMA chunk of the next K-tile), a barrier, an MFMA
+// segment (lgkmcnt(0), 16 MFMAs at s_setprio 1) and a second barrier.  Waves
+// 4-7 (rows 128-255) run one barrier behind waves 0-3, so on every SIMD one
+// wave's MFMA segment coincides with its partner's LOAD segment and the two
+// never compete for the matrix pipe.  Same chunks, quadrant order, MFMA
+// operands and per-accumulator k order as q64 (bit-identical outputs).
+//
+// Chunk j of K-tile t+1 is issued in phase j of tile t.  With the groups one
+// barrier apart, the data a phase reads must be waited for (each wave's counted
+// vmcnt) in the PREVIOUS phase's LOAD segment, so the barriers ending both
+// groups' segments of that phase order it before every reader: chunks 0, 1 in
+// phase 3 of the previous tile, chunk 2 in phase 0, chunk 3 in phase 1.  WAR:
+// chunk j's refill (phase j of tile t+1) comes 4-5 phases after its last read.
+template <int DIRECT, int MODE>
+__global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
+  constexpr int IMG_U4 = 256 * 8;
+  constexpr int TILE_U4 = 2 * IMG_U4;
+  constexpr int SM_U4 = 2 * TILE_U4 > SMEM_U4_EPI + 256 ? 2 * TILE_U4 : SMEM_U4_EPI + 256;
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  int64_t m0, n0;
+  const bool dyn = p.m_dev != nullptr;
+  const int32_t mlive = dyn ? *p.m_dev : 0;
+  if (dyn ? !tile_256_host_interleaved(p, m0, n0) : !tile_256(p, m0, n0)) return;
+
+  const bf16_t* src[4][2];
+  int dst_row[4][2];
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row0 = q64_row(j, 16 * wu + 8 * i);
+      dst_row[j][i] = row0;
+      const int r = row0 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      if (j == 0 || j == 3) {
+        int64_t m = m0 + r;
+        m = m < p.M ? m : p.M - 1;
+        src[j][i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
+      } else {
+        int64_t n = n0 + r;
+        n = n < p.N ? n : p.N - 1;
+        src[j][i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
+      }
+    }
+  const uint32_t lds0 = lds_u32(smem);
+  auto issue_chunk = [&](int j, int64_t kt) {
+    const uint32_t base = lds0 + (uint32_t)((kt & 1) * TILE_U4 * 16) + ((j == 0 || j == 3) ? 0u : IMG_U4 * 16u);
+    const int64_t koff = kt * TK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(src[j][i] + koff, __builtin_amdgcn_readfirstlane(base + (uint32_t)(dst_row[j][i] * 128)));
+  };
+
+  const int wm = w >> 2, wn = w & 3;
+  float4_t bvec[4];     // bias of the lane's 16 epilogue columns, loaded under the main loop
+  if (DIRECT) load_cols16(p.bias, p.N, n0 + wn * 64 + g * 4, bvec);
+  float4_t acc[4][8];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nk = p.K / TK;
+  short8 fa[2][4];
+  short8 fb[2][2][2];
+  auto read_a = [&](const uint4* sA, int mh) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int im = 0; im < 4; ++im) {
+        const int r = wm * 128 + mh * 64 + im * 16 + li;
+        uint4 v = sA[r * 8 + ((kh * 4 + g) ^ (r & 7))];
+        fa[kh][im] = *reinterpret_cast<short8*>(&v);
+      }
+  };
+  auto read_b = [&](const uint4* sB, int nh) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) {
+        const int r = wn * 64 + nh * 32 + jn * 16 + li;
+        uint4 v = sB[r * 8 + ((kh * 4 + g) ^ (r & 7))];
+        fb[nh][kh][jn] = *reinterpret_cast<short8*>(&v);
+      }
+  };
+  auto mfma_q = [&](int mh, int nh) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int im = 0; im < 4; ++im)
+          acc[nh * 2 + jn][mh * 4 + im] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][kh][jn], fa[kh][im], acc[nh * 2 + jn][mh * 4 + im], 0,
+                                                      0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: the whole of K-tile 0; chunks 0 and 1 (phase 0) landed for every wave
+#pragma unroll
+  for (int j = 0; j < 4; ++j) issue_chunk(j, 0);
+  if (dyn) {
+    p.M = mlive < p.M ? (mlive > 0 ? mlive : 0) : p.M;
+    if (m0 >= p.M) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  barrier();
+  const bool grp1 = wu >= 4;
+  if (grp1) barrier();          // waves 4-7: one barrier behind from here on
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
+    const uint4* sB = sA + IMG_U4;
+    // phase 0, quadrant (0,0): wait chunk 2 of this tile (read in phase 1); younger: chunk 3
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    read_a(sA, 0);
+    read_b(sB, 0);
+    if (more) issue_chunk(0, kt + 1);
+    barrier();
+    mfma_q(0, 0);
+    barrier();
+    // phase 1, (0,1): wait chunk 3 (read in phase 2); younger: chunk 0 of the next tile
+    if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    read_b(sB, 1);
+    if (more) issue_chunk(1, kt + 1);
+    barrier();
+    mfma_q(0, 1);
+    barrier();
+    // phase 2, (1,1): nothing to wait for
+    read_a(sA, 1);
+    if (more) issue_chunk(2, kt + 1);
+    barrier();
+    mfma_q(1, 1);
+    barrier();
+    // phase 3, (1,0): operands in registers; wait chunks 0, 1 of the next tile; younger: chunk 2
+    if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (more) issue_chunk(3, kt + 1);
+    barrier();
+    mfma_q(1, 0);
+    barrier();
+  }
+  if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
+  if (DIRECT) {                 // no LDS staging: only the head partials use LDS (after this barrier)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (p.head_w) barrier();
+    epilogue_direct<DIRECT == 2>(p, acc, bvec, smem, 0, m0, n0, tid, wm, wn, g, li);
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_256<MODE>(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
+}
+
 template <int NS>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
   constexpr int LOOP_U4 = NS * PSTAGE_U4;
@@ -897,7 +1272,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
       }
-      hp[im] += v[0] * hw[0] + v[1] * hw[1] + v[2] * hw[2] + v[3] * hw[3];
+      hp[im] = head_dot4(hp[im], v, hw);
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
@@ -1129,6 +1504,18 @@ __global__ __launch_bounds__(HNT, 2) void gemm_nt_bf16_h128(P256 p) {
 
 int g_gemm_variant = -1;
 
+// the epilogue specialisation a call can use (epilogue_t)
+int epi_mode_of(const P256& p) {
+  if (p.drop_p > 0.f) return EPI_ANY;
+  if (p.head_w)
+    return p.act == LLP_ACT_RELU && p.alpha == 1.f && !p.aux && !p.mask_in && !p.mask_out ? EPI_HEAD_RELU : EPI_ANY;
+  if (!p.C) return EPI_ANY;
+  if (p.act == LLP_ACT_RELU && p.alpha == 1.f && !p.aux && !p.mask_in) return EPI_FWD_RELU;
+  if (p.act == LLP_ACT_NONE && p.alpha == 1.f && !p.aux && !p.mask_in && !p.mask_out) return EPI_FWD_NONE;
+  if (p.act == LLP_ACT_RELU_BWD && p.mask_in && !p.bias && !p.mask_out) return EPI_BWD_MASK;
+  return EPI_ANY;
+}
+
 }  // namespace
 
 // NT main-loop variant for the large-tile bf16 path (tuning / A-B in one
@@ -1139,12 +1526,21 @@ int g_gemm_variant = -1;
 int llp_gemm_variant() {
   if (g_gemm_variant < 0) {
     const char* e = getenv("LLP_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : LLP_GEMM_Q64S1;
+    g_gemm_variant = e ? atoi(e) : LLP_GEMM_PP8M;
   }
   return g_gemm_variant;
 }
+extern "C" const char* llp_gemm_variant_name(void) {
+  static const char* names[] = {"gemm_nt_bf16_256p<4>", "gemm_nt_bf16_pp<4, 2>", "gemm_nt_bf16_pp<5, 3>",
+                                "gemm_nt_bf16_q64<false, 0>", "gemm_nt_bf16_q64<true, 0>", "gemm_nt_bf16_h128",
+                                "gemm_nt_bf16_q64<true, 1>", "gemm_nt_bf16_q64<true, 2>", "gemm_nt_bf16_pp8<0, 0>",
+                                "gemm_nt_bf16_pp8<1, 0>", "gemm_nt_bf16_pp8<2, 0>", "gemm_nt_bf16_pp8<0, mode>"};
+  const int v = llp_gemm_variant();
+  return v >= 0 && v < (int)(sizeof(names) / sizeof(names[0])) ? names[v] : "?";
+}
+
 extern "C" int llp_set_gemm_variant(int v) {
-  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_Q64S2, "llp_set_gemm_variant: %d", v);
+  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_PP8M, "llp_set_gemm_variant: %d", v);
   const int old = llp_gemm_variant();
   g_gemm_variant = v;
   return old;
@@ -1197,6 +1593,24 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
     hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 1>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
   else if (variant == LLP_GEMM_Q64S2)
     hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_PP8)
+    hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_PP8M) {
+    const int mode = epi_mode_of(p);
+    if (mode == EPI_FWD_RELU)
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_FWD_RELU>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    else if (mode == EPI_FWD_NONE)
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_FWD_NONE>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    else if (mode == EPI_BWD_MASK)
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_BWD_MASK>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    else if (mode == EPI_HEAD_RELU)
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_HEAD_RELU>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  } else if (variant == LLP_GEMM_PP8D)
+    hipLaunchKernelGGL((gemm_nt_bf16_pp8<1, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  else if (variant == LLP_GEMM_PP8L)
+    hipLaunchKernelGGL((gemm_nt_bf16_pp8<2, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
 
   else if (variant == LLP_GEMM_H128)
     hipLaunchKernelGGL(gemm_nt_bf16_h128, dim3((unsigned)tiles), dim3(HNT), 0, s, p);

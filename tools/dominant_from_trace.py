@@ -1,14 +1,14 @@
 """Per-launch duration of bench.py's dominant kernel (student layer-2 forward
-GEMM = the 2nd gemm_nt_bf16_256p dispatch after each step's context_walk_kernel)
+GEMM = the 2nd NT GEMM dispatch after each step's context_walk_kernel)
 from a rocprofv3 --kernel-trace CSV, to check against bench.py's event timing.
 
-    python tools/dominant_from_trace.py gpurun_out/prof_r01/bench_kernel_trace.csv [out.json]
+    python tools/dominant_from_trace.py gpurun_out/prof_r02/bench_kernel_trace.csv [out.json] [kernel name prefix]
 """
 import csv
 import json
 import sys
 
-KERNEL = "gemm_nt_bf16_q64<true, 1>"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "gemm_nt_bf16_pp8"
 
 
 def main():

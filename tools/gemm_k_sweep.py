@@ -1,5 +1,6 @@
 """Split an NT GEMM's time into the K-proportional main loop and the per-tile
-constant (prologue + epilogue): time(K) = a + b*K at fixed M, N."""
+constant (prologue + epilogue): time(K) = a + b*K at fixed M, N, for each
+main-loop variant in LLP_AB_VARIANTS (interleaved in one process)."""
 import os
 import sys
 
@@ -9,8 +10,11 @@ import torch  # noqa: E402
 
 import llp_hip as K  # noqa: E402
 
+VARIANTS = tuple(int(v) for v in os.environ.get("LLP_AB_VARIANTS", "6").split(","))
+KS = tuple(int(v) for v in os.environ.get("LLP_KS", "1024,2048,4096").split(","))
 
-def t(fn, it=20):
+
+def t(fn, it=10):
     fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -22,30 +26,35 @@ def t(fn, it=20):
 
 
 def main():
+    L = K.lib()
     dev, bf = "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    M, N = 225_334, 1024
+    M, N = int(os.environ.get("LLP_M", 225_334)), 1024
     out = torch.empty(M, N, device=dev, dtype=bf)
-    aux = torch.randn(M, N, device=dev, dtype=bf, generator=g)
     bias = torch.randn(N, device=dev, generator=g)
-    for mode in ("plain", "bias+relu", "relu-bwd"):
-        res = []
-        for Kd in (256, 512, 1024, 2048):
-            A = torch.randn(M, Kd, device=dev, dtype=bf, generator=g)
-            W = (torch.randn(N, Kd, device=dev, generator=g) * 0.03).to(bf)
-            if mode == "plain":
-                fn = lambda: K.gemm_nt(K.operand(A), K.operand(W), M, N, Kd, out, 1)
-            elif mode == "bias+relu":
+    ops = {}
+    for Kd in KS:
+        A = torch.randn(M, Kd, device=dev, dtype=bf, generator=g)
+        W = (torch.randn(N, Kd, device=dev, generator=g) * 0.03).to(bf)
+        ops[Kd] = (A, W)
+    res = {(v, Kd): [] for v in VARIANTS for Kd in KS}
+    for rnd in range(5):
+        for Kd in KS:
+            A, W = ops[Kd]
+            for v in VARIANTS:
+                L.llp_set_gemm_variant(v)
                 fn = lambda: K.gemm_nt(K.operand(A), K.operand(W), M, N, Kd, out, 1, bias=bias, act=K.ACT_RELU)
-            else:
-                fn = lambda: K.gemm_nt(K.operand(A), K.operand(W), M, N, Kd, out, 1, act=K.ACT_RELU_BWD, aux=aux)
-            ms = min(t(fn) for _ in range(3))
-            res.append((Kd, ms))
-            print(f"{mode:10s} K={Kd:5d} {ms:.3f} ms {2 * M * N * Kd / ms / 1e9:.0f} TF", flush=True)
-        (k1, t1), (k2, t2) = res[1], res[3]
+                res[(v, Kd)].append(t(fn))
+    for v in VARIANTS:
+        pts = []
+        for Kd in KS:
+            ms = sorted(res[(v, Kd)])[2]
+            pts.append((Kd, ms))
+            print(f"variant {v} K={Kd:5d} {ms:.3f} ms {2 * M * N * Kd / ms / 1e9:.0f} TF", flush=True)
+        (k1, t1), (k2, t2) = pts[0], pts[-1]
         b = (t2 - t1) / (k2 - k1)
         a = t1 - b * k1
-        print(f"{mode:10s} per-call constant {a:.3f} ms; K=1024 main loop {b * 1024:.3f} ms "
+        print(f"variant {v}: per-call constant {a:.3f} ms; main loop {2 * M * N / b / 1e9:.0f} TF marginal "
               f"(constant = {100 * a / (a + b * 1024):.0f} % at K=1024)", flush=True)
 
 

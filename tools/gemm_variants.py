@@ -17,7 +17,8 @@ import torch  # noqa: E402
 import llp_hip as K  # noqa: E402
 
 VARIANTS = tuple(int(v) for v in os.environ.get("LLP_AB_VARIANTS", "4,6").split(","))
-NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean", 5: "h128", 6: "q64-stag", 7: "q64-stag-late-dma"}
+NAMES = {0: "pipe4", 1: "pp42", 2: "pp53", 3: "q64", 4: "q64-lean", 5: "h128", 6: "q64-stag", 7: "q64-stag-late-dma",
+         8: "pp8", 9: "pp8-direct", 10: "pp8-lines", 11: "pp8-mode"}
 
 
 def main():
@@ -43,6 +44,38 @@ def main():
     out = torch.empty(R1, 1024, device=dev, dtype=bf)
     hr = torch.relu(h[:225334])     # activation-like operand (half zeros), as in the step
     outs = torch.empty(N0, 256, device=dev, dtype=bf)
+    step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    drop = K.Dropout(0.5, 1234, step_ctr.data_ptr(), 3)
+    mask = torch.zeros(R1, 1024 // 8, dtype=torch.uint8, device=dev)
+    mask_in = torch.randint(0, 256, (R1, 1024 // 8), dtype=torch.uint8, device=dev, generator=g)
+    hw = torch.randn(1024, device=dev, generator=g)
+    hpart = torch.zeros(K.head_parts(1024), R2, device=dev)
+    # epilogue features (checked for bit-identity; not in the timing table)
+    extra = {
+        "L2 fwd relu + mask_out": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1, bias=bias,
+                                                     act=K.ACT_RELU, aux=mask), (out, mask)),
+        "L2 dgrad relu-bwd mask_in": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1,
+                                                        act=K.ACT_RELU_BWD, aux=mask_in, alpha=2.0), (out,)),
+        "P fwd dropout": (lambda: K.gemm_nt(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024, out[:R2], 1, bias=bias,
+                                            act=K.ACT_RELU, dropout=drop), (out,)),
+        "P fwd head": (lambda: K.gemm_nt_head(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024, out[:R2], hw, hpart,
+                                              bias=bias, act=K.ACT_RELU, dropout=drop), (out, hpart)),
+        "P fwd head, no C": (lambda: K.gemm_nt_head(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024, None, hw, hpart,
+                                                    bias=bias, act=K.ACT_RELU), (hpart,)),
+        "ragged 1000x264x1024": (lambda: K.gemm_nt(K.operand(h[:1000]), K.operand(W[:264]), 1000, 264, 1024,
+                                                   out[:1000, :264], 1, bias=bias, act=K.ACT_RELU), (out,)),
+    }
+    for name, (fn, outs_) in extra.items():
+        res = []
+        for v in VARIANTS:
+            L.llp_set_gemm_variant(v)
+            for o in outs_:
+                o.zero_()
+            fn()
+            torch.cuda.synchronize()
+            res.append([o.clone() for o in outs_])
+        same = all(all(torch.equal(a, b) for a, b in zip(res[0], r)) for r in res[1:])
+        print(f"{name}: variants bit-identical: {same}", flush=True)
     cases = {
         "L1 fwd gather 747214x1024x128": (lambda: K.gemm_nt(K.operand(x, idx), K.operand(W1), R1, 1024, 128, out, 1,
                                                             bias=bias, act=K.ACT_RELU), 2 * R1 * 1024 * 128, out),
