@@ -367,6 +367,20 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
   return;
 #endif
   const uint64_t dstream = drop ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  // ReLU-backward bit mask: this thread's 16 bytes (one per store below) are loaded
+  // first, so their latency hides under the staging work instead of under each store
+  constexpr int chunks_per_row = TN / 8;
+  constexpr int ITERS = TMv * chunks_per_row / NTHR;
+  const bool mask_rd = rbwd && (MODE == EPI_BWD_MASK || p.mask_in);
+  uint32_t mb[ITERS];
+  if (mask_rd) {
+#pragma unroll
+    for (int i = 0; i < ITERS; ++i) {
+      const int q = tid + i * NTHR;
+      const int64_t row = m0 + q / chunks_per_row, col = n0 + (q % chunks_per_row) * 8;
+      mb[i] = (row < p.M && col < p.N) ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
+    }
+  }
   uint4* stg = smem;
   float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -430,17 +444,17 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
     p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = s;
   }
   if (!p.C) return;
-  const int chunks_per_row = TN / 8;
-#pragma unroll 4
-  for (int q = tid; q < TMv * chunks_per_row; q += NTHR) {
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int q = tid + i * NTHR;
     const int rl = q / chunks_per_row, c = q % chunks_per_row;
     const int64_t row = m0 + rl, col = n0 + c * 8;
     const bool ok = row < p.M && col < p.N;
     uint4 v = stg[rl * EPI_ROW_U4 + c];
     if (rbwd) {
       uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-      if (MODE == EPI_BWD_MASK || p.mask_in) {
-        const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
+      if (mask_rd) {
+        const uint32_t bits = mb[i];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           vv[e] = ((bits >> (2 * e)) & 1u ? (vv[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (vv[e] & 0xFFFF0000u) : 0u);

@@ -84,6 +84,12 @@ def main():
         "L2 dgrad relu-bwd 747214x1024x1024": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1,
                                                                  act=K.ACT_RELU_BWD, aux=aux), 2 * R1 * 1024 * 1024,
                                                out),
+        "L2 dgrad mask-bwd 747214x1024x1024": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1,
+                                                                 act=K.ACT_RELU_BWD, aux=mask_in),
+                                               2 * R1 * 1024 * 1024, out),
+        "P fwd+head 603032x1024x1024": (lambda: K.gemm_nt_head(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024,
+                                                               out[:R2], hw, hpart, bias=bias, act=K.ACT_RELU),
+                                        2 * R2 * 1024 * 1024, out),
         "P fwd 603032x1024x1024": (lambda: K.gemm_nt(K.operand(h[:R2]), K.operand(W), R2, 1024, 1024, out[:R2], 1,
                                                      bias=bias, act=K.ACT_RELU), 2 * R2 * 1024 * 1024, out),
         "U fwd 225334x1024x1024": (lambda: K.gemm_nt(K.operand(h[:225334]), K.operand(W), 225334, 1024, 1024,
