@@ -124,6 +124,11 @@ enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 
                           LLP_GEMM_PP8M = 11 /* as 8, epilogue specialised per call (bias/ReLU fwd, mask bwd) */ };
 int llp_set_gemm_variant(int variant);
 const char* llp_gemm_variant_name(void);
+/* Main-loop variant of the bf16 weight-gradient (TN) kernel, process wide (A/B knob):
+ * 0 lockstep, 1 / 2 waves 4-7 staggered by one stage (2: their DMA late; default),
+ * 3 / 4 ping-pong LOAD / MFMA segments with waves 4-7 one barrier behind (one or two
+ * pairs per stage; measured slower).  All bit-identical.  Returns the previous one. */
+int llp_set_gemm_tn_variant(int variant);
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
  * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then

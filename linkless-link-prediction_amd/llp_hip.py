@@ -52,6 +52,7 @@ _SIGS = {
     "llp_head_finish": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_set_gemm_variant": (c_int, [c_int]),
     "llp_gemm_variant_name": (C.c_char_p, []),
+    "llp_set_gemm_tn_variant": (c_int, [c_int]),
     "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
     "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_vp, c_i64, c_vp]),
