@@ -127,7 +127,8 @@ const char* llp_gemm_variant_name(void);
 /* Main-loop variant of the bf16 weight-gradient (TN) kernel, process wide (A/B knob):
  * 0 lockstep, 1 / 2 waves 4-7 staggered by one stage (2: their DMA late; default),
  * 3 / 4 ping-pong LOAD / MFMA segments with waves 4-7 one barrier behind (one or two
- * pairs per stage; measured slower).  All bit-identical.  Returns the previous one. */
+ * pairs per stage; measured slower); + 8 places the blocks tile-major (round-1 order)
+ * instead of split-major.  All bit-identical.  Returns the previous one. */
 int llp_set_gemm_tn_variant(int variant);
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).

@@ -34,10 +34,8 @@ struct PTN {
   float* ws;
   float* ws_colsum;   // [splits][P] column sums of A (bias gradient), or NULL
   const int32_t* m_dev;   // device row count (llp_operand.rows_dev) or NULL
+  int zmajor;             // block -> (split, tile) order: split-major (default) or tile-major
 };
-
-typedef __attribute__((address_space(3))) short4_t lds_s4;
-typedef __attribute__((address_space(3))) char lds_char;
 
 __device__ __forceinline__ int64_t xcd_remap3(int64_t bid, int64_t nwg) {
   if (nwg < 8) return bid;
@@ -45,6 +43,23 @@ __device__ __forceinline__ int64_t xcd_remap3(int64_t bid, int64_t nwg) {
   const int64_t xcd = bid % 8, loc = bid / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
+
+// Block -> (tile, split).  Split-major: the blocks of one split -- every tile of the same
+// rows of A and B -- are consecutive, so xcd_remap3 places them on one XCD, whose L2 then
+// serves each staged row to all tiles (A rows to the Q/256 column tiles, B rows to the P/256
+// row tiles).  Tile-major (the old order) put the splits of one tile together: each row
+// came from beyond L2 once per tile.
+__device__ __forceinline__ void tn_block(int zmajor, int tiles, int splits, int64_t& tile, int64_t& z) {
+  const int lt = (int)xcd_remap3(blockIdx.x, (int64_t)tiles * splits);
+  const int d = zmajor ? tiles : splits;
+  const int hi = lt / d, lo = lt - hi * d;
+  tile = zmajor ? lo : hi;
+  z = zmajor ? hi : lo;
+}
+
+typedef __attribute__((address_space(3))) short4_t lds_s4;
+typedef __attribute__((address_space(3))) char lds_char;
+
 
 // swizzle of the 16-B chunk index within a 512-B image row (low 4 bits only):
 // T10 image (b); conflict-free for the transposed reads below.
@@ -73,8 +88,8 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
   const int g = lane >> 4, li = lane & 15;
   const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
   const int64_t tilesP = (p.P + TP - 1) / TP;
-  const int64_t lt = xcd_remap3(blockIdx.x, tilesP * tilesQ * p.splits);
-  const int64_t tile = lt / p.splits, z = lt % p.splits;
+  int64_t tile, z;
+  tn_block(p.zmajor, (int)(tilesP * tilesQ), (int)p.splits, tile, z);
   const int64_t p0 = (tile / tilesQ) * TP, q0 = (tile % tilesQ) * TQ;
   if (p.m_dev) {   // live rows from the device count; the grid (splits) is the host M's
     const int64_t c = *p.m_dev;
@@ -268,8 +283,8 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_pp(PTN p) {
   const int g = lane >> 4, li = lane & 15;
   const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
   const int64_t tilesP = (p.P + TP - 1) / TP;
-  const int64_t lt = xcd_remap3(blockIdx.x, tilesP * tilesQ * p.splits);
-  const int64_t tile = lt / p.splits, z = lt % p.splits;
+  int64_t tile, z;
+  tn_block(p.zmajor, (int)(tilesP * tilesQ), (int)p.splits, tile, z);
   const int64_t p0 = (tile / tilesQ) * TP, q0 = (tile % tilesQ) * TQ;
   if (p.m_dev) {
     const int64_t c = *p.m_dev;
@@ -452,9 +467,10 @@ int g_tn_variant = -1;   // main-loop variant of the TN kernel (LLP_TN_STAG; llp
 }
 
 // 0 lockstep, 1 waves 4-7 staggered by one stage, 2 = 1 with late DMA (default),
-// 3 ping-pong, 4 ping-pong with two LOAD/MFMA pairs per stage (3, 4: measured slower)
+// 3 ping-pong, 4 ping-pong with two LOAD/MFMA pairs per stage (3, 4: measured slower);
+// + 8: tile-major block order (the round-1 placement) instead of split-major
 extern "C" int llp_set_gemm_tn_variant(int v) {
-  LLP_CHECK_ARG(v >= 0 && v <= 4, "llp_set_gemm_tn_variant: %d", v);
+  LLP_CHECK_ARG(v >= 0 && v <= 12 && (v & 7) <= 4, "llp_set_gemm_tn_variant: %d", v);
   const int old = g_tn_variant >= 0 ? g_tn_variant : 2;
   g_tn_variant = v;
   return old;
@@ -486,7 +502,9 @@ int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.splits = splits;
   p.ws = ws;
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  const int stag = g_tn_variant >= 0 ? g_tn_variant : (g_tn_variant = getenv("LLP_TN_STAG") ? atoi(getenv("LLP_TN_STAG")) : 2);
+  const int var = g_tn_variant >= 0 ? g_tn_variant : (g_tn_variant = getenv("LLP_TN_STAG") ? atoi(getenv("LLP_TN_STAG")) : 2);
+  const int stag = var & 7;
+  p.zmajor = (var & 8) ? 0 : 1;
   if (stag == 3)
     hipLaunchKernelGGL(gemm_tn_bf16_pp<false>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   else if (stag == 4)
