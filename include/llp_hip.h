@@ -227,15 +227,18 @@ int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr
                          const int32_t* u_dev, void* stream);
 int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
 /* Backward of the predictor input h[i] * h[j] (src/main.py:102-103,126) reduced
- * straight onto the unique nodes: dh[u] = sum over the target rows of node u
- * (seg_ptr / rows from llp_dedup_rows, row order) of each row's Hadamard
- * gradient, f32 accumulation, one write per node.  Row layouts as
- * llp_hadamard_bwd_blocks; h is the unique-node table [U, H], pos maps target
- * rows to it; drow (dZ = NULL) is the 'inner' predictor's per-pair scalar. */
+ * straight onto the unique nodes, bit-identical to llp_hadamard_bwd_blocks (hidx =
+ * pos) followed by llp_segment_sum_rows: dh[u] = sum over the target rows of node u
+ * (seg_ptr / rows from llp_dedup_rows, row order) of each row's Hadamard gradient
+ * as the row kernel would store it, f32 accumulation, one write per node, without
+ * the [R1, H] row buffer.  anchor_rows: caller-owned [B, H] scratch (compute dtype)
+ * for the anchors' context sums.  Row layouts as llp_hadamard_bwd_blocks; h is the
+ * unique-node table [U, H], pos maps target rows to it; drow (dZ = NULL) is the
+ * 'inner' predictor's per-pair scalar. */
 int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
                               const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos, const void* dZ,
-                              const float* drow, const void* h, void* dh, int64_t ld_dh, const int32_t* u_dev,
-                              void* stream);
+                              const float* drow, const void* h, void* anchor_rows, void* dh, int64_t ld_dh,
+                              const int32_t* u_dev, void* stream);
 
 /* Generic scatter form (full-batch train(), src/main.py:173-214, where rows of
  * h repeat): dh[ia[r]] += dZ[r]*h2[ib[r]],  dh[ib[r]] += dZ[r]*h1[ia[r]]

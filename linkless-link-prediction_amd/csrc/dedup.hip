@@ -111,18 +111,22 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, 
   *reinterpret_cast<uint4*>(out + orow * ldo + c * E) = V8<T>::pack(acc);
 }
 
-// Fused Hadamard backward + per-node reduction (the unique-node student path).
-// The predictor input of pair row z is h[a_z] * h[b_z]; its gradient dZ[z]
-// reaches a_z as dZ[z] * h[b_z] and b_z as dZ[z] * h[a_z].  Target rows (the
-// student's gathered layout, src/main.py:95) are [B anchors x (1 + C)] then
-// [L2 sources | L2 destinations]; pair rows are [B x C anchor-context] then
-// [L2 links].  For unique node u this sums, over its target rows in row order,
-//   anchor row b*C1      : sum_cc dZ[b*C+cc] * h[pos[b*C1+1+cc]]
-//   context row b*C1+1+cc: dZ[b*C+cc] * h[pos[b*C1]]
-//   source row base+i    : dZ[B*C+i] * h[pos[base+L2+i]]
-//   dest row base+L2+i   : dZ[B*C+i] * h[pos[base+i]]
-// in f32 registers and writes dh[u] once (drow: 'inner' predictor, dZ[z] = drow[z]
-// broadcast).  One thread per 16-B column chunk, 256/cpr nodes per block.
+// Fused Hadamard backward + per-node reduction (the unique-node student path),
+// bit-identical to llp_hadamard_bwd_blocks + llp_segment_sum_rows.  The predictor
+// input of pair row z is h[a_z] * h[b_z]; its gradient dZ[z] reaches a_z as
+// dZ[z] * h[b_z] and b_z as dZ[z] * h[a_z].  Target rows (the student's gathered
+// layout, src/main.py:95) are [B anchors x (1 + C)] then [L2 sources | L2
+// destinations]; pair rows are [B x C anchor-context] then [L2 links].
+//   pass 1 (anchor rows): arow[b] = sum_cc dZ[b*C+cc] * h[pos[b*C1+1+cc]]  (f32 fma
+//          chain in cc order, rounded once to the compute dtype)
+//   pass 2 (per node u, its target rows in row order, f32 sum of each row's value
+//          rounded to the compute dtype exactly as the row kernel stores it):
+//          anchor row b*C1 -> arow[b]; context row b*C1+1+cc -> dZ[b*C+cc] * h[pos[b*C1]];
+//          source row base+i -> dZ[B*C+i] * h[pos[base+L2+i]]; destination row
+//          base+L2+i -> dZ[B*C+i] * h[pos[base+i]].
+// Against the two-kernel path this drops the [R1, H] row-gradient buffer: its write
+// and its read (2 x 1.5 GB at the collab shape) for a second read of the context
+// pairs' dZ rows.  drow: the 'inner' predictor's per-pair scalar (dZ = NULL).
 template <typename T>
 __device__ __forceinline__ void load16(const T* p, float* v) {
   const uint4 r = *reinterpret_cast<const uint4*>(p);
@@ -139,11 +143,52 @@ __device__ __forceinline__ void load16(const T* p, float* v) {
 }
 
 template <typename T>
+__device__ __forceinline__ float round_to(float x) {
+  if constexpr (sizeof(T) == 2) return __uint_as_float(((uint32_t)f2bf(x)) << 16);
+  else return x;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void hadamard_anchor_rows_kernel(int64_t B, int64_t C, int64_t H,
+                                                                   const T* __restrict__ dZ,
+                                                                   const float* __restrict__ drow,
+                                                                   const T* __restrict__ h,
+                                                                   const int32_t* __restrict__ pos,
+                                                                   T* __restrict__ arow) {
+  constexpr int E = V8<T>::E;
+  const int cpr = (int)(H / E);
+  const int apb = 256 / cpr;
+  const int c = threadIdx.x % cpr, slot = threadIdx.x / cpr;
+  const int64_t b = (int64_t)blockIdx.x * apb + slot;
+  if (slot >= apb || b >= B) return;
+  const int64_t col = (int64_t)c * E, C1 = C + 1;
+  const int32_t* pc = pos + b * C1 + 1;
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+#pragma unroll 4
+  for (int64_t cc = 0; cc < C; ++cc) {
+    const int64_t z = b * C + cc;
+    float d[E], hc[E];
+    if (drow) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) d[i] = drow[z];
+    } else {
+      load16<T>(dZ + z * H + col, d);
+    }
+    load16<T>(h + (int64_t)pc[cc] * H + col, hc);
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] = fmaf(d[i], hc[i], acc[i]);
+  }
+  *reinterpret_cast<uint4*>(arow + b * H + col) = V8<T>::pack(acc);
+}
+
+template <typename T>
 __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
     int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ rows, const int32_t* __restrict__ pos, const T* __restrict__ dZ,
-    const float* __restrict__ drow, const T* __restrict__ h, T* __restrict__ dh, int64_t ldo,
-    const int32_t* __restrict__ u_dev) {
+    const float* __restrict__ drow, const T* __restrict__ h, const T* __restrict__ arow, T* __restrict__ dh,
+    int64_t ldo, const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
   const int cpr = (int)(H / E);
   const int spb = 256 / cpr;
@@ -152,40 +197,65 @@ __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
   if (u_dev && (int64_t)*u_dev < U) U = *u_dev;
   if (slot >= spb || u >= U) return;
   const int64_t C1 = C + 1, base = B * C1, col = (int64_t)c * E;
+  // row r -> (first operand row, h row of the partner, is-anchor); branch-free so the
+  // loads of two rows issue together (the partner of an anchor row is unused: row 0)
+  struct Src { const T* a; const T* hp; float s; bool anchor; };
+  auto src_of = [&](int64_t r) -> Src {
+    Src o;
+    int64_t z, hr;
+    bool anchor = false;
+    if (r < base) {
+      const int64_t b = r / C1, j = r - b * C1;
+      anchor = j == 0;
+      z = anchor ? b : b * C + j - 1;
+      hr = anchor ? 0 : pos[b * C1];
+    } else {
+      const int64_t i = r - base;
+      const bool src_side = i < L2;
+      const int64_t li = src_side ? i : i - L2;
+      z = B * C + li;
+      hr = pos[src_side ? base + L2 + li : base + li];
+    }
+    o.anchor = anchor;
+    o.a = anchor ? arow + z * H + col : (dZ ? dZ + z * H + col : h);
+    o.s = (!anchor && drow) ? drow[z] : 0.f;
+    o.hp = h + hr * H + col;
+    return o;
+  };
+  auto value = [&](const Src& o, const float* va, const float* vh, float* out) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const float d = (drow && !o.anchor) ? o.s : va[i];
+      out[i] = o.anchor ? va[i] : round_to<T>(d * vh[i]);
+    }
+  };
   float acc[E];
 #pragma unroll
   for (int i = 0; i < E; ++i) acc[i] = 0.f;
-  auto add_pair = [&](int64_t z, int64_t hr) {
-    float d[E], hv[E];
-    if (drow) {
-      const float s = drow[z];
-#pragma unroll
-      for (int i = 0; i < E; ++i) d[i] = s;
-    } else {
-      load16<T>(dZ + z * H + col, d);
-    }
-    load16<T>(h + hr * H + col, hv);
-#pragma unroll
-    for (int i = 0; i < E; ++i) acc[i] += d[i] * hv[i];
-  };
   const int beg = seg_ptr[u], end = seg_ptr[u + 1];
-  for (int k = beg; k < end; ++k) {
-    const int64_t r = rows[k];
-    if (r < base) {
-      const int64_t b = r / C1, j = r - b * C1;
-      if (j == 0) {
-        const int32_t* pc = pos + b * C1 + 1;
-        const int64_t z0 = b * C;
-#pragma unroll 4
-        for (int64_t cc = 0; cc < C; ++cc) add_pair(z0 + cc, pc[cc]);
-      } else {
-        add_pair(b * C + j - 1, pos[b * C1]);
-      }
-    } else {
-      const int64_t i = r - base;
-      if (i < L2) add_pair(B * C + i, pos[base + L2 + i]);
-      else add_pair(B * C + (i - L2), pos[base + (i - L2)]);
-    }
+  int k = beg;
+  for (; k + 1 < end; k += 2) {   // two rows (four loads) in flight
+    const Src o0 = src_of(rows[k]), o1 = src_of(rows[k + 1]);
+    float a0[E], h0[E], a1[E], h1[E], v0[E], v1[E];
+    load16<T>(o0.a, a0);
+    load16<T>(o0.hp, h0);
+    load16<T>(o1.a, a1);
+    load16<T>(o1.hp, h1);
+    value(o0, a0, h0, v0);
+    value(o1, a1, h1, v1);
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += v0[i];
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += v1[i];
+  }
+  if (k < end) {
+    const Src o0 = src_of(rows[k]);
+    float a0[E], h0[E], v0[E];
+    load16<T>(o0.a, a0);
+    load16<T>(o0.hp, h0);
+    value(o0, a0, h0, v0);
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += v0[i];
   }
   *reinterpret_cast<uint4*>(dh + u * ldo + col) = V8<T>::pack(acc);
 }
@@ -477,23 +547,36 @@ extern "C" int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src,
 
 extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
                                          const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos,
-                                         const void* dZ, const float* drow, const void* h, void* dh, int64_t ld_dh,
-                                         const int32_t* u_dev, void* stream) {
-  LLP_CHECK_ARG(seg_ptr && rows && pos && h && dh && (dZ || drow), "llp_hadamard_bwd_segments: null");
+                                         const void* dZ, const float* drow, const void* h, void* anchor_rows,
+                                         void* dh, int64_t ld_dh, const int32_t* u_dev, void* stream) {
+  LLP_CHECK_ARG(seg_ptr && rows && pos && h && dh && (dZ || drow) && (anchor_rows || B == 0),
+                "llp_hadamard_bwd_segments: null");
   const int E = dtype == LLP_BF16 ? 8 : 4;
   const int es = dtype == LLP_BF16 ? 2 : 4;
   LLP_CHECK_ARG(H % E == 0 && H / E <= 256 && (ld_dh * es) % 16 == 0 && (uintptr_t)h % 16 == 0 &&
-                    (uintptr_t)dh % 16 == 0 && (!dZ || (uintptr_t)dZ % 16 == 0),
+                    (uintptr_t)dh % 16 == 0 && (!dZ || (uintptr_t)dZ % 16 == 0) &&
+                    (uintptr_t)anchor_rows % 16 == 0,
                 "llp_hadamard_bwd_segments: rows must be 16-B aligned, H <= 256 chunks");
   if (U == 0) return LLP_OK;
   const int64_t cpr = H / E, spb = 256 / cpr;
   hipStream_t s = (hipStream_t)stream;
+  if (B > 0) {
+    if (dtype == LLP_BF16)
+      hipLaunchKernelGGL(hadamard_anchor_rows_kernel<bf16_t>, dim3(ceil_div_u(B, spb)), dim3(256), 0, s, B, C, H,
+                         (const bf16_t*)dZ, drow, (const bf16_t*)h, pos, (bf16_t*)anchor_rows);
+    else
+      hipLaunchKernelGGL(hadamard_anchor_rows_kernel<float>, dim3(ceil_div_u(B, spb)), dim3(256), 0, s, B, C, H,
+                         (const float*)dZ, drow, (const float*)h, pos, (float*)anchor_rows);
+    LLP_LAUNCH_CHECK();
+  }
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(hadamard_bwd_segments_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
-                       H, seg_ptr, rows, pos, (const bf16_t*)dZ, drow, (const bf16_t*)h, (bf16_t*)dh, ld_dh, u_dev);
+                       H, seg_ptr, rows, pos, (const bf16_t*)dZ, drow, (const bf16_t*)h, (const bf16_t*)anchor_rows,
+                       (bf16_t*)dh, ld_dh, u_dev);
   else
     hipLaunchKernelGGL(hadamard_bwd_segments_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
-                       H, seg_ptr, rows, pos, (const float*)dZ, drow, (const float*)h, (float*)dh, ld_dh, u_dev);
+                       H, seg_ptr, rows, pos, (const float*)dZ, drow, (const float*)h, (const float*)anchor_rows,
+                       (float*)dh, ld_dh, u_dev);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void hadamard_bwd_blocks_vec_kernel(int64_t B,
       float o[E];
 #pragma unroll
       for (int i = 0; i < E; ++i) {
-        acc[i] += d.v[i] * hc.v[i];
+        acc[i] = fmaf(d.v[i], hc.v[i], acc[i]);   // the order llp_hadamard_bwd_segments repeats
         o[i] = d.v[i] * ha.v[i];
       }
       store_chunk<T>(dh + (b * C1 + 1 + cc) * H + col, o);

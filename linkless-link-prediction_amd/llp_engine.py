@@ -29,11 +29,11 @@ import torch.distributed as dist
 import llp_hip as K
 from contextlib import nullcontext as _nullctx
 
-# unique-node path: LLP_SEGMENT_FUSED=1 reduces the Hadamard backward straight onto the unique nodes
-# (llp_hadamard_bwd_segments, f32 accumulation, no [R1, H] row gradients).  It reads every pair row's
-# gradient twice (once per endpoint) and measured 14.99 vs 14.83 ms/step on the collab bench against
-# the default two-kernel path (row gradients in pair-block order + segment sum), so it is opt-in.
-_SEGMENT_FUSED = os.environ.get("LLP_SEGMENT_FUSED", "0") == "1"
+# unique-node path: the Hadamard backward is reduced straight onto the unique nodes
+# (llp_hadamard_bwd_segments: the anchors' context sums, then one pass per node over its rows),
+# bit-identical to the row gradients + segment sum (LLP_SEGMENT_FUSED=0) without their [R1, H]
+# buffer: collab step 12.87 -> 12.66 ms (same-box A/B)
+_SEGMENT_FUSED = os.environ.get("LLP_SEGMENT_FUSED", "1") == "1"
 # unique-node path: the unique count stays on the device (GEMM grids sized by the bound min(R1, N));
 # LLP_DEVICE_COUNT=0 reads it on the host instead (a sync per step, not capturable; A/B knob)
 _DEVICE_COUNT = os.environ.get("LLP_DEVICE_COUNT", "1") != "0"
@@ -807,8 +807,9 @@ class DistillEngine(EngineBase):
         if dedup and _SEGMENT_FUSED:
             # Hadamard backward reduced straight onto the unique nodes (no [R1, H] row gradients)
             dh = self._buf("gS0", (rows_s, H), dt)
+            arow = self._buf("anchor_rows", (max(B, 1), H), dt)
             K.hadamard_bwd_segments(rows_s, B, C, n_lab, H, seg_ptr, seg_rows, pos, dZ0 if mlp else None, h, dh,
-                                    drow=None if mlp else dlogit, count=n_u)
+                                    arow, drow=None if mlp else dlogit, count=n_u)
         else:
             dh_rows = self._buf("dh_rows" if dedup else "gS0", (R1, H), dt)
             hidx = pos if dedup else None

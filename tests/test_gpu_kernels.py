@@ -511,9 +511,16 @@ def test_hadamard_bwd_segments(dtype, inner):
     dZ = torch.randn(R2, H, generator=g).to(DEV, dtype)
     drow = torch.randn(R2, generator=g).to(DEV)
     out = torch.empty(U, H, device=DEV, dtype=dtype)
-    k.hadamard_bwd_segments(U, B, C, L2, H, segp, segr, pos, None if inner else dZ, h, out,
+    arow = torch.empty(B, H, device=DEV, dtype=dtype)
+    k.hadamard_bwd_segments(U, B, C, L2, H, segp, segr, pos, None if inner else dZ, h, out, arow,
                             drow=drow if inner else None)
+    # bit-identical to the two-kernel path (row gradients, then the per-node segment sum)
+    rows_dev = torch.empty(R1, H, device=DEV, dtype=dtype)
+    k.hadamard_bwd_blocks(B, C, L2, H, None if inner else dZ, h, rows_dev, drow=drow if inner else None, hidx=pos)
+    out2 = torch.empty(U, H, device=DEV, dtype=dtype)
+    k.segment_sum_rows(U, segp, segr, rows_dev, out2)
     torch.cuda.synchronize()
+    assert torch.equal(out, out2), (out.float() - out2.float()).abs().max().item()
     hr = h.float().cpu()[pos.cpu().long()]                              # [R1, H] rows of h per target row
     d = drow.cpu().unsqueeze(1).expand(R2, H) if inner else dZ.float().cpu()
     C1 = C + 1
