@@ -24,6 +24,7 @@ constexpr int NTT = 512;
 constexpr int NS = 4;                          // LDS ring depth (stages of TKM rows)
 constexpr int IMG_U4 = TKM * 32;               // one [32][256] bf16 image = 1024 uint4 = 16 KiB
 constexpr int STAGE_T = 2 * IMG_U4;            // A image + B image = 32 KiB
+constexpr int IDX_LDS = 8192;                  // gather indices staged in LDS (int32 slots)
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_row[64];   // 1 KiB of zeros (static init)
 
@@ -83,7 +84,9 @@ __device__ __forceinline__ void vm_wait(int64_t ahead) {   // 4 glds per wave pe
 // DMA issued after those MFMAs.  Bit-identical (same per-accumulator order).
 template <int STAG>
 __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE_T];   // 128 KiB
+  // the ring (128 KiB), then the split's gather indices (32 KiB; one __shared__ array, so
+  // hipcc's waitcnt pass sees no second object beside the LDS-DMA ring)
+  __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE_T + IDX_LDS / 4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
@@ -123,6 +126,23 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
     pb[i] = p.B + (mbeg + r) * p.ldb + q0 + min(lc8, capB);
   }
   const int64_t strideA = (int64_t)TKM * p.lda, strideB = (int64_t)TKM * p.ldb;
+  // gathered rows (x[this_target], the first student layer): the split's indices are
+  // staged in LDS before any DMA, so reading them never waits on the vector-memory
+  // counter (a global index load would drain the in-flight DMA ring every stage)
+  const int n_idx = (p.ia ? 1 : 0) + (p.ib ? 1 : 0);
+  const int64_t nrows = mend > mbeg ? mend - mbeg : 0;
+  const int64_t idx_cap = n_idx ? IDX_LDS / n_idx : 0;
+  const bool idx_lds = n_idx > 0 && nrows <= idx_cap;
+  int32_t* sidx = reinterpret_cast<int32_t*>(smem + NS * STAGE_T);
+  const int32_t* sia = sidx;
+  const int32_t* sib = sidx + (p.ia ? idx_cap : 0);
+  if (idx_lds) {
+    for (int64_t t = tid; t < nrows; t += NTT) {
+      if (p.ia) sidx[t] = p.ia[mbeg + t];
+      if (p.ib) sidx[(p.ia ? idx_cap : 0) + t] = p.ib[mbeg + t];
+    }
+    __syncthreads();   // no DMA in flight yet: this barrier's vmcnt(0) waits for the index loads only
+  }
   auto issue = [&](int64_t st) {
     const int64_t mt = mbeg + st * TKM;
     const uint32_t sA = lds0 + (uint32_t)((st % NS) * STAGE_T * 16);
@@ -145,8 +165,14 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
       const int64_t m = mt + r;
       const bool v = m < mend;
       const int64_t mm = v ? m : mbeg;
-      const int64_t ra = p.ia ? (int64_t)p.ia[mm] : mm;
-      const int64_t rb = p.ib ? (int64_t)p.ib[mm] : mm;
+      int64_t ra, rb;
+      if (idx_lds) {
+        ra = p.ia ? (int64_t)sia[mm - mbeg] : mm;
+        rb = p.ib ? (int64_t)sib[mm - mbeg] : mm;
+      } else {
+        ra = p.ia ? (int64_t)p.ia[mm] : mm;
+        rb = p.ib ? (int64_t)p.ib[mm] : mm;
+      }
       const bf16_t* srcA = v ? p.A + ra * p.lda + p0 + ca : zrow + ca;
       const bf16_t* srcB = v ? p.B + rb * p.ldb + q0 + cb : zrow + cb;
       const uint32_t off = (uint32_t)((4 * wu + 2 * i) * 32 * 16);
