@@ -62,6 +62,15 @@ __device__ __forceinline__ float head_dot4(float hp, const float (&v)[4], const 
   return fmaf(v[3], w[3], fmaf(v[2], w[2], fmaf(v[1], w[1], fmaf(v[0], w[0], hp))));
 }
 
+// byte of quad lane 0 | byte of lane 1 << 8 | lane 2 << 16 | lane 3 << 24, valid in
+// lane 0 of every 4-lane quad.  Two DPP quad_perm moves (VALU) instead of three
+// ds_bpermute round trips through the LDS pipe, whose latency every mask store
+// waited for.  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t quad_pack_bytes(uint32_t byte) {
+  const uint32_t t = byte | ((uint32_t)__builtin_amdgcn_mov_dpp((int)byte, 0xB1, 0xF, 0xF, false) << 8);   // [1,0,3,2]
+  return t | ((uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x4E, 0xF, 0xF, false) << 16);                    // [2,3,0,1]
+}
+
 __device__ __forceinline__ int64_t xcd_remap2(int64_t bid, int64_t nwg) {
   if (nwg < 8) return bid;
   const int64_t q = nwg / 8, r = nwg % 8;
@@ -349,9 +358,14 @@ __device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
 // no bias / dropout / head.  The host picks the mode (epi_mode_of).
 constexpr int EPI_ANY = 0, EPI_FWD_RELU = 1, EPI_FWD_NONE = 2, EPI_BWD_MASK = 3, EPI_HEAD_RELU = 4;
 
-template <int TMv, int NTHR, int MODE = EPI_ANY>
+// MASK_LDS (TMv 256, NTHR 512 only): the ReLU-backward bit mask of the tile (256 rows x
+// 32 bytes) is read with ONE 16-byte load per thread into LDS at smem + head_off_u4 + 256
+// (512 uint4 past the head partials; the caller's LDS must hold them) and each store
+// iteration takes its byte from there, instead of 16 one-byte global loads per thread.
+template <int TMv, int NTHR, int MODE = EPI_ANY, bool MASK_LDS = false>
 __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
                                            int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
+  static_assert(!MASK_LDS || (TMv == 256 && NTHR == 512 && TN == 256), "MASK_LDS: one 16-B mask piece per thread");
   const bool relu = MODE == EPI_FWD_RELU || MODE == EPI_HEAD_RELU || (MODE == EPI_ANY && p.act == LLP_ACT_RELU);
   const bool drop = MODE == EPI_ANY && p.drop_p > 0.f;
   const bool headw = MODE == EPI_HEAD_RELU || (MODE == EPI_ANY && p.head_w);
@@ -373,7 +387,25 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
   constexpr int ITERS = TMv * chunks_per_row / NTHR;
   const bool mask_rd = rbwd && (MODE == EPI_BWD_MASK || p.mask_in);
   uint32_t mb[ITERS];
-  if (mask_rd) {
+  const uint8_t* mask_lds = reinterpret_cast<const uint8_t*>(smem + head_off_u4 + 256);
+  if (MASK_LDS && mask_rd) {
+    // row tid/2 of the tile, bytes 16*(tid&1) .. +15 (columns n0 + 128*(tid&1) ..)
+    const int64_t row = m0 + (tid >> 1);
+    const int64_t cb = (n0 >> 3) + 16 * (tid & 1);
+    const uint8_t* src = p.mask_in + row * p.ld_mask + cb;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (row < p.M) {
+      if (8 * (cb + 16) <= p.N && ((uintptr_t)src & 15) == 0) {
+        v = *reinterpret_cast<const uint4*>(src);
+      } else {
+        uint8_t b[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) b[e] = 8 * (cb + e) < p.N ? src[e] : (uint8_t)0;
+        v = *reinterpret_cast<const uint4*>(b);
+      }
+    }
+    reinterpret_cast<uint4*>(smem + head_off_u4 + 256)[tid] = v;   // read after the barrier below
+  } else if (mask_rd) {
 #pragma unroll
     for (int i = 0; i < ITERS; ++i) {
       const int q = tid + i * NTHR;
@@ -454,7 +486,7 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
     if (rbwd) {
       uint32_t vv[4] = {v.x, v.y, v.z, v.w};
       if (mask_rd) {
-        const uint32_t bits = mb[i];
+        const uint32_t bits = MASK_LDS ? (uint32_t)mask_lds[rl * 32 + c] : mb[i];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           vv[e] = ((bits >> (2 * e)) & 1u ? (vv[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (vv[e] & 0xFFFF0000u) : 0u);
@@ -494,17 +526,16 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
         byte |= (__uint_as_float(vw[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
         byte |= (__uint_as_float(vw[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
       }
-      const uint32_t b1 = __shfl_down(byte, 1, 64), b2 = __shfl_down(byte, 2, 64), b3 = __shfl_down(byte, 3, 64);
-      if ((q & 3) == 0 && ok)
-        *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      const uint32_t word = quad_pack_bytes(byte);
+      if ((q & 3) == 0 && ok) *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = word;
     }
   }
 }
 
-template <int MODE = EPI_ANY>
+template <int MODE = EPI_ANY, bool MASK_LDS = false>
 __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8], uint4* smem, int head_off_u4,
                                              int64_t m0, int64_t n0, int tid, int wm, int wn, int g, int li) {
-  epilogue_t<TM, NT2, MODE>(p, acc, smem, head_off_u4, m0, n0, tid, wm, wn, g, li);
+  epilogue_t<TM, NT2, MODE, MASK_LDS>(p, acc, smem, head_off_u4, m0, n0, tid, wm, wn, g, li);
 }
 
 // ---------------------------------------------------------------------------
@@ -1014,7 +1045,8 @@ template <int DIRECT, int MODE>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   constexpr int IMG_U4 = 256 * 8;
   constexpr int TILE_U4 = 2 * IMG_U4;
-  constexpr int SM_U4 = 2 * TILE_U4 > SMEM_U4_EPI + 256 ? 2 * TILE_U4 : SMEM_U4_EPI + 256;
+  // staging + head partials (256 uint4) + the ReLU-backward mask tile (512 uint4, MASK_LDS)
+  constexpr int SM_U4 = 2 * TILE_U4 > SMEM_U4_EPI + 768 ? 2 * TILE_U4 : SMEM_U4_EPI + 768;
   __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -1162,7 +1194,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  epilogue_256<MODE>(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
+  epilogue_256<MODE, true>(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
 }
 
 template <int NS>
@@ -1356,9 +1388,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
         byte |= (__uint_as_float(vw[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
         byte |= (__uint_as_float(vw[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
       }
-      const uint32_t b1 = __shfl_down(byte, 1, 64), b2 = __shfl_down(byte, 2, 64), b3 = __shfl_down(byte, 3, 64);
-      if ((q & 3) == 0 && ok)
-        *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      const uint32_t word = quad_pack_bytes(byte);
+      if ((q & 3) == 0 && ok) *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = word;
     }
   }
 }
