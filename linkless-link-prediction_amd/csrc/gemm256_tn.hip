@@ -79,7 +79,7 @@ __device__ __forceinline__ void vm_wait(int64_t ahead) {   // 4 glds per wave pe
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
-// STAG (default 2; A/B knob LLP_TN_STAG): 1 = waves 4-7 run each stage's MFMAs one stage
+// STAG (2 = LLP_TN_STAG 2; the default is its lean form, gemm_tn_bf16_256c): 1 = waves 4-7 run each stage's MFMAs one stage
 // late (after the next barrier, before that stage's reads); 2 = as 1 with their
 // DMA issued after those MFMAs.  Bit-identical (same per-accumulator order).
 template <int STAG>
@@ -486,18 +486,261 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_pp(PTN p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Lean form of the staggered loop (LLP_TN_STAG 5 = lean STAG 2, 6 = lean STAG 1),
+// plain (non-gathered) operands only.  Same stages, DMA pieces, fragments, MFMA
+// operands and per-accumulator order as gemm_tn_bf16_256 (bit-identical slabs),
+// without its per-stage VALU work, which at two waves per SIMD competed with the
+// MFMAs for vector issue (about 2.3 VALU + 1.8 SALU per MFMA in the old loop):
+//  * LDS: A images of the 4 stages in [0, 64 KiB), B images in [64, 128 KiB), so a
+//    fragment read is (per-lane offset, computed once) + slot * 16 KiB, a constant
+//    that folds into the ds_read offset field (the loop is unrolled by the 4 slots);
+//  * DMA in SADDR form: per-lane 32-bit offsets fixed for the kernel, the stage's
+//    row base in SGPRs advanced by a scalar add;
+//  * per-wave roles hoisted out of the loop: waves 0-3 (the only ones that can
+//    carry the ones-fragment bias MFMAs) run the plain body, waves 4-7 the
+//    staggered one; the steady loop has no data-dependent branch and a constant
+//    vmcnt; the last stages (and a ragged one) run the generic body.
+constexpr int LIMG = 16384;                 // bytes of one [32][256] bf16 image
+constexpr int LB0 = NS * LIMG;              // B images start here
+
+__device__ __forceinline__ void glds16_s(uint32_t voff, const bf16_t* sbase, uint32_t lds_addr_uniform) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase),
+               "s"(lds_addr_uniform)
+               : "memory", "m0");
+}
+
+template <int STAG>
+__global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE_T];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
+  const int64_t tilesP = (p.P + TP - 1) / TP;
+  int64_t tile, z;
+  tn_block(p.zmajor, (int)(tilesP * tilesQ), (int)p.splits, tile, z);
+  const int64_t p0 = (tile / tilesQ) * TP, q0 = (tile % tilesQ) * TQ;
+  if (p.m_dev) {
+    const int64_t c = *p.m_dev;
+    p.M = c < p.M ? (c > 0 ? c : 0) : p.M;
+    const int64_t mc = (p.M + p.splits - 1) / p.splits;
+    p.mchunk = mc > 0 ? (mc + TKM - 1) / TKM * TKM : TKM;
+  }
+  const int64_t mbeg = z * p.mchunk;
+  const int64_t mend = min(p.M, mbeg + p.mchunk);
+
+  const int pc = lane & 31;
+  const int rbase = 4 * w + (lane >> 5);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int capA = (int)max((int64_t)0, (p.P - p0) - 8), capB = (int)max((int64_t)0, (p.Q - q0) - 8);
+  const bf16_t* zrow = reinterpret_cast<const bf16_t*>(g_zero_row);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)smem);
+  const int64_t nfull = mend > mbeg ? (mend - mbeg) / TKM : 0;
+  const int64_t nsteps = mend > mbeg ? (mend - mbeg + TKM - 1) / TKM : 0;
+
+  // DMA: wave w's piece i covers image rows 4w + 2i, 4w + 2i + 1 (lane >> 5), physical chunk lane & 31
+  uint32_t voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = rbase + 2 * i;
+    const int lc8 = (pc ^ swz(r)) * 8;
+    voA[i] = (uint32_t)((r * p.lda + min(lc8, capA)) * 2);
+    voB[i] = (uint32_t)((r * p.ldb + min(lc8, capB)) * 2);
+  }
+  const bf16_t* gA = p.A + mbeg * p.lda + p0;
+  const bf16_t* gB = p.B + mbeg * p.ldb + q0;
+  const int64_t stepA = (int64_t)TKM * p.lda, stepB = (int64_t)TKM * p.ldb;
+  const uint32_t ldw = lds0 + (uint32_t)(4 * wu * 512);
+  auto issue_fast = [&](int64_t st, int slot) {
+    const bf16_t* ba = gA + st * stepA;
+    const bf16_t* bb = gB + st * stepB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16_s(voA[i], ba, __builtin_amdgcn_readfirstlane(ldw + (uint32_t)(slot * LIMG + i * 1024)));
+      glds16_s(voB[i], bb, __builtin_amdgcn_readfirstlane(ldw + (uint32_t)(LB0 + slot * LIMG + i * 1024)));
+    }
+  };
+  auto issue = [&](int64_t st) {   // any stage (rows past the split's end read zeros)
+    const int slot = (int)(st % NS);
+    if (st < nfull) { issue_fast(st, slot); return; }
+    const int64_t mt = mbeg + st * TKM;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = rbase + 2 * i;
+      const int lc8 = (pc ^ swz(r)) * 8;
+      const int64_t m = mt + r;
+      const bool v = m < mend;
+      const bf16_t* srcA = v ? p.A + m * p.lda + p0 + min(lc8, capA) : zrow + min(lc8, capA);
+      const bf16_t* srcB = v ? p.B + m * p.ldb + q0 + min(lc8, capB) : zrow + min(lc8, capB);
+      glds16(srcA, __builtin_amdgcn_readfirstlane(ldw + (uint32_t)(slot * LIMG + i * 1024)));
+      glds16(srcB, __builtin_amdgcn_readfirstlane(ldw + (uint32_t)(LB0 + slot * LIMG + i * 1024)));
+    }
+  };
+
+  const int wq = w >> 2, wp = w & 3;
+  float4_t acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+  const int q4 = li >> 2, pp = li & 3;
+  const bool do_cs = p.ws_colsum != nullptr && q0 == 0 && wq == 0;
+  float4_t accb[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) accb[b] = float4_t{0.f, 0.f, 0.f, 0.f};
+  short8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
+
+  // per-lane fragment offsets (bytes from smem) of slot 0: rows row0 and row0 + 4
+  const int row0 = 8 * g + q4;
+  auto img_off = [&](int row, int col) {
+    return row * 512 + 16 * ((col >> 3) ^ swz(row)) + 8 * ((col >> 2) & 1);
+  };
+  int oA[4][2], oB[8][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) oA[ip][h] = img_off(row0 + 4 * h, wp * 64 + ip * 16 + 4 * pp);
+#pragma unroll
+    for (int jq = 0; jq < 8; ++jq) oB[jq][h] = LB0 + img_off(row0 + 4 * h, wq * 128 + jq * 16 + 4 * pp);
+  }
+  lds_char* sbase = (lds_char*)((__attribute__((address_space(3))) uint4*)smem);
+  auto trd = [&](int off) -> short4_t { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(sbase + off)); };
+
+  short8 fp[4];
+  short8 fq[8];
+  auto read_p = [&](int sl) {
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip)
+      fp[ip] = __builtin_shufflevector(trd(oA[ip][0] + sl * LIMG), trd(oA[ip][1] + sl * LIMG), 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto read_q = [&](int sl, int j0) {
+#pragma unroll
+    for (int jq = j0; jq < j0 + 4; ++jq)
+      fq[jq] = __builtin_shufflevector(trd(oB[jq][0] + sl * LIMG), trd(oB[jq][1] + sl * LIMG), 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto mfma_cs = [&]() {
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip)
+      accb[ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fp[ip], accb[ip], 0, 0, 0);
+  };
+  auto mfma_half = [&](int jh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int ip = 0; ip < 4; ++ip)
+        acc[4 * jh + jj][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[4 * jh + jj], fp[ip], acc[4 * jh + jj][ip], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto head = [&](int64_t st, bool steady) {   // wait for stage st, barrier
+    if (steady) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else vm_wait(min(nsteps - 1, st + NS - 2) - st);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // plain body (waves 0-3; CS: this tile carries the bias-gradient MFMAs)
+  auto body_plain = [&](auto CS, int sl, int64_t st, bool steady) {
+    head(st, steady);
+    if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
+    else if (st + NS - 1 < nsteps) issue(st + NS - 1);
+    read_p(sl);
+    read_q(sl, 0);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+    if constexpr (decltype(CS)::value) mfma_cs();
+    mfma_half(0);
+    read_q(sl, 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_half(1);
+  };
+  // staggered body (waves 4-7): the previous stage's MFMAs after the barrier, then (STAG 2)
+  // the DMA, then this stage's fragments
+  auto body_stag = [&](int sl, int64_t st, bool steady) {
+    head(st, steady);
+    if (STAG == 1) {
+      if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
+      else if (st + NS - 1 < nsteps) issue(st + NS - 1);
+    }
+    if (st > 0) { mfma_half(0); mfma_half(1); }
+    if (STAG == 2) {
+      if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
+      else if (st + NS - 1 < nsteps) issue(st + NS - 1);
+    }
+    read_p(sl);
+    read_q(sl, 0);
+    read_q(sl, 4);
+  };
+
+  if (nsteps > 0) {
+    for (int64_t s = 0; s < NS - 1 && s < nsteps; ++s) issue(s);
+    int64_t st = 0;
+    // steady groups of NS stages: every DMA they issue (up to stage st + 2 NS - 2) is full
+    const int64_t nsteady = nfull >= 2 * NS - 1 ? ((nfull - (2 * NS - 2)) / NS) * NS : 0;
+    if (wu >= 4) {
+      for (; st < nsteady; st += NS) {
+        body_stag(0, st, true);
+        body_stag(1, st + 1, true);
+        body_stag(2, st + 2, true);
+        body_stag(3, st + 3, true);
+      }
+      for (; st < nsteps; ++st) body_stag((int)(st % NS), st, false);
+      mfma_half(0);
+      mfma_half(1);
+    } else if (do_cs) {
+      for (; st < nsteady; st += NS) {
+        body_plain(std::true_type{}, 0, st, true);
+        body_plain(std::true_type{}, 1, st + 1, true);
+        body_plain(std::true_type{}, 2, st + 2, true);
+        body_plain(std::true_type{}, 3, st + 3, true);
+      }
+      for (; st < nsteps; ++st) body_plain(std::true_type{}, (int)(st % NS), st, false);
+    } else {
+      for (; st < nsteady; st += NS) {
+        body_plain(std::false_type{}, 0, st, true);
+        body_plain(std::false_type{}, 1, st + 1, true);
+        body_plain(std::false_type{}, 2, st + 2, true);
+        body_plain(std::false_type{}, 3, st + 3, true);
+      }
+      for (; st < nsteps; ++st) body_plain(std::false_type{}, (int)(st % NS), st, false);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (do_cs && g == 0) {
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) {
+      const int64_t pr = p0 + wp * 64 + ip * 16 + li;
+      if (pr < p.P) p.ws_colsum[z * p.P + pr] = accb[ip][0];
+    }
+  }
+  float* out = p.ws + z * p.P * p.Q;
+#pragma unroll
+  for (int ip = 0; ip < 4; ++ip) {
+    const int64_t pr = p0 + wp * 64 + ip * 16 + li;
+    if (pr >= p.P) continue;
+#pragma unroll
+    for (int jq = 0; jq < 8; ++jq) {
+      const int64_t qc = q0 + wq * 128 + jq * 16 + 4 * g;
+      if (qc >= p.Q) continue;
+      *reinterpret_cast<float4_t*>(out + pr * p.Q + qc) = acc[jq][ip];
+    }
+  }
+}
+
 }  // namespace
 
 namespace {
 int g_tn_variant = -1;   // main-loop variant of the TN kernel (LLP_TN_STAG; llp_set_gemm_tn_variant)
 }
 
-// 0 lockstep, 1 waves 4-7 staggered by one stage, 2 = 1 with late DMA (default),
-// 3 ping-pong, 4 ping-pong with two LOAD/MFMA pairs per stage (3, 4: measured slower);
+// 0 lockstep, 1 waves 4-7 staggered by one stage, 2 = 1 with late DMA,
+// 3 ping-pong, 4 ping-pong with two LOAD/MFMA pairs per stage (3, 4: measured slower),
+// 5 = 2 as the lean loop (default; gathered operands fall back to 2), 6 = 1 as the lean loop;
 // + 8: tile-major block order (the round-1 placement) instead of split-major
 extern "C" int llp_set_gemm_tn_variant(int v) {
-  LLP_CHECK_ARG(v >= 0 && v <= 12 && (v & 7) <= 4, "llp_set_gemm_tn_variant: %d", v);
-  const int old = g_tn_variant >= 0 ? g_tn_variant : 2;
+  LLP_CHECK_ARG(v >= 0 && v <= 14 && (v & 7) <= 6, "llp_set_gemm_tn_variant: %d", v);
+  const int old = g_tn_variant >= 0 ? g_tn_variant : 5;
   g_tn_variant = v;
   return old;
 }
@@ -528,16 +771,21 @@ int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.splits = splits;
   p.ws = ws;
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  const int var = g_tn_variant >= 0 ? g_tn_variant : (g_tn_variant = getenv("LLP_TN_STAG") ? atoi(getenv("LLP_TN_STAG")) : 2);
+  const int var = g_tn_variant >= 0 ? g_tn_variant : (g_tn_variant = getenv("LLP_TN_STAG") ? atoi(getenv("LLP_TN_STAG")) : 5);
   const int stag = var & 7;
   p.zmajor = (var & 8) ? 0 : 1;
-  if (stag == 3)
+  const bool lean_ok = !A->idx && !B->idx;   // the lean loop stages plain operands only
+  if (stag == 5 && lean_ok)
+    hipLaunchKernelGGL(gemm_tn_bf16_256c<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  else if (stag == 6 && lean_ok)
+    hipLaunchKernelGGL(gemm_tn_bf16_256c<1>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  else if (stag == 3)
     hipLaunchKernelGGL(gemm_tn_bf16_pp<false>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   else if (stag == 4)
     hipLaunchKernelGGL(gemm_tn_bf16_pp<true>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   else if (stag == 1)
     hipLaunchKernelGGL(gemm_tn_bf16_256<1>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
-  else if (stag == 2)
+  else if (stag == 2 || stag >= 5)
     hipLaunchKernelGGL(gemm_tn_bf16_256<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   else
     hipLaunchKernelGGL(gemm_tn_bf16_256<0>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);

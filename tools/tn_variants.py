@@ -16,7 +16,7 @@ import torch  # noqa: E402
 import llp_hip as K  # noqa: E402
 
 VARIANTS = tuple(int(v) for v in os.environ.get("LLP_TN_VARIANTS", "2,3").split(","))
-NAMES = {0: "lockstep", 1: "stag", 2: "stag-late", 3: "pingpong", 4: "pingpong-split", 10: "stag-late-tilemajor"}
+NAMES = {0: "lockstep", 1: "stag", 2: "stag-late", 3: "pingpong", 4: "pingpong-split", 5: "lean-stag-late", 6: "lean-stag", 10: "stag-late-tilemajor"}
 
 
 def main():
