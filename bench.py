@@ -113,18 +113,21 @@ def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, 
     R1 = A.numel() // lin.in_f if cnt is not None else eng.last_student_rows
     out = eng._buf("H1", (R1, lin.out_f), eng.dtype)
     a_op = K.operand(A[:R1 * lin.in_f].view(R1, lin.in_f), count=cnt)
+    hm = eng._bufs.get("Hm1")                 # the step's launch also writes the ReLU bit mask
+    hm = hm[:R1 * (lin.out_f // 8)].view(R1, lin.out_f // 8) if hm is not None else None
     for _ in range(n):
-        K.gemm_nt(a_op, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, eng.dc, bias=lin.b, act=K.ACT_RELU)
+        K.gemm_nt(a_op, K.operand(lin.Wcomp), R1, lin.out_f, lin.in_f, out, eng.dc, bias=lin.b, act=K.ACT_RELU,
+                  aux=hm)
     torch.cuda.synchronize()
     print(json.dumps({"dominant_rows": R1, "H": lin.out_f, "launches": n}), flush=True)
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_dominant.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r02_pmc_dominant.json")
 
 
 def pmc_traffic(rows, H, dtype):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC passes (profiles/r01_pmc_dominant.json, tools/pmc_summary.py):
+    PMC passes (profiles/r02_pmc_dominant.json, tools/pmc_summary.py):
     2 x FETCH_SIZE (gfx950 reports half of a wide streaming read) + WRITE_SIZE,
     per dispatch.  None when the profile is absent or for another shape."""
     try:
@@ -410,7 +413,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": f"{K.lib().llp_gemm_variant_name().decode()} student layer-2 forward "
                          f"({rows_exec}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": pmc_traffic(rows_exec, H, opt.dtype),
-                         "algorithmic_bytes": 2.0 * rows_exec * H * 2 + 2.0 * H * H, "kernel_ms": k_ms},
+                         "algorithmic_bytes": 2.0 * rows_exec * H * 2 + 2.0 * H * H + rows_exec * H / 8.0,
+                         "kernel_ms": k_ms},
             "loss": loss,
             "hipgraph": bool(graph is not None),
         }

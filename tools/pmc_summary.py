@@ -53,7 +53,8 @@ def main():
     # FETCH_SIZE / WRITE_SIZE are in KiB
     f_b = 1024.0 * sum(fetch) / len(fetch)
     w_b = 1024.0 * sum(write) / len(write)
-    alg = 2.0 * a.rows * a.H * 2 + 2.0 * a.H * a.H
+    # A read + C write (bf16) + W read + the ReLU bit mask the step's launch writes
+    alg = 2.0 * a.rows * a.H * 2 + 2.0 * a.H * a.H + a.rows * a.H / 8.0
     out = {"kernel": names[-1] if names else a.kernel, "rows": a.rows, "H": a.H, "dtype": a.dtype,
            "dispatches": len(fetch), "fetch_size_bytes": f_b, "write_size_bytes": w_b,
            "traffic_bytes_per_launch": 2.0 * f_b + w_b, "algorithmic_bytes": alg,
