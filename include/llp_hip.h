@@ -226,6 +226,13 @@ int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr
                          const void* src, int64_t ld_src, void* out, int64_t ld_out, const int32_t* out_rows,
                          const int32_t* u_dev, void* stream);
 int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
+/* out row r = src row idx[r] (row_bytes each; leading dimensions in bytes) for
+ * r < min(n, *count_dev) (count_dev may be NULL): data.x[this_target]
+ * (src/main.py:95) materialised once per step, so the first student layer's
+ * forward and weight-gradient GEMMs read plain rows (the unique-node student:
+ * idx = uniq, count_dev = n_unique). */
+int llp_gather_rows(int64_t n, int64_t row_bytes, const int32_t* idx, const void* src, int64_t ld_src_bytes,
+                    void* out, int64_t ld_out_bytes, const int32_t* count_dev, void* stream);
 /* Backward of the predictor input h[i] * h[j] (src/main.py:102-103,126) reduced
  * straight onto the unique nodes, bit-identical to llp_hadamard_bwd_blocks (hidx =
  * pos) followed by llp_segment_sum_rows: dh[u] = sum over the target rows of node u

@@ -260,6 +260,24 @@ __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
   *reinterpret_cast<uint4*>(dh + u * ldo + col) = V8<T>::pack(acc);
 }
 
+// out row r = src row idx[r] for r < min(n, *count): 16-byte chunks, one thread each
+__global__ void gather_rows16_kernel(int64_t n, int64_t chunks, const int32_t* __restrict__ idx,
+                                     const uint4* __restrict__ src, int64_t ld_src16, uint4* __restrict__ out,
+                                     int64_t ld_out16, const int32_t* __restrict__ count) {
+  const int64_t live = count ? min(n, (int64_t)*count) : n;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t r = t / chunks, c = t - r * chunks;
+  if (r < live) out[r * ld_out16 + c] = src[(int64_t)idx[r] * ld_src16 + c];
+}
+__global__ void gather_rows1_kernel(int64_t n, int64_t bytes, const int32_t* __restrict__ idx,
+                                    const uint8_t* __restrict__ src, int64_t ld_src, uint8_t* __restrict__ out,
+                                    int64_t ld_out, const int32_t* __restrict__ count) {
+  const int64_t live = count ? min(n, (int64_t)*count) : n;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t r = t / bytes, c = t - r * bytes;
+  if (r < live) out[r * ld_out + c] = src[(int64_t)idx[r] * ld_src + c];
+}
+
 __global__ void gather_i32_kernel(int64_t n, const int32_t* __restrict__ idx, const int32_t* __restrict__ src,
                                   int32_t* __restrict__ out) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -541,6 +559,27 @@ extern "C" int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src,
   if (n == 0) return LLP_OK;
   hipLaunchKernelGGL(gather_i32_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, idx, src,
                      out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_gather_rows(int64_t n, int64_t row_bytes, const int32_t* idx, const void* src,
+                               int64_t ld_src_bytes, void* out, int64_t ld_out_bytes, const int32_t* count_dev,
+                               void* stream) {
+  LLP_CHECK_ARG(n >= 0 && row_bytes >= 0 && (n == 0 || (idx && src && out)), "llp_gather_rows: null / negative");
+  LLP_CHECK_ARG(ld_src_bytes >= row_bytes && ld_out_bytes >= row_bytes, "llp_gather_rows: ld < row_bytes");
+  if (n == 0 || row_bytes == 0) return LLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool v16 = row_bytes % 16 == 0 && ld_src_bytes % 16 == 0 && ld_out_bytes % 16 == 0 &&
+                   (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
+  if (v16) {
+    const int64_t ch = row_bytes / 16;
+    hipLaunchKernelGGL(gather_rows16_kernel, dim3(ceil_div_u(n * ch, 256)), dim3(256), 0, s, n, ch, idx,
+                       (const uint4*)src, ld_src_bytes / 16, (uint4*)out, ld_out_bytes / 16, count_dev);
+  } else {
+    hipLaunchKernelGGL(gather_rows1_kernel, dim3(ceil_div_u(n * row_bytes, 256)), dim3(256), 0, s, n, row_bytes,
+                       idx, (const uint8_t*)src, ld_src_bytes, (uint8_t*)out, ld_out_bytes, count_dev);
+  }
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -500,12 +500,19 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, int64_t splits,
 // kernel above keeps one load in flight per thread and is latency-bound at
 // large S (the teacher's TN splits, S = 128).
 constexpr int SR_G = 4, SR_L = 256 / SR_G;
-__global__ __launch_bounds__(256) void slab_reduce_v4_kernel(const float4* __restrict__ ws, int64_t S, int64_t n4,
-                                                             int64_t Q4, float* __restrict__ C, int64_t ldc,
-                                                             int accumulate) {
+struct SlabJob {           // C[e4 / Q4][(e4 % Q4) * 4 ..] (+)= sum_z ws[z][e4], e4 < n4
+  const float4* ws; int64_t S, n4, Q4; float* C; int64_t ldc;
+};
+// One launch can carry two jobs (the weight slabs and the bias-gradient slabs of a TN
+// GEMM): blocks [0, nblk0) take job 0, the rest job 1.
+__global__ __launch_bounds__(256) void slab_reduce_v4_kernel(SlabJob j0, SlabJob j1, int64_t nblk0, int accumulate) {
   __shared__ float4 part[SR_G][SR_L];
+  const bool second = (int64_t)blockIdx.x >= nblk0;
+  const SlabJob& j = second ? j1 : j0;
+  const float4* __restrict__ ws = j.ws;
+  const int64_t S = j.S, n4 = j.n4;
   const int lane = threadIdx.x % SR_L, g = threadIdx.x / SR_L;
-  const int64_t e4 = (int64_t)blockIdx.x * SR_L + lane;
+  const int64_t e4 = ((int64_t)blockIdx.x - (second ? nblk0 : 0)) * SR_L + lane;
   const int64_t z1 = (g + 1) * S / SR_G;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e4 < n4) {
@@ -533,7 +540,7 @@ __global__ __launch_bounds__(256) void slab_reduce_v4_kernel(const float4* __res
     const float4 v = part[k][lane];
     t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
   }
-  float4* dst = reinterpret_cast<float4*>(C + (e4 / Q4) * ldc + (e4 % Q4) * 4);
+  float4* dst = reinterpret_cast<float4*>(j.C + (e4 / j.Q4) * j.ldc + (e4 % j.Q4) * 4);
   if (accumulate) {
     const float4 o = *dst;
     t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
@@ -541,19 +548,33 @@ __global__ __launch_bounds__(256) void slab_reduce_v4_kernel(const float4* __res
   *dst = t;
 }
 
-// C (+)= sum of the S slabs [S][P][Q] (f32), deterministic.
+// C (+)= sum of the S slabs [S][P][Q] (f32), deterministic; with C2, in the same
+// launch when both take the vector form, also C2 (+)= sum of the S slabs [S][P2] at ws2
+// (a TN GEMM's bias-gradient column sums).
 void slab_reduce(const float* ws, int64_t S, int64_t P, int64_t Q, float* C, int64_t ldc, int accumulate,
-                 hipStream_t s) {
+                 hipStream_t s, const float* ws2 = nullptr, int64_t P2 = 0, float* C2 = nullptr) {
   const int64_t n = P * Q;
-  if (n == 0) return;
-  if (Q % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)ws % 16 == 0) {
-    const int64_t n4 = n / 4;
-    hipLaunchKernelGGL(slab_reduce_v4_kernel, dim3(ceil_div_u(n4, SR_L)), dim3(256), 0, s,
-                       reinterpret_cast<const float4*>(ws), S, n4, Q / 4, C, ldc, accumulate);
-  } else {
+  auto vec_ok = [](const float* w, int64_t q, const float* c, int64_t ld) {
+    return q % 4 == 0 && ld % 4 == 0 && (uintptr_t)c % 16 == 0 && (uintptr_t)w % 16 == 0;
+  };
+  const bool v1 = n > 0 && vec_ok(ws, Q, C, ldc);
+  const bool two = C2 && P2 > 0;
+  const bool v2 = two && vec_ok(ws2, P2, C2, P2);
+  if (v1) {
+    SlabJob j0{reinterpret_cast<const float4*>(ws), S, n / 4, Q / 4, C, ldc};
+    SlabJob j1 = j0;
+    const int64_t nb0 = ceil_div_u(n / 4, SR_L);
+    int64_t nb = nb0;
+    if (v2) {
+      j1 = SlabJob{reinterpret_cast<const float4*>(ws2), S, P2 / 4, P2 / 4, C2, P2};
+      nb += ceil_div_u(P2 / 4, SR_L);
+    }
+    hipLaunchKernelGGL(slab_reduce_v4_kernel, dim3((unsigned)nb), dim3(256), 0, s, j0, j1, nb0, accumulate);
+  } else if (n > 0) {
     const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, ws, S, P, Q, C, ldc, accumulate);
   }
+  if (two && !(v1 && v2)) slab_reduce(ws2, S, (int64_t)1, P2, C2, P2, accumulate, s);
 }
 
 Op to_op(const llp_operand* o) {
@@ -758,12 +779,9 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     float* wcs = colsum_a ? ws + sp * P * Q : nullptr;
     const int rc = llp_gemm_tn_bf16_256(A, B, M, P, Q, ws, wcs, sp, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (256 tile): %s", hipGetErrorString((hipError_t)rc));
-    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s);
+    // weight slabs and the [sp][P] column-sum slabs in one launch
+    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s, wcs, colsum_a ? P : 0, colsum_a);
     LLP_LAUNCH_CHECK();
-    if (colsum_a) {   // [sp][P] column-sum slabs: P rows of one column
-      slab_reduce(wcs, sp, (int64_t)1, P, colsum_a, P, accumulate, s);
-      LLP_LAUNCH_CHECK();
-    }
     return LLP_OK;
   }
   const int64_t splits = tn_splits(dtype, M, P, Q);

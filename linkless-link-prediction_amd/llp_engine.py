@@ -43,6 +43,11 @@ _DEVICE_COUNT = os.environ.get("LLP_DEVICE_COUNT", "1") != "0"
 # bit mask: 1 teacher predictor beside the student forward; 2 the predictor's first-layer weight
 # gradient beside the Hadamard backward; 4 every other weight gradient beside its data gradient
 _OVERLAP = int(os.environ.get("LLP_OVERLAP", "0"))
+# minibatch step, bf16: x[this_target] (src/main.py:95) is gathered once into a plain buffer
+# (llp_gather_rows) that the first student layer's forward and weight-gradient GEMMs read, so the
+# weight gradient runs the lean TN loop (gathered operands fall back to the staggered one);
+# LLP_GATHER_X=0 keeps the gathered GEMM operands (A/B knob)
+_GATHER_X = os.environ.get("LLP_GATHER_X", "1") != "0"
 
 # dropout Philox keys (EngineBase._dropout): one per module, one stream per layer and step
 DROP_ENCODER, DROP_PREDICTOR, DROP_TEACHER_PRED = 0, 1, 2
@@ -761,7 +766,13 @@ class DistillEngine(EngineBase):
 
         # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
         acts = []
-        A = K.operand(self.x, gather_s, count=n_u)
+        x_rows = None
+        if _GATHER_X and self.dtype == torch.bfloat16:
+            x_rows = self._buf("Xg", (rows_s, self.x.shape[1]), dt)
+            K.gather_rows(self.x, gather_s, x_rows, count=n_u)
+            A = K.operand(x_rows, count=n_u)
+        else:
+            A = K.operand(self.x, gather_s, count=n_u)
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (rows_s, lin.out_f), dt)
@@ -822,7 +833,7 @@ class DistillEngine(EngineBase):
                 K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh, count=n_u)
             else:
                 dh = dh_rows
-        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap)
+        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap, x_rows=x_rows)
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
@@ -1011,10 +1022,11 @@ class DistillEngine(EngineBase):
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, overlap=False):
+    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, overlap=False, x_rows=None):
         """count: int32 device row count (unique-node student) or None.  dh lives in
         buffer 'gS0'.  overlap: weight-gradient GEMMs on the side stream, as in
-        _predictor_backward (three data-gradient buffers)."""
+        _predictor_backward (three data-gradient buffers).  x_rows: x[target]
+        materialised by the forward (else the first layer's input is gathered)."""
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
         names = ["gS0", "gS1", "gS2"] if overlap & 4 else ["gS0", "gS1"]
@@ -1022,7 +1034,12 @@ class DistillEngine(EngineBase):
         for l in range(len(self.stu) - 1, -1, -1):
             lin = self.stu[l]
             gcur = self._buf(names[k % len(names)], (R1, lin.out_f), dt)
-            A_in = K.operand(acts[l - 1], count=count) if l > 0 else K.operand(self.x, target, count=count)
+            if l > 0:
+                A_in = K.operand(acts[l - 1], count=count)
+            elif x_rows is not None:
+                A_in = K.operand(x_rows, count=count)
+            else:
+                A_in = K.operand(self.x, target, count=count)
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
             dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad

@@ -72,6 +72,7 @@ _SIGS = {
     "llp_hadamard_bwd_segments": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_i64, c_vp, c_vp]),
     "llp_gather_i32": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_gather_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "llp_hadamard_bwd_scatter": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_context_sampler": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
                                     c_i64, c_vp, c_vp]),
@@ -298,6 +299,16 @@ def gather_i32(idx, src, out):
     L = lib()
     check(L.llp_gather_i32(idx.numel(), idx.data_ptr(), src.data_ptr(), out.data_ptr(), stream_ptr()),
           "llp_gather_i32")
+
+
+def gather_rows(src, idx, out, count=None):
+    """out[r] = src[idx[r]] for r < min(out rows, *count) (count: device int32[1] or None)."""
+    L = lib()
+    n = out.shape[0]
+    rb = out.shape[1] * out.element_size()
+    check(L.llp_gather_rows(n, rb, idx.data_ptr(), src.data_ptr(), src.stride(0) * src.element_size(),
+                            out.data_ptr(), out.stride(0) * out.element_size(), ptr(count), stream_ptr()),
+          "llp_gather_rows")
 
 
 def hadamard_rows(a, ia, b, ib, out):

@@ -487,6 +487,25 @@ def test_dedup_rows_and_segment_sum(N, R, hub):
     assert np.array_equal(o.cpu().numpy(), inv[idx.numpy()])
 
 
+@pytest.mark.parametrize("dtype,F", [(torch.bfloat16, 128), (torch.bfloat16, 13), (torch.float32, 37)])
+def test_gather_rows(dtype, F):
+    """llp_gather_rows: out[r] = x[idx[r]] bit-exact, rows past the device count untouched
+    (x[this_target], src/main.py:95)."""
+    k = K()
+    g = torch.Generator().manual_seed(F)
+    N, R, live = 1000, 777, 500
+    x = torch.randn(N, F, generator=g).to(DEV, dtype)
+    idx = torch.randint(0, N, (R,), generator=g, dtype=torch.int32).to(DEV)
+    out = torch.full((R, F), 7.0, device=DEV, dtype=dtype)
+    k.gather_rows(x, idx, out)
+    assert torch.equal(out, x[idx.long()])
+    out.fill_(7.0)
+    cnt = torch.tensor([live], dtype=torch.int32, device=DEV)
+    k.gather_rows(x, idx, out, count=cnt)
+    assert torch.equal(out[:live], x[idx[:live].long()])
+    assert bool((out[live:] == 7.0).all())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("inner", [False, True])
 def test_hadamard_bwd_segments(dtype, inner):
