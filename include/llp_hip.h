@@ -290,6 +290,20 @@ int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, const int32
 int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* samples,
                                 int32_t* ia, int32_t* ib, void* stream);
 
+/* One minibatch step's index building in ONE launch (the collab path of
+ * train_minibatch: neighbor_samplers src/main.py:33-50 + torch.randint negatives
+ * :83-84 + this_target :95 + the teacher's pair index :104,106): exactly
+ * llp_context_sampler(.., stream_offset, samples) + llp_randint_pairs(num_nodes, P,
+ * P_total, p_offset, seed, step_ctr, neg_stream_offset, neg) + llp_build_targets(B,
+ * C1, samples, pairs, perm, NULL, 0, P, neg, P, P, target) +
+ * llp_pair_index_from_samples(B, C, samples, t_ia, t_ib), same draws, bit for bit. */
+int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_nodes, const int32_t* start,
+                         int64_t B, int64_t b_offset, int ps_method, int rw_step, int hops, int ns_rate,
+                         uint64_t seed, const int64_t* step_ctr, int64_t stream_offset, const int32_t* pairs,
+                         const int32_t* perm, int64_t P, int64_t P_total, int64_t p_offset,
+                         int64_t neg_stream_offset, int32_t* samples, int32_t* neg, int32_t* target,
+                         int32_t* t_ia, int32_t* t_ib, void* stream);
+
 /* ---------------------------------------------------------------- full-batch step (src/main.py:147-236)
  * Dense negative sampling, replacing PyG 2.2.0 negative_sampling(edge_index,
  * num_nodes, num_neg_samples, method='dense') (src/main.py:206,
@@ -400,6 +414,10 @@ int llp_convert(int src_dtype, int dst_dtype, int64_t n, const void* src, void* 
 /* Sum loss terms into a running total (device), so an epoch needs one host sync. */
 int llp_accumulate(int64_t n, const float* src, float weight, double* dst, void* stream);
 int llp_increment(int64_t* ctr, void* stream);
+/* The end of a training step in one launch: *loss_sum += (double)*loss * weight (the
+ * epoch's total_loss += loss.item() * num_examples, src/main.py:140-141) and
+ * *step_ctr += 1 (the device step counter that keys every Philox stream). */
+int llp_step_end(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, void* stream);
 /* hipMemsetAsync(p, 0, bytes) on the stream. */
 int llp_zero(void* p, int64_t bytes, void* stream);
 

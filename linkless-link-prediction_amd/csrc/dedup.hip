@@ -419,6 +419,62 @@ __global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __rest
   }
 }
 
+// segsort_short_kernel + segsort_long_kernel in one launch: each thread sorts its short
+// segment in its LDS row and lists a long one in the block's LDS list; then the block
+// ranks its long segments one at a time (the rows buffer reused, or `scratch` past it).
+// Same result (every segment in row-id order).
+__global__ __launch_bounds__(256) void segsort_kernel(const int32_t* __restrict__ n_unique,
+                                                      const int32_t* __restrict__ seg_ptr,
+                                                      int32_t* __restrict__ seg_rows, int32_t* __restrict__ scratch) {
+  __shared__ int32_t buf[256][SHORT_SEG + 1];
+  __shared__ int32_t longs[256];
+  __shared__ int32_t n_longs;
+  if (threadIdx.x == 0) n_longs = 0;
+  __syncthreads();
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s < *n_unique) {
+    const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
+    if (len > SHORT_SEG) {
+      longs[atomicAdd(&n_longs, 1)] = (int32_t)s;
+    } else if (len > 1) {
+      int32_t* a = buf[threadIdx.x];
+      for (int i = 0; i < len; ++i) a[i] = seg_rows[b + i];
+      for (int i = 1; i < len; ++i) {
+        const int32_t x = a[i];
+        int j = i - 1;
+        while (j >= 0 && a[j] > x) {
+          a[j + 1] = a[j];
+          --j;
+        }
+        a[j + 1] = x;
+      }
+      for (int i = 0; i < len; ++i) seg_rows[b + i] = a[i];
+    }
+  }
+  __syncthreads();
+  const int nl = n_longs;
+  int32_t* flat = &buf[0][0];
+  constexpr int FLAT = 256 * (SHORT_SEG + 1);
+  for (int i = 0; i < nl; ++i) {
+    const int32_t sg = longs[i];
+    const int32_t b = seg_ptr[sg], len = seg_ptr[sg + 1] - b;
+    const bool in_lds = len <= FLAT;
+    const int32_t* src = in_lds ? flat : scratch + b;
+    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
+      if (in_lds) flat[k] = seg_rows[b + k];
+      else scratch[b + k] = seg_rows[b + k];
+    }
+    __syncthreads();
+    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
+      const int32_t x = src[k];
+      int32_t rank = 0;
+      for (int32_t j = 0; j < len; ++j) rank += src[j] < x ? 1 : 0;
+      seg_rows[b + rank] = x;
+    }
+    __syncthreads();
+  }
+}
+
 bool use_counting() {
   static const bool c = [] {
     const char* e = getenv("LLP_DEDUP_SORT");
@@ -478,10 +534,17 @@ static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, i
                      seg_rows);
   LLP_LAUNCH_CHECK();
   const int64_t ubound = R < num_nodes ? R : num_nodes;
-  hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
-                     seg_rows, long_list, n_long);
-  LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows, scratch);
+  static const bool two_pass = getenv("LLP_SEGSORT_2PASS") != nullptr;   // A/B: the old short + long launches
+  if (two_pass) {
+    hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
+                       seg_rows, long_list, n_long);
+    LLP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows,
+                       scratch);
+  } else {
+    hipLaunchKernelGGL(segsort_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr, seg_rows,
+                       scratch);
+  }
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

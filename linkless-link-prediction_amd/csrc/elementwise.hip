@@ -396,9 +396,11 @@ __global__ void convert_kernel(int src_bf16, int dst_bf16, int64_t n, const void
   }
 }
 
-__global__ void accumulate_kernel(int64_t n, const float* __restrict__ src, float weight, double* __restrict__ dst) {
+__global__ void accumulate_kernel(int64_t n, const float* __restrict__ src, float weight, double* __restrict__ dst,
+                                  int64_t* __restrict__ ctr) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) dst[i] += (double)src[i] * (double)weight;
+  if (ctr && i == 0) *ctr += 1;
 }
 
 int64_t max_chunks_of(int64_t max_numel) { return (max_numel + OPT_CHUNK - 1) / OPT_CHUNK; }
@@ -539,7 +541,7 @@ extern "C" int llp_convert(int src_dtype, int dst_dtype, int64_t n, const void* 
 extern "C" int llp_accumulate(int64_t n, const float* src, float weight, double* dst, void* stream) {
   LLP_CHECK_ARG(src && dst, "llp_accumulate: null pointer");
   hipLaunchKernelGGL(accumulate_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, src, weight,
-                     dst);
+                     dst, nullptr);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
@@ -549,6 +551,14 @@ extern "C" int llp_zero(void* p, int64_t bytes, void* stream) {
   if (bytes == 0) return LLP_OK;
   hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
   if (e != hipSuccess) return llp::set_error((int)e, "llp_zero: %s", hipGetErrorString(e));
+  return LLP_OK;
+}
+
+extern "C" int llp_step_end(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, void* stream) {
+  LLP_CHECK_ARG(loss && loss_sum && step_ctr, "llp_step_end: null pointer");
+  hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (int64_t)1, loss, weight, loss_sum,
+                     step_ctr);
+  LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
 

@@ -366,13 +366,18 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t R, int64_t H, const
 // partial sums per lane so four loads are in flight, then an LDS tree over the
 // lanes.  (One column chain of ~1,000 dependent loads per 16 lanes took ~20 us.)
 constexpr int SUM_CB = 4;
-__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int64_t nslab, int64_t H,
-                                                       float* __restrict__ out, int accumulate) {
+struct SumJob { const float* slab; int64_t nslab, H; float* out; };
+// blocks [0, nblk0) take job 0 (the weight-gradient columns), the rest job 1 (the bias)
+__global__ __launch_bounds__(256) void slab_sum_kernel(SumJob j0, SumJob j1, int64_t nblk0, int accumulate) {
   __shared__ float red[256];
+  const bool second = (int64_t)blockIdx.x >= nblk0;
+  const SumJob& j = second ? j1 : j0;
+  const float* __restrict__ slab = j.slab;
+  const int64_t nslab = j.nslab, H = j.H;
   const int cb = H >= SUM_CB ? SUM_CB : 1;
   const int nl = 256 / cb;
   const int cl = threadIdx.x % cb, sl = threadIdx.x / cb;
-  const int64_t n = (int64_t)blockIdx.x * cb + cl;
+  const int64_t n = ((int64_t)blockIdx.x - (second ? nblk0 : 0)) * cb + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (n < H) {
     int64_t i = sl;
@@ -392,7 +397,7 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   }
   if (sl == 0 && n < H) {
     const float v = red[cl];
-    out[n] = accumulate ? out[n] + v : v;
+    j.out[n] = accumulate ? j.out[n] + v : v;
   }
 }
 
@@ -487,13 +492,11 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
     }
     LLP_LAUNCH_CHECK();
   }
-  if (dw) {
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(ceil_div_u(H, H >= SUM_CB ? SUM_CB : 1)), dim3(256), 0, s, slab, ns, H,
-                       dw, accumulate);
-    LLP_LAUNCH_CHECK();
-  }
-  if (db) {
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(1), dim3(256), 0, s, slab_b, ns, (int64_t)1, db, accumulate);
+  if (dw || db) {   // the dw columns and the db scalar in one launch
+    const SumJob jw{slab, ns, H, dw}, jb{slab_b, ns, (int64_t)1, db};
+    const int64_t nbw = dw ? ceil_div_u(H, H >= SUM_CB ? SUM_CB : 1) : 0;
+    hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)(nbw + (db ? 1 : 0))), dim3(256), 0, s, dw ? jw : jb, jb,
+                       nbw > 0 ? nbw : (int64_t)1, accumulate);
     LLP_LAUNCH_CHECK();
   }
   return LLP_OK;

@@ -95,7 +95,108 @@ __global__ void pair_index_kernel(int64_t B, int64_t C, const int32_t* __restric
   ib[t] = samples[b * (C + 1) + 1 + c];
 }
 
+// All of one minibatch step's index building in one launch (the collab path: device
+// walks + randint negatives): the thread ranges do exactly what context_walk_kernel,
+// context_neg_kernel, randint_pairs_kernel, build_targets_kernel and pair_index_kernel
+// do, with the same Philox draws, and each writes every array slot its value lands in
+// (samples, target, the teacher's pair index) instead of a later kernel copying it.
+struct MbSample {
+  const int32_t* rowptr; const int32_t* col; int64_t num_nodes;
+  const int32_t* start; int64_t B, b_offset; int n_walks, walk_len, ps_nb, rw_step; int64_t nneg, C, C1;
+  uint64_t seed; const int64_t* step_ctr; int64_t stream_offset;
+  const int32_t* pairs; const int32_t* perm; int64_t P, P_total, p_offset, neg_stream;
+  int32_t* samples; int32_t* neg; int32_t* target; int32_t* t_ia; int32_t* t_ib;
+};
+
+__global__ void minibatch_sample_kernel(MbSample a) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nw = a.B * a.n_walks, nn = a.B * a.nneg, BC1 = a.B * a.C1, n_lab = 2 * a.P;
+  const int64_t step = *a.step_ctr;
+  if (t < nw) {   // walk w of anchor b (context_walk_kernel)
+    const int64_t b = t % a.B;
+    const int w = (int)(t / a.B);
+    const uint64_t stream = (uint64_t)(16 * step + a.stream_offset + w);
+    const int64_t bg = b + a.b_offset;
+    const int32_t anchor = a.start[b];
+    int32_t cur = anchor;
+    if (w == 0) { a.samples[b * a.C1] = anchor; a.target[b * a.C1] = anchor; }
+    const int64_t colbase = a.ps_nb ? (int64_t)w * a.walk_len : 0;
+    for (int l = 0; l < a.walk_len; ++l) {
+      const uint32_t x = philox_u32(a.seed, stream, (uint64_t)(bg * a.walk_len + l));
+      const int32_t lo = a.rowptr[cur];
+      const int32_t deg = a.rowptr[cur + 1] - lo;
+      if (deg > 0) cur = a.col[lo + uniform_index(x, deg)];
+      const int64_t c = colbase + l;          // context column c + 1 of row b
+      a.samples[b * a.C1 + c + 1] = cur;
+      a.target[b * a.C1 + c + 1] = cur;
+      a.t_ia[b * a.C + c] = anchor;
+      a.t_ib[b * a.C + c] = cur;
+    }
+    return;
+  }
+  int64_t u = t - nw;
+  if (u < nn) {   // context negative q of anchor b (context_neg_kernel)
+    const uint64_t stream = (uint64_t)(16 * step + a.stream_offset + a.rw_step);
+    const int64_t b = u / a.nneg, q = u % a.nneg;
+    const uint32_t x = philox_u32(a.seed, stream, (uint64_t)((b + a.b_offset) * a.nneg + q));
+    const int32_t v = (int32_t)randint_index(x, a.num_nodes);
+    const int64_t c = a.C - a.nneg + q;       // negatives follow the walk columns
+    a.samples[b * a.C1 + c + 1] = v;
+    a.target[b * a.C1 + c + 1] = v;
+    a.t_ia[b * a.C + c] = a.start[b];
+    a.t_ib[b * a.C + c] = v;
+    return;
+  }
+  u -= nn;
+  if (u < 2 * a.P) {   // label negative (randint_pairs_kernel) -> neg[side][i], target
+    const uint64_t stream = (uint64_t)(16 * step + a.neg_stream);
+    const int64_t side = u / a.P, i = u % a.P;
+    const uint64_t draw = (uint64_t)(side * a.P_total + a.p_offset + i);
+    const int32_t v = (int32_t)randint_index(philox_u32(a.seed, stream, draw), a.num_nodes);
+    a.neg[u] = v;
+    a.target[BC1 + side * n_lab + a.P + i] = v;
+    return;
+  }
+  u -= 2 * a.P;
+  if (u < 2 * a.P) {   // label positive pos_train_edge[link_perm] (build_targets_kernel)
+    const int64_t side = u / a.P, i = u % a.P;
+    a.target[BC1 + side * n_lab + i] = a.pairs[2 * (int64_t)a.perm[i] + side];
+  }
+}
+
 }  // namespace
+
+extern "C" int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
+                                    const int32_t* start, int64_t B, int64_t b_offset, int ps_method, int rw_step,
+                                    int hops, int ns_rate, uint64_t seed, const int64_t* step_ctr,
+                                    int64_t stream_offset, const int32_t* pairs, const int32_t* perm, int64_t P,
+                                    int64_t P_total, int64_t p_offset, int64_t neg_stream_offset, int32_t* samples,
+                                    int32_t* neg, int32_t* target, int32_t* t_ia, int32_t* t_ib, void* stream) {
+  LLP_CHECK_ARG(rowptr && col && start && samples && step_ctr && target && t_ia && t_ib &&
+                    (P == 0 || (pairs && perm && neg)),
+                "llp_minibatch_sample: null pointer");
+  LLP_CHECK_ARG(ps_method == 0 || ps_method == 1, "llp_minibatch_sample: ps_method must be 0 (rw) or 1 (nb)");
+  LLP_CHECK_ARG(rw_step >= 1 && hops >= 1 && ns_rate >= 0 && rw_step < 15, "llp_minibatch_sample: bad step/hops");
+  LLP_CHECK_ARG(p_offset + P <= P_total, "llp_minibatch_sample: shard out of range");
+  MbSample a;
+  a.rowptr = rowptr; a.col = col; a.num_nodes = num_nodes; a.start = start; a.B = B; a.b_offset = b_offset;
+  a.n_walks = ps_method == 1 ? rw_step : 1;
+  a.walk_len = ps_method == 1 ? hops : rw_step * hops;
+  a.ps_nb = ps_method;
+  a.rw_step = rw_step;
+  a.nneg = (int64_t)rw_step * hops * ns_rate;
+  a.C = (int64_t)rw_step * hops * (1 + ns_rate);
+  a.C1 = a.C + 1;
+  a.seed = seed; a.step_ctr = step_ctr; a.stream_offset = stream_offset;
+  a.pairs = pairs; a.perm = perm; a.P = P; a.P_total = P_total; a.p_offset = p_offset;
+  a.neg_stream = neg_stream_offset;
+  a.samples = samples; a.neg = neg; a.target = target; a.t_ia = t_ia; a.t_ib = t_ib;
+  const int64_t total = B * a.n_walks + B * a.nneg + 4 * P;
+  if (total == 0) return LLP_OK;
+  hipLaunchKernelGGL(minibatch_sample_kernel, dim3(ceil_div_u(total, 256)), dim3(256), 0, (hipStream_t)stream, a);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
 
 extern "C" int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
                                    const int32_t* start, int64_t B, int64_t b_offset, int ps_method, int rw_step,

@@ -48,6 +48,10 @@ _OVERLAP = int(os.environ.get("LLP_OVERLAP", "0"))
 # weight gradient runs the lean TN loop (gathered operands fall back to the staggered one);
 # LLP_GATHER_X=0 keeps the gathered GEMM operands (A/B knob)
 _GATHER_X = os.environ.get("LLP_GATHER_X", "1") != "0"
+# minibatch step with device sampling and randint negatives (collab): one launch builds the
+# samples, negatives, target rows and teacher pair index (llp_minibatch_sample, bit-identical
+# to the five separate kernels); LLP_FUSED_SAMPLE=0 runs them separately (A/B knob)
+_FUSED_SAMPLE = os.environ.get("LLP_FUSED_SAMPLE", "1") != "0"
 
 # dropout Philox keys (EngineBase._dropout): one per module, one stream per layer and step
 DROP_ENCODER, DROP_PREDICTOR, DROP_TEACHER_PRED = 0, 1, 2
@@ -672,10 +676,14 @@ class DistillEngine(EngineBase):
             lab = torch.arange(P2, device=self.dev, dtype=torch.int64)
             ia_lab = B * C1 + lab
             ib_lab = B * C1 + P2 + lab
-            ia = torch.cat([ia_ctx, ia_lab]).to(torch.int32).contiguous()
-            ib = torch.cat([ib_ctx, ib_lab]).to(torch.int32).contiguous()
-            self._bufs[key] = (ia, ib)
-        return self._bufs[key]
+            iab = torch.stack([torch.cat([ia_ctx, ia_lab]), torch.cat([ib_ctx, ib_lab])]).to(torch.int32).contiguous()
+            self._bufs[key] = (iab[0], iab[1], iab)
+        return self._bufs[key][:2]
+
+    def _rows_index_flat(self, B, C, P2):
+        """_rows_index's two arrays as one contiguous [2 * R2] index (one gather launch)."""
+        self._rows_index(B, C, P2)
+        return self._bufs[("rows", B, C, P2)][2].view(-1)
 
     # ------------------------------------------------------------------ the step
     def step_minibatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
@@ -704,21 +712,33 @@ class DistillEngine(EngineBase):
         dt, dc = self.dtype, self.dc
 
         # ---- a1-a3: negatives and samples (src/main.py:80-84,93)
-        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
-        n_lab = P + n_neg                  # train_edges columns (src/main.py:86)
-        R1 = B * C1 + 2 * n_lab
-        R2 = B * C + n_lab
         samp = self._buf("samples", (B, C1), torch.int32)
-        if samples is not None:
-            samp.copy_(samples.to(torch.int32))
-        else:
-            K.context_sampler(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
-                              self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
-        target = self._buf("target", (R1,), torch.int32)
-        K.build_targets(B, C1, samp, pairs, link_ids, None, 0, P, negb, target, n_neg=n_neg)
         t_ia = self._buf("t_ia", (B * C,), torch.int32)
         t_ib = self._buf("t_ib", (B * C,), torch.int32)
-        K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
+        if _FUSED_SAMPLE and samples is None and neg is None and not dense_negatives:
+            # collab path: walks, context negatives, randint label negatives, the student's
+            # target rows and the teacher's pair index in one launch (llp_minibatch_sample)
+            negb, n_neg, n_neg_total = self._buf("neg", (2, max(P, 1)), torch.int32), P, P_total
+            n_lab = P + n_neg
+            R1 = B * C1 + 2 * n_lab
+            R2 = B * C + n_lab
+            target = self._buf("target", (R1,), torch.int32)
+            K.minibatch_sample(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
+                               self.seed, self.step_ctr, 0, pairs, link_ids, P, P_total, p_offset, 15, samp, negb,
+                               target, t_ia, t_ib, b_offset=b_offset)
+        else:
+            negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+            n_lab = P + n_neg                  # train_edges columns (src/main.py:86)
+            R1 = B * C1 + 2 * n_lab
+            R2 = B * C + n_lab
+            if samples is not None:
+                samp.copy_(samples.to(torch.int32))
+            else:
+                K.context_sampler(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
+                                  self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
+            target = self._buf("target", (R1,), torch.int32)
+            K.build_targets(B, C1, samp, pairs, link_ids, None, 0, P, negb, target, n_neg=n_neg)
+            K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
         ia, ib = self._rows_index(B, C, n_lab)
         p_drop = float(a.dropout)
         overlap = _OVERLAP if (self.overlap and self._seg is None) else 0
@@ -746,10 +766,9 @@ class DistillEngine(EngineBase):
             seg_rows = self._buf("seg_rows", (R1,), torch.int32)
             wsd = self._buf("ws_dedup", (K.dedup_ws_bytes(self.N, R1) // 4 + 16,), torch.float32)
             K.dedup_rows(self.N, R1, target, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
-            ia_h = self._buf("ia_u", (R2,), torch.int32)
-            ib_h = self._buf("ib_u", (R2,), torch.int32)
-            K.gather_i32(ia, pos, ia_h)
-            K.gather_i32(ib, pos, ib_h)
+            iab_h = self._buf("iab_u", (2, R2), torch.int32)   # both pair sides in one gather
+            K.gather_i32(self._rows_index_flat(B, C, n_lab), pos, iab_h.view(-1))
+            ia_h, ib_h = iab_h[0], iab_h[1]
             # No host read of U: the student kernels are launched for the bound
             # min(R1, N) and run on the *n_unique live rows (llp_operand.rows_dev),
             # so the step stays asynchronous and hipGraph-capturable.
@@ -835,8 +854,7 @@ class DistillEngine(EngineBase):
                 dh = dh_rows
         self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap, x_rows=x_rows)
         self._allreduce_and_update()
-        K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
-        K.increment(self.step_ctr)
+        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
 
     # ------------------------------------------------------------------ full-batch step
     def step_fullbatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
@@ -956,8 +974,7 @@ class DistillEngine(EngineBase):
                 K.convert(dh32, dh)
         self._student_backward(dh, N, None, acts, p_drop)
         self._allreduce_and_update()
-        K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
-        K.increment(self.step_ctr)
+        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
         return n_neg
 
     def capture_minibatch(self, anchors, link_ids, pairs, **kw):

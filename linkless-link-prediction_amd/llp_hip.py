@@ -73,6 +73,9 @@ _SIGS = {
                                           c_vp, c_i64, c_vp, c_vp]),
     "llp_gather_i32": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_gather_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "llp_minibatch_sample": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
+                                     c_i64, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp]),
     "llp_hadamard_bwd_scatter": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_context_sampler": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
                                     c_i64, c_vp, c_vp]),
@@ -99,6 +102,7 @@ _SIGS = {
     "llp_convert": (c_int, [c_int, c_int, c_i64, c_vp, c_vp, c_vp]),
     "llp_accumulate": (c_int, [c_i64, c_vp, c_f32, c_vp, c_vp]),
     "llp_increment": (c_int, [c_vp, c_vp]),
+    "llp_step_end": (c_int, [c_vp, c_f32, c_vp, c_vp, c_vp]),
     "llp_zero": (c_int, [c_vp, c_i64, c_vp]),
     "llp_hadamard_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_relu_bwd": (c_int, [c_int, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
@@ -332,6 +336,18 @@ def context_sampler(rowptr, col, num_nodes, start, B, ps_method, rw_step, hops, 
                                 stream_offset, samples.data_ptr(), stream_ptr()), "llp_context_sampler")
 
 
+def minibatch_sample(rowptr, col, num_nodes, start, B, ps_method, rw_step, hops, ns_rate, seed, step_ctr,
+                     stream_offset, pairs, perm, P, P_total, p_offset, neg_stream_offset, samples, neg, target, t_ia,
+                     t_ib, b_offset=0):
+    """context_sampler + randint_pairs + build_targets + pair_index_from_samples in one launch."""
+    L = lib()
+    check(L.llp_minibatch_sample(rowptr.data_ptr(), col.data_ptr(), num_nodes, start.data_ptr(), B, b_offset,
+                                 1 if ps_method == "nb" else 0, rw_step, hops, ns_rate, seed, step_ctr.data_ptr(),
+                                 stream_offset, pairs.data_ptr(), perm.data_ptr(), P, P_total, p_offset,
+                                 neg_stream_offset, samples.data_ptr(), neg.data_ptr(), target.data_ptr(),
+                                 t_ia.data_ptr(), t_ib.data_ptr(), stream_ptr()), "llp_minibatch_sample")
+
+
 def randint_pairs(num_nodes, n, seed, step_ctr, stream_offset, out, n_total=None, offset=0):
     L = lib()
     n_total = n if n_total is None else n_total
@@ -482,6 +498,11 @@ def accumulate(src, weight, dst):
 def zero_(t):
     L = lib()
     check(L.llp_zero(t.data_ptr(), t.numel() * t.element_size(), stream_ptr()), "llp_zero")
+
+
+def step_end(loss, weight, loss_sum, ctr):
+    L = lib()
+    check(L.llp_step_end(loss.data_ptr(), weight, loss_sum.data_ptr(), ctr.data_ptr(), stream_ptr()), "llp_step_end")
 
 
 def increment(ctr):

@@ -308,6 +308,39 @@ def test_context_sampler_bit_exact(ps, rw_step, hops, ns_rate, sorted_):
     assert np.array_equal(out2.cpu().numpy(), ref[60:])
 
 
+@pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 2, 3, 0)])
+@pytest.mark.parametrize("b_off,p_off", [(0, 0), (40, 300)])
+def test_minibatch_sample_equals_separate_kernels(ps, rw_step, hops, ns_rate, b_off, p_off):
+    """llp_minibatch_sample == context_sampler + randint_pairs + build_targets +
+    pair_index_from_samples, bit for bit (also for a rank's shard)."""
+    import llp_engine
+    k = K()
+    rng = np.random.default_rng(11)
+    N, B, P, P_total, E = 400, 77, 150, 600, 2000
+    u, v = rng.integers(0, N, E), rng.integers(0, N, E)
+    ei = np.stack([np.stack([u, v], 1), np.stack([v, u], 1)], 1).reshape(-1, 2).T
+    ei = ei[:, ei[0] % 13 != 5]                                   # some isolated nodes
+    rowptr, col = (torch.from_numpy(a).to(DEV) for a in llp_engine.build_sampler_csr(ei[0], ei[1], N, False))
+    pairs = torch.from_numpy(np.stack([u, v], 1).astype(np.int32)).to(DEV)
+    start = torch.from_numpy(rng.permutation(N)[:B].astype(np.int32)).to(DEV)
+    perm = torch.from_numpy(rng.integers(0, E, P).astype(np.int32)).to(DEV)
+    C = rw_step * hops * (1 + ns_rate)
+    C1, R1 = C + 1, B * (C + 1) + 4 * P
+    ctr = torch.tensor([5], dtype=torch.int64, device=DEV)
+    s1, s2 = (torch.full((B, C1), -1, dtype=torch.int32, device=DEV) for _ in range(2))
+    n1, n2 = (torch.full((2, P), -1, dtype=torch.int32, device=DEV) for _ in range(2))
+    t1, t2 = (torch.full((R1,), -1, dtype=torch.int32, device=DEV) for _ in range(2))
+    a1, a2, b1, b2 = (torch.full((B * C,), -1, dtype=torch.int32, device=DEV) for _ in range(4))
+    k.context_sampler(rowptr, col, N, start, B, ps, rw_step, hops, ns_rate, 31, ctr, 0, s1, b_offset=b_off)
+    k.randint_pairs(N, P, 31, ctr, 15, n1, n_total=P_total, offset=p_off)
+    k.build_targets(B, C1, s1, pairs, perm, None, 0, P, n1, t1)
+    k.pair_index_from_samples(B, C, s1, a1, b1)
+    k.minibatch_sample(rowptr, col, N, start, B, ps, rw_step, hops, ns_rate, 31, ctr, 0, pairs, perm, P, P_total,
+                       p_off, 15, s2, n2, t2, a2, b2, b_offset=b_off)
+    for x, y in ((s1, s2), (n1, n2), (t1, t2), (a1, a2), (b1, b2)):
+        assert torch.equal(x, y)
+
+
 def test_random_walk_follows_unsorted_csr_semantics():
     """Q1: with coalesced=False the walk indexes col in array order."""
     import llp_engine
