@@ -15,6 +15,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 namespace {
 
 __global__ void mark_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ mark) {
@@ -127,6 +129,20 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, 
 // Against the two-kernel path this drops the [R1, H] row-gradient buffer: its write
 // and its read (2 x 1.5 GB at the collab shape) for a second read of the context
 // pairs' dZ rows.  drow: the 'inner' predictor's per-pair scalar (dZ = NULL).
+template <typename T>
+__device__ __forceinline__ void unpack16(const uint4 r, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t u[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  } else {
+    v[0] = __uint_as_float(r.x); v[1] = __uint_as_float(r.y); v[2] = __uint_as_float(r.z); v[3] = __uint_as_float(r.w);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void load16(const T* p, float* v) {
   const uint4 r = *reinterpret_cast<const uint4*>(p);
@@ -258,6 +274,110 @@ __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
     for (int i = 0; i < E; ++i) acc[i] += v0[i];
   }
   *reinterpret_cast<uint4*>(dh + u * ldo + col) = V8<T>::pack(acc);
+}
+
+// Same sums, NPW nodes per wave (LPN = 64 / NPW lanes per node; lane l of a node owns
+// the 16-B chunks l, l + LPN, ..., NCH of them: H / E = LPN * NCH).  The kernel above
+// walks a node's rows two at a time, each behind a chain of dependent loads (row id ->
+// slot of the partner -> the two operand rows), so a node costs about three memory
+// latencies per pair of rows and the launch is latency-bound (≈3.4 TB/s at the collab
+// shape).  Here lane j of a node resolves row j of its segment (row id, pair row z,
+// partner slot, anchor flag, inner scalar) in one parallel step, and the operand loads
+// of G rows at a time are issued together from the broadcast descriptors; several
+// nodes per wave keep more of those chains in flight.  Same values, same f32 additions
+// in row order: bit-identical to the kernel above.
+template <typename T, int NCH, int G, int NPW>
+__global__ __launch_bounds__(256) void hadamard_bwd_segments_wave_kernel(
+    int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ pos, const T* __restrict__ dZ,
+    const float* __restrict__ drow, const T* __restrict__ h, const T* __restrict__ arow, T* __restrict__ dh,
+    int64_t ldo, const int32_t* __restrict__ u_dev) {
+  constexpr int E = V8<T>::E;
+  constexpr int LPN = 64 / NPW;
+  const int lane = threadIdx.x & 63;
+  const int nl = lane % LPN, nbase = lane - nl;   // lane within the node, first lane of the node
+  const int64_t u = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * NPW + lane / LPN;
+  if (u_dev && (int64_t)*u_dev < U) U = *u_dev;
+  const bool live = u < U;
+  const int64_t C1 = C + 1, base = B * C1;
+  float acc[NCH][E];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[j][i] = 0.f;
+  const int beg = live ? seg_ptr[u] : 0, end = live ? seg_ptr[u + 1] : 0;
+  // every node of the wave runs the same number of rounds (the shuffles need all lanes)
+  int len = end - beg;
+#pragma unroll
+  for (int o = LPN; o < 64; o <<= 1) len = max(len, __shfl_xor(len, o, 64));
+  for (int k0 = 0; k0 < len; k0 += LPN) {
+    const int cnt = max(0, min(LPN, end - beg - k0));   // this node's rows in this round
+    int64_t z = 0, hr = 0;
+    int anch = 0;
+    float sc = 0.f;
+    if (nl < cnt) {   // lane nl: descriptor of the node's row beg + k0 + nl
+      const int64_t r = rows[beg + k0 + nl];
+      if (r < base) {
+        const int64_t b = r / C1, jj = r - b * C1;
+        anch = jj == 0;
+        z = anch ? b : b * C + jj - 1;
+        hr = anch ? 0 : pos[b * C1];
+      } else {
+        const int64_t i = r - base;
+        const bool src_side = i < L2;
+        const int64_t li = src_side ? i : i - L2;
+        z = B * C + li;
+        hr = pos[src_side ? base + L2 + li : base + li];
+      }
+      if (drow && !anch) sc = drow[z];
+    }
+    const int32_t zl = (int32_t)z, hl = (int32_t)hr;
+    int cmax = cnt;
+#pragma unroll
+    for (int o = LPN; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
+    for (int g0 = 0; g0 < cmax; g0 += G) {
+      uint4 ra[G][NCH], rh[G][NCH];
+      int an[G];
+      float s[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int src = nbase + min(g0 + g, max(cnt - 1, 0));
+        const int64_t zg = __shfl(zl, src, 64), hg = __shfl(hl, src, 64);
+        an[g] = __shfl(anch, src, 64);
+        s[g] = __shfl(sc, src, 64);
+        const T* pa = an[g] ? arow + zg * H : (dZ ? dZ + zg * H : h);
+        const T* ph = h + hg * H;
+        if (g0 + g < cnt) {
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            const int64_t col = (int64_t)(nl + LPN * j) * E;
+            ra[g][j] = *reinterpret_cast<const uint4*>(pa + col);
+            rh[g][j] = *reinterpret_cast<const uint4*>(ph + col);
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (g0 + g < cnt) {
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            float va[E], vh[E];
+            unpack16<T>(ra[g][j], va);
+            unpack16<T>(rh[g][j], vh);
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+              const float d = (drow && !an[g]) ? s[g] : va[i];
+              acc[j][i] += an[g] ? va[i] : round_to<T>(d * vh[i]);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+    *reinterpret_cast<uint4*>(dh + u * ldo + (int64_t)(nl + LPN * j) * E) = V8<T>::pack(acc[j]);
 }
 
 // out row r = src row idx[r] for r < min(n, *count): 16-byte chunks, one thread each
@@ -670,6 +790,36 @@ extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_
       hipLaunchKernelGGL(hadamard_anchor_rows_kernel<float>, dim3(ceil_div_u(B, spb)), dim3(256), 0, s, B, C, H,
                          (const float*)dZ, drow, (const float*)h, pos, (float*)anchor_rows);
     LLP_LAUNCH_CHECK();
+  }
+  // NPW nodes per wave when a row is 64 * NCH 16-B chunks (LLP_SEG_WAVE=0: the thread-group
+  // kernel; LLP_SEG_NPW = 1 (default), 2 or 4 nodes per wave: 487, 530, 633 us at the collab shape)
+  static const bool wave_env = getenv("LLP_SEG_WAVE") ? atoi(getenv("LLP_SEG_WAVE")) != 0 : true;
+  static const int npw_env = getenv("LLP_SEG_NPW") ? atoi(getenv("LLP_SEG_NPW")) : 1;
+  const int npw = (npw_env == 2 || npw_env == 4) ? npw_env : 1;
+  const int nch = (cpr % 64 == 0) ? (int)(cpr * npw / 64) : 0;   // chunks per lane
+  if (wave_env && (nch == 1 || nch == 2 || nch == 4 || nch == 8)) {
+    auto launch = [&](auto kern, auto* dz, auto* hh, auto* ar, auto* out) {
+      hipLaunchKernelGGL(kern, dim3(ceil_div_u(U, 4 * npw)), dim3(256), 0, s, U, B, C, L2, H, seg_ptr, rows, pos, dz,
+                         drow, hh, ar, out, ld_dh, u_dev);
+    };
+    auto pick = [&](auto* dz, auto* hh, auto* ar, auto* out) {
+      using TT = std::remove_const_t<std::remove_pointer_t<decltype(dz)>>;
+      if (npw == 1 && nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, 1, 8, 1>, dz, hh, ar, out);
+      else if (npw == 1 && nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 1>, dz, hh, ar, out);
+      else if (npw == 1 && nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 1>, dz, hh, ar, out);
+      else if (npw == 2 && nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 2>, dz, hh, ar, out);
+      else if (npw == 2 && nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 2>, dz, hh, ar, out);
+      else if (npw == 2 && nch == 8) launch(hadamard_bwd_segments_wave_kernel<TT, 8, 1, 2>, dz, hh, ar, out);
+      else if (npw == 4 && nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 4>, dz, hh, ar, out);
+      else if (npw == 4 && nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 4>, dz, hh, ar, out);
+      else launch(hadamard_bwd_segments_wave_kernel<TT, 8, 1, 4>, dz, hh, ar, out);
+    };
+    if (dtype == LLP_BF16)
+      pick((const bf16_t*)dZ, (const bf16_t*)h, (const bf16_t*)anchor_rows, (bf16_t*)dh);
+    else
+      pick((const float*)dZ, (const float*)h, (const float*)anchor_rows, (float*)dh);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
   }
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(hadamard_bwd_segments_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,

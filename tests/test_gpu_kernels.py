@@ -541,12 +541,15 @@ def test_gather_rows(dtype, F):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("inner", [False, True])
-def test_hadamard_bwd_segments(dtype, inner):
+@pytest.mark.parametrize("N,H", [(400, 256), (400, 1024), (5, 512)])
+def test_hadamard_bwd_segments(dtype, inner, N, H):
     """Fused Hadamard backward reduced onto unique nodes == per-row gradients
-    (anchor rows sum their C contexts) index-added by node, f32."""
+    (anchor rows sum their C contexts) index-added by node, f32.  H picks the
+    thread-group kernel (bf16 H=256) or the wave-per-node kernel (rows of 64, 128
+    or 256 16-B chunks); N=5 gives segments longer than one wave's 64 rows."""
     k = K()
     g = torch.Generator().manual_seed(5)
-    N, B, C, L2, H = 400, 37, 6, 53, 256
+    B, C, L2 = 37, 6, 53
     R1 = B * (C + 1) + 2 * L2
     R2 = B * C + L2
     target = torch.randint(0, N, (R1,), generator=g, dtype=torch.int32)

@@ -33,6 +33,7 @@ def main():
     g.manual_seed(0)
     R1, R2, N0 = 747_214, 603_032, 235_868
     x = torch.randn(N0, 128, device=dev, dtype=bf, generator=g)
+    xg = x[:225334].contiguous()
     idx = torch.randint(0, N0, (R1,), device=dev, dtype=torch.int32, generator=g)
     h = torch.randn(R1, 1024, device=dev, dtype=bf, generator=g)
     W = (torch.randn(1024, 1024, device=dev, generator=g) * 0.03).to(bf)
@@ -79,6 +80,9 @@ def main():
     cases = {
         "L1 fwd gather 747214x1024x128": (lambda: K.gemm_nt(K.operand(x, idx), K.operand(W1), R1, 1024, 128, out, 1,
                                                             bias=bias, act=K.ACT_RELU), 2 * R1 * 1024 * 128, out),
+        "U L0 fwd 225334x1024x128": (lambda: K.gemm_nt(K.operand(xg), K.operand(W1), 225334, 1024, 128, out[:225334],
+                                                       1, bias=bias, act=K.ACT_RELU, aux=mask[:225334]),
+                                     2 * 225334 * 1024 * 128, out),
         "L2 fwd 747214x1024x1024": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1, bias=bias,
                                                       act=K.ACT_RELU), 2 * R1 * 1024 * 1024, out),
         "L2 dgrad relu-bwd 747214x1024x1024": (lambda: K.gemm_nt(K.operand(h), K.operand(W), R1, 1024, 1024, out, 1,
