@@ -206,13 +206,14 @@ def test_gemm_tn_gathered_hadamard_operand():
 
 # ------------------------------------------------------------------ heads, colsum
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
-def test_head_fwd_bwd_and_colsum(dt):
+@pytest.mark.parametrize("R,H", [(1000, 200), (150_000, 1024)])
+def test_head_fwd_bwd_and_colsum(dt, R, H):
+    """R=150k: ~18 four-row batches per thread (both halves of the ping-pong loop)."""
     k = K()
     g = torch.Generator().manual_seed(4)
     tdt = torch.float32 if dt == "fp32" else torch.bfloat16
-    R, H = 1000, 200
     Z = torch.relu(torch.randn(R, H, generator=g))
-    w = torch.randn(H, generator=g)
+    w = torch.randn(H, generator=g) * (200 / H) ** 0.5   # logits O(1) at every H
     b = torch.randn(1, generator=g)
     Zd = Z.to(DEV, tdt)
     Zr = Z if dt == "fp32" else _bf(Z)
@@ -231,11 +232,11 @@ def test_head_fwd_bwd_and_colsum(dt):
     ref_dZ = 1.5 * dlogit[:, None] * w[None, :] * (Zr > 0)
     tol = 1e-6 if dt == "fp32" else 1e-2
     assert torch.allclose(dZ.float().cpu(), ref_dZ, rtol=tol, atol=tol)
-    assert torch.allclose(dw.cpu(), dlogit @ Zr, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(dw.cpu(), dlogit @ Zr, rtol=1e-4, atol=1e-3 * max(1.0, (R / 1000) ** 0.5))
     assert torch.allclose(db.cpu(), dlogit.sum().reshape(1), rtol=1e-5, atol=1e-4)
     cs = torch.empty(H, device=DEV)
     k.colsum(Zd, R, H, cs, ws)
-    assert torch.allclose(cs.cpu(), Zr.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(cs.cpu(), Zr.sum(0), rtol=1e-5, atol=1e-3 * max(1.0, R / 1000))
 
 
 # ------------------------------------------------------------------ fused LLP loss
