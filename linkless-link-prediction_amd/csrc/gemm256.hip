@@ -17,6 +17,8 @@
 // stores; the ReLU-backward mask (aux) is read with the same 16-byte pattern.
 #include "llp_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int TM = 256, TN = 256, TK = 64;
@@ -52,6 +54,7 @@ struct P256 {
   const int32_t* m_dev;
   int64_t head_ld;
   int nt_store;   // epilogue stores with the non-temporal hint (default; LLP_GEMM_NT_STORE=0 turns it off)
+  int lean_epi;   // pp8 mode kernels: lean epilogue on full tiles (default; LLP_GEMM_LEAN_EPI=0 turns it off)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -1026,6 +1029,136 @@ __device__ __forceinline__ void epilogue_direct(const P256& p, float4_t (&acc)[4
 }
 
 // ---------------------------------------------------------------------------
+// Lean epilogue of the pp8 kernel for FULL 256 x 256 tiles of the per-call modes
+// EPI_FWD_RELU / EPI_FWD_NONE / EPI_BWD_MASK (same values and bits as epilogue_t).
+// epilogue_t spends ~1,450 VALU per wave on a ReLU-forward tile (per-element
+// bias loads and f32 ReLU, 64-bit store addressing and bounds tests per store,
+// per-bit mask compares); here:
+//  * bias from registers loaded before the main loop, packed f32 adds (v_pk_add /
+//    v_pk_fma as before), ReLU AFTER rounding as a packed int16 max on the bf16
+//    pair (identical bits for every non-NaN value: a negative bf16 is a negative
+//    int16; a NaN now propagates like torch.relu instead of becoming 0);
+//  * LDS staging at per-thread bases + compile-time offsets;
+//  * stores from a uniform tile-corner base (SGPRs, advanced per 16 rows) plus one
+//    32-bit lane offset, no bounds tests;
+//  * ReLU mask byte of 8 non-negative bf16: nonzero tests as packed u16 min(x, 1),
+//    three shift-ors and a fold (11 VALU instead of ~35).
+template <int MODE>
+__device__ __forceinline__ bool lean_tile_ok(const P256& p, int64_t m0, int64_t n0) {
+  if (!p.lean_epi || m0 + TM > p.M || n0 + TN > p.N || (p.ldc & 7) || ((uintptr_t)p.C & 15)) return false;
+  if (MODE == EPI_FWD_RELU && p.mask_out && ((p.ld_mask & 3) || ((uintptr_t)p.mask_out & 3))) return false;
+  if (MODE == EPI_BWD_MASK && ((p.ld_mask & 15) || ((uintptr_t)p.mask_in & 15))) return false;
+  return true;
+}
+
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef short short2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float2_t v) {   // one v_cvt_pk_bf16_f32 (RNE, as f2bf)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ uint32_t relu_pk_bf16(uint32_t x) {   // v_pk_max_i16(x, 0)
+  const short2_t r = __builtin_elementwise_max(__builtin_bit_cast(short2_t, x), (short2_t){0, 0});
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t nz_pk_u16(uint32_t x, uint32_t ones) {   // v_pk_min_u16(x, 1): 1 per nonzero half
+  uint32_t r;   // (asm: hipcc turns the builtin min into per-half compares and selects)
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ones));
+  return r;
+}
+
+// 0xFFFF where bit B of `bits` is set | 0xFFFF0000 where bit B+1 is: two sign-extended
+// one-bit fields and a bitfield insert (hipcc makes ~10 VALU of the plain expression)
+template <int B>
+__device__ __forceinline__ uint32_t half_mask(uint32_t bits, uint32_t lo16) {   // lo16 = 0xFFFF (SGPR)
+  uint32_t lo, hi;
+  asm("v_bfe_i32 %0, %2, %3, 1\n\t"
+      "v_bfe_i32 %1, %2, %4, 1\n\t"
+      "v_bfi_b32 %0, %5, %0, %1"
+      : "=&v"(lo), "=&v"(hi)
+      : "v"(bits), "i"(B), "i"(B + 1), "s"(lo16));
+  return lo;
+}
+
+template <int MODE>
+__device__ __forceinline__ void epilogue_lean(const P256& p, float4_t (&acc)[4][8], const float4_t (&bvec)[4],
+                                              uint4* smem, int64_t m0, int64_t n0, int tid, int wm, int wn, int g,
+                                              int li) {
+  constexpr bool RELU = MODE == EPI_FWD_RELU;
+  constexpr bool BWD = MODE == EPI_BWD_MASK;
+  constexpr int ROWB = EPI_ROW_U4 * 16;   // bytes per staged row
+  uint8_t* mlds = reinterpret_cast<uint8_t*>(smem + SMEM_U4_EPI + 256);
+  if (BWD) {   // the tile's 256 x 32 mask bytes: one 16-B piece per thread (row tid/2, half tid&1)
+    const uint8_t* src = p.mask_in + (m0 + (tid >> 1)) * p.ld_mask + (n0 >> 3) + 16 * (tid & 1);
+    reinterpret_cast<uint4*>(mlds)[tid] = *reinterpret_cast<const uint4*>(src);
+  }
+  // phase 1: row wm*128 + im*16 + li, columns wn*64 + jn*16 + g*4 .. +3
+  char* sb = reinterpret_cast<char*>(smem) + (wm * 128 + li) * ROWB + (wn * 64 + g * 4) * 2;
+  const float2_t al = {p.alpha, p.alpha}, z2 = {0.f, 0.f};
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn) {
+    const float2_t b01 = {bvec[jn][0], bvec[jn][1]}, b23 = {bvec[jn][2], bvec[jn][3]};
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      float2_t v01 = {acc[jn][im][0], acc[jn][im][1]}, v23 = {acc[jn][im][2], acc[jn][im][3]};
+      if (BWD) {   // alpha * acc + 0 (v_pk_fma, as epilogue_t)
+        v01 = __builtin_elementwise_fma(v01, al, z2);
+        v23 = __builtin_elementwise_fma(v23, al, z2);
+      } else {   // acc + bias (zeros without a bias, as epilogue_t adds)
+        v01 = v01 + b01;
+        v23 = v23 + b23;
+      }
+      uint32_t lo = pk_bf16(v01), hi = pk_bf16(v23);
+      if (RELU) { lo = relu_pk_bf16(lo); hi = relu_pk_bf16(hi); }
+      *reinterpret_cast<uint2*>(sb + im * 16 * ROWB + jn * 32) = make_uint2(lo, hi);
+    }
+  }
+  __syncthreads();
+  // phase 2: chunk (row rl0 + 16 i, 16-B column chunk c) per iteration
+  const int rl0 = tid >> 5, c = tid & 31;
+  const char* rb = reinterpret_cast<const char*>(smem) + rl0 * ROWB + c * 16;
+  char* cbase = reinterpret_cast<char*>(p.C + m0 * p.ldc + n0);
+  const uint32_t toff = (uint32_t)((rl0 * p.ldc + c * 8) * 2);
+  const int64_t cstep = 16 * p.ldc * 2;
+  const bool mo = RELU && p.mask_out;
+  char* mbase = mo ? reinterpret_cast<char*>(p.mask_out + m0 * p.ld_mask + (n0 >> 3)) : nullptr;
+  const uint32_t moff = (uint32_t)(rl0 * p.ld_mask + c);
+  const int64_t mstep = 16 * p.ld_mask;
+  const uint32_t ones = 0x00010001u;
+  const uint32_t lo16 = __builtin_amdgcn_readfirstlane(0xFFFFu);
+  auto run = [&](auto NTS) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      uint4 v = *reinterpret_cast<const uint4*>(rb + i * 16 * ROWB);
+      if (BWD) {
+        const uint32_t bits = mlds[(rl0 + 16 * i) * 32 + c];
+        v.x &= half_mask<0>(bits, lo16);
+        v.y &= half_mask<2>(bits, lo16);
+        v.z &= half_mask<4>(bits, lo16);
+        v.w &= half_mask<6>(bits, lo16);
+      }
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 sv = {v.x, v.y, v.z, v.w};
+      u32x4* dst = reinterpret_cast<u32x4*>(cbase + i * cstep + toff);
+      if constexpr (decltype(NTS)::value) __builtin_nontemporal_store(sv, dst);
+      else *dst = sv;
+      if (RELU) {
+        if (mo) {
+          const uint32_t u = nz_pk_u16(v.x, ones) | (nz_pk_u16(v.y, ones) << 2) | (nz_pk_u16(v.z, ones) << 4) |
+                             (nz_pk_u16(v.w, ones) << 6);
+          const uint32_t word = quad_pack_bytes((u | (u >> 15)) & 0xFFu);
+          if ((c & 3) == 0) *reinterpret_cast<uint32_t*>(mbase + i * mstep + moff) = word;
+        }
+      }
+    }
+  };
+  if (p.nt_store) run(std::true_type{});
+  else run(std::false_type{});
+}
+
+// ---------------------------------------------------------------------------
 // Ping-pong variant of the q64 loop (cdna_hip_programming.md §5 "The 256²
 // 8-phase template"): every quadrant phase is a LOAD segment (counted vmcnt,
 // the phase's ds_reads, its DMA chunk of the next K-tile), a barrier, an MFMA
@@ -1087,7 +1220,11 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
 
   const int wm = w >> 2, wn = w & 3;
   float4_t bvec[4];     // bias of the lane's 16 epilogue columns, loaded under the main loop
-  if (DIRECT) load_cols16(p.bias, p.N, n0 + wn * 64 + g * 4, bvec);
+  // lean epilogue modes (the fused-head mode measured slower: its bias and head weights
+  // in registers make the kernel spill)
+  constexpr bool LEAN = DIRECT == 0 && (MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK);
+  if (DIRECT || (LEAN && MODE != EPI_BWD_MASK)) load_cols16(p.bias, p.N, n0 + wn * 64 + g * 4, bvec);
+  else if (LEAN) bvec[0] = bvec[1] = bvec[2] = bvec[3] = float4_t{0.f, 0.f, 0.f, 0.f};
   float4_t acc[4][8];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -1193,6 +1330,13 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
     return;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (LEAN) {
+    if (lean_tile_ok<MODE>(p, m0, n0)) {
+      __syncthreads();
+      epilogue_lean<MODE>(p, acc, bvec, smem, m0, n0, tid, wm, wn, g, li);
+      return;
+    }
+  }
   __syncthreads();
   epilogue_256<MODE, true>(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
 }
@@ -1612,6 +1756,8 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.head_ld = M;
   static const int nt_store_env = getenv("LLP_GEMM_NT_STORE") ? atoi(getenv("LLP_GEMM_NT_STORE")) : 1;
   p.nt_store = nt_store_env;
+  static const int lean_env = getenv("LLP_GEMM_LEAN_EPI") ? atoi(getenv("LLP_GEMM_LEAN_EPI")) : 1;
+  p.lean_epi = lean_env;
   p.C = (bf16_t*)C; p.ldc = ldc;
   p.bias = bias; p.act = act; p.aux = (const bf16_t*)aux; p.ld_aux = ld_aux; p.alpha = alpha;
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
