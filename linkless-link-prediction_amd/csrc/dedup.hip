@@ -445,6 +445,26 @@ __global__ void count_kernel(int64_t R, const int32_t* __restrict__ target, int3
   if (r < R) atomicAdd(&cnt[target[r]], 1);
 }
 
+// count pass that also records each row's arrival rank within its node (returning
+// atomic), so the scatter needs no atomics (default; LLP_DEDUP_RANK=0: the atomic-cursor
+// scatter).  Collab R = 747k rows: count 45 -> 46 us, scatter 57 -> 13 us; same outputs
+// (the segment sort restores row order either way).
+__global__ void count_rank_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ cnt,
+                                  int32_t* __restrict__ rank) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < R) rank[r] = atomicAdd(&cnt[target[r]], 1);
+}
+
+__global__ void scatter_rank_kernel(int64_t R, const int32_t* __restrict__ target, const int32_t* __restrict__ uidx,
+                                    const int32_t* __restrict__ start, const int32_t* __restrict__ rank,
+                                    int32_t* __restrict__ pos, int32_t* __restrict__ seg_rows) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int32_t v = target[r];
+  pos[r] = uidx[v];
+  seg_rows[start[v] + rank[r]] = (int32_t)r;
+}
+
 __global__ void compact_count_kernel(int64_t N, int64_t R, const int32_t* __restrict__ cnt,
                                      const uint64_t* __restrict__ pre, int32_t* __restrict__ uniq,
                                      int32_t* __restrict__ seg_ptr, int32_t* __restrict__ uidx,
@@ -639,9 +659,13 @@ static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, i
   void* scan_tmp = w;
   size_t scan_b = scan64_bytes(num_nodes);
 
+  static const bool rank_env = !(getenv("LLP_DEDUP_RANK") && atoi(getenv("LLP_DEDUP_RANK")) == 0);
   hipError_t e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
   if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
-  hipLaunchKernelGGL(count_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt);
+  if (rank_env)   // the rank goes to `scratch` (free until the segment sort)
+    hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt, scratch);
+  else
+    hipLaunchKernelGGL(count_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt);
   LLP_LAUNCH_CHECK();
   auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
   e = rocprim::exclusive_scan(scan_tmp, scan_b, it, pre, (uint64_t)0, (size_t)num_nodes, rocprim::plus<uint64_t>(),
@@ -650,8 +674,12 @@ static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, i
   hipLaunchKernelGGL(compact_count_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, R, cnt, pre,
                      uniq, seg_ptr, uidx, cursor, n_unique, n_long);
   LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, pos,
-                     seg_rows);
+  if (rank_env)   // cursor[v] = segment start of v (compact_count_kernel)
+    hipLaunchKernelGGL(scatter_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, scratch,
+                       pos, seg_rows);
+  else
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, pos,
+                       seg_rows);
   LLP_LAUNCH_CHECK();
   const int64_t ubound = R < num_nodes ? R : num_nodes;
   static const bool two_pass = getenv("LLP_SEGSORT_2PASS") != nullptr;   // A/B: the old short + long launches
