@@ -1,5 +1,5 @@
 """Per-launch duration of bench.py's dominant kernel (student layer-2 forward
-GEMM = the 2nd NT GEMM dispatch after each step's context_walk_kernel)
+GEMM = the 2nd NT GEMM dispatch after each step's sampling kernel)
 from a rocprofv3 --kernel-trace CSV, to check against bench.py's event timing.
 
     python tools/dominant_from_trace.py gpurun_out/prof_r02/bench_kernel_trace.csv [out.json] [kernel name prefix]
@@ -21,7 +21,7 @@ def main():
     durs = []
     k = None
     for s, e, name in rows:
-        if "context_walk_kernel" in name:
+        if "context_walk_kernel" in name or "minibatch_sample_kernel" in name:
             k = 0
             continue
         if k is not None and KERNEL in name:
