@@ -2,6 +2,8 @@
 // (multi-tensor, fused with the bf16 weight-shadow refresh), small utilities.
 #include "llp_common.h"
 
+#include <type_traits>
+
 namespace {
 
 template <typename T>
@@ -199,6 +201,65 @@ __global__ __launch_bounds__(256) void hadamard_rows_kernel(int64_t R, int64_t H
                    __float_as_uint(__uint_as_float(x.w) * __uint_as_float(y.w)));
   }
   *reinterpret_cast<uint4*>(out + r * H + c * E) = o;
+}
+
+// Same products, G row groups per wave.  LPR = 64: a row is 64 * NCH 16-B chunks, lane
+// l owns chunks l, l + 64, ..., and the row indices are wave-uniform (scalar loads, once
+// per row instead of once per chunk); LPR = 32: a row is 32 chunks, each half-wave takes
+// one row of the group.  The 2 * G * NCH operand loads of a lane issue together, and a
+// block covers 4 * G * (64 / LPR) rows (301k blocks -> 38k at the collab shape).
+template <typename T, int NCH, int G, int LPR>
+__global__ __launch_bounds__(256) void hadamard_rows_wave_kernel(int64_t R, int64_t H, const T* __restrict__ a,
+                                                                  const int32_t* __restrict__ ia,
+                                                                  const T* __restrict__ b,
+                                                                  const int32_t* __restrict__ ib, T* __restrict__ out) {
+  constexpr int E = 16 / sizeof(T);
+  constexpr int RPG = 64 / LPR;   // rows per group (one per LPR lanes)
+  const int lane = threadIdx.x & 63;
+  const int c = lane % LPR, sub = lane / LPR;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * G * RPG;
+  if (r0 >= R) return;
+  int64_t ra[G], rb[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t rr = r0 + g * RPG + sub;
+    const int64_t r = rr < R ? rr : R - 1;
+    ra[g] = ia ? (int64_t)ia[r] : r;
+    rb[g] = ib ? (int64_t)ib[r] : r;
+  }
+  uint4 x[G][NCH], y[G][NCH];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int64_t col = (int64_t)(c + LPR * j) * E;
+      x[g][j] = *reinterpret_cast<const uint4*>(a + ra[g] * H + col);
+      y[g][j] = *reinterpret_cast<const uint4*>(b + rb[g] * H + col);
+    }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t r = r0 + g * RPG + sub;
+    if (r0 + g * RPG >= R) break;   // (wave-uniform)
+    if (r >= R) continue;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      uint4 o;
+      const uint4 p = x[g][j], q = y[g][j];
+      if constexpr (sizeof(T) == 2) {
+        auto m2 = [](uint32_t u, uint32_t v) {
+          return (uint32_t)f2bf(__uint_as_float(u << 16) * __uint_as_float(v << 16)) |
+                 ((uint32_t)f2bf(__uint_as_float(u & 0xFFFF0000u) * __uint_as_float(v & 0xFFFF0000u)) << 16);
+        };
+        o = make_uint4(m2(p.x, q.x), m2(p.y, q.y), m2(p.z, q.z), m2(p.w, q.w));
+      } else {
+        o = make_uint4(__float_as_uint(__uint_as_float(p.x) * __uint_as_float(q.x)),
+                       __float_as_uint(__uint_as_float(p.y) * __uint_as_float(q.y)),
+                       __float_as_uint(__uint_as_float(p.z) * __uint_as_float(q.z)),
+                       __float_as_uint(__uint_as_float(p.w) * __uint_as_float(q.w)));
+      }
+      *reinterpret_cast<uint4*>(out + r * H + (int64_t)(c + LPR * j) * E) = o;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- optimiser
@@ -454,6 +515,25 @@ extern "C" int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a,
   const int64_t n = R * (H * es / 16);
   if (n == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
+  // rows of 32, 64, 128 or 256 chunks: row groups per wave (LLP_HADA_WAVE=0: one chunk per thread)
+  static const bool wave_env = !(getenv("LLP_HADA_WAVE") && atoi(getenv("LLP_HADA_WAVE")) == 0);
+  const int64_t cpr = H * es / 16;
+  if (wave_env && (cpr == 32 || cpr == 64 || cpr == 128 || cpr == 256)) {
+    auto go = [&](auto kern, auto* pa, auto* pb, auto* po, int rows_per_wave) {
+      hipLaunchKernelGGL(kern, dim3(ceil_div_u(R, 4 * rows_per_wave)), dim3(256), 0, s, R, H, pa, ia, pb, ib, po);
+    };
+    auto pick = [&](auto* pa, auto* pb, auto* po) {
+      using TT = std::remove_const_t<std::remove_pointer_t<decltype(pa)>>;
+      if (cpr == 32) go(hadamard_rows_wave_kernel<TT, 1, 4, 32>, pa, pb, po, 8);
+      else if (cpr == 64) go(hadamard_rows_wave_kernel<TT, 1, 8, 64>, pa, pb, po, 8);
+      else if (cpr == 128) go(hadamard_rows_wave_kernel<TT, 2, 4, 64>, pa, pb, po, 4);
+      else go(hadamard_rows_wave_kernel<TT, 4, 2, 64>, pa, pb, po, 2);
+    };
+    if (dtype == LLP_BF16) pick((const bf16_t*)a, (const bf16_t*)b, (bf16_t*)out);
+    else pick((const float*)a, (const float*)b, (float*)out);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
   if (dtype == LLP_BF16)
     hipLaunchKernelGGL(hadamard_rows_kernel<bf16_t>, dim3(ceil_div_u(n, 256)), dim3(256), 0, s, R, H,
                        (const bf16_t*)a, ia, (const bf16_t*)b, ib, (bf16_t*)out);

@@ -204,6 +204,34 @@ def test_gemm_tn_gathered_hadamard_operand():
     assert (out.cpu().double() - ref).abs().max().item() < 1e-3
 
 
+# ------------------------------------------------------------------ Hadamard rows
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [200, 128, 256, 512, 1024, 2048])
+@pytest.mark.parametrize("R", [1, 7, 1003])
+def test_hadamard_rows_exact(dt, H, R):
+    """out[r] = a[ia[r]] * b[ib[r]], rounded once to the storage dtype: bit-exact vs torch
+    for the thread-per-chunk kernel (bf16 H=200, fp32 H=128/2048) and the row-group kernel
+    (rows of 32, 64, 128, 256 16-B chunks), R not a multiple of the rows per wave."""
+    k = K()
+    g = torch.Generator().manual_seed(H + R)
+    es = 2 if dt == torch.bfloat16 else 4
+    if (H * es) % 16:
+        pytest.skip("rows must be 16-byte multiples")
+    na, nb = 300, 41
+    a = torch.randn(na, H, generator=g).to(DEV, dt)
+    b = torch.randn(nb, H, generator=g).to(DEV, dt)
+    ia = torch.randint(0, na, (R,), generator=g, dtype=torch.int32).to(DEV)
+    ib = torch.randint(0, nb, (R,), generator=g, dtype=torch.int32).to(DEV)
+    out = torch.empty(R, H, device=DEV, dtype=dt)
+    k.hadamard_rows(a, ia, b, ib, out)
+    ref = (a[ia.long()].float() * b[ib.long()].float()).to(dt)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    out2 = torch.empty(min(R, na), H, device=DEV, dtype=dt)     # no index: rows in order
+    k.hadamard_rows(a, None, a, None, out2)
+    assert torch.equal(out2, (a[:out2.shape[0]].float() * a[:out2.shape[0]].float()).to(dt))
+
+
 # ------------------------------------------------------------------ heads, colsum
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("R,H", [(1000, 200), (150_000, 1024)])
