@@ -252,9 +252,11 @@ def main():
     ap.add_argument("--profile-kernels", action="store_true", help="exit right after the timed region")
     ap.add_argument("--dominant-only", type=int, default=0,
                     help="run only the dominant kernel this many times (rocprofv3 --pmc passes) and exit")
-    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
                     help="replay the step from a captured hipGraph (N>1: graph segments with the RCCL "
-                         "all-reduces between them; --no-graph: eager launches)")
+                         "all-reduces between them; --no-graph: eager launches).  Default: on at N=1, off "
+                         "at N>1 (a replay of the segmented capture faulted at the collab size on the one-GPU "
+                         "gloo rehearsal, DESIGN.md §5; eager N>1 steps are verified)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
     ap.add_argument("--no-physics", action="store_true")
@@ -262,6 +264,8 @@ def main():
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single GPU: run only rank 0's shard of an R-rank job (no collective) and report "
                          "its per-step time, to see the per-rank fixed costs of strong scaling")
+    ap.add_argument("--emulate-rank", type=int, default=0,
+                    help="with --emulate-ranks R: which rank's shard (offsets) to run, default 0")
     opt = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -309,8 +313,9 @@ def main():
     n_full = min(E_train // P_full, N // B_full)
     # this rank's shard of every global batch
     shards = opt.emulate_ranks if (opt.emulate_ranks and world == 1) else world
-    b0, b1 = rank * B_full // shards, (rank + 1) * B_full // shards
-    p0, p1 = rank * P_full // shards, (rank + 1) * P_full // shards
+    srank = opt.emulate_rank if (opt.emulate_ranks and world == 1) else rank
+    b0, b1 = srank * B_full // shards, (srank + 1) * B_full // shards
+    p0, p1 = srank * P_full // shards, (srank + 1) * P_full // shards
 
     kern_ev = []
 
@@ -324,9 +329,18 @@ def main():
     if opt.dominant_only:
         dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, opt.dominant_only)
         return
-    use_graph = opt.graph
+    use_graph = opt.graph if opt.graph is not None else world == 1
+    debug = os.environ.get("LLP_BENCH_DEBUG") == "1"   # stage markers, each after a device sync
+
+    def mark(what):
+        if debug:
+            torch.cuda.synchronize()
+            print(f"[rank {rank}] {what}", flush=True)
+
+    mark("engine ready")
     for s in range(opt.warmup):
         one_step(s, False)
+        mark(f"warmup step {s}")
     graph = None
     if use_graph:
         # persistent input slots, refilled before each replay (device-to-device copies)
@@ -337,6 +351,7 @@ def main():
         try:
             graph = eng.capture_minibatch(g_anchors, g_links, pairs, b_offset=b0, p_offset=p0, B_total=B_full,
                                           P_total=P_full)
+            mark("captured")
         except RuntimeError as e:   # keep the run alive: eager launches instead (reported as hipgraph: false)
             print(f"bench.py: hipGraph capture failed ({e}); timing eager steps", file=sys.stderr, flush=True)
             graph = None
@@ -353,6 +368,7 @@ def main():
             g_anchors.copy_(node_perm[j * B_full + b0: j * B_full + b1])
             g_links.copy_(link_perm[j * P_full + p0: j * P_full + p1])
             graph.replay()
+            mark(f"replay {s}")
         else:
             one_step(opt.warmup + s, True)
     torch.cuda.synchronize()
@@ -369,7 +385,7 @@ def main():
             dist.destroy_process_group()
         return
     if opt.emulate_ranks and world == 1:
-        print(json.dumps({"emulated_ranks": shards, "rank0_ms_per_step": dt / opt.steps * 1e3,
+        print(json.dumps({"emulated_ranks": shards, "rank": srank, "rank0_ms_per_step": dt / opt.steps * 1e3,
                           "anchors": b1 - b0, "edges": p1 - p0,
                           "student_rows": eng.last_student_rows}), flush=True)
         return

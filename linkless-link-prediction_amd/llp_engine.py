@@ -443,6 +443,7 @@ class EngineBase:
         ws = self._ws("ws_col", K.head_bwd_ws_bytes(R2, max(Hh, 1)))
         K.head_bwd(dlogit, Zl, R2, Hh, self.head.weight.data.view(-1), True, g, self.head.weight.grad.view(-1),
                    self.head.bias.grad, ws, alpha=alpha)
+        self._dbg_cut("head backward")
         names = ["gP0", "gP1", "gP2"] if overlap & 4 else ["gP0", "gP1"]
         k = 0
         for l in range(len(self.prd) - 1, -1, -1):
@@ -465,6 +466,7 @@ class EngineBase:
             else:
                 K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
                           self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
+                self._dbg_cut(f"predictor weight gradient {l}")
                 if l == 0:
                     self._allreduce_tail_begin()      # every predictor gradient is final here
             k += 1
@@ -547,6 +549,17 @@ class EngineBase:
         if self._seg is None:
             fn()
         else:
+            self._seg.cut(fn)
+
+    def _dbg_cut(self, what):
+        """LLP_SEG_DEBUG=1 while a multi-rank step is captured: one more segment cut here,
+        whose eager step syncs the device and names the stage (locates a faulting segment)."""
+        if self._seg is not None and os.environ.get("LLP_SEG_DEBUG") == "1":
+            rank = self.rank
+
+            def fn():
+                torch.cuda.synchronize()
+                print(f"[rank {rank}] segment ok: {what}", flush=True)
             self._seg.cut(fn)
 
     def _allreduce_and_update(self):
@@ -726,6 +739,7 @@ class DistillEngine(EngineBase):
             K.minibatch_sample(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                self.seed, self.step_ctr, 0, pairs, link_ids, P, P_total, p_offset, 15, samp, negb,
                                target, t_ia, t_ib, b_offset=b_offset)
+            self._dbg_cut("sample")
         else:
             negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
             n_lab = P + n_neg                  # train_edges columns (src/main.py:86)
@@ -766,6 +780,7 @@ class DistillEngine(EngineBase):
             seg_rows = self._buf("seg_rows", (R1,), torch.int32)
             wsd = self._buf("ws_dedup", (K.dedup_ws_bytes(self.N, R1) // 4 + 16,), torch.float32)
             K.dedup_rows(self.N, R1, target, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
+            self._dbg_cut("sample + dedup")
             iab_h = self._buf("iab_u", (2, R2), torch.int32)   # both pair sides in one gather
             K.gather_i32(self._rows_index_flat(B, C, n_lab), pos, iab_h.view(-1))
             ia_h, ib_h = iab_h[0], iab_h[1]
@@ -813,7 +828,9 @@ class DistillEngine(EngineBase):
 
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
         logit = self._buf("logit", (R2,), torch.float32)
+        self._dbg_cut("student forward")
         A0, zacts = self._predictor_forward(h, ia_h, ib_h, R2, logit, p_drop)
+        self._dbg_cut("predictor forward")
 
         # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
         t_r = self._buf("t_r", (B * C,), torch.float32)
@@ -832,6 +849,7 @@ class DistillEngine(EngineBase):
                    float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms, ws)
 
         # ---- a10: backward
+        self._dbg_cut("teacher + loss")
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop, overlap=overlap)
         mlp = self.predictor_kind == "mlp"
         if dedup and _SEGMENT_FUSED:
@@ -988,8 +1006,9 @@ class DistillEngine(EngineBase):
         With several ranks the step is captured as segments cut at the gradient
         all-reduces, which run eagerly between them at replay (_SegmentedGraph);
         the returned object has the same ``replay()``."""
-        if self.world > 1:
+        if self.world > 1 or os.environ.get("LLP_FORCE_SEGMENTED") == "1":
             # RCCL stays outside the graphs: one segment per stretch between collectives
+            # (LLP_FORCE_SEGMENTED=1: the same segmented capture on one rank, a debug aid)
             torch.cuda.synchronize(self.dev)
             seg = _SegmentedGraph(self.dev)
             seg.stream.wait_stream(torch.cuda.current_stream(self.dev))
