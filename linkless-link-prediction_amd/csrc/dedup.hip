@@ -465,6 +465,89 @@ __global__ void scatter_rank_kernel(int64_t R, const int32_t* __restrict__ targe
   seg_rows[start[v] + rank[r]] = (int32_t)r;
 }
 
+// ------------------------------------------------ own scan (LLP_DEDUP_SCAN=own, opt-in)
+// Exclusive scan of PackCount(cnt[v]) over v < n without rocprim and without a
+// hipMemsetAsync node (cnt zeroed by a kernel): a diagnosis aid for the segmented
+// multi-rank capture and a rocprim-free alternative.  u64 integer sums,
+// so any association gives the same result.
+constexpr int OS_T = 256, OS_I = 8, OS_B = OS_T * OS_I;   // 2,048 values per block
+
+__device__ __forceinline__ uint64_t pack_count(int32_t c) {
+  return (c > 0 ? (1ull << 32) : 0ull) | (uint64_t)(uint32_t)c;
+}
+
+__global__ void zero_i32_kernel(int64_t n, int32_t* __restrict__ p) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
+__global__ __launch_bounds__(OS_T) void os_block_sum_kernel(int64_t n, const int32_t* __restrict__ cnt,
+                                                            uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t red[OS_T];
+  const int64_t base = blockIdx.x * (int64_t)OS_B + threadIdx.x * OS_I;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < OS_I; ++i) s += base + i < n ? pack_count(cnt[base + i]) : 0ull;
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = OS_T / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0];
+}
+
+// one block: bsum[0..nb) -> exclusive prefix, 1,024 values per round with a carry
+__global__ __launch_bounds__(1024) void os_scan_sums_kernel(int64_t nb, uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t buf[1024];
+  const int t = threadIdx.x;
+  uint64_t carry = 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
+    const int64_t i = c0 + t;
+    const uint64_t x = i < nb ? bsum[i] : 0ull;
+    buf[t] = x;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const uint64_t y = t >= o ? buf[t - o] : 0ull;
+      __syncthreads();
+      buf[t] += y;
+      __syncthreads();
+    }
+    if (i < nb) bsum[i] = carry + buf[t] - x;
+    carry += buf[1023];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(OS_T) void os_block_scan_kernel(int64_t n, const int32_t* __restrict__ cnt,
+                                                             const uint64_t* __restrict__ boff,
+                                                             uint64_t* __restrict__ pre) {
+  __shared__ uint64_t ts[OS_T];
+  const int t = threadIdx.x;
+  const int64_t base = blockIdx.x * (int64_t)OS_B + t * OS_I;
+  uint64_t v[OS_I];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < OS_I; ++i) {
+    v[i] = base + i < n ? pack_count(cnt[base + i]) : 0ull;
+    s += v[i];
+  }
+  ts[t] = s;
+  __syncthreads();
+  for (int o = 1; o < OS_T; o <<= 1) {
+    const uint64_t y = t >= o ? ts[t - o] : 0ull;
+    __syncthreads();
+    ts[t] += y;
+    __syncthreads();
+  }
+  uint64_t run = boff[blockIdx.x] + ts[t] - s;
+#pragma unroll
+  for (int i = 0; i < OS_I; ++i) {
+    if (base + i < n) pre[base + i] = run;
+    run += v[i];
+  }
+}
+
 __global__ void compact_count_kernel(int64_t N, int64_t R, const int32_t* __restrict__ cnt,
                                      const uint64_t* __restrict__ pre, int32_t* __restrict__ uniq,
                                      int32_t* __restrict__ seg_ptr, int32_t* __restrict__ uidx,
@@ -631,7 +714,7 @@ static int64_t radix_ws_bytes(int64_t num_nodes, int64_t R) {
 }
 static int64_t counting_ws_bytes(int64_t num_nodes, int64_t R) {
   return 3 * al256((num_nodes + 1) * 4) + al256(num_nodes * 8) + 2 * al256(R * 4) + al256(256) +
-         al256((int64_t)scan64_bytes(num_nodes)) + 512;
+         al256((int64_t)scan64_bytes(num_nodes)) + al256(((num_nodes + OS_B - 1) / OS_B) * 8) + 512;
 }
 
 extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) {
@@ -658,19 +741,36 @@ static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, i
   w += al256(256);
   void* scan_tmp = w;
   size_t scan_b = scan64_bytes(num_nodes);
+  w += al256((int64_t)scan_b);
+  uint64_t* os_sums = reinterpret_cast<uint64_t*>(w);   // own scan: per-block sums / offsets
 
   static const bool rank_env = !(getenv("LLP_DEDUP_RANK") && atoi(getenv("LLP_DEDUP_RANK")) == 0);
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
-  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
+  static const bool own_scan = getenv("LLP_DEDUP_SCAN") && strcmp(getenv("LLP_DEDUP_SCAN"), "own") == 0;
+  hipError_t e = hipSuccess;
+  if (own_scan) {
+    hipLaunchKernelGGL(zero_i32_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, cnt);
+    LLP_LAUNCH_CHECK();
+  } else {
+    e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
+    if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
+  }
   if (rank_env)   // the rank goes to `scratch` (free until the segment sort)
     hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt, scratch);
   else
     hipLaunchKernelGGL(count_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt);
   LLP_LAUNCH_CHECK();
-  auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
-  e = rocprim::exclusive_scan(scan_tmp, scan_b, it, pre, (uint64_t)0, (size_t)num_nodes, rocprim::plus<uint64_t>(),
-                              s);
-  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: scan");
+  if (own_scan) {
+    const int64_t nb = (num_nodes + OS_B - 1) / OS_B;
+    hipLaunchKernelGGL(os_block_sum_kernel, dim3((unsigned)nb), dim3(OS_T), 0, s, num_nodes, cnt, os_sums);
+    hipLaunchKernelGGL(os_scan_sums_kernel, dim3(1), dim3(1024), 0, s, nb, os_sums);
+    hipLaunchKernelGGL(os_block_scan_kernel, dim3((unsigned)nb), dim3(OS_T), 0, s, num_nodes, cnt, os_sums, pre);
+    LLP_LAUNCH_CHECK();
+  } else {
+    auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
+    e = rocprim::exclusive_scan(scan_tmp, scan_b, it, pre, (uint64_t)0, (size_t)num_nodes,
+                                rocprim::plus<uint64_t>(), s);
+    if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: scan");
+  }
   hipLaunchKernelGGL(compact_count_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, R, cnt, pre,
                      uniq, seg_ptr, uidx, cursor, n_unique, n_long);
   LLP_LAUNCH_CHECK();

@@ -122,7 +122,9 @@ class _SegmentedGraph:
     def _open(self):
         self.g = torch.cuda.CUDAGraph()
         # thread_local: the process group's own threads may query events meanwhile
-        self.g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
+        # (LLP_SEG_CAPTURE_MODE: "global" / "relaxed" for the diagnosis in DESIGN.md §5)
+        mode = os.environ.get("LLP_SEG_CAPTURE_MODE", "thread_local")
+        self.g.capture_begin(pool=self.pool, capture_error_mode=mode)
 
     def _close(self):
         self.g.capture_end()
