@@ -61,6 +61,12 @@ def step_flops(B, C, P, F, H, L, rows_student=None):
     return 3 * (fwd_mlp + fwd_pred) - 2 * rows_mlp * F * H + fwd_t
 
 
+def use_graph(flag, world):
+    """--graph / --no-graph, else the default: the hipGraph replay at N=1, eager steps
+    at N>1 (the segmented multi-rank capture has an open replay fault)."""
+    return flag if flag is not None else world == 1
+
+
 def cpu_baseline(data, a, t_h, init_params, B_full, P_full, sample_P=8192, steps=3):
     """The CPU oracle (torch-CPU restatement of train_minibatch) on a bounded
     sample of the same workload: one link batch of sample_P edges and the
@@ -329,7 +335,7 @@ def main():
     if opt.dominant_only:
         dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, opt.dominant_only)
         return
-    use_graph = opt.graph if opt.graph is not None else world == 1
+    graph_on = use_graph(opt.graph, world)
     debug = os.environ.get("LLP_BENCH_DEBUG") == "1"   # stage markers, each after a device sync
 
     def mark(what):
@@ -342,7 +348,7 @@ def main():
         one_step(s, False)
         mark(f"warmup step {s}")
     graph = None
-    if use_graph:
+    if graph_on:
         # persistent input slots, refilled before each replay (device-to-device copies)
         g_anchors = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
         g_links = torch.empty(p1 - p0, dtype=torch.int32, device=dev)
