@@ -360,6 +360,9 @@ __device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
 // ReLU mask out, no dropout / head / aux; EPI_BWD_MASK: ReLU backward through a bit mask, alpha,
 // no bias / dropout / head.  The host picks the mode (epi_mode_of).
 constexpr int EPI_ANY = 0, EPI_FWD_RELU = 1, EPI_FWD_NONE = 2, EPI_BWD_MASK = 3, EPI_HEAD_RELU = 4;
+// opt-in (LLP_GEMM_HEAD_LEAN=1): EPI_HEAD_RELU with the head dot taken from the staged
+// bf16 outputs in the lean epilogue's second phase (pp8 only; epilogue_lean_head)
+constexpr int EPI_HEAD_LEAN = 5;
 
 // MASK_LDS (TMv 256, NTHR 512 only): the ReLU-backward bit mask of the tile (256 rows x
 // 32 bytes) is read with ONE 16-byte load per thread into LDS at smem + head_off_u4 + 256
@@ -1158,6 +1161,88 @@ __device__ __forceinline__ void epilogue_lean(const P256& p, float4_t (&acc)[4][
   else run(std::false_type{});
 }
 
+// Lean epilogue of the fused Linear(N,1) head (EPI_HEAD_LEAN, opt-in): phase 1 as
+// EPI_FWD_RELU (bias, bf16 rounding, packed ReLU, LDS staging); phase 2 reads each
+// staged 16-B chunk once for the optional store of C AND the head dot of its 8
+// columns (head weights in 8 registers per thread), so the per-element f32 dot of
+// epilogue_t (4 fma per accumulator quad + 16 cross-lane adds per tile row) goes.
+// The dot is taken over the ROUNDED bf16 outputs (the values the head backward reads
+// back), in a fixed order: 8 fma per chunk, quad sums by DPP ([1,0,3,2] then
+// [2,3,0,1]), the row's 8 quad partials summed in column order -- deterministic, but
+// not bit-identical to EPI_HEAD_RELU's f32 dot (differences of bf16 rounding size).
+// Runs on EVERY tile (no generic fallback in the kernel, which made it spill): the host
+// launches it only for N % 256 == 0, 16-B aligned head weights and C rows; rows past M
+// (the last m-tile, or a device row count) are neither stored nor summed.
+__device__ __forceinline__ float dpp_quad_sum(float d) {
+  d += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
+  return d + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), 0x4E, 0xF, 0xF, false));   // [2,3,0,1]
+}
+
+__device__ __forceinline__ void epilogue_lean_head(const P256& p, float4_t (&acc)[4][8], uint4* smem, int64_t m0,
+                                                   int64_t n0, int tid, int wm, int wn, int g, int li) {
+  constexpr int ROWB = EPI_ROW_U4 * 16;
+  const int rl0 = tid >> 5, c = tid & 31;
+  // this thread's 8 head weights (columns n0 + 8c ..), issued first: their latency
+  // hides under phase 1
+  const float4_t hw0 = *reinterpret_cast<const float4_t*>(p.head_w + n0 + 8 * c);
+  const float4_t hw1 = *reinterpret_cast<const float4_t*>(p.head_w + n0 + 8 * c + 4);
+  float4_t bl[4];
+  load_cols16(p.bias, p.N, n0 + wn * 64 + g * 4, bl);
+  char* sb = reinterpret_cast<char*>(smem) + (wm * 128 + li) * ROWB + (wn * 64 + g * 4) * 2;
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn) {
+    const float2_t b01 = {bl[jn][0], bl[jn][1]}, b23 = {bl[jn][2], bl[jn][3]};
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const float2_t v01 = float2_t{acc[jn][im][0], acc[jn][im][1]} + b01;
+      const float2_t v23 = float2_t{acc[jn][im][2], acc[jn][im][3]} + b23;
+      *reinterpret_cast<uint2*>(sb + im * 16 * ROWB + jn * 32) =
+          make_uint2(relu_pk_bf16(pk_bf16(v01)), relu_pk_bf16(pk_bf16(v23)));
+    }
+  }
+  __syncthreads();
+  // phase 2: chunk (row rl0 + 16 i, columns 8c .. 8c+7); quad partials to LDS past the
+  // staging, [256 rows][8 quads] floats (8 KiB of the 12 KiB the kernel reserves there)
+  float* part = reinterpret_cast<float*>(smem + SMEM_U4_EPI);
+  const char* rb = reinterpret_cast<const char*>(smem) + rl0 * ROWB + c * 16;
+  const bool st = p.C != nullptr;
+  char* cbase = st ? reinterpret_cast<char*>(p.C + m0 * p.ldc + n0) : nullptr;
+  const uint32_t toff = st ? (uint32_t)((rl0 * p.ldc + c * 8) * 2) : 0u;
+  const int64_t cstep = st ? 16 * p.ldc * 2 : 0;
+  const int64_t rows = p.M - m0;   // live rows of this tile (>= 1)
+  auto run = [&](auto NTS) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint4 v = *reinterpret_cast<const uint4*>(rb + i * 16 * ROWB);
+      if (st && rl0 + 16 * i < rows) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 sv = {v.x, v.y, v.z, v.w};
+        u32x4* dst = reinterpret_cast<u32x4*>(cbase + i * cstep + toff);
+        if constexpr (decltype(NTS)::value) __builtin_nontemporal_store(sv, dst);
+        else *dst = sv;
+      }
+      float d = __uint_as_float(v.x << 16) * hw0[0];
+      d = fmaf(__uint_as_float(v.x & 0xFFFF0000u), hw0[1], d);
+      d = fmaf(__uint_as_float(v.y << 16), hw0[2], d);
+      d = fmaf(__uint_as_float(v.y & 0xFFFF0000u), hw0[3], d);
+      d = fmaf(__uint_as_float(v.z << 16), hw1[0], d);
+      d = fmaf(__uint_as_float(v.z & 0xFFFF0000u), hw1[1], d);
+      d = fmaf(__uint_as_float(v.w << 16), hw1[2], d);
+      d = fmaf(__uint_as_float(v.w & 0xFFFF0000u), hw1[3], d);
+      d = dpp_quad_sum(d);
+      if ((c & 3) == 0) part[(rl0 + 16 * i) * 8 + (c >> 2)] = d;
+    }
+  };
+  if (p.nt_store) run(std::true_type{});
+  else run(std::false_type{});
+  __syncthreads();
+  if (tid < TM && tid < rows) {
+    const float4_t a = *reinterpret_cast<const float4_t*>(part + tid * 8);
+    const float4_t b = *reinterpret_cast<const float4_t*>(part + tid * 8 + 4);
+    p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Ping-pong variant of the q64 loop (cdna_hip_programming.md §5 "The 256²
 // 8-phase template"): every quadrant phase is a LOAD segment (counted vmcnt,
@@ -1330,15 +1415,21 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
     return;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if constexpr (LEAN) {
-    if (lean_tile_ok<MODE>(p, m0, n0)) {
-      __syncthreads();
-      epilogue_lean<MODE>(p, acc, bvec, smem, m0, n0, tid, wm, wn, g, li);
-      return;
+  if constexpr (MODE == EPI_HEAD_LEAN) {   // every tile (the host checked the shapes)
+    __syncthreads();
+    epilogue_lean_head(p, acc, smem, m0, n0, tid, wm, wn, g, li);
+    return;
+  } else {
+    if constexpr (LEAN) {
+      if (lean_tile_ok<MODE>(p, m0, n0)) {
+        __syncthreads();
+        epilogue_lean<MODE>(p, acc, bvec, smem, m0, n0, tid, wm, wn, g, li);
+        return;
+      }
     }
+    __syncthreads();
+    epilogue_256<MODE, true>(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
   }
-  __syncthreads();
-  epilogue_256<MODE, true>(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
 }
 
 template <int NS>
@@ -1758,6 +1849,10 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.nt_store = nt_store_env;
   static const int lean_env = getenv("LLP_GEMM_LEAN_EPI") ? atoi(getenv("LLP_GEMM_LEAN_EPI")) : 1;
   p.lean_epi = lean_env;
+  // opt-in until measured: the head dot over the staged bf16 outputs (epilogue_lean_head);
+  // read per call (a few head calls per step, captured once) so one process can A/B it
+  const char* head_lean_s = head_w ? getenv("LLP_GEMM_HEAD_LEAN") : nullptr;
+  const int head_lean_env = head_lean_s ? atoi(head_lean_s) : 0;
   p.C = (bf16_t*)C; p.ldc = ldc;
   p.bias = bias; p.act = act; p.aux = (const bf16_t*)aux; p.ld_aux = ld_aux; p.alpha = alpha;
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
@@ -1794,6 +1889,9 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
       hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_FWD_NONE>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
     else if (mode == EPI_BWD_MASK)
       hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_BWD_MASK>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+    else if (mode == EPI_HEAD_RELU && head_lean_env && lean_env && N % TN == 0 && !((uintptr_t)head_w & 15) &&
+             (!C || (!(ldc & 7) && !((uintptr_t)C & 15))))
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_HEAD_LEAN>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
     else if (mode == EPI_HEAD_RELU)
       hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_HEAD_RELU>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
     else

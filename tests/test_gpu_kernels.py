@@ -1,5 +1,7 @@
 """Parity of each libllp_hip kernel against the CPU oracle / a torch fp32
 reference of the same op.  Run on the MI355X: pytest -m gpu."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -132,6 +134,40 @@ def test_gemm_nt_head_fused(M, N, Kd):
     hpart2 = torch.empty(parts, M, device=DEV)
     k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, None, hw, hpart2, bias=b, act=k.ACT_RELU)
     assert torch.equal(hpart, hpart2)
+
+
+@pytest.mark.skipif(os.environ.get("LLP_TEST_HEAD_LEAN") != "1",
+                    reason="opt-in head epilogue (LLP_GEMM_HEAD_LEAN) not yet run on the GPU; LLP_TEST_HEAD_LEAN=1")
+@pytest.mark.parametrize("M,N,Kd", [(1000, 1024, 128), (513, 256, 256), (4096, 1024, 1024)])
+def test_gemm_nt_head_lean(M, N, Kd):
+    """The opt-in lean head epilogue (gemm256.hip epilogue_lean_head): C bit-identical
+    to the default head epilogue; the head dot over the ROUNDED bf16 outputs, within
+    f32 summation-order tolerance of bf16(y) @ hw; deterministic with and without C."""
+    k = K()
+    g = torch.Generator().manual_seed(M + 1)
+    A = (torch.randn(M, Kd, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * (0.3 / Kd ** 0.5)).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    hw = torch.randn(N, generator=g).to(DEV)
+    parts = k.head_parts(N)
+    C0 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C0, hw, torch.empty(parts, M, device=DEV), bias=b,
+                   act=k.ACT_RELU)
+    os.environ["LLP_GEMM_HEAD_LEAN"] = "1"
+    try:
+        C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        h1 = torch.empty(parts, M, device=DEV)
+        k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C1, hw, h1, bias=b, act=k.ACT_RELU)
+        h2 = torch.empty(parts, M, device=DEV)
+        k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, None, hw, h2, bias=b, act=k.ACT_RELU)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["LLP_GEMM_HEAD_LEAN"]
+    assert torch.equal(C1, C0)
+    assert torch.equal(h1, h2)
+    ref = C0.float() @ hw
+    got = h1.sum(0)
+    assert torch.allclose(got, ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item())), (got - ref).abs().max()
 
 
 def test_gemm_nt_bf16_dropout_matches_fp32_mask():
