@@ -1,0 +1,13 @@
+# First GPU call of the next round (one box, ~10 min): the whole GPU suite on the
+# current tree, the opt-in head epilogue's gated test + kernel traces + step A/B, then
+# the segmented-capture bisection LAST (its steps may fault; everything before it is
+# already written under gpurun_out/).  Stops at the first failure.
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_r3.log 2>&1 || { echo "gpu suite failed"; exit 1; }
+echo "gpu suite: ok"
+bash tools/gpu_head_lean.sh || { echo "head epilogue A/B failed"; exit 1; }
+echo "head epilogue A/B: done"
+bash tools/gpu_seg_bisect.sh
+echo rc=$?
