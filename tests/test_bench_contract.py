@@ -50,3 +50,28 @@ def test_collab_configuration():
     assert (a.hidden_channels, a.num_layers, a.hops, a.rw_step, a.ns_rate) == (1024, 3, 3, 3, 3)
     assert a.link_batch_size == 65_536 and a.dropout == 0.0 and a.minibatch
     assert a.ps_method == "nb" and a.predictor == "mlp"
+
+
+def test_cpu_baseline_leg_runs_on_the_host():
+    """bench.py's cpu_baseline leg (the oracle's train_minibatch on a bounded sample),
+    at a reduced shape: the fields the bench line carries."""
+    import torch
+
+    import llp_data
+    import models
+    a = bench.collab_args()
+    a.hidden_channels = 32
+    data = llp_data.synthetic_collab(seed=0, scale=0.01, with_eval=False)
+    torch.manual_seed(1)
+    H = a.hidden_channels
+    model = models.MLP(a.num_layers, data.F, H, H, 0.0)
+    pred = models.LinkPredictor("mlp", H, H, 1, a.num_layers, 0.0)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0)
+    init = tuple([p.detach().clone() for p in m.parameters()] for m in (model, pred, tpred))
+    t_h = torch.randn(data.N, 256) * 0.3
+    P_full = 1024
+    B_full = int(data.N / (data.train_pairs.shape[0] / P_full))
+    r = bench.cpu_baseline(data, a, t_h, init, B_full, P_full, sample_P=128, steps=1)
+    assert r["kind"] == "port" and r["unit"] == "edges/s" and r["value"] > 0
+    assert r["cores"] == torch.get_num_threads()
+    assert "128 edges" in r["sample"]
