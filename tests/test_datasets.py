@@ -95,3 +95,31 @@ def test_synthetic_split_is_reference_layout(workdir):
     assert not os.path.exists(workdir / "data" / "cora.pkl")       # never the reference's cache
     _, se2 = llp_datasets.load_transductive("cora", ddir, synthetic=True)
     assert torch.equal(se2["train"]["edge"], tr)
+
+
+def test_synthetic_collab_matches_the_benchmark_spec():
+    """The bench's synthetic ogbl-collab: full-size counts,
+    OGB-interleaved unsorted edges (Q1), ~5 % duplicate pairs (Q2), ~90 % of the
+    non-duplicate pairs inside a planted community, no self loops, features of F=128."""
+    import llp_data
+    d = llp_data.synthetic_collab(seed=0, scale=1.0, with_eval=True)
+    C = llp_data.COLLAB
+    assert (d.N, d.F) == (C["N"], C["F"]) == (235_868, 128)
+    assert tuple(d.train_pairs.shape) == (C["E_train"], 2)
+    assert d.edge_index.shape[1] == 2 * C["E_train"] == 2_358_104
+    ei = d.edge_index.numpy()
+    assert np.array_equal(ei[:, 0::2], d.train_pairs.numpy().T)          # (u,v), (v,u), ...
+    assert np.array_equal(ei[:, 1::2], d.train_pairs.numpy().T[::-1])
+    assert (np.diff(ei[0]) < 0).any()                                    # row NOT sorted
+    p = d.train_pairs.numpy()
+    assert (p[:, 0] != p[:, 1]).all()
+    key = p[:, 0].astype(np.int64) * d.N + p[:, 1]
+    dup = 1.0 - np.unique(key).size / key.size
+    assert 0.05 < dup < 0.065       # 5 % drawn as copies + chance repeats inside ~236-node communities
+    comm = llp_data.planted_pairs.last_comm                              # the held-out draw reuses it
+    intra = (comm[p[:, 0]] == comm[p[:, 1]]).mean()
+    assert 0.88 < intra < 0.92
+    for s, n in (("valid", C["n_valid"]), ("test", C["n_test"])):
+        assert tuple(d.split_edge[s]["edge"].shape) == (n, 2)
+        assert tuple(d.split_edge[s]["edge_neg"].shape) == (C["n_neg"], 2)
+    assert d.x.dtype == torch.float32 and tuple(d.x.shape) == (d.N, 128)
