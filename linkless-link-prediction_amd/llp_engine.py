@@ -99,6 +99,11 @@ class _Linear:
         return self.Wc if self.Wc is not None else self.W
 
 
+def _acc_dtype(t):
+    """f32, or the tensor's own dtype when that is wider (gloo has no bf16 sums)."""
+    return t.dtype if t.dtype in (torch.float32, torch.float64) else torch.float32
+
+
 class _SegmentedGraph:
     """A multi-rank step as hipGraph segments with the collectives between them.
 
@@ -179,6 +184,7 @@ class EngineBase:
         self._forked = False
         self._side_reads = {}   # buffer name -> event after the side-stream launches that read it
         self._seg = None        # _SegmentedGraph while a multi-rank step is being captured
+        self.emulate_shard = None   # (rank, world): time one rank's full-batch student slice (_fb_shard)
 
     def _fork(self):
         """Context that runs the enclosed launches on the side stream, after
@@ -926,20 +932,30 @@ class DistillEngine(EngineBase):
         ia, ib = ia_ib[:R2], ia_ib[R2:]
         K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
 
-        # ---- a4: student MLP over all nodes (src/main.py:173)
+        # ---- a4: student MLP over all nodes (src/main.py:173); with LLP_FB_SHARD=1 each rank
+        # runs it on its own slice of the nodes and the slices are all-gathered (_fb_shard)
+        shard = self._fb_shard(p_drop, float(a.KD_RM))
+        r0, n_rows, n_loc, s_world, s_rank = (0, N, N, 1, 0) if shard is None else shard
+        x_loc = self.x if shard is None else self.x[r0:r0 + n_rows]
         acts = []
-        A = K.operand(self.x)
+        A = K.operand(x_loc)
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
-            out = self._buf(f"H{l}", (N, lin.out_f), dt)
-            hm = None if last else self._mask(f"Hm{l}", N, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
+            out = self._buf(f"H{l}", (n_loc, lin.out_f), dt)
+            hm = None if last else self._mask(f"Hm{l}", n_rows, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
             self._act_mask[id(out)] = hm
-            K.gemm_nt(A, K.operand(lin.Wcomp), N, lin.out_f, lin.k_in, out, dc, bias=lin.b,
+            K.gemm_nt(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, out, dc, bias=lin.b,
                       act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
                       dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
             acts.append(out)
             A = K.operand(out)
-        h = acts[-1]
+        if shard is None:
+            h = acts[-1]
+        else:
+            h_full = self._buf("fb_hfull", (s_world * n_loc, H), dt)
+            h_loc = acts[-1]
+            self._collective(lambda: self._all_gather_rows(h_full, h_loc, s_world, s_rank))
+            h = h_full[:N]
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
@@ -979,7 +995,15 @@ class DistillEngine(EngineBase):
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
         mlp = self.predictor_kind == "mlp"
-        if grouped:
+        if grouped and shard is not None:
+            # every rank's d(h) over all nodes, summed onto the owners' slices (reduce-scatter)
+            dh_full = self._buf("fb_dhfull", (s_world * n_loc, H), dt)
+            self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh_full[:N])
+            if s_world * n_loc > N:
+                dh_full[N:].zero_()
+            dh = self._buf("gS0", (n_loc, H), dt)
+            self._collective(lambda: self._reduce_scatter_rows(dh, dh_full, s_world, s_rank))
+        elif grouped:
             dh = self._buf("gS0", (N, H), dt)
             self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh)
         else:
@@ -992,10 +1016,53 @@ class DistillEngine(EngineBase):
             else:
                 dh = self._buf("gS0", (N, H), dt)
                 K.convert(dh32, dh)
-        self._student_backward(dh, N, None, acts, p_drop)
+        self._student_backward(dh, n_rows, None, acts, p_drop, x_rows=None if shard is None else x_loc)
         self._allreduce_and_update()
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
         return n_neg
+
+    def _fb_shard(self, p_drop, w_rm):
+        """(first row, rows, rows per rank, world, rank) of this rank's slice of the full-batch student,
+        or None: the student over all N nodes on every rank, as in the reference
+        (src/main.py:173).  Opt-in (LLP_FB_SHARD=1) until measured on the GPU: several
+        ranks, no dropout (the GEMM's dropout draws are keyed by the row within the call)
+        and no KD_RM (its f32 scatter target covers all rows).  The slices are all-gathered
+        after the forward; d(h) of all nodes is reduce-scattered onto them before the
+        student backward, whose weight gradients the usual all-reduce sums.
+        ``emulate_shard = (rank, world)`` on a one-rank engine times that rank's slice
+        with the collectives replaced by local copies (tools/physics_bench.py)."""
+        world, rank = self.world, self.rank
+        if world <= 1 and self.emulate_shard is not None:
+            rank, world = self.emulate_shard
+        if world <= 1 or os.environ.get("LLP_FB_SHARD") != "1" or p_drop > 0.0 or w_rm != 0.0:
+            return None
+        n_loc = -(-self.N // world)
+        r0 = rank * n_loc
+        n_rows = min(self.N, r0 + n_loc) - r0
+        return (r0, n_rows, n_loc, world, rank) if n_rows > 0 else None
+
+    def _all_gather_rows(self, full, part, world, rank):
+        """full [world * n, H] <- every rank's part [n, H] in rank order."""
+        if self.world <= 1:   # emulated shard (timing): this rank's rows stand in for every slice
+            full.view(world, *part.shape).copy_(part.unsqueeze(0).expand(world, *part.shape))
+        elif dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(full, part, group=self.group)
+        else:   # gloo (CPU rehearsal / tests): all_reduce is its one CUDA collective; exact in f32
+            t = torch.zeros(full.shape, dtype=_acc_dtype(full), device=full.device)
+            t.view(self.world, *part.shape)[self.rank].copy_(part)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            full.copy_(t)
+
+    def _reduce_scatter_rows(self, part, full, world, rank):
+        """part [n, H] <- rows [rank * n, (rank + 1) * n) of the SUM over ranks of full."""
+        if self.world <= 1:   # emulated shard: this rank's own contribution (timing)
+            part.copy_(full.view(world, *part.shape)[rank])
+        elif dist.get_backend(self.group) == "nccl":
+            dist.reduce_scatter_tensor(part, full, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            t = full.to(_acc_dtype(full))
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            part.copy_(t.view(self.world, *part.shape)[self.rank])
 
     def capture_minibatch(self, anchors, link_ids, pairs, **kw):
         """Capture one step_minibatch into a hipGraph (torch.cuda.CUDAGraph).

@@ -231,6 +231,26 @@ def test_two_ranks_fullbatch_equal_one_rank():
     draws the same dense negatives and keeps its columns) == the whole batch on one."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    _fullbatch_compare()
+
+
+@pytest.mark.skipif(os.environ.get("LLP_TEST_FB_SHARD") != "1",
+                    reason="opt-in node-sharded full-batch student (LLP_FB_SHARD) not yet run on the GPU; "
+                           "LLP_TEST_FB_SHARD=1")
+def test_two_ranks_fullbatch_sharded_student_equal_one_rank():
+    """LLP_FB_SHARD=1: each rank runs the student on half of the nodes, the halves are
+    all-gathered and d(h) is reduce-scattered back (DistillEngine._fb_shard); same bar
+    as the replicated student."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    os.environ["LLP_FB_SHARD"] = "1"
+    try:
+        _fullbatch_compare()
+    finally:
+        del os.environ["LLP_FB_SHARD"]
+
+
+def _fullbatch_compare():
     single = {}
     _run_fullbatch(0, 1, 0, single)
     ctx = mp.get_context("spawn")

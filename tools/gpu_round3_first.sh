@@ -1,5 +1,6 @@
 # First GPU call of the next round (one box, ~10 min): the whole GPU suite on the
-# current tree, the opt-in head epilogue's gated test + kernel traces + step A/B, then
+# current tree, the opt-in head epilogue's gated test + kernel traces + step A/B, the
+# node-sharded full-batch student's gated test + emulated 4-rank cost, then
 # the segmented-capture bisection LAST (its steps may fault; everything before it is
 # already written under gpurun_out/).  Stops at the first failure.
 export TMPDIR=/tmp
@@ -9,5 +10,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 echo "gpu suite: ok"
 bash tools/gpu_head_lean.sh || { echo "head epilogue A/B failed"; exit 1; }
 echo "head epilogue A/B: done"
+bash tools/gpu_fb_shard.sh || { echo "sharded full-batch student failed"; exit 1; }
+echo "sharded full-batch student: done"
 bash tools/gpu_seg_bisect.sh
 echo rc=$?

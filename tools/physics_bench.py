@@ -54,6 +54,8 @@ def run(dtype, steps, warmup, emulate, split):
     row, col = td.edge_index
     eng = llp_engine.DistillEngine(model, pred, tpred, td.x.to(dev), t_h.to(dev), row.numpy(), col.numpy(), N, a,
                                    opt, dtype=dtype, seed=11)
+    if emulate and os.environ.get("LLP_FB_SHARD") == "1":
+        eng.emulate_shard = (0, emulate)      # rank 0's slice of the node-sharded student (opt-in)
     pairs = td.edge_index.t().to(torch.int32).to(dev).contiguous()      # pos_train_edge (src/main.py:153)
     g = torch.Generator(device=dev)
     g.manual_seed(3)
@@ -80,7 +82,7 @@ def run(dtype, steps, warmup, emulate, split):
     dt = (time.perf_counter() - t0) / steps
     loss = eng.end_epoch(steps * P_full)
     return {"dtype": dtype, "ms_per_step": dt * 1e3, "edges_per_s": P_full / dt if not emulate else None,
-            "emulated_ranks": emulate or None, "N_old": N, "F": F, "E_train_directed": E, "anchors_per_step": B_full,
+            "emulated_ranks": emulate or None, "fb_shard": eng.emulate_shard is not None, "N_old": N, "F": F, "E_train_directed": E, "anchors_per_step": B_full,
             "contexts_per_anchor": a.rw_step * a.hops * (1 + a.ns_rate), "edges_per_step": P_full,
             "steps_per_epoch": -(-E // P_full), "loss": loss}
 
