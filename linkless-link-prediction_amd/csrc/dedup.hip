@@ -698,6 +698,49 @@ __global__ __launch_bounds__(256) void segsort_kernel(const int32_t* __restrict_
   }
 }
 
+// LLP_SEGSORT=wave (opt-in until measured): the long segments listed by
+// segsort_short_kernel are ranked one WAVE per segment across the whole grid (up to
+// WAVE_SEG rows, from the wave's own LDS row; all lanes read the same element, an LDS
+// broadcast), so hot nodes with neighbouring ids no longer queue on the few blocks that
+// own those ids (segsort_kernel ranks a block's long segments one at a time).  Longer
+// segments go on to a second list for segsort_long_kernel.  Same result: every segment
+// in row-id order.  Control flow is wave-uniform (one segment per wave per round), so
+// the LDS row needs only wave-scope ordering, no block barrier.
+constexpr int WAVE_SEG = 1024;
+
+__global__ __launch_bounds__(256) void segsort_mid_wave_kernel(const int32_t* __restrict__ n_long,
+                                                               const int32_t* __restrict__ long_list,
+                                                               const int32_t* __restrict__ seg_ptr,
+                                                               int32_t* __restrict__ seg_rows,
+                                                               int32_t* __restrict__ huge_list,
+                                                               int32_t* __restrict__ n_huge) {
+  __shared__ int32_t buf[4][WAVE_SEG];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int32_t* b = buf[w];
+  const int32_t nl = *n_long;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < nl; i += (int64_t)gridDim.x * 4) {
+    const int32_t sg = long_list[i];
+    const int32_t beg = seg_ptr[sg], len = seg_ptr[sg + 1] - beg;
+    if (len > WAVE_SEG) {
+      if (lane == 0) huge_list[atomicAdd(n_huge, 1)] = sg;
+      continue;
+    }
+    for (int k = lane; k < len; k += 64) b[k] = seg_rows[beg + k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = lane; k < len; k += 64) {
+      const int32_t x = b[k];
+      int32_t rank = 0;
+      for (int j = 0; j < len; ++j) rank += b[j] < x ? 1 : 0;
+      seg_rows[beg + rank] = x;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // every lane's reads before the next fill
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 bool use_counting() {
   static const bool c = [] {
     const char* e = getenv("LLP_DEDUP_SORT");
@@ -783,7 +826,18 @@ static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, i
   LLP_LAUNCH_CHECK();
   const int64_t ubound = R < num_nodes ? R : num_nodes;
   static const bool two_pass = getenv("LLP_SEGSORT_2PASS") != nullptr;   // A/B: the old short + long launches
-  if (two_pass) {
+  const char* ss_env = getenv("LLP_SEGSORT");   // read per call (once per step): "wave" = segsort_mid_wave_kernel
+  if (ss_env && strcmp(ss_env, "wave") == 0) {
+    int32_t* huge_list = long_list + (R + 1) / 2;   // long segments are > 32 rows: fewer than R / 33 of them
+    int32_t* n_huge = n_long + 1;
+    hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
+                       seg_rows, long_list, n_long);
+    hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(256), 0, s, (int64_t)1, n_huge);
+    hipLaunchKernelGGL(segsort_mid_wave_kernel, dim3(1024), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows,
+                       huge_list, n_huge);
+    hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_huge, huge_list, seg_ptr, seg_rows,
+                       scratch);
+  } else if (two_pass) {
     hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
                        seg_rows, long_list, n_long);
     LLP_LAUNCH_CHECK();

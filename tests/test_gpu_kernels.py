@@ -542,6 +542,44 @@ def test_clip_and_adam_match_oracle(case, nan_group):
 
 
 # ------------------------------------------------------------------ unique-node compaction
+@pytest.mark.skipif(os.environ.get("LLP_TEST_SEGSORT_WAVE") != "1",
+                    reason="opt-in wave-per-segment sort (LLP_SEGSORT=wave) not yet run on the GPU; "
+                           "LLP_TEST_SEGSORT_WAVE=1")
+@pytest.mark.parametrize("N,R,hot,hub", [(235868, 747214, 2000, 0.0), (3000, 40000, 0, 0.3), (50, 1000, 0, 0.0)])
+def test_dedup_segsort_wave(N, R, hot, hub):
+    """LLP_SEGSORT=wave (dedup.hip segsort_mid_wave_kernel): segments of 33..1024 rows
+    ranked one wave each, longer ones by a block; outputs equal the stable sort's.
+    hot: a quarter of the rows on ids 0..hot-1 (the stress probe: ~94-row segments on
+    neighbouring ids); hub: as test_dedup_rows_and_segment_sum (a 12k-row segment)."""
+    k = K()
+    g = torch.Generator().manual_seed(R + 5)
+    target = torch.randint(0, N, (R,), generator=g, dtype=torch.int32)
+    if hot:
+        target[: R // 4] = torch.randint(0, hot, (R // 4,), generator=g, dtype=torch.int32)
+    if hub:
+        u = torch.rand(R, generator=g)
+        target[u < hub] = 7
+    tg = target.to(DEV)
+    uniq = torch.empty(R, dtype=torch.int32, device=DEV)
+    pos = torch.empty(R, dtype=torch.int32, device=DEV)
+    nu = torch.empty(1, dtype=torch.int32, device=DEV)
+    segp = torch.empty(R + 1, dtype=torch.int32, device=DEV)
+    segr = torch.empty(R, dtype=torch.int32, device=DEV)
+    ws = torch.empty(k.dedup_ws_bytes(N, R) // 4 + 16, device=DEV)
+    os.environ["LLP_SEGSORT"] = "wave"
+    try:
+        k.dedup_rows(N, R, tg, uniq, pos, nu, segp, segr, ws)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["LLP_SEGSORT"]
+    u_ref, inv = np.unique(target.numpy(), return_inverse=True)
+    U = int(nu.item())
+    assert U == u_ref.size
+    assert np.array_equal(uniq[:U].cpu().numpy(), u_ref)
+    assert np.array_equal(pos.cpu().numpy(), inv)
+    assert np.array_equal(segr.cpu().numpy(), np.argsort(inv, kind="stable"))
+
+
 @pytest.mark.parametrize("N,R,hub", [(50, 1000, 0.0), (235868, 20000, 0.0), (7, 7, 0.0), (3000, 40000, 0.3)])
 def test_dedup_rows_and_segment_sum(N, R, hub):
     """hub > 0: that fraction of the rows on node 7 and 2 % on each of nodes 11..15, so the

@@ -1,6 +1,7 @@
 # First GPU call of the next round (one box, ~10 min): the whole GPU suite on the
 # current tree, the opt-in head epilogue's gated test + kernel traces + step A/B, the
-# node-sharded full-batch student's gated test + emulated 4-rank cost, then
+# node-sharded full-batch student's gated test + emulated 4-rank cost, the dedup's
+# wave-per-segment sort (gated test + traces), then
 # the segmented-capture bisection LAST (its steps may fault; everything before it is
 # already written under gpurun_out/).  Stops at the first failure.
 export TMPDIR=/tmp
@@ -12,5 +13,7 @@ bash tools/gpu_head_lean.sh || { echo "head epilogue A/B failed"; exit 1; }
 echo "head epilogue A/B: done"
 bash tools/gpu_fb_shard.sh || { echo "sharded full-batch student failed"; exit 1; }
 echo "sharded full-batch student: done"
+bash tools/gpu_segsort_wave.sh || { echo "segsort wave failed"; exit 1; }
+echo "segsort wave: done"
 bash tools/gpu_seg_bisect.sh
 echo rc=$?
