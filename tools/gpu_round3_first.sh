@@ -1,9 +1,9 @@
-# First GPU call of the next round (one box, ~10 min): the whole GPU suite on the
+# First GPU call of the next round (one box, ~15 min; gpurun --timeout 1200): the whole GPU suite on the
 # current tree, the opt-in head epilogue's gated test + kernel traces + step A/B, the
 # node-sharded full-batch student's gated test + emulated 4-rank cost, the dedup's
-# wave-per-segment sort (gated test + traces), then
-# the segmented-capture bisection LAST (its steps may fault; everything before it is
-# already written under gpurun_out/).  Stops at the first failure.
+# wave-per-segment sort (gated test + traces).  Stops at the first failure.  The
+# segmented-capture bisection (tools/gpu_seg_bisect.sh, whose steps may fault) is the
+# second call, on its own.
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -15,5 +15,4 @@ bash tools/gpu_fb_shard.sh || { echo "sharded full-batch student failed"; exit 1
 echo "sharded full-batch student: done"
 bash tools/gpu_segsort_wave.sh || { echo "segsort wave failed"; exit 1; }
 echo "segsort wave: done"
-bash tools/gpu_seg_bisect.sh
-echo rc=$?
+echo rc=0
