@@ -1037,9 +1037,11 @@ class DistillEngine(EngineBase):
         if world <= 1 or os.environ.get("LLP_FB_SHARD") != "1" or p_drop > 0.0 or w_rm != 0.0:
             return None
         n_loc = -(-self.N // world)
+        if self.N - (world - 1) * n_loc <= 0:   # a rank without rows: off on every rank alike
+            return None
         r0 = rank * n_loc
         n_rows = min(self.N, r0 + n_loc) - r0
-        return (r0, n_rows, n_loc, world, rank) if n_rows > 0 else None
+        return r0, n_rows, n_loc, world, rank
 
     def _all_gather_rows(self, full, part, world, rank):
         """full [world * n, H] <- every rank's part [n, H] in rank order."""

@@ -139,3 +139,24 @@ def test_node_sharded_student_sums_to_the_batch_gradient(world):
         assert p.exitcode == 0
     assert abs(loss - full_loss) <= 1e-12 * max(1.0, abs(full_loss)), (loss, full_loss)
     np.testing.assert_allclose(flat, full, rtol=1e-10, atol=1e-13)
+
+
+def test_fb_shard_gating(monkeypatch):
+    """_fb_shard is off unless LLP_FB_SHARD=1 with several (or emulated) ranks, no dropout
+    and no KD_RM; slices cover the nodes with ceil(N / world) rows, the last one ragged."""
+    sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
+    import llp_engine
+    f = llp_engine.DistillEngine._fb_shard
+    eng = types.SimpleNamespace(world=4, rank=3, N=10, emulate_shard=None)
+    monkeypatch.delenv("LLP_FB_SHARD", raising=False)
+    assert f(eng, 0.0, 0.0) is None
+    monkeypatch.setenv("LLP_FB_SHARD", "1")
+    assert f(eng, 0.0, 0.0) == (9, 1, 3, 4, 3)
+    assert f(eng, 0.5, 0.0) is None and f(eng, 0.0, 1.0) is None
+    one = types.SimpleNamespace(world=1, rank=0, N=10, emulate_shard=None)
+    assert f(one, 0.0, 0.0) is None
+    one.emulate_shard = (1, 4)
+    assert f(one, 0.0, 0.0) == (3, 3, 3, 4, 1)
+    for r in range(4):   # N=7 over 4 ranks: 2, 2, 2, 1 rows; N=6: rank 3 would have none -> off on every rank
+        assert f(types.SimpleNamespace(world=4, rank=r, N=7, emulate_shard=None), 0.0, 0.0)[1] == (1 if r == 3 else 2)
+        assert f(types.SimpleNamespace(world=4, rank=r, N=6, emulate_shard=None), 0.0, 0.0) is None
