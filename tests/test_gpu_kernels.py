@@ -304,8 +304,10 @@ def test_head_fwd_bwd_and_colsum(dt, R, H):
 
 
 # ------------------------------------------------------------------ fused LLP loss
-@pytest.mark.parametrize("B,C,margin", [(37, 12, 0.1), (64, 36, 0.01), (5, 70, 0.2), (3, 2, 0.05)])
+@pytest.mark.parametrize("B,C,margin", [(37, 12, 0.1), (64, 36, 0.01), (5, 70, 0.2), (3, 2, 0.05), (3, 720, 0.05)])
 def test_llp_loss_matches_oracle(B, C, margin):
+    """C = 720: the largest contexts per anchor of the collab sweep
+    (configurations/collab_transductive.yaml), 258,840 rank pairs per anchor."""
     k = K()
     g = torch.Generator().manual_seed(B * C)
     s_logit = torch.randn(B, C, generator=g) * 2
