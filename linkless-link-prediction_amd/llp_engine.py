@@ -500,6 +500,14 @@ class EngineBase:
         (llp_hadamard_bwd_blocks, label-row layout; drow: the 'inner' predictor's scalar) and
         every node's rows are summed in row order (f32) into its row of ``out``; other rows are 0."""
         N, H = self.N, h.shape[1]
+        if not self._grouped_ok(H):
+            # rows wider than the grouping kernels take: f32 scatter-add (atomics, so not
+            # bit-reproducible), then into ``out`` (possibly a strided slot, another dtype)
+            d32 = self._buf("hb_d32", (N, H), torch.float32)
+            d32.zero_()
+            K.hadamard_bwd_scatter(R, H, dZ, tgt[:R], tgt[R:], h, d32, drow=drow)
+            out.copy_(d32)
+            return
         R2 = 2 * R
         uniq = self._buf("hb_uniq", (R2,), torch.int32)
         pos = self._buf("hb_pos", (R2,), torch.int32)
@@ -512,6 +520,13 @@ class EngineBase:
         K.hadamard_bwd_blocks(0, 1, R, H, dZ, h, dh_rows, drow=drow, hidx=tgt)
         out.zero_()
         K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, out, count=n_u, out_rows=uniq)
+
+    def _grouped_ok(self, H):
+        """The node-grouped Hadamard-backward kernels (llp_hadamard_bwd_segments,
+        llp_segment_sum_rows, llp_hadamard_bwd_blocks with an index) take rows of up to
+        256 16-B chunks: H <= 2048 in bf16, <= 1024 in fp32 (the collab sweep's 2048 in
+        fp32 takes the row-wise / scatter paths)."""
+        return H * (2 if self.dtype == torch.bfloat16 else 4) <= 256 * 16
 
     def _relu_aux(self, act):
         """What the ReLU-backward GEMM reads for activation ``act``: its bit mask when
@@ -775,7 +790,7 @@ class DistillEngine(EngineBase):
         # ---- unique-node compaction: without dropout the student is a row-wise
         # function, so duplicate rows of x[this_target] give identical activations;
         # run it on the U distinct nodes and sum each node's row gradients.
-        dedup = self.dedup and p_drop == 0.0
+        dedup = self.dedup and p_drop == 0.0 and self._grouped_ok(H)
         n_u = None
         if dedup:
             fresh = "uniq" not in self._bufs or self._bufs["uniq"].numel() < R1
@@ -934,7 +949,7 @@ class DistillEngine(EngineBase):
 
         # ---- a4: student MLP over all nodes (src/main.py:173); with LLP_FB_SHARD=1 each rank
         # runs it on its own slice of the nodes and the slices are all-gathered (_fb_shard)
-        shard = self._fb_shard(p_drop, float(a.KD_RM))
+        shard = self._fb_shard(p_drop, float(a.KD_RM) == 0.0 and self._grouped_ok(H))
         r0, n_rows, n_loc, s_world, s_rank = (0, N, N, 1, 0) if shard is None else shard
         x_loc = self.x if shard is None else self.x[r0:r0 + n_rows]
         acts = []
@@ -977,7 +992,7 @@ class DistillEngine(EngineBase):
         # d(loss)/dh: without KD_RM, the pair rows' Hadamard gradients are grouped by node and
         # summed in row order (deterministic, straight into the compute-dtype buffer); with KD_RM
         # (which adds at the anchors) they accumulate by f32 scatter-add, then convert
-        grouped = w_rm == 0.0
+        grouped = w_rm == 0.0 and self._grouped_ok(H)
         if not grouped:   # in fp32 mode dh32 IS the student backward's first gradient buffer
             dh32 = self._buf("gS0" if dt == torch.float32 else "dh32", (N, H), torch.float32)
             dh32.zero_()
@@ -1021,12 +1036,13 @@ class DistillEngine(EngineBase):
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
         return n_neg
 
-    def _fb_shard(self, p_drop, w_rm):
+    def _fb_shard(self, p_drop, grouped):
         """(first row, rows, rows per rank, world, rank) of this rank's slice of the full-batch student,
         or None: the student over all N nodes on every rank, as in the reference
         (src/main.py:173).  Opt-in (LLP_FB_SHARD=1) until measured on the GPU: several
         ranks, no dropout (the GEMM's dropout draws are keyed by the row within the call)
-        and no KD_RM (its f32 scatter target covers all rows).  The slices are all-gathered
+        and the node-grouped d(h) (``grouped``: no KD_RM, whose f32 scatter target covers
+        all rows, and rows the grouping kernels take).  The slices are all-gathered
         after the forward; d(h) of all nodes is reduce-scattered onto them before the
         student backward, whose weight gradients the usual all-reduce sums.
         ``emulate_shard = (rank, world)`` on a one-rank engine times that rank's slice
@@ -1034,7 +1050,7 @@ class DistillEngine(EngineBase):
         world, rank = self.world, self.rank
         if world <= 1 and self.emulate_shard is not None:
             rank, world = self.emulate_shard
-        if world <= 1 or os.environ.get("LLP_FB_SHARD") != "1" or p_drop > 0.0 or w_rm != 0.0:
+        if world <= 1 or os.environ.get("LLP_FB_SHARD") != "1" or p_drop > 0.0 or not grouped:
             return None
         n_loc = -(-self.N // world)
         if self.N - (world - 1) * n_loc <= 0:   # a rank without rows: off on every rank alike

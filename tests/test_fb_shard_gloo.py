@@ -79,7 +79,7 @@ def _worker(rank, world, port, q):
     N, x, t_h, samples, edge, neg, (sw, sb, pw, pb, tw, tb), args = prob
     fake = types.SimpleNamespace(world=world, rank=rank, group=None, N=N, emulate_shard=None)
     os.environ["LLP_FB_SHARD"] = "1"
-    r0, n_rows, n_loc, s_world, s_rank = llp_engine.DistillEngine._fb_shard(fake, 0.0, 0.0)
+    r0, n_rows, n_loc, s_world, s_rank = llp_engine.DistillEngine._fb_shard(fake, 0.0, True)
     assert (s_world, s_rank, n_loc) == (world, rank, -(-N // world))
     lw = [w.clone().requires_grad_() for w in sw]
     lb = [b.clone().requires_grad_() for b in sb]
@@ -149,14 +149,14 @@ def test_fb_shard_gating(monkeypatch):
     f = llp_engine.DistillEngine._fb_shard
     eng = types.SimpleNamespace(world=4, rank=3, N=10, emulate_shard=None)
     monkeypatch.delenv("LLP_FB_SHARD", raising=False)
-    assert f(eng, 0.0, 0.0) is None
+    assert f(eng, 0.0, True) is None
     monkeypatch.setenv("LLP_FB_SHARD", "1")
-    assert f(eng, 0.0, 0.0) == (9, 1, 3, 4, 3)
-    assert f(eng, 0.5, 0.0) is None and f(eng, 0.0, 1.0) is None
+    assert f(eng, 0.0, True) == (9, 1, 3, 4, 3)
+    assert f(eng, 0.5, True) is None and f(eng, 0.0, False) is None
     one = types.SimpleNamespace(world=1, rank=0, N=10, emulate_shard=None)
-    assert f(one, 0.0, 0.0) is None
+    assert f(one, 0.0, True) is None
     one.emulate_shard = (1, 4)
-    assert f(one, 0.0, 0.0) == (3, 3, 3, 4, 1)
+    assert f(one, 0.0, True) == (3, 3, 3, 4, 1)
     for r in range(4):   # N=7 over 4 ranks: 2, 2, 2, 1 rows; N=6: rank 3 would have none -> off on every rank
-        assert f(types.SimpleNamespace(world=4, rank=r, N=7, emulate_shard=None), 0.0, 0.0)[1] == (1 if r == 3 else 2)
-        assert f(types.SimpleNamespace(world=4, rank=r, N=6, emulate_shard=None), 0.0, 0.0) is None
+        assert f(types.SimpleNamespace(world=4, rank=r, N=7, emulate_shard=None), 0.0, True)[1] == (1 if r == 3 else 2)
+        assert f(types.SimpleNamespace(world=4, rank=r, N=6, emulate_shard=None), 0.0, True) is None

@@ -1,6 +1,8 @@
 """The fused HIP distillation step (llp_engine) replayed on the golden vectors
 produced by the reference's own train_minibatch (tests/golden/gen_golden.py),
 with every random tensor injected.  fp32 path: logits/losses within 1e-4."""
+import os
+
 import pytest
 import torch
 
@@ -293,3 +295,55 @@ def test_engine_fused_segment_backward_bit_identical():
                 assert torch.equal(a, b), (dt, tuple(a.shape), (a - b).abs().max().item())
     finally:
         llp_engine._SEGMENT_FUSED = saved
+
+
+@pytest.mark.skipif(os.environ.get("LLP_TEST_WIDE") != "1",
+                    reason="fp32 rows wider than the grouping kernels (row-wise / scatter fallbacks) not yet run "
+                           "on the GPU; LLP_TEST_WIDE=1")
+def test_engine_fp32_hidden_2048_matches_oracle():
+    """The collab sweep's hidden_channels=2048 in fp32: 8 KiB rows exceed the node-grouped
+    Hadamard-backward kernels (256 16-B chunks), so the engine runs the row-wise student
+    (EngineBase._grouped_ok); one step with injected samples against the oracle."""
+    import types
+
+    import numpy as np
+    from oracle import llp_oracle as O
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, F_, H, L = 400, 64, 2048, 2
+    args = types.SimpleNamespace(rw_step=1, hops=2, ns_rate=2, ps_method="nb", dropout=0.0, margin=0.05,
+                                 LLP_D=1.0, LLP_R=1.0, True_label=0.5, predictor="mlp", lr=0.001)
+    g = torch.Generator().manual_seed(0)
+    u = torch.randint(0, N, (3000,), generator=g)
+    v = torch.randint(0, N, (3000,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
+    x = torch.randn(N, F_, generator=g) * 0.3
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    eng, model, pred = _make_engine("fp32", N, F_, H, L, 3, args, x, t_h, ei)
+    assert not eng._grouped_ok(H)
+    B, C, P = 16, 6, 64
+    samples = torch.randint(0, N, (B, C + 1), generator=g)
+    link = torch.randperm(pairs.size(0), generator=g)[:P]
+    neg = torch.randint(0, N, (2, P), generator=g)
+    anchors = samples[:, 0].to(torch.int32)
+    params0 = [p.detach().cpu().clone() for p in list(model.parameters()) + list(pred.parameters())]
+    tpar = [p.detach().cpu().clone() for p in eng.tpred.parameters()]
+    eng.step_minibatch(anchors.to(DEV), link.to(torch.int32).to(DEV), pairs.to(torch.int32).to(DEV),
+                       samples=samples.to(DEV), neg=neg.to(torch.int32).to(DEV))
+    torch.cuda.synchronize()
+    t = eng.terms.cpu()
+    leaves = [p.clone().requires_grad_() for p in params0]
+    sw, sb = leaves[0:2 * L:2], leaves[1:2 * L:2]
+    pw, pb = leaves[2 * L::2], leaves[2 * L + 1::2]
+    tw, tb = tpar[0::2], tpar[1::2]
+    r = O.distill_losses_minibatch(x, t_h, samples, pairs[link].t(), neg, sw, sb, pw, pb, tw, tb, args)
+    assert abs(t[1].item() - r["label_loss"].item()) <= 1e-4 * max(1, abs(r["label_loss"].item()))
+    assert abs(t[2].item() - r["llp_d"].item()) <= 1e-4 * max(1, abs(r["llp_d"].item()))
+    assert abs(t[3].item() - r["llp_r"].item()) <= 1e-4 * max(1, abs(r["llp_r"].item()))
+    grads = torch.autograd.grad(r["loss"], leaves)
+    for p, ref in zip(list(model.parameters()) + list(pred.parameters()), grads):
+        ok, err = _grad_close(p.grad.detach().cpu(), ref, 2e-4)
+        assert ok, (tuple(p.shape), err)
+    assert np.isfinite(t.numpy()).all()
