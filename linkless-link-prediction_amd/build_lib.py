@@ -26,11 +26,11 @@ def _newest_header():
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
-def _compile(src, obj, force):
+def _compile(src, obj, force, extra=()):
     if not force and os.path.exists(obj):
         if os.path.getmtime(obj) >= max(os.path.getmtime(src), _newest_header()):
             return obj, None
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
@@ -41,20 +41,40 @@ def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(os.path.join(CSRC, "build"), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     objs = [os.path.join(CSRC, "build", os.path.basename(s) + ".o") for s in srcs]
+    return _build(srcs, objs, OUT, force, verbose, [])
+
+
+def build_variant(out: str, defines, sources=("dedup.hip",), verbose: bool = True) -> str:
+    """An A/B build of the library at ``out``: ``sources`` compiled with the extra
+    ``-D`` ``defines`` (objects under csrc/build/<tag>/), every other object shared
+    with the default build.  Used by tools/ for same-box comparisons (LLP_LIB)."""
+    build(verbose=False)
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    tag = os.path.splitext(os.path.basename(out))[0]
+    os.makedirs(os.path.join(CSRC, "build", tag), exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    objs = [os.path.join(CSRC, "build", tag if os.path.basename(s) in sources else "", os.path.basename(s) + ".o")
+            for s in srcs]
+    return _build(srcs, objs, out, False, verbose, ["-D" + d for d in defines],
+                  only={os.path.basename(s) for s in srcs if os.path.basename(s) in sources})
+
+
+def _build(srcs, objs, out, force, verbose, extra, only=None):
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    todo = [(s, o) for s, o in zip(srcs, objs) if only is None or os.path.basename(s) in only]
     with cf.ThreadPoolExecutor(max_workers=max(jobs, 1)) as ex:
-        results = list(ex.map(lambda so: _compile(so[0], so[1], force), zip(srcs, objs)))
+        results = list(ex.map(lambda so: _compile(so[0], so[1], force, extra), todo))
     errs = [e for _, e in results if e]
     if errs:
         raise RuntimeError("libllp_hip build failed:\n" + "\n".join(errs))
-    if force or not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *objs, "-o", OUT]
+    if force or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *objs, "-o", out]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
-            print(f"built {OUT}")
-    return OUT
+            print(f"built {out}")
+    return out
 
 
 if __name__ == "__main__":

@@ -9,45 +9,14 @@
 // row order) before the student backward.
 #include "llp_common.h"
 
-#include <rocprim/device/device_radix_sort.hpp>
+#ifdef LLP_DEDUP_ROCPRIM_SCAN
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
-#include <stdlib.h>
-#include <string.h>
+#endif
 
 #include <type_traits>
 
 namespace {
-
-__global__ void mark_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ mark) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r < R) mark[target[r]] = 1;
-}
-
-// after the exclusive scan: uidx[v] = slot of node v (valid where mark[v] was 1)
-__global__ void compact_kernel(int64_t N, const int32_t* __restrict__ mark, const int32_t* __restrict__ uidx,
-                               int32_t* __restrict__ uniq, int32_t* __restrict__ n_unique) {
-  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (v < N && mark[v]) uniq[uidx[v]] = (int32_t)v;
-  if (v == N - 1) *n_unique = uidx[v] + mark[v];
-}
-
-__global__ void pos_kernel(int64_t R, const int32_t* __restrict__ target, const int32_t* __restrict__ uidx,
-                           int32_t* __restrict__ pos, int32_t* __restrict__ rows) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r < R) {
-    pos[r] = uidx[target[r]];
-    rows[r] = (int32_t)r;
-  }
-}
-
-// seg_ptr[u] = first position of key u in the sorted keys (keys are dense 0..U-1)
-__global__ void seg_ptr_kernel(int64_t R, const int32_t* __restrict__ skeys, int32_t* __restrict__ seg_ptr,
-                               const int32_t* __restrict__ n_unique) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < R && (i == 0 || skeys[i] != skeys[i - 1])) seg_ptr[skeys[i]] = (int32_t)i;
-  if (i == 0) seg_ptr[*n_unique] = (int32_t)R;
-}
 
 template <typename T>
 struct V8;
@@ -404,51 +373,44 @@ __global__ void gather_i32_kernel(int64_t n, const int32_t* __restrict__ idx, co
   if (i < n) out[i] = src[idx[i]];
 }
 
-size_t scan_bytes(int64_t N) {
-  size_t b = 0;
-  rocprim::exclusive_scan(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)N,
-                          rocprim::plus<int32_t>());
-  return b;
-}
-size_t sort_bytes(int64_t R) {
-  size_t b = 0;
-  rocprim::radix_sort_pairs(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
-                            (int32_t*)nullptr, (unsigned int)R);
-  return b;
-}
 int64_t al256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
-// ---------------------------------------------------------------- counting path
-// Same outputs as the radix path, without the sort: per-node row counts
-// (integer atomics: exact), one exclusive scan of (present, count) packed in a
-// u64 gives every node its slot and its segment start, rows are scattered to
-// their segment through an atomic cursor (any order), then every segment is
-// sorted by row id, which restores row order: bit-identical to the stable sort.
+// ---------------------------------------------------------------- compaction
+// Per-node row counts (integer atomics: exact) with each row's arrival rank, one
+// exclusive scan of (present, count) packed in a u64 gives every node its slot and its
+// segment start, rows are scattered to start + rank without atomics, then every segment
+// is sorted by row id, which restores row order: the same outputs as a stable sort of
+// the rows by node.
+//
+// Every pass is a kernel of this file (no hipMemsetAsync node, no rocprim): the whole
+// compaction is plain kernel nodes under stream capture, which the multi-rank step's
+// segmented hipGraph replays.  Build-time alternatives for A/B runs of
+// tools/seg_diag.py: -DLLP_DEDUP_MEMSET (the count zeroed by hipMemsetAsync),
+// -DLLP_DEDUP_ROCPRIM_SCAN (rocprim's lookback scan), -DLLP_DEDUP_SEGSORT_WAVE (long
+// segments ranked one wave each across the grid).
 constexpr int SHORT_SEG = 32;   // segments up to this length sort in one thread's LDS row
 constexpr int LONG_LDS = 4096;  // longer ones: one block each, ranks counted in LDS up to this length
 
-struct PackCount {
-  __host__ __device__ uint64_t operator()(int32_t c) const {
-    return (c > 0 ? (1ull << 32) : 0ull) | (uint64_t)(uint32_t)c;
-  }
-};
+__device__ __host__ __forceinline__ uint64_t pack_count(int32_t c) {
+  return (c > 0 ? (1ull << 32) : 0ull) | (uint64_t)(uint32_t)c;
+}
 
+#ifdef LLP_DEDUP_ROCPRIM_SCAN
+struct PackCount {
+  __host__ __device__ uint64_t operator()(int32_t c) const { return pack_count(c); }
+};
 size_t scan64_bytes(int64_t N) {
   size_t b = 0;
   auto it = rocprim::make_transform_iterator((const int32_t*)nullptr, PackCount());
   rocprim::exclusive_scan(nullptr, b, it, (uint64_t*)nullptr, (uint64_t)0, (size_t)N, rocprim::plus<uint64_t>());
   return b;
 }
-
-__global__ void count_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ cnt) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r < R) atomicAdd(&cnt[target[r]], 1);
-}
+#else
+size_t scan64_bytes(int64_t) { return 0; }
+#endif
 
 // count pass that also records each row's arrival rank within its node (returning
-// atomic), so the scatter needs no atomics (default; LLP_DEDUP_RANK=0: the atomic-cursor
-// scatter).  Collab R = 747k rows: count 45 -> 46 us, scatter 57 -> 13 us; same outputs
-// (the segment sort restores row order either way).
+// atomic), so the scatter needs no atomics.  Collab R = 747k rows: 46 us.
 __global__ void count_rank_kernel(int64_t R, const int32_t* __restrict__ target, int32_t* __restrict__ cnt,
                                   int32_t* __restrict__ rank) {
   const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -465,21 +427,15 @@ __global__ void scatter_rank_kernel(int64_t R, const int32_t* __restrict__ targe
   seg_rows[start[v] + rank[r]] = (int32_t)r;
 }
 
-// ------------------------------------------------ own scan (LLP_DEDUP_SCAN=own, opt-in)
-// Exclusive scan of PackCount(cnt[v]) over v < n without rocprim and without a
-// hipMemsetAsync node (cnt zeroed by a kernel): a diagnosis aid for the segmented
-// multi-rank capture and a rocprim-free alternative.  u64 integer sums,
-// so any association gives the same result.
-constexpr int OS_T = 256, OS_I = 8, OS_B = OS_T * OS_I;   // 2,048 values per block
-
-__device__ __forceinline__ uint64_t pack_count(int32_t c) {
-  return (c > 0 ? (1ull << 32) : 0ull) | (uint64_t)(uint32_t)c;
-}
-
 __global__ void zero_i32_kernel(int64_t n, int32_t* __restrict__ p) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0;
 }
+
+// Exclusive scan of pack_count(cnt[v]) over v < n in three launches: per-block sums,
+// one block scanning the sums, per-block scans with their offsets.  u64 integer sums,
+// so any association gives the same result.
+constexpr int OS_T = 256, OS_I = 8, OS_B = OS_T * OS_I;   // 2,048 values per block
 
 __global__ __launch_bounds__(OS_T) void os_block_sum_kernel(int64_t n, const int32_t* __restrict__ cnt,
                                                             uint64_t* __restrict__ bsum) {
@@ -568,38 +524,12 @@ __global__ void compact_count_kernel(int64_t N, int64_t R, const int32_t* __rest
     const int32_t U = slot + (c > 0 ? 1 : 0);
     *n_unique = U;
     seg_ptr[U] = (int32_t)R;
-    *n_long = 0;
+    n_long[0] = 0;
+    n_long[1] = 0;
   }
 }
 
-__global__ void scatter_rows_kernel(int64_t R, const int32_t* __restrict__ target, const int32_t* __restrict__ uidx,
-                                    int32_t* __restrict__ cursor, int32_t* __restrict__ pos,
-                                    int32_t* __restrict__ seg_rows) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const int32_t v = target[r];
-  pos[r] = uidx[v];
-  seg_rows[atomicAdd(&cursor[v], 1)] = (int32_t)r;
-}
-
-// one thread per segment: insertion sort of up to SHORT_SEG row ids in its own
-// LDS row; longer segments are listed for segsort_long_kernel
-__global__ __launch_bounds__(256) void segsort_short_kernel(const int32_t* __restrict__ n_unique,
-                                                            const int32_t* __restrict__ seg_ptr,
-                                                            int32_t* __restrict__ seg_rows,
-                                                            int32_t* __restrict__ long_list,
-                                                            int32_t* __restrict__ n_long) {
-  __shared__ int32_t buf[256][SHORT_SEG + 1];
-  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (s >= *n_unique) return;
-  const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
-  if (len <= 1) return;
-  if (len > SHORT_SEG) {
-    long_list[atomicAdd(n_long, 1)] = (int32_t)s;
-    return;
-  }
-  int32_t* a = buf[threadIdx.x];
-  for (int i = 0; i < len; ++i) a[i] = seg_rows[b + i];
+__device__ __forceinline__ void insertion_sort(int32_t* a, int len) {
   for (int i = 1; i < len; ++i) {
     const int32_t x = a[i];
     int j = i - 1;
@@ -609,43 +539,33 @@ __global__ __launch_bounds__(256) void segsort_short_kernel(const int32_t* __res
     }
     a[j + 1] = x;
   }
-  for (int i = 0; i < len; ++i) seg_rows[b + i] = a[i];
 }
 
-// one block per long segment (grid-strided over the list): each row id's rank
-// = the number of smaller ids in the segment (ids are distinct); the segment is
-// read from LDS, or from a copy in `scratch` past LONG_LDS rows
-__global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __restrict__ n_long,
-                                                           const int32_t* __restrict__ long_list,
-                                                           const int32_t* __restrict__ seg_ptr,
-                                                           int32_t* __restrict__ seg_rows,
-                                                           int32_t* __restrict__ scratch) {
-  __shared__ int32_t buf[LONG_LDS];
-  const int32_t nl = *n_long;
-  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
-    const int32_t s = long_list[i];
-    const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
-    const bool in_lds = len <= LONG_LDS;
-    const int32_t* src = in_lds ? buf : scratch + b;
-    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
-      if (in_lds) buf[k] = seg_rows[b + k];
-      else scratch[b + k] = seg_rows[b + k];
-    }
-    __syncthreads();
-    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
-      const int32_t x = src[k];
-      int32_t rank = 0;
-      for (int32_t j = 0; j < len; ++j) rank += src[j] < x ? 1 : 0;
-      seg_rows[b + rank] = x;
-    }
-    __syncthreads();
+// rank-by-count of one long segment by a whole block: each row id's rank = the number
+// of smaller ids in the segment (ids are distinct); read from LDS (`buf`, `cap` ints) or
+// from a copy in `scratch` past that
+__device__ __forceinline__ void rank_segment_block(int32_t* __restrict__ seg_rows, int32_t b, int32_t len,
+                                                   int32_t* buf, int cap, int32_t* __restrict__ scratch) {
+  const bool in_lds = len <= cap;
+  const int32_t* src = in_lds ? buf : scratch + b;
+  for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
+    if (in_lds) buf[k] = seg_rows[b + k];
+    else scratch[b + k] = seg_rows[b + k];
   }
+  __syncthreads();
+  for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
+    const int32_t x = src[k];
+    int32_t rank = 0;
+    for (int32_t j = 0; j < len; ++j) rank += src[j] < x ? 1 : 0;
+    seg_rows[b + rank] = x;
+  }
+  __syncthreads();
 }
 
-// segsort_short_kernel + segsort_long_kernel in one launch: each thread sorts its short
-// segment in its LDS row and lists a long one in the block's LDS list; then the block
-// ranks its long segments one at a time (the rows buffer reused, or `scratch` past it).
-// Same result (every segment in row-id order).
+#ifndef LLP_DEDUP_SEGSORT_WAVE
+// Every segment sorted by row id in one launch: each thread sorts its short segment in
+// its LDS row and lists a long one in the block's LDS list; then the block ranks its
+// long segments one at a time (the rows buffer reused, or `scratch` past it).
 __global__ __launch_bounds__(256) void segsort_kernel(const int32_t* __restrict__ n_unique,
                                                       const int32_t* __restrict__ seg_ptr,
                                                       int32_t* __restrict__ seg_rows, int32_t* __restrict__ scratch) {
@@ -662,50 +582,46 @@ __global__ __launch_bounds__(256) void segsort_kernel(const int32_t* __restrict_
     } else if (len > 1) {
       int32_t* a = buf[threadIdx.x];
       for (int i = 0; i < len; ++i) a[i] = seg_rows[b + i];
-      for (int i = 1; i < len; ++i) {
-        const int32_t x = a[i];
-        int j = i - 1;
-        while (j >= 0 && a[j] > x) {
-          a[j + 1] = a[j];
-          --j;
-        }
-        a[j + 1] = x;
-      }
+      insertion_sort(a, len);
       for (int i = 0; i < len; ++i) seg_rows[b + i] = a[i];
     }
   }
   __syncthreads();
   const int nl = n_longs;
-  int32_t* flat = &buf[0][0];
-  constexpr int FLAT = 256 * (SHORT_SEG + 1);
   for (int i = 0; i < nl; ++i) {
     const int32_t sg = longs[i];
     const int32_t b = seg_ptr[sg], len = seg_ptr[sg + 1] - b;
-    const bool in_lds = len <= FLAT;
-    const int32_t* src = in_lds ? flat : scratch + b;
-    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
-      if (in_lds) flat[k] = seg_rows[b + k];
-      else scratch[b + k] = seg_rows[b + k];
-    }
-    __syncthreads();
-    for (int32_t k = threadIdx.x; k < len; k += blockDim.x) {
-      const int32_t x = src[k];
-      int32_t rank = 0;
-      for (int32_t j = 0; j < len; ++j) rank += src[j] < x ? 1 : 0;
-      seg_rows[b + rank] = x;
-    }
-    __syncthreads();
+    rank_segment_block(seg_rows, b, len, &buf[0][0], 256 * (SHORT_SEG + 1), scratch);
   }
 }
+#else
+// one thread per segment: insertion sort of up to SHORT_SEG row ids in its own LDS row;
+// longer segments go on the global list for segsort_mid_wave_kernel
+__global__ __launch_bounds__(256) void segsort_short_kernel(const int32_t* __restrict__ n_unique,
+                                                            const int32_t* __restrict__ seg_ptr,
+                                                            int32_t* __restrict__ seg_rows,
+                                                            int32_t* __restrict__ long_list,
+                                                            int32_t* __restrict__ n_long) {
+  __shared__ int32_t buf[256][SHORT_SEG + 1];
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s >= *n_unique) return;
+  const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
+  if (len <= 1) return;
+  if (len > SHORT_SEG) {
+    long_list[atomicAdd(n_long, 1)] = (int32_t)s;
+    return;
+  }
+  int32_t* a = buf[threadIdx.x];
+  for (int i = 0; i < len; ++i) a[i] = seg_rows[b + i];
+  insertion_sort(a, len);
+  for (int i = 0; i < len; ++i) seg_rows[b + i] = a[i];
+}
 
-// LLP_SEGSORT=wave (opt-in until measured): the long segments listed by
-// segsort_short_kernel are ranked one WAVE per segment across the whole grid (up to
-// WAVE_SEG rows, from the wave's own LDS row; all lanes read the same element, an LDS
-// broadcast), so hot nodes with neighbouring ids no longer queue on the few blocks that
-// own those ids (segsort_kernel ranks a block's long segments one at a time).  Longer
-// segments go on to a second list for segsort_long_kernel.  Same result: every segment
-// in row-id order.  Control flow is wave-uniform (one segment per wave per round), so
-// the LDS row needs only wave-scope ordering, no block barrier.
+// the long segments ranked one WAVE per segment across the whole grid (up to WAVE_SEG
+// rows, from the wave's own LDS row), so hot nodes with neighbouring ids do not queue on
+// the few blocks that own those ids; longer segments go on to a second list for
+// segsort_long_kernel.  Control flow is wave-uniform, so the LDS row needs only
+// wave-scope ordering.
 constexpr int WAVE_SEG = 1024;
 
 __global__ __launch_bounds__(256) void segsort_mid_wave_kernel(const int32_t* __restrict__ n_long,
@@ -741,32 +657,40 @@ __global__ __launch_bounds__(256) void segsort_mid_wave_kernel(const int32_t* __
   }
 }
 
-bool use_counting() {
-  static const bool c = [] {
-    const char* e = getenv("LLP_DEDUP_SORT");
-    return !(e && strcmp(e, "radix") == 0);
-  }();
-  return c;
+// one block per huge segment (grid-strided over the list)
+__global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __restrict__ n_huge,
+                                                           const int32_t* __restrict__ huge_list,
+                                                           const int32_t* __restrict__ seg_ptr,
+                                                           int32_t* __restrict__ seg_rows,
+                                                           int32_t* __restrict__ scratch) {
+  __shared__ int32_t buf[LONG_LDS];
+  const int32_t nh = *n_huge;
+  for (int32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const int32_t s = huge_list[i];
+    const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
+    rank_segment_block(seg_rows, b, len, buf, LONG_LDS, scratch);
+  }
 }
+#endif
 
 }  // namespace
 
-static int64_t radix_ws_bytes(int64_t num_nodes, int64_t R) {
-  return 2 * al256((num_nodes + 1) * 4) + 3 * al256(R * 4) + al256((int64_t)scan_bytes(num_nodes)) +
-         al256((int64_t)sort_bytes(R)) + 512;
-}
 static int64_t counting_ws_bytes(int64_t num_nodes, int64_t R) {
   return 3 * al256((num_nodes + 1) * 4) + al256(num_nodes * 8) + 2 * al256(R * 4) + al256(256) +
          al256((int64_t)scan64_bytes(num_nodes)) + al256(((num_nodes + OS_B - 1) / OS_B) * 8) + 512;
 }
 
 extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) {
-  const int64_t a = radix_ws_bytes(num_nodes, R), b = counting_ws_bytes(num_nodes, R);
-  return a > b ? a : b;
+  return counting_ws_bytes(num_nodes, R);
 }
 
-static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
-                          int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace, hipStream_t s) {
+extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
+                              int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
+                              int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(target && uniq && pos && n_unique && seg_ptr && seg_rows && workspace, "llp_dedup_rows: null");
+  LLP_CHECK_ARG(num_nodes > 0 && num_nodes < (1ll << 31) && R > 0 && R < (1ll << 31), "llp_dedup_rows: sizes");
+  LLP_CHECK_ARG(workspace_bytes >= llp_dedup_rows_workspace_bytes(num_nodes, R), "llp_dedup_rows: workspace");
+  hipStream_t s = (hipStream_t)stream;
   char* w = reinterpret_cast<char*>(workspace);
   int32_t* cnt = reinterpret_cast<int32_t*>(w);
   w += al256((num_nodes + 1) * 4);
@@ -778,121 +702,64 @@ static int dedup_counting(int64_t num_nodes, int64_t R, const int32_t* target, i
   w += al256(num_nodes * 8);
   int32_t* long_list = reinterpret_cast<int32_t*>(w);
   w += al256(R * 4);
-  int32_t* scratch = reinterpret_cast<int32_t*>(w);
+  int32_t* scratch = reinterpret_cast<int32_t*>(w);   // row ranks until the segment sort
   w += al256(R * 4);
-  int32_t* n_long = reinterpret_cast<int32_t*>(w);
+  int32_t* n_long = reinterpret_cast<int32_t*>(w);    // [0] long segments, [1] huge ones (wave sort)
   w += al256(256);
   void* scan_tmp = w;
-  size_t scan_b = scan64_bytes(num_nodes);
+  const size_t scan_b = scan64_bytes(num_nodes);
   w += al256((int64_t)scan_b);
-  uint64_t* os_sums = reinterpret_cast<uint64_t*>(w);   // own scan: per-block sums / offsets
+  uint64_t* os_sums = reinterpret_cast<uint64_t*>(w);   // per-block sums / offsets of the own scan
+  (void)scan_tmp;
 
-  static const bool rank_env = !(getenv("LLP_DEDUP_RANK") && atoi(getenv("LLP_DEDUP_RANK")) == 0);
-  static const bool own_scan = getenv("LLP_DEDUP_SCAN") && strcmp(getenv("LLP_DEDUP_SCAN"), "own") == 0;
-  hipError_t e = hipSuccess;
-  if (own_scan) {
-    hipLaunchKernelGGL(zero_i32_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, cnt);
-    LLP_LAUNCH_CHECK();
-  } else {
-    e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
-    if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
-  }
-  if (rank_env)   // the rank goes to `scratch` (free until the segment sort)
-    hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt, scratch);
-  else
-    hipLaunchKernelGGL(count_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt);
+#ifdef LLP_DEDUP_MEMSET
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
+  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
+#else
+  hipLaunchKernelGGL(zero_i32_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, cnt);
+#endif
+  hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt, scratch);
   LLP_LAUNCH_CHECK();
-  if (own_scan) {
+#ifdef LLP_DEDUP_ROCPRIM_SCAN
+  {
+    auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
+    size_t sb = scan_b;
+    const hipError_t e2 = rocprim::exclusive_scan(scan_tmp, sb, it, pre, (uint64_t)0, (size_t)num_nodes,
+                                                  rocprim::plus<uint64_t>(), s);
+    if (e2 != hipSuccess) return ::llp::set_error((int)e2, "llp_dedup_rows: scan");
+  }
+#else
+  {
     const int64_t nb = (num_nodes + OS_B - 1) / OS_B;
     hipLaunchKernelGGL(os_block_sum_kernel, dim3((unsigned)nb), dim3(OS_T), 0, s, num_nodes, cnt, os_sums);
     hipLaunchKernelGGL(os_scan_sums_kernel, dim3(1), dim3(1024), 0, s, nb, os_sums);
     hipLaunchKernelGGL(os_block_scan_kernel, dim3((unsigned)nb), dim3(OS_T), 0, s, num_nodes, cnt, os_sums, pre);
     LLP_LAUNCH_CHECK();
-  } else {
-    auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
-    e = rocprim::exclusive_scan(scan_tmp, scan_b, it, pre, (uint64_t)0, (size_t)num_nodes,
-                                rocprim::plus<uint64_t>(), s);
-    if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: scan");
   }
+#endif
   hipLaunchKernelGGL(compact_count_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, R, cnt, pre,
                      uniq, seg_ptr, uidx, cursor, n_unique, n_long);
   LLP_LAUNCH_CHECK();
-  if (rank_env)   // cursor[v] = segment start of v (compact_count_kernel)
-    hipLaunchKernelGGL(scatter_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, scratch,
-                       pos, seg_rows);
-  else
-    hipLaunchKernelGGL(scatter_rows_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, pos,
-                       seg_rows);
+  // cursor[v] = segment start of v (compact_count_kernel); scratch[r] = rank of row r
+  hipLaunchKernelGGL(scatter_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, cursor, scratch,
+                     pos, seg_rows);
   LLP_LAUNCH_CHECK();
   const int64_t ubound = R < num_nodes ? R : num_nodes;
-  static const bool two_pass = getenv("LLP_SEGSORT_2PASS") != nullptr;   // A/B: the old short + long launches
-  const char* ss_env = getenv("LLP_SEGSORT");   // read per call (once per step): "wave" = segsort_mid_wave_kernel
-  if (ss_env && strcmp(ss_env, "wave") == 0) {
+#ifdef LLP_DEDUP_SEGSORT_WAVE
+  {
     int32_t* huge_list = long_list + (R + 1) / 2;   // long segments are > 32 rows: fewer than R / 33 of them
-    int32_t* n_huge = n_long + 1;
     hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
                        seg_rows, long_list, n_long);
-    hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(256), 0, s, (int64_t)1, n_huge);
     hipLaunchKernelGGL(segsort_mid_wave_kernel, dim3(1024), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows,
-                       huge_list, n_huge);
-    hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_huge, huge_list, seg_ptr, seg_rows,
-                       scratch);
-  } else if (two_pass) {
-    hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
-                       seg_rows, long_list, n_long);
-    LLP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows,
-                       scratch);
-  } else {
-    hipLaunchKernelGGL(segsort_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr, seg_rows,
+                       huge_list, n_long + 1);
+    hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long + 1, huge_list, seg_ptr, seg_rows,
                        scratch);
   }
-  LLP_LAUNCH_CHECK();
-  return LLP_OK;
-}
-
-extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
-                              int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
-                              int64_t workspace_bytes, void* stream) {
-  LLP_CHECK_ARG(target && uniq && pos && n_unique && seg_ptr && seg_rows && workspace, "llp_dedup_rows: null");
-  LLP_CHECK_ARG(num_nodes > 0 && num_nodes < (1ll << 31) && R > 0 && R < (1ll << 31), "llp_dedup_rows: sizes");
-  LLP_CHECK_ARG(workspace_bytes >= llp_dedup_rows_workspace_bytes(num_nodes, R), "llp_dedup_rows: workspace");
-  hipStream_t s = (hipStream_t)stream;
-  if (use_counting())
-    return dedup_counting(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, workspace, s);
-  char* w = reinterpret_cast<char*>(workspace);
-  int32_t* mark = reinterpret_cast<int32_t*>(w);
-  w += al256((num_nodes + 1) * 4);
-  int32_t* uidx = reinterpret_cast<int32_t*>(w);
-  w += al256((num_nodes + 1) * 4);
-  int32_t* keys_out = reinterpret_cast<int32_t*>(w);
-  w += al256(R * 4);
-  int32_t* rows_in = reinterpret_cast<int32_t*>(w);
-  w += al256(R * 4);
-  w += al256(R * 4);   // spare
-  void* scan_tmp = w;
-  size_t scan_b = scan_bytes(num_nodes);
-  w += al256((int64_t)scan_b);
-  void* sort_tmp = w;
-  size_t sort_b = sort_bytes(R);
-
-  hipError_t e = hipMemsetAsync(mark, 0, (size_t)num_nodes * 4, s);
-  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
-  hipLaunchKernelGGL(mark_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, mark);
-  LLP_LAUNCH_CHECK();
-  e = rocprim::exclusive_scan(scan_tmp, scan_b, mark, uidx, 0, (size_t)num_nodes, rocprim::plus<int32_t>(), s);
-  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: scan");
-  hipLaunchKernelGGL(compact_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, mark, uidx, uniq,
-                     n_unique);
-  LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(pos_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, uidx, pos, rows_in);
-  LLP_LAUNCH_CHECK();
-  // stable sort of the rows by their unique slot: each node's rows stay in row order
-  int bits = 1;
-  while ((1ll << bits) < num_nodes) ++bits;
-  e = rocprim::radix_sort_pairs(sort_tmp, sort_b, pos, keys_out, rows_in, seg_rows, (unsigned int)R, 0, bits, s);
-  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: sort");
-  hipLaunchKernelGGL(seg_ptr_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, keys_out, seg_ptr, n_unique);
+#else
+  (void)long_list;
+  hipLaunchKernelGGL(segsort_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr, seg_rows,
+                     scratch);
+#endif
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
@@ -973,28 +840,21 @@ extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_
                          (const float*)dZ, drow, (const float*)h, pos, (float*)anchor_rows);
     LLP_LAUNCH_CHECK();
   }
-  // NPW nodes per wave when a row is 64 * NCH 16-B chunks (LLP_SEG_WAVE=0: the thread-group
-  // kernel; LLP_SEG_NPW = 1 (default), 2 or 4 nodes per wave: 487, 530, 633 us at the collab shape)
-  static const bool wave_env = getenv("LLP_SEG_WAVE") ? atoi(getenv("LLP_SEG_WAVE")) != 0 : true;
-  static const int npw_env = getenv("LLP_SEG_NPW") ? atoi(getenv("LLP_SEG_NPW")) : 1;
-  const int npw = (npw_env == 2 || npw_env == 4) ? npw_env : 1;
-  const int nch = (cpr % 64 == 0) ? (int)(cpr * npw / 64) : 0;   // chunks per lane
-  if (wave_env && (nch == 1 || nch == 2 || nch == 4 || nch == 8)) {
+  // one wave per node when a row is 64 * NCH 16-B chunks (1, 2, 4 or 8 per lane): 487 us at the
+  // collab shape against 598 for the thread-group kernel below; two or four nodes per wave
+  // measured 530 / 633 us (profiles/r02_seg_npw.txt)
+  const int nch = (cpr % 64 == 0) ? (int)(cpr / 64) : 0;   // chunks per lane
+  if (nch == 1 || nch == 2 || nch == 4 || nch == 8) {
     auto launch = [&](auto kern, auto* dz, auto* hh, auto* ar, auto* out) {
-      hipLaunchKernelGGL(kern, dim3(ceil_div_u(U, 4 * npw)), dim3(256), 0, s, U, B, C, L2, H, seg_ptr, rows, pos, dz,
-                         drow, hh, ar, out, ld_dh, u_dev);
+      hipLaunchKernelGGL(kern, dim3(ceil_div_u(U, 4)), dim3(256), 0, s, U, B, C, L2, H, seg_ptr, rows, pos, dz, drow,
+                         hh, ar, out, ld_dh, u_dev);
     };
     auto pick = [&](auto* dz, auto* hh, auto* ar, auto* out) {
       using TT = std::remove_const_t<std::remove_pointer_t<decltype(dz)>>;
-      if (npw == 1 && nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, 1, 8, 1>, dz, hh, ar, out);
-      else if (npw == 1 && nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 1>, dz, hh, ar, out);
-      else if (npw == 1 && nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 1>, dz, hh, ar, out);
-      else if (npw == 2 && nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 2>, dz, hh, ar, out);
-      else if (npw == 2 && nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 2>, dz, hh, ar, out);
-      else if (npw == 2 && nch == 8) launch(hadamard_bwd_segments_wave_kernel<TT, 8, 1, 2>, dz, hh, ar, out);
-      else if (npw == 4 && nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 4>, dz, hh, ar, out);
-      else if (npw == 4 && nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 4>, dz, hh, ar, out);
-      else launch(hadamard_bwd_segments_wave_kernel<TT, 8, 1, 4>, dz, hh, ar, out);
+      if (nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, 1, 8, 1>, dz, hh, ar, out);
+      else if (nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 1>, dz, hh, ar, out);
+      else if (nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 1>, dz, hh, ar, out);
+      else launch(hadamard_bwd_segments_wave_kernel<TT, 8, 1, 1>, dz, hh, ar, out);
     };
     if (dtype == LLP_BF16)
       pick((const bf16_t*)dZ, (const bf16_t*)h, (const bf16_t*)anchor_rows, (bf16_t*)dh);

@@ -112,10 +112,11 @@ class _SegmentedGraph:
     so RCCL (or gloo) orders itself against the segments by the stream, exactly
     as in an eager step.  All segments share one memory pool."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, mode="thread_local"):
         self.items = []
         self.stream = torch.cuda.Stream(device=dev)
         self.pool = torch.cuda.graph_pool_handle()
+        self.mode = mode
         self.g = None
         self._ctx = None
 
@@ -127,9 +128,7 @@ class _SegmentedGraph:
     def _open(self):
         self.g = torch.cuda.CUDAGraph()
         # thread_local: the process group's own threads may query events meanwhile
-        # (LLP_SEG_CAPTURE_MODE: "global" / "relaxed" for the diagnosis in DESIGN.md §5)
-        mode = os.environ.get("LLP_SEG_CAPTURE_MODE", "thread_local")
-        self.g.capture_begin(pool=self.pool, capture_error_mode=mode)
+        self.g.capture_begin(pool=self.pool, capture_error_mode=self.mode)
 
     def _close(self):
         self.g.capture_end()
@@ -184,6 +183,7 @@ class EngineBase:
         self._forked = False
         self._side_reads = {}   # buffer name -> event after the side-stream launches that read it
         self._seg = None        # _SegmentedGraph while a multi-rank step is being captured
+        self._seg_debug = False  # extra segment cuts that sync and name the stage (capture_minibatch)
         self.emulate_shard = None   # (rank, world): time one rank's full-batch student slice (_fb_shard)
 
     def _fork(self):
@@ -575,9 +575,9 @@ class EngineBase:
             self._seg.cut(fn)
 
     def _dbg_cut(self, what):
-        """LLP_SEG_DEBUG=1 while a multi-rank step is captured: one more segment cut here,
-        whose eager step syncs the device and names the stage (locates a faulting segment)."""
-        if self._seg is not None and os.environ.get("LLP_SEG_DEBUG") == "1":
+        """capture_minibatch(debug_cuts=True): one more segment cut here, whose eager step
+        syncs the device and names the stage (locates a faulting segment)."""
+        if self._seg is not None and self._seg_debug:
             rank = self.rank
 
             def fn():
@@ -1082,7 +1082,8 @@ class DistillEngine(EngineBase):
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             part.copy_(t.view(self.world, *part.shape)[self.rank])
 
-    def capture_minibatch(self, anchors, link_ids, pairs, **kw):
+    def capture_minibatch(self, anchors, link_ids, pairs, segmented=None, debug_cuts=False, mode="thread_local",
+                          **kw):
         """Capture one step_minibatch into a hipGraph (torch.cuda.CUDAGraph).
 
         ``anchors`` / ``link_ids`` must be persistent device buffers: refill them
@@ -1092,19 +1093,24 @@ class DistillEngine(EngineBase):
         after at least one eager step (kernels and buffers already loaded).
         With several ranks the step is captured as segments cut at the gradient
         all-reduces, which run eagerly between them at replay (_SegmentedGraph);
-        the returned object has the same ``replay()``."""
-        if self.world > 1 or os.environ.get("LLP_FORCE_SEGMENTED") == "1":
+        the returned object has the same ``replay()``.  ``segmented=True`` takes the
+        segmented capture on one rank too, ``debug_cuts`` adds a synchronising cut after
+        each stage, ``mode`` is the segments' capture mode (tests, tools/seg_diag.py)."""
+        if segmented is None:
+            segmented = self.world > 1
+        if segmented:
             # RCCL stays outside the graphs: one segment per stretch between collectives
-            # (LLP_FORCE_SEGMENTED=1: the same segmented capture on one rank, a debug aid)
             torch.cuda.synchronize(self.dev)
-            seg = _SegmentedGraph(self.dev)
+            seg = _SegmentedGraph(self.dev, mode)
             seg.stream.wait_stream(torch.cuda.current_stream(self.dev))
             self._seg = seg
+            self._seg_debug = bool(debug_cuts)
             try:
                 seg.begin()
                 self.step_minibatch(anchors, link_ids, pairs, **kw)
             finally:
                 self._seg = None
+                self._seg_debug = False
                 seg.end()
             torch.cuda.current_stream(self.dev).wait_stream(seg.stream)
             return seg
