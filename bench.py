@@ -62,9 +62,9 @@ def step_flops(B, C, P, F, H, L, rows_student=None):
 
 
 def use_graph(flag, world):
-    """--graph / --no-graph, else the default: the hipGraph replay at N=1, eager steps
-    at N>1 (the segmented multi-rank capture has an open replay fault)."""
-    return flag if flag is not None else world == 1
+    """--graph / --no-graph, else the default: the step replayed from a hipGraph at every
+    N (at N>1 as graph segments with the RCCL all-reduces between them)."""
+    return True if flag is None else bool(flag)
 
 
 def cpu_baseline(data, a, t_h, init_params, B_full, P_full, sample_P=8192, steps=3):
@@ -260,9 +260,7 @@ def main():
                     help="run only the dominant kernel this many times (rocprofv3 --pmc passes) and exit")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
                     help="replay the step from a captured hipGraph (N>1: graph segments with the RCCL "
-                         "all-reduces between them; --no-graph: eager launches).  Default: on at N=1, off "
-                         "at N>1 (a replay of the segmented capture faulted at the collab size on the one-GPU "
-                         "gloo rehearsal, DESIGN.md §5; eager N>1 steps are verified)")
+                         "all-reduces between them; --no-graph: eager launches).  Default: on")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
     ap.add_argument("--no-physics", action="store_true")

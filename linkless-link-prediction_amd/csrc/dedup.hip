@@ -9,10 +9,6 @@
 // row order) before the student backward.
 #include "llp_common.h"
 
-#ifdef LLP_DEDUP_ROCPRIM_SCAN
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
-#endif
 
 #include <type_traits>
 
@@ -383,31 +379,20 @@ int64_t al256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 // the rows by node.
 //
 // Every pass is a kernel of this file (no hipMemsetAsync node, no rocprim): the whole
-// compaction is plain kernel nodes under stream capture, which the multi-rank step's
-// segmented hipGraph replays.  Build-time alternatives for A/B runs of
-// tools/seg_diag.py: -DLLP_DEDUP_MEMSET (the count zeroed by hipMemsetAsync),
-// -DLLP_DEDUP_ROCPRIM_SCAN (rocprim's lookback scan), -DLLP_DEDUP_SEGSORT_WAVE (long
-// segments ranked one wave each across the grid).
+// compaction is plain kernel nodes under stream capture.  A hipMemsetAsync node in a
+// thread-local segment capture made the multi-rank step's segmented hipGraph replay
+// fault at the collab size in round 2; with the count zeroed by a kernel the replays are
+// bit-identical to eager steps, with rocprim's scan or this file's.
+// Segments are sorted one thread each up to SHORT_SEG rows, one wave each up to WAVE_SEG
+// rows (spread over the whole grid, so hot nodes with neighbouring ids do not queue on
+// one block: 389 -> 28 us on the skewed probe of tools/dedup_probe.py), one block each
+// past that.
 constexpr int SHORT_SEG = 32;   // segments up to this length sort in one thread's LDS row
 constexpr int LONG_LDS = 4096;  // longer ones: one block each, ranks counted in LDS up to this length
 
 __device__ __host__ __forceinline__ uint64_t pack_count(int32_t c) {
   return (c > 0 ? (1ull << 32) : 0ull) | (uint64_t)(uint32_t)c;
 }
-
-#ifdef LLP_DEDUP_ROCPRIM_SCAN
-struct PackCount {
-  __host__ __device__ uint64_t operator()(int32_t c) const { return pack_count(c); }
-};
-size_t scan64_bytes(int64_t N) {
-  size_t b = 0;
-  auto it = rocprim::make_transform_iterator((const int32_t*)nullptr, PackCount());
-  rocprim::exclusive_scan(nullptr, b, it, (uint64_t*)nullptr, (uint64_t)0, (size_t)N, rocprim::plus<uint64_t>());
-  return b;
-}
-#else
-size_t scan64_bytes(int64_t) { return 0; }
-#endif
 
 // count pass that also records each row's arrival rank within its node (returning
 // atomic), so the scatter needs no atomics.  Collab R = 747k rows: 46 us.
@@ -562,39 +547,6 @@ __device__ __forceinline__ void rank_segment_block(int32_t* __restrict__ seg_row
   __syncthreads();
 }
 
-#ifndef LLP_DEDUP_SEGSORT_WAVE
-// Every segment sorted by row id in one launch: each thread sorts its short segment in
-// its LDS row and lists a long one in the block's LDS list; then the block ranks its
-// long segments one at a time (the rows buffer reused, or `scratch` past it).
-__global__ __launch_bounds__(256) void segsort_kernel(const int32_t* __restrict__ n_unique,
-                                                      const int32_t* __restrict__ seg_ptr,
-                                                      int32_t* __restrict__ seg_rows, int32_t* __restrict__ scratch) {
-  __shared__ int32_t buf[256][SHORT_SEG + 1];
-  __shared__ int32_t longs[256];
-  __shared__ int32_t n_longs;
-  if (threadIdx.x == 0) n_longs = 0;
-  __syncthreads();
-  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (s < *n_unique) {
-    const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
-    if (len > SHORT_SEG) {
-      longs[atomicAdd(&n_longs, 1)] = (int32_t)s;
-    } else if (len > 1) {
-      int32_t* a = buf[threadIdx.x];
-      for (int i = 0; i < len; ++i) a[i] = seg_rows[b + i];
-      insertion_sort(a, len);
-      for (int i = 0; i < len; ++i) seg_rows[b + i] = a[i];
-    }
-  }
-  __syncthreads();
-  const int nl = n_longs;
-  for (int i = 0; i < nl; ++i) {
-    const int32_t sg = longs[i];
-    const int32_t b = seg_ptr[sg], len = seg_ptr[sg + 1] - b;
-    rank_segment_block(seg_rows, b, len, &buf[0][0], 256 * (SHORT_SEG + 1), scratch);
-  }
-}
-#else
 // one thread per segment: insertion sort of up to SHORT_SEG row ids in its own LDS row;
 // longer segments go on the global list for segsort_mid_wave_kernel
 __global__ __launch_bounds__(256) void segsort_short_kernel(const int32_t* __restrict__ n_unique,
@@ -671,13 +623,12 @@ __global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __rest
     rank_segment_block(seg_rows, b, len, buf, LONG_LDS, scratch);
   }
 }
-#endif
 
 }  // namespace
 
 static int64_t counting_ws_bytes(int64_t num_nodes, int64_t R) {
   return 3 * al256((num_nodes + 1) * 4) + al256(num_nodes * 8) + 2 * al256(R * 4) + al256(256) +
-         al256((int64_t)scan64_bytes(num_nodes)) + al256(((num_nodes + OS_B - 1) / OS_B) * 8) + 512;
+         al256(((num_nodes + OS_B - 1) / OS_B) * 8) + 512;
 }
 
 extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) {
@@ -706,29 +657,11 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
   w += al256(R * 4);
   int32_t* n_long = reinterpret_cast<int32_t*>(w);    // [0] long segments, [1] huge ones (wave sort)
   w += al256(256);
-  void* scan_tmp = w;
-  const size_t scan_b = scan64_bytes(num_nodes);
-  w += al256((int64_t)scan_b);
-  uint64_t* os_sums = reinterpret_cast<uint64_t*>(w);   // per-block sums / offsets of the own scan
-  (void)scan_tmp;
+  uint64_t* os_sums = reinterpret_cast<uint64_t*>(w);   // per-block sums / offsets of the scan
 
-#ifdef LLP_DEDUP_MEMSET
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)num_nodes * 4, s);
-  if (e != hipSuccess) return ::llp::set_error((int)e, "llp_dedup_rows: memset");
-#else
   hipLaunchKernelGGL(zero_i32_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, cnt);
-#endif
   hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, cnt, scratch);
   LLP_LAUNCH_CHECK();
-#ifdef LLP_DEDUP_ROCPRIM_SCAN
-  {
-    auto it = rocprim::make_transform_iterator((const int32_t*)cnt, PackCount());
-    size_t sb = scan_b;
-    const hipError_t e2 = rocprim::exclusive_scan(scan_tmp, sb, it, pre, (uint64_t)0, (size_t)num_nodes,
-                                                  rocprim::plus<uint64_t>(), s);
-    if (e2 != hipSuccess) return ::llp::set_error((int)e2, "llp_dedup_rows: scan");
-  }
-#else
   {
     const int64_t nb = (num_nodes + OS_B - 1) / OS_B;
     hipLaunchKernelGGL(os_block_sum_kernel, dim3((unsigned)nb), dim3(OS_T), 0, s, num_nodes, cnt, os_sums);
@@ -736,7 +669,6 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
     hipLaunchKernelGGL(os_block_scan_kernel, dim3((unsigned)nb), dim3(OS_T), 0, s, num_nodes, cnt, os_sums, pre);
     LLP_LAUNCH_CHECK();
   }
-#endif
   hipLaunchKernelGGL(compact_count_kernel, dim3(ceil_div_u(num_nodes, 256)), dim3(256), 0, s, num_nodes, R, cnt, pre,
                      uniq, seg_ptr, uidx, cursor, n_unique, n_long);
   LLP_LAUNCH_CHECK();
@@ -745,21 +677,13 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
                      pos, seg_rows);
   LLP_LAUNCH_CHECK();
   const int64_t ubound = R < num_nodes ? R : num_nodes;
-#ifdef LLP_DEDUP_SEGSORT_WAVE
-  {
-    int32_t* huge_list = long_list + (R + 1) / 2;   // long segments are > 32 rows: fewer than R / 33 of them
-    hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
-                       seg_rows, long_list, n_long);
-    hipLaunchKernelGGL(segsort_mid_wave_kernel, dim3(1024), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows,
-                       huge_list, n_long + 1);
-    hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long + 1, huge_list, seg_ptr, seg_rows,
-                       scratch);
-  }
-#else
-  (void)long_list;
-  hipLaunchKernelGGL(segsort_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr, seg_rows,
+  int32_t* huge_list = long_list + (R + 1) / 2;   // long segments are > 32 rows: fewer than R / 33 of them
+  hipLaunchKernelGGL(segsort_short_kernel, dim3(ceil_div_u(ubound, 256)), dim3(256), 0, s, n_unique, seg_ptr,
+                     seg_rows, long_list, n_long);
+  hipLaunchKernelGGL(segsort_mid_wave_kernel, dim3(1024), dim3(256), 0, s, n_long, long_list, seg_ptr, seg_rows,
+                     huge_list, n_long + 1);
+  hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long + 1, huge_list, seg_ptr, seg_rows,
                      scratch);
-#endif
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -37,10 +37,10 @@ def test_pmc_traffic_reads_committed_profile():
     assert bench.pmc_traffic(p["rows"], p["H"], "fp32") is None
 
 
-def test_graph_default_per_world_size():
+def test_graph_default_at_every_world_size():
     assert bench.use_graph(None, 1) is True
-    assert bench.use_graph(None, 2) is False
-    assert bench.use_graph(None, 8) is False
+    assert bench.use_graph(None, 2) is True
+    assert bench.use_graph(None, 8) is True
     assert bench.use_graph(True, 8) is True
     assert bench.use_graph(False, 1) is False
 

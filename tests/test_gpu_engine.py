@@ -297,13 +297,12 @@ def test_engine_fused_segment_backward_bit_identical():
         llp_engine._SEGMENT_FUSED = saved
 
 
-@pytest.mark.skipif(os.environ.get("LLP_TEST_WIDE") != "1",
-                    reason="fp32 rows wider than the grouping kernels (row-wise / scatter fallbacks) not yet run "
-                           "on the GPU; LLP_TEST_WIDE=1")
-def test_engine_fp32_hidden_2048_matches_oracle():
-    """The collab sweep's hidden_channels=2048 in fp32: 8 KiB rows exceed the node-grouped
-    Hadamard-backward kernels (256 16-B chunks), so the engine runs the row-wise student
-    (EngineBase._grouped_ok); one step with injected samples against the oracle."""
+@pytest.mark.parametrize("mode", ["minibatch", "fullbatch"])
+def test_engine_fp32_hidden_2048_matches_oracle(mode):
+    """The collab sweep's hidden_channels=2048 in fp32 (configurations/collab_transductive.yaml):
+    8 KiB rows exceed the node-grouped Hadamard-backward kernels (256 16-B chunks), so the
+    engine runs the row-wise student (minibatch) and the f32 scatter d(h) (both steps;
+    EngineBase._grouped_ok); one step with injected samples against the oracle."""
     import types
 
     import numpy as np
@@ -312,7 +311,8 @@ def test_engine_fp32_hidden_2048_matches_oracle():
         pytest.skip("no GPU")
     N, F_, H, L = 400, 64, 2048, 2
     args = types.SimpleNamespace(rw_step=1, hops=2, ns_rate=2, ps_method="nb", dropout=0.0, margin=0.05,
-                                 LLP_D=1.0, LLP_R=1.0, True_label=0.5, predictor="mlp", lr=0.001)
+                                 LLP_D=1.0, LLP_R=1.0, True_label=0.5, predictor="mlp", lr=0.001, KD_RM=0.0,
+                                 KD_LM=0.0)
     g = torch.Generator().manual_seed(0)
     u = torch.randint(0, N, (3000,), generator=g)
     v = torch.randint(0, N, (3000,), generator=g)
@@ -330,15 +330,20 @@ def test_engine_fp32_hidden_2048_matches_oracle():
     anchors = samples[:, 0].to(torch.int32)
     params0 = [p.detach().cpu().clone() for p in list(model.parameters()) + list(pred.parameters())]
     tpar = [p.detach().cpu().clone() for p in eng.tpred.parameters()]
-    eng.step_minibatch(anchors.to(DEV), link.to(torch.int32).to(DEV), pairs.to(torch.int32).to(DEV),
-                       samples=samples.to(DEV), neg=neg.to(torch.int32).to(DEV))
+    step = eng.step_minibatch if mode == "minibatch" else eng.step_fullbatch
+    step(anchors.to(DEV), link.to(torch.int32).to(DEV), pairs.to(torch.int32).to(DEV), samples=samples.to(DEV),
+         neg=neg.to(torch.int32).to(DEV))
     torch.cuda.synchronize()
     t = eng.terms.cpu()
     leaves = [p.clone().requires_grad_() for p in params0]
     sw, sb = leaves[0:2 * L:2], leaves[1:2 * L:2]
     pw, pb = leaves[2 * L::2], leaves[2 * L + 1::2]
     tw, tb = tpar[0::2], tpar[1::2]
-    r = O.distill_losses_minibatch(x, t_h, samples, pairs[link].t(), neg, sw, sb, pw, pb, tw, tb, args)
+    if mode == "minibatch":
+        r = O.distill_losses_minibatch(x, t_h, samples, pairs[link].t(), neg, sw, sb, pw, pb, tw, tb, args)
+    else:
+        r = O.distill_losses_fullbatch(x, t_h, samples, anchors.long(), pairs[link].t(), neg, sw, sb, pw, pb, tw, tb,
+                                       args)
     assert abs(t[1].item() - r["label_loss"].item()) <= 1e-4 * max(1, abs(r["label_loss"].item()))
     assert abs(t[2].item() - r["llp_d"].item()) <= 1e-4 * max(1, abs(r["llp_d"].item()))
     assert abs(t[3].item() - r["llp_r"].item()) <= 1e-4 * max(1, abs(r["llp_r"].item()))

@@ -544,22 +544,13 @@ def test_clip_and_adam_match_oracle(case, nan_group):
 
 
 # ------------------------------------------------------------------ unique-node compaction
-_WAVE_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin",
-                         "libllp_hip_wave.so")
-
-
-@pytest.mark.skipif(not os.path.exists(_WAVE_LIB), reason="A/B build with -DLLP_DEDUP_SEGSORT_WAVE not present")
 @pytest.mark.parametrize("N,R,hot,hub", [(235868, 747214, 2000, 0.0), (3000, 40000, 0, 0.3), (50, 1000, 0, 0.0)])
 def test_dedup_segsort_wave(N, R, hot, hub):
-    """-DLLP_DEDUP_SEGSORT_WAVE (dedup.hip segsort_mid_wave_kernel): segments of 33..1024 rows
-    ranked one wave each, longer ones by a block; outputs equal the stable sort's.
+    """dedup.hip's segment sort: segments of 33..1024 rows ranked one wave each across the
+    grid (segsort_mid_wave_kernel), longer ones by a block; outputs equal the stable sort's.
     hot: a quarter of the rows on ids 0..hot-1 (the stress probe: ~94-row segments on
     neighbouring ids); hub: as test_dedup_rows_and_segment_sum (a 12k-row segment)."""
-    import ctypes
     k = K()
-    wl = ctypes.CDLL(_WAVE_LIB)
-    fn = wl.llp_dedup_rows
-    fn.restype, fn.argtypes = k._SIGS["llp_dedup_rows"]
     g = torch.Generator().manual_seed(R + 5)
     target = torch.randint(0, N, (R,), generator=g, dtype=torch.int32)
     if hot:
@@ -574,9 +565,7 @@ def test_dedup_segsort_wave(N, R, hot, hub):
     segp = torch.empty(R + 1, dtype=torch.int32, device=DEV)
     segr = torch.empty(R, dtype=torch.int32, device=DEV)
     ws = torch.empty(k.dedup_ws_bytes(N, R) // 4 + 16, device=DEV)
-    rc = fn(N, R, tg.data_ptr(), uniq.data_ptr(), pos.data_ptr(), nu.data_ptr(), segp.data_ptr(), segr.data_ptr(),
-            ws.data_ptr(), ws.numel() * 4, k.stream_ptr())
-    assert rc == 0
+    k.dedup_rows(N, R, tg, uniq, pos, nu, segp, segr, ws)
     torch.cuda.synchronize()
     u_ref, inv = np.unique(target.numpy(), return_inverse=True)
     U = int(nu.item())

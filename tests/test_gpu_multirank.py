@@ -23,18 +23,18 @@ def _free_port():
     return p
 
 
-def _problem():
-    N, F_, H, L = 2000, 64, 128, 3
+def _problem(N=2000, n_pairs=12000, B=256, P=1024):
+    F_, H, L = 64, 128, 3
     g = torch.Generator().manual_seed(0)
-    u = torch.randint(0, N, (12000,), generator=g)
-    v = torch.randint(0, N, (12000,), generator=g)
+    u = torch.randint(0, N, (n_pairs,), generator=g)
+    v = torch.randint(0, N, (n_pairs,), generator=g)
     keep = u != v
     pairs = torch.stack([u[keep], v[keep]], 1)
     ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
     x = torch.randn(N, F_, generator=g) * 0.3
     t_h = torch.randn(N, 256, generator=g) * 0.3
-    anchors = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:256].to(torch.int32)
-    links = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(2))[:1024].to(torch.int32)
+    anchors = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:B].to(torch.int32)
+    links = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(2))[:P].to(torch.int32)
     args = types.SimpleNamespace(rw_step=2, hops=2, ns_rate=2, ps_method="nb", dropout=0.0, margin=0.05, LLP_D=1.0,
                                  LLP_R=1.0, True_label=0.5, predictor="mlp", lr=0.01)
     return N, F_, H, L, pairs, ei, x, t_h, anchors, links, args
@@ -84,7 +84,7 @@ def _run(rank, world, dtype, port, out):
         dist.destroy_process_group()
 
 
-def _run_graph(rank, world, port, out, use_graph):
+def _run_graph(rank, world, port, out, use_graph, size):
     """Three steps of a 2-rank job: eager, or one eager step then two replays of
     the segmented hipGraph (capture_minibatch at world > 1)."""
     import sys
@@ -97,7 +97,7 @@ def _run_graph(rank, world, port, out, use_graph):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    N, F_, H, L, pairs, ei, x, t_h, anchors, links, args = _problem()
+    N, F_, H, L, pairs, ei, x, t_h, anchors, links, args = _problem(**size)
     torch.manual_seed(3)
     model = models.MLP(L, F_, H, H, 0.0).to(dev)
     pred = models.LinkPredictor("mlp", H, H, 1, L, 0.0).to(dev)
@@ -118,6 +118,7 @@ def _run_graph(rank, world, port, out, use_graph):
     eng.step_minibatch(a_dev, l_dev, pr, **kw)
     if use_graph:
         g = eng.capture_minibatch(a_dev, l_dev, pr, **kw)
+        assert isinstance(g, llp_engine._SegmentedGraph)
         out["segments"] = sum(isinstance(it, torch.cuda.CUDAGraph) for it in g.items)
         for _ in range(2):
             g.replay()
@@ -135,18 +136,18 @@ def _run_graph(rank, world, port, out, use_graph):
     dist.destroy_process_group()
 
 
-def _graph_worker(rank, world, port, q, use_graph):
+def _graph_worker(rank, world, port, q, use_graph, size):
     out = {}
-    _run_graph(rank, world, port, out, use_graph)
+    _run_graph(rank, world, port, out, use_graph, size)
     if rank == 0:
         q.put(out)
 
 
-def _two_ranks(use_graph):
+def _two_ranks(use_graph, size):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, q, use_graph)) for r in range(2)]
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, q, use_graph, size)) for r in range(2)]
     for p in procs:
         p.start()
     out = q.get(timeout=300)
@@ -156,13 +157,17 @@ def _two_ranks(use_graph):
     return out
 
 
-def test_two_ranks_segmented_graph_matches_eager():
+@pytest.mark.parametrize("size", [{}, dict(N=235_868, n_pairs=400_000, B=4096, P=16384)],
+                         ids=["small", "collab_nodes"])
+def test_two_ranks_segmented_graph_matches_eager(size):
     """BASELINE configs[4]: the multi-rank step replayed from hipGraph segments (the
-    all-reduces run between them) is bit-identical to eager multi-rank steps."""
+    all-reduces run between them) is bit-identical to eager multi-rank steps.  At the
+    collab node count the unique-node compaction's scan runs over 116 blocks (the round-2
+    replay fault was there); the 2,000-node case is one block."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    eager = _two_ranks(False)
-    graph = _two_ranks(True)
+    eager = _two_ranks(False, size)
+    graph = _two_ranks(True, size)
     # cuts: the predictor's all-reduce, one bucket per student layer but the first, the rest + clip/Adam
     assert graph["segments"] == 5
     assert graph["loss"] == eager["loss"], (graph["loss"], eager["loss"])
