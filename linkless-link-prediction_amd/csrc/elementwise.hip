@@ -626,11 +626,27 @@ extern "C" int llp_accumulate(int64_t n, const float* src, float weight, double*
   return LLP_OK;
 }
 
+// zero `bytes` bytes at p: 16-B stores over the aligned body, byte stores for the ends.
+// A kernel, not hipMemsetAsync: a memset node in a captured hipGraph left half of its
+// buffer unzeroed at replay on this ROCm (tools/memset_capture_probe.py).
+__global__ void zero_bytes_kernel(uint8_t* __restrict__ p, int64_t head, int64_t n16, int64_t bytes) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n16) reinterpret_cast<uint4*>(p + head)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i < head) p[i] = 0;
+  const int64_t t = head + n16 * 16 + i;
+  if (i < 16 && t < bytes) p[t] = 0;
+}
+
 extern "C" int llp_zero(void* p, int64_t bytes, void* stream) {
   LLP_CHECK_ARG(p || bytes == 0, "llp_zero: null pointer");
+  LLP_CHECK_ARG(bytes >= 0, "llp_zero: negative size");
   if (bytes == 0) return LLP_OK;
-  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
-  if (e != hipSuccess) return llp::set_error((int)e, "llp_zero: %s", hipGetErrorString(e));
+  const int64_t head = std::min<int64_t>(bytes, (16 - (int64_t)((uintptr_t)p % 16)) % 16);
+  const int64_t n16 = (bytes - head) / 16;
+  const int64_t threads = std::max<int64_t>(std::max<int64_t>(n16, 16), head);
+  hipLaunchKernelGGL(zero_bytes_kernel, dim3(ceil_div_u(threads, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (uint8_t*)p, head, n16, bytes);
+  LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
 

@@ -777,3 +777,16 @@ def test_gemm_device_row_count(dt, Mmax, Mlive):
     got = o.float().cpu()
     assert torch.allclose(got[:Mlive], exp[:Mlive], rtol=1e-2, atol=1e-2)
     assert bool((got[Mlive:] == 7.0).all())
+
+
+@pytest.mark.parametrize("off,nbytes", [(0, 4096), (3, 517), (16, 15), (1, 1), (5, 1_000_003)])
+def test_zero_bytes_exact_region(off, nbytes):
+    """llp_zero (a kernel, not a memset node): exactly bytes [off, off + nbytes) become 0."""
+    k = K()
+    buf = torch.full((nbytes + off + 64,), 0xAB, dtype=torch.uint8, device=DEV)
+    view = buf[off:off + nbytes]
+    k.zero_(view)
+    torch.cuda.synchronize()
+    h = buf.cpu()
+    assert int((h[off:off + nbytes] != 0).sum()) == 0
+    assert int((h[:off] != 0xAB).sum()) == 0 and int((h[off + nbytes:] != 0xAB).sum()) == 0
