@@ -105,31 +105,6 @@ int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, cons
 int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit,
                     float* prob, void* stream);
 
-/* Main-loop variant of the large-tile bf16 NT kernel (a tuning knob, process
- * wide, for A/B measurements in one process).  Default LLP_GEMM_PP8M: K64
- * quadrant phases with 128-B DMA lines, each phase a LOAD and an MFMA segment
- * between barriers with waves 4-7 one barrier behind waves 0-3 (ping-pong), and
- * the epilogue compiled per call kind.  Others: the lockstep / staggered q64
- * loops, ping-pong rings of 64-B lines, the lockstep 4-stage ring, half-height
- * tiles.  All variants give bit-identical results.  Returns the previous
- * variant (or an error code); llp_gemm_variant_name() names the current one's
- * kernel (profiles: rocprofv3 kernel names). */
-enum llp_gemm_variant_e { LLP_GEMM_PIPE = 0, LLP_GEMM_PP42 = 1, LLP_GEMM_PP53 = 2, LLP_GEMM_Q64 = 3, LLP_GEMM_Q64L = 4,
-                          LLP_GEMM_H128 = 5 /* 128 x 256 tiles, two workgroups per CU */,
-                          LLP_GEMM_Q64S1 = 6 /* q64 lean, waves 4-7 staggered by one phase */,
-                          LLP_GEMM_Q64S2 = 7 /* as 6, their DMA issued after the MFMAs */,
-                          LLP_GEMM_PP8 = 8 /* q64 phases as LOAD/MFMA segments, waves 4-7 one barrier behind */,
-                          LLP_GEMM_PP8D = 9 /* as 8, register-direct epilogue (no LDS staging) */,
-                          LLP_GEMM_PP8L = 10 /* as 9, stores of whole 128-B lines */,
-                          LLP_GEMM_PP8M = 11 /* as 8, epilogue specialised per call (bias/ReLU fwd, mask bwd) */ };
-int llp_set_gemm_variant(int variant);
-const char* llp_gemm_variant_name(void);
-/* Main-loop variant of the bf16 weight-gradient (TN) kernel, process wide (A/B knob):
- * 0 lockstep, 1 / 2 waves 4-7 staggered by one stage (2: their DMA late; default),
- * 3 / 4 ping-pong LOAD / MFMA segments with waves 4-7 one barrier behind (one or two
- * pairs per stage; measured slower); + 8 places the blocks tile-major (round-1 order)
- * instead of split-major.  All bit-identical.  Returns the previous one. */
-int llp_set_gemm_tn_variant(int variant);
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
  * Split over m into slabs in `workspace` (llp_gemm_tn_workspace_bytes), then
@@ -216,15 +191,17 @@ int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t L2, int64_t
  * fixed order: deterministic); out_rows (may be NULL): group u is written to
  * out row out_rows[u] (uniq: a scatter onto node rows, e.g. the teacher's
  * dh[N, H], src/train_teacher_gnn.py:62); u_dev (may be NULL): device count,
- * the call covers min(U, *u_dev) groups (grid sized by U: capturable).
+ * the call covers min(U, *u_dev) groups (grid sized by U: capturable);
+ * out_dtype: dtype, or LLP_F32 for unrounded sums (bf16 input; a cross-rank
+ * reduction follows, DistillEngine._fb_shard).
  * llp_gather_i32: out[i] = src[idx[i]]. */
 int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R);
 int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
                    int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
                    int64_t workspace_bytes, void* stream);
 int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
-                         const void* src, int64_t ld_src, void* out, int64_t ld_out, const int32_t* out_rows,
-                         const int32_t* u_dev, void* stream);
+                         const void* src, int64_t ld_src, void* out, int64_t ld_out, int out_dtype,
+                         const int32_t* out_rows, const int32_t* u_dev, void* stream);
 int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream);
 /* out row r = src row idx[r] (row_bytes each; leading dimensions in bytes) for
  * r < min(n, *count_dev) (count_dev may be NULL): data.x[this_target]

@@ -48,11 +48,13 @@ struct V8<float> {
 
 // out[u] = sum over k in [seg_ptr[u], seg_ptr[u+1]) of src[rows[k]] (f32 accumulate,
 // row order): one thread per 16-B column chunk, a block covers 256/cpr segments.
-template <typename T>
+// TO: the output type (the input's, or f32: the sums unrounded, e.g. for a following
+// cross-rank reduction).
+template <typename T, typename TO>
 __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, const int32_t* __restrict__ seg_ptr,
                                                           const int32_t* __restrict__ rows,
                                                           const T* __restrict__ src, int64_t lds_,
-                                                          T* __restrict__ out, int64_t ldo,
+                                                          TO* __restrict__ out, int64_t ldo,
                                                           const int32_t* __restrict__ out_rows,
                                                           const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
@@ -75,7 +77,13 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int64_t U, int64_t H, 
   }
   if (k < end) V8<T>::add(acc, *reinterpret_cast<const uint4*>(src + (int64_t)rows[k] * lds_ + c * E));
   const int64_t orow = out_rows ? (int64_t)out_rows[u] : u;
-  *reinterpret_cast<uint4*>(out + orow * ldo + c * E) = V8<T>::pack(acc);
+  if constexpr (std::is_same<T, TO>::value) {
+    *reinterpret_cast<uint4*>(out + orow * ldo + c * E) = V8<T>::pack(acc);
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; i += 4)
+      *reinterpret_cast<uint4*>(out + orow * ldo + c * E + i) = V8<float>::pack(acc + i);
+  }
 }
 
 // Fused Hadamard backward + per-node reduction (the unique-node student path),
@@ -689,22 +697,28 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
 }
 
 extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
-                                    const void* src, int64_t ld_src, void* out, int64_t ld_out,
+                                    const void* src, int64_t ld_src, void* out, int64_t ld_out, int out_dtype,
                                     const int32_t* out_rows, const int32_t* u_dev, void* stream) {
   LLP_CHECK_ARG(seg_ptr && rows && src && out, "llp_segment_sum_rows: null");
+  LLP_CHECK_ARG(out_dtype == dtype || out_dtype == LLP_F32, "llp_segment_sum_rows: out_dtype must be dtype or f32");
   const int E = dtype == LLP_BF16 ? 8 : 4;
   const int es = dtype == LLP_BF16 ? 2 : 4;
-  LLP_CHECK_ARG(H % E == 0 && H / E <= 256 && (ld_src * es) % 16 == 0 && (ld_out * es) % 16 == 0 &&
+  const int eo = out_dtype == LLP_BF16 ? 2 : 4;
+  LLP_CHECK_ARG(H % E == 0 && H / E <= 256 && (ld_src * es) % 16 == 0 && (ld_out * eo) % 16 == 0 &&
                     (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0,
                 "llp_segment_sum_rows: rows must be 16-B aligned, H <= 256 chunks");
   if (U == 0) return LLP_OK;
   const int64_t cpr = H / E, spb = 256 / cpr;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == LLP_BF16)
-    hipLaunchKernelGGL(segment_sum_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
+  const dim3 grid(ceil_div_u(U, spb));
+  if (dtype == LLP_BF16 && out_dtype == LLP_BF16)
+    hipLaunchKernelGGL((segment_sum_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, s, U, H, seg_ptr, rows,
                        (const bf16_t*)src, ld_src, (bf16_t*)out, ld_out, out_rows, u_dev);
+  else if (dtype == LLP_BF16)
+    hipLaunchKernelGGL((segment_sum_kernel<bf16_t, float>), grid, dim3(256), 0, s, U, H, seg_ptr, rows,
+                       (const bf16_t*)src, ld_src, (float*)out, ld_out, out_rows, u_dev);
   else
-    hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, H, seg_ptr, rows,
+    hipLaunchKernelGGL((segment_sum_kernel<float, float>), grid, dim3(256), 0, s, U, H, seg_ptr, rows,
                        (const float*)src, ld_src, (float*)out, ld_out, out_rows, u_dev);
   LLP_LAUNCH_CHECK();
   return LLP_OK;

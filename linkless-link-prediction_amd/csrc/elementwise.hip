@@ -515,10 +515,9 @@ extern "C" int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a,
   const int64_t n = R * (H * es / 16);
   if (n == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
-  // rows of 32, 64, 128 or 256 chunks: row groups per wave (LLP_HADA_WAVE=0: one chunk per thread)
-  static const bool wave_env = !(getenv("LLP_HADA_WAVE") && atoi(getenv("LLP_HADA_WAVE")) == 0);
+  // rows of 32, 64, 128 or 256 chunks: row groups per wave, else one chunk per thread
   const int64_t cpr = H * es / 16;
-  if (wave_env && (cpr == 32 || cpr == 64 || cpr == 128 || cpr == 256)) {
+  if ((cpr == 32 || cpr == 64 || cpr == 128 || cpr == 256)) {
     auto go = [&](auto kern, auto* pa, auto* pb, auto* po, int rows_per_wave) {
       hipLaunchKernelGGL(kern, dim3(ceil_div_u(R, 4 * rows_per_wave)), dim3(256), 0, s, R, H, pa, ia, pb, ib, po);
     };

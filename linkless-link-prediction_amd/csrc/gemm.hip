@@ -648,9 +648,8 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   LLP_CHECK_ARG(tiles < (1ll << 31), "llp_gemm_nt: too many tiles");
   hipStream_t s = (hipStream_t)stream;
   // Large-tile bf16 kernel (gemm256.hip) whenever the layout allows it.
-  static const bool force_v1 = getenv("LLP_GEMM_V1") != nullptr;
   auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
-  if (!force_v1 && dtype == LLP_BF16 && c_dtype == LLP_BF16 && K > 0 && K % 64 == 0 && N % 8 == 0 && !B->ptr2 &&
+  if (dtype == LLP_BF16 && c_dtype == LLP_BF16 && K > 0 && K % 64 == 0 && N % 8 == 0 && !B->ptr2 &&
       a16(A->ptr, A->ld) && (!A->ptr2 || a16(A->ptr2, A->ld2)) && a16(B->ptr, B->ld) && a16(C, ldc) &&
       (act != LLP_ACT_RELU_BWD || mask || (aux_dtype == LLP_BF16 && a16(aux, ld_aux))) &&
       (!mask || (N % 32 == 0 && ld_aux % 4 == 0 && (uintptr_t)aux % 4 == 0))) {
@@ -769,9 +768,8 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     return llp::set_error(LLP_E_WORKSPACE, "llp_gemm_tn: workspace %lld < %lld", (long long)workspace_bytes,
                           (long long)llp_gemm_tn_workspace_bytes(dtype, M, P, Q));
   hipStream_t s = (hipStream_t)stream;
-  static const bool force_v1 = getenv("LLP_GEMM_V1") != nullptr;
   auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
-  if (!force_v1 && dtype == LLP_BF16 && P % 8 == 0 && Q % 8 == 0 && !A->ptr2 && !B->ptr2 && a16(A->ptr, A->ld) &&
+  if (dtype == LLP_BF16 && P % 8 == 0 && Q % 8 == 0 && !A->ptr2 && !B->ptr2 && a16(A->ptr, A->ld) &&
       a16(B->ptr, B->ld)) {
     // large-tile glds kernel (gemm256_tn.hip), bias gradient fused
     const int64_t sp = llp_gemm_tn_256_splits(M, P, Q);

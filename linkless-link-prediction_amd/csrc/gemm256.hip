@@ -53,8 +53,8 @@ struct P256 {
   // the grid and head_part's row stride (head_ld) stay the host M
   const int32_t* m_dev;
   int64_t head_ld;
-  int nt_store;   // epilogue stores with the non-temporal hint (default; LLP_GEMM_NT_STORE=0 turns it off)
-  int lean_epi;   // pp8 mode kernels: lean epilogue on full tiles (default; LLP_GEMM_LEAN_EPI=0 turns it off)
+  int nt_store;   // epilogue stores with the non-temporal hint
+  int lean_epi;   // pp8 mode kernels: lean epilogue on full tiles
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -316,24 +316,13 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined variant for plain / gathered A (no Hadamard): BK = 32 per stage
-// (32 KiB: A and B images of [256 rows][64 B]), NS-stage LDS ring, NS-1
-// stages of global_load_lds in flight across raw barriers with a counted
-// vmcnt (cdna_hip_programming.md §5 "Pipelining across barriers").  The
-// single-stage-in-flight loop above measured latency-bound (no-load ablation
-// 1.28 PF/s vs 0.79 PF/s full, L2->CU traffic ~19 GB/s per CU).
-// 64-B image rows: 16-B chunk swizzle phys = logical ^ ((row >> 2) & 2) is
-// conflict-free for ds_read_b128 fragment reads of 16 consecutive rows
-// (checked against the four 16-lane bank groups of ds_read_b128).
-constexpr int PK = 32;
-constexpr int PSTAGE_U4 = (TM + TN) * 4;   // 2048 uint4 = 32 KiB
-
-__device__ __forceinline__ int swz64(int row) { return (row >> 2) & 2; }
-
+// LDS-DMA helpers of the pipelined kernels.  64-B image rows: 16-B chunk swizzle
+// phys = logical ^ ((row >> 2) & 2) is conflict-free for ds_read_b128 fragment reads of
+// 16 consecutive rows (checked against the four 16-lane bank groups of ds_read_b128).
 // global_load_lds_dwordx4 issued from inline asm: hipcc's waitcnt pass then does
 // not see the LDS-DMA and does not put s_waitcnt vmcnt(0) in front of every
 // ds_read of the ring (it cannot prove the reads do not alias the DMA).  The
-// kernel owns the counting: vm_wait_stages + s_barrier before a stage is read.
+// kernel owns the counting: a counted s_waitcnt vmcnt + s_barrier before a stage is read.
 __device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_addr_uniform) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr),
                "s"(lds_addr_uniform)
@@ -341,15 +330,6 @@ __device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_addr_unifo
 }
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)p);
-}
-
-template <int NS>
-__device__ __forceinline__ void vm_wait_stages(int64_t ahead) {
-  // each stage is 4 global_load_lds per wave; wait until only `ahead` stages remain
-  if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
 // Shared epilogue of the 256x256 kernels: alpha, bias, ReLU, dropout, fused
@@ -545,122 +525,6 @@ __device__ __forceinline__ void epilogue_256(const P256& p, float4_t (&acc)[4][8
 }
 
 // ---------------------------------------------------------------------------
-// Ping-pong variant (cdna_hip_programming.md §5 "The 256² 8-phase template":
-// wave groups staggered by one barrier).  Waves 0-3 (rows 0-127 of the tile)
-// and 4-7 (rows 128-255) alternate: while one group runs its 32 MFMAs of a
-// k-step, the other group (the second wave on every SIMD) issues its 12
-// ds_read_b128 fragment reads and the next stages' LDS-DMA, so LDS latency
-// and DMA issue hide under the partner's MFMAs instead of stalling both.
-//   per k-step s:  [R_s: ds_read stage s, DMA stage s+D] bar [M_s: 32 MFMA] bar
-// group 1 runs one barrier behind group 0.  RAW: every wave waits (counted
-// vmcnt) for its part of stage s+1 in the segment that ends at the barrier
-// before group 0's R_{s+1}.  WAR: the DMA into stage s+D's buffer (last read
-// as stage s+D-NS) is issued >= 2 barriers after those reads drained, which
-// needs NS >= D + 2.
-template <int NS, int D>
-__global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp(P256 p) {
-  static_assert(NS >= D + 2, "ring too short for the prefetch distance");
-  constexpr int LOOP_U4 = NS * PSTAGE_U4;
-  constexpr int SM_U4 = LOOP_U4 > SMEM_U4_EPI + 256 ? LOOP_U4 : SMEM_U4_EPI + 256;
-  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int64_t m0, n0;
-  if (!tile_256(p, m0, n0)) return;
-
-  const bf16_t* ga[2];
-  const bf16_t* gb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = 32 * w + 16 * i + (lane >> 2);
-    const int lc = (lane & 3) ^ swz64(r);
-    int64_t m = m0 + r;
-    m = m < p.M ? m : p.M - 1;
-    ga[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
-    int64_t n = n0 + r;
-    n = n < p.N ? n : p.N - 1;
-    gb[i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
-  }
-  const uint32_t lds0 = lds_u32(smem);
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto issue = [&](int64_t kt) {
-    const uint32_t sA = lds0 + (uint32_t)((kt % NS) * PSTAGE_U4 * 16);
-    const uint32_t sB = sA + TM * 4 * 16;
-    const int64_t koff = kt * PK;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t off = (uint32_t)((32 * wu + 16 * i) * 4 * 16);
-      glds16(ga[i] + koff, __builtin_amdgcn_readfirstlane(sA + off));
-      glds16(gb[i] + koff, __builtin_amdgcn_readfirstlane(sB + off));
-    }
-  };
-
-  const int wm = w >> 2, wn = w & 3;
-  const bool grp1 = __builtin_amdgcn_readfirstlane(wm) == 1;
-  float4_t acc[4][8];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t nk = p.K / PK;
-  for (int64_t s = 0; s < D && s < nk; ++s) issue(s);
-  // stage 0 landed (this wave's part), then visible to all
-  vm_wait_stages<NS>(min((int64_t)D, nk) - 1);
-  __builtin_amdgcn_s_barrier();
-  if (grp1) __builtin_amdgcn_s_barrier();   // stagger: group 1 one barrier behind
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    // ---- R: fragments of stage kt, DMA of stage kt + D
-    const uint4* sA = smem + (int)(kt % NS) * PSTAGE_U4;
-    const uint4* sB = sA + TM * 4;
-    short8 fw[4], fx[8];
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      const int r = wn * 64 + jn * 16 + li;
-      uint4 v = sB[r * 4 + (g ^ swz64(r))];
-      fw[jn] = *reinterpret_cast<short8*>(&v);
-    }
-#pragma unroll
-    for (int im = 0; im < 8; ++im) {
-      const int r = wm * 128 + im * 16 + li;
-      uint4 v = sA[r * 4 + (g ^ swz64(r))];
-      fx[im] = *reinterpret_cast<short8*>(&v);
-    }
-#ifndef LLP_ABLATE_NOLOAD
-    if (kt + D < nk) issue(kt + D);
-#endif
-    const int64_t ahead = min(nk - 1, kt + D) - (kt + 1);   // stages issued beyond kt+1
-    if (grp1 && kt + 1 < nk) vm_wait_stages<NS>(ahead);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- M: 32 MFMAs on the fragments
-#ifndef LLP_ABLATE_NOMFMA
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn)
-#pragma unroll
-      for (int im = 0; im < 8; ++im)
-        acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#else
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
-#pragma unroll
-    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
-#endif
-    if (!grp1 && kt + 1 < nk) vm_wait_stages<NS>(ahead);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (!grp1) __builtin_amdgcn_s_barrier();   // group 0 matches group 1's barrier count
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  epilogue_256(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
-}
-
-// ---------------------------------------------------------------------------
 // K64 quadrant-phase variant: full 128-byte lines per DMA piece.
 // A K-tile of 64 (A and B images [256 rows][128 B], 64 KiB) is consumed in 4
 // phases; phase p computes one quadrant (m-half mh, n-half nh) of every wave's
@@ -683,213 +547,7 @@ __device__ __forceinline__ int q64_row(int chunk, int cr) {
   }
 }
 
-// LEAN: phase 3 keeps B-half 0 in registers from phase 0 (no re-read) and
-// drops its barrier — its operands were published by the barriers of phases 0
-// and 2, and chunk 3's refill target (A-half 1 of the other buffer) was last
-// read three barriers earlier.
-// STAG (waves 4-7 only; waves 0-3 run the plain order): 1 = each phase runs
-// the PREVIOUS phase's MFMAs before its own LDS reads, so on every SIMD one
-// wave computes while its partner (waves w and w+4 share a SIMD) waits on its
-// reads; 2 = as 1, and the phase's DMA chunk is issued after the MFMAs.  The
-// reads and barriers stay where they are (LDS safety unchanged) and every
-// accumulator sees its MFMAs in the same k order: outputs are bit-identical.
-template <bool LEAN, int STAG>
-__global__ __launch_bounds__(NT2) void gemm_nt_bf16_q64(P256 p) {
-  constexpr int IMG_U4 = 256 * 8;                  // one operand image [256][8 chunks]
-  constexpr int TILE_U4 = 2 * IMG_U4;              // A then B: 64 KiB
-  constexpr int SM_U4 = 2 * TILE_U4 > SMEM_U4_EPI + 256 ? 2 * TILE_U4 : SMEM_U4_EPI + 256;
-  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int64_t m0, n0;
-  // device row count: load it now, wait for it only after the K-tile-0 DMA is
-  // issued (rows up to the host M are addressable: stale, never stored)
-  const bool dyn = p.m_dev != nullptr;
-  const int32_t mlive = dyn ? *p.m_dev : 0;
-  if (dyn ? !tile_256_host_interleaved(p, m0, n0) : !tile_256(p, m0, n0)) return;
-
-  // per (chunk, piece): this lane's source pointer (k-tile 0) and the piece's
-  // wave-uniform LDS row offset
-  const bf16_t* src[4][2];
-  int dst_row[4][2];
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row0 = q64_row(j, 16 * wu + 8 * i);       // 8 consecutive rows per piece
-      dst_row[j][i] = row0;
-      const int r = row0 + (lane >> 3);
-      const int lc = (lane & 7) ^ (r & 7);                 // source swizzle: image chunk lane&7 holds lc
-      if (j == 0 || j == 3) {
-        int64_t m = m0 + r;
-        m = m < p.M ? m : p.M - 1;
-        src[j][i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
-      } else {
-        int64_t n = n0 + r;
-        n = n < p.N ? n : p.N - 1;
-        src[j][i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
-      }
-    }
-  const uint32_t lds0 = lds_u32(smem);
-  auto issue_chunk = [&](int j, int64_t kt) {
-    const uint32_t base = lds0 + (uint32_t)((kt & 1) * TILE_U4 * 16) + ((j == 0 || j == 3) ? 0u : IMG_U4 * 16u);
-    const int64_t koff = kt * TK;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      glds16(src[j][i] + koff, __builtin_amdgcn_readfirstlane(base + (uint32_t)(dst_row[j][i] * 128)));
-  };
-
-  const int wm = w >> 2, wn = w & 3;
-  float4_t acc[4][8];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t nk = p.K / TK;
-  short8 fa[2][4];        // [k32 half][im] for the current m-half
-  short8 fb[2][2][2];     // [n-half][k32 half][jn]
-  auto read_a = [&](const uint4* sA, int mh) {
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int im = 0; im < 4; ++im) {
-        const int r = wm * 128 + mh * 64 + im * 16 + li;
-        uint4 v = sA[r * 8 + ((kh * 4 + g) ^ (r & 7))];
-        fa[kh][im] = *reinterpret_cast<short8*>(&v);
-      }
-  };
-  auto read_b = [&](const uint4* sB, int nh) {
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn) {
-        const int r = wn * 64 + nh * 32 + jn * 16 + li;
-        uint4 v = sB[r * 8 + ((kh * 4 + g) ^ (r & 7))];
-        fb[nh][kh][jn] = *reinterpret_cast<short8*>(&v);
-      }
-  };
-  auto mfma_q = [&](int mh, int nh) {
-#ifndef LLP_ABLATE_NOMFMA
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-        for (int im = 0; im < 4; ++im)
-          acc[nh * 2 + jn][mh * 4 + im] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][kh][jn], fa[kh][im], acc[nh * 2 + jn][mh * 4 + im], 0,
-                                                      0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#else
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-      for (int im = 0; im < 4; ++im) asm volatile("" ::"v"(fa[kh][im]));
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn) asm volatile("" ::"v"(fb[nh][kh][jn]));
-    }
-#endif
-  };
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: the whole of K-tile 0
-#pragma unroll
-  for (int j = 0; j < 4; ++j) issue_chunk(j, 0);
-  if (dyn) {
-    p.M = mlive < p.M ? (mlive > 0 ? mlive : 0) : p.M;
-    if (m0 >= p.M) {   // a tile past the live rows: drain its DMA and leave
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      return;
-    }
-  }
-  const bool stag = STAG > 0 && wu >= 4;
-  const bool late_dma = STAG == 2 && wu >= 4;
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
-    const uint4* sB = sA + IMG_U4;
-    // (stag: the previous phase's quadrant before this phase's reads)
-    // phase 0: quadrant (0,0) needs chunks 0, 1 of this tile; younger: chunks 2, 3
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    barrier();
-#ifndef LLP_ABLATE_NOLOAD
-    if (more && !late_dma) issue_chunk(0, kt + 1);
-#endif
-    if (stag && kt > 0) mfma_q(1, 0);
-    if (more && late_dma) issue_chunk(0, kt + 1);
-    read_a(sA, 0);
-    read_b(sB, 0);
-    if (!stag) mfma_q(0, 0);
-    // phase 1: (0,1) needs chunk 2; younger: chunk 3 (+ chunk 0 of the next tile)
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    barrier();
-#ifndef LLP_ABLATE_NOLOAD
-    if (more && !late_dma) issue_chunk(1, kt + 1);
-#endif
-    if (stag) mfma_q(0, 0);
-    if (more && late_dma) issue_chunk(1, kt + 1);
-    read_b(sB, 1);
-    if (!stag) mfma_q(0, 1);
-    // phase 2: (1,1) needs chunk 3; younger: chunks 0, 1 of the next tile
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier();
-#ifndef LLP_ABLATE_NOLOAD
-    if (more && !late_dma) issue_chunk(2, kt + 1);
-#endif
-    if (stag) mfma_q(0, 1);
-    if (more && late_dma) issue_chunk(2, kt + 1);
-    read_a(sA, 1);
-    if (!stag) mfma_q(1, 1);
-    // phase 3: (1,0), everything resident
-    if (!LEAN) barrier();
-    else __builtin_amdgcn_sched_barrier(0);
-#ifndef LLP_ABLATE_NOLOAD
-    if (more && !late_dma) issue_chunk(3, kt + 1);
-#endif
-    if (stag) mfma_q(1, 1);
-    if (more && late_dma) issue_chunk(3, kt + 1);
-    if (!LEAN) read_b(sB, 0);
-    if (!stag) mfma_q(1, 0);
-  }
-  if (stag && nk > 0) mfma_q(1, 0);   // the staggered half's last quadrant
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  epilogue_256(p, acc, smem, SMEM_U4_EPI, m0, n0, tid, wm, wn, g, li);
-}
-
-// ---------------------------------------------------------------------------
-// Register-direct epilogue of the 256x256 kernels (no LDS staging of the C
-// tile).  After the MFMAs lane (g, li) of wave (wm, wn) holds, per (jn, im),
-// four consecutive columns 16 jn + 4 g .. +3 of row 16 im + li.  One
-// v_permlane16_swap per packed dword exchanges lane rows 1<->0 and 3<->2
-// between the jn = 2q and 2q+1 registers, so every lane then holds EIGHT
-// consecutive bf16 columns, 32 q + 16 (g & 1) + 8 (g >> 1) .. +7: one 16-B
-// store each, 16 rows x 64 contiguous bytes per wave-instruction.  Values and
-// rounding are those of epilogue_t (bit-identical); bias / head weights for the
-// lane's 16 columns come from registers loaded before the main loop (bvec).
-__device__ __forceinline__ void store_c16(const P256& p, const uint32_t (&o)[4], bool ok, int64_t row, int64_t col) {
-#ifdef LLP_ABLATE_NOSTORE
-  asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
-  return;
-#endif
-  if (!ok) return;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 vv = {o[0], o[1], o[2], o[3]};
-  if (p.nt_store)
-    __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p.C + row * p.ldc + col));
-  else
-    *reinterpret_cast<u32x4*>(p.C + row * p.ldc + col) = vv;
-}
-
+// bias (or head weights) of 16 columns c0 .. c0 + 15, four per float4 (0 past N)
 __device__ __forceinline__ void load_cols16(const float* v, int64_t N, int64_t c0, float4_t (&out)[4]) {
   // columns c0 + 16 jn + 0..3 of v (v null -> 0); c0 % 4 == 0
 #pragma unroll
@@ -900,133 +558,6 @@ __device__ __forceinline__ void load_cols16(const float* v, int64_t N, int64_t c
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[jn][r] = (v && c + r < N) ? v[c + r] : 0.f;
-    }
-  }
-}
-
-template <bool LINES>
-__device__ __forceinline__ void epilogue_direct(const P256& p, float4_t (&acc)[4][8], const float4_t (&bvec)[4],
-                                                uint4* smem, int head_off_u4, int64_t m0, int64_t n0, int tid,
-                                                int wm, int wn, int g, int li) {
-#ifdef LLP_ABLATE_NOEPI
-#pragma unroll
-  for (int jn = 0; jn < 4; ++jn)
-#pragma unroll
-    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(acc[jn][im]));
-  return;
-#endif
-  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
-  const int64_t cw = n0 + wn * 64;               // first column of this wave
-  float4_t hw[4];
-  load_cols16(p.head_w, p.N, cw + g * 4, hw);
-  float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bool relu = p.act == LLP_ACT_RELU;
-  const bool drop = p.drop_p > 0.f;
-  // lane's store column (relative to cw) after the swaps of pair q: 32 q + cq
-  const int cq = 16 * (g & 1) + 8 * (g >> 1);
-#pragma unroll
-  for (int im = 0; im < 8; ++im) {
-    const int ml = wm * 128 + im * 16 + li;
-    const int64_t row = m0 + ml;
-    uint32_t d[4][2];
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = p.alpha * acc[jn][im][r] + bvec[jn][r];
-        if (relu) v[r] = fmaxf(v[r], 0.f);
-      }
-      if (drop) {
-        const uint4 x4 = philox4((uint64_t)(row * p.N + cw + jn * 16 + g * 4) >> 2, dstream, p.drop_seed);
-        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
-      }
-      hp[im] = head_dot4(hp[im], v, hw[jn]);
-      d[jn][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      d[jn][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    }
-    if (!p.C) continue;
-    uint32_t oq[2][4];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      uint32_t (&o)[4] = oq[q];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(d[2 * q][e], d[2 * q + 1][e], false, false);
-        o[e] = sw[0];
-        o[2 + e] = sw[1];
-      }
-      const int64_t col = cw + 32 * q + cq;
-      const bool ok = row < p.M && col < p.N;
-      if (p.act == LLP_ACT_RELU_BWD) {
-        if (p.mask_in) {
-          const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            o[e] = ((bits >> (2 * e)) & 1u ? (o[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (o[e] & 0xFFFF0000u) : 0u);
-        } else if (ok) {
-          const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
-          const uint32_t av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
-            const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
-            o[e] = (k0 ? (o[e] & 0xFFFFu) : 0u) | (k1 ? (o[e] & 0xFFFF0000u) : 0u);
-          }
-        }
-      }
-      if (!LINES) store_c16(p, o, ok, row, col);
-      if (p.mask_out) {
-        // bit e of the byte for columns col..col+7 = (bf16 output e > 0); the row's four
-        // lanes (g = 0..3: columns +0, +16, +8, +24 of 32 q) form one 32-bit word
-        uint32_t byte = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          byte |= (__uint_as_float(o[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
-          byte |= (__uint_as_float(o[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
-        }
-        const uint32_t b1 = __shfl(byte, li + 16, 64), b2 = __shfl(byte, li + 32, 64), b3 = __shfl(byte, li + 48, 64);
-        if (g == 0 && ok)   // bytes in column order: g0 (+0), g2 (+8), g1 (+16), g3 (+24)
-          *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + ((cw + 32 * q) >> 3)) =
-              byte | (b2 << 8) | (b1 << 16) | (b3 << 24);
-      }
-    }
-    if (LINES) {
-      // full 128-B lines: lane li^8's pair-1 chunk moves here (DPP row_ror:8), so store A
-      // writes rows 0-7 of the 16 (lanes li < 8: own pair 0, li >= 8: row li-8's pair 1)
-      // and store B rows 8-15 -- 8 rows x 128 B per wave-instruction
-      uint32_t r1[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) r1[e] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)oq[1][e], 0x128, 0xF, 0xF, false);
-      const bool lo = li < 8;
-      uint32_t sa[4], sb[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sa[e] = lo ? oq[0][e] : r1[e];
-        sb[e] = lo ? r1[e] : oq[0][e];
-      }
-      const int64_t rbase = m0 + wm * 128 + im * 16;
-      const int64_t ra = rbase + (lo ? li : li - 8), rb = rbase + (lo ? li + 8 : li);
-      const int64_t ca = cw + (lo ? 0 : 32) + cq, cb = cw + (lo ? 32 : 0) + cq;
-      store_c16(p, sa, ra < p.M && ca < p.N, ra, ca);
-      store_c16(p, sb, rb < p.M && cb < p.N, rb, cb);
-    }
-  }
-  if (p.head_w) {
-    float* part = reinterpret_cast<float*>(smem + head_off_u4);   // [4 wn][256 rows]
-#pragma unroll
-    for (int im = 0; im < 8; ++im) {
-      float v = hp[im];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (g == 0) part[wn * TM + wm * 128 + im * 16 + li] = v;
-    }
-    __syncthreads();
-    if (tid < TM && m0 + tid < p.M) {
-      const float sum = part[tid] + part[TM + tid] + part[2 * TM + tid] + part[3 * TM + tid];
-      p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = sum;
     }
   }
 }
@@ -1259,7 +790,7 @@ __device__ __forceinline__ void epilogue_lean_head(const P256& p, float4_t (&acc
 // groups' segments of that phase order it before every reader: chunks 0, 1 in
 // phase 3 of the previous tile, chunk 2 in phase 0, chunk 3 in phase 1.  WAR:
 // chunk j's refill (phase j of tile t+1) comes 4-5 phases after its last read.
-template <int DIRECT, int MODE>
+template <int MODE>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   constexpr int IMG_U4 = 256 * 8;
   constexpr int TILE_U4 = 2 * IMG_U4;
@@ -1307,8 +838,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   float4_t bvec[4];     // bias of the lane's 16 epilogue columns, loaded under the main loop
   // lean epilogue modes (the fused-head mode measured slower: its bias and head weights
   // in registers make the kernel spill)
-  constexpr bool LEAN = DIRECT == 0 && (MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK);
-  if (DIRECT || (LEAN && MODE != EPI_BWD_MASK)) load_cols16(p.bias, p.N, n0 + wn * 64 + g * 4, bvec);
+  constexpr bool LEAN = MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK;
+  if (LEAN && MODE != EPI_BWD_MASK) load_cols16(p.bias, p.N, n0 + wn * 64 + g * 4, bvec);
   else if (LEAN) bvec[0] = bvec[1] = bvec[2] = bvec[3] = float4_t{0.f, 0.f, 0.f, 0.f};
   float4_t acc[4][8];
 #pragma unroll
@@ -1408,12 +939,6 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
     barrier();
   }
   if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
-  if (DIRECT) {                 // no LDS staging: only the head partials use LDS (after this barrier)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    if (p.head_w) barrier();
-    epilogue_direct<DIRECT == 2>(p, acc, bvec, smem, 0, m0, n0, tid, wm, wn, g, li);
-    return;
-  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if constexpr (MODE == EPI_HEAD_LEAN) {   // every tile (the host checked the shapes)
     __syncthreads();
@@ -1432,357 +957,9 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   }
 }
 
-template <int NS>
-__global__ __launch_bounds__(NT2) void gemm_nt_bf16_256p(P256 p) {
-  constexpr int LOOP_U4 = NS * PSTAGE_U4;
-  constexpr int SM_U4 = LOOP_U4 > SMEM_U4_EPI ? LOOP_U4 : SMEM_U4_EPI;
-  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4 + 256];   // + 4 KiB head partials
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int64_t m0, n0;
-  if (!tile_256(p, m0, n0)) return;
+}  // namespace
 
-  // glds: wave w stages rows [32w, 32w+32): 2 instructions per operand, each 16
-  // rows x 64 B; lane -> row 32w + 16i + (lane>>2), physical chunk lane & 3.
-  const bf16_t* ga[2];
-  const bf16_t* gb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = 32 * w + 16 * i + (lane >> 2);
-    const int lc = (lane & 3) ^ swz64(r);
-    int64_t m = m0 + r;
-    m = m < p.M ? m : p.M - 1;
-    ga[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
-    int64_t n = n0 + r;
-    n = n < p.N ? n : p.N - 1;
-    gb[i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
-  }
-  const uint32_t lds0 = lds_u32(smem);
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto issue = [&](int64_t kt) {
-    const uint32_t sA = lds0 + (uint32_t)((kt % NS) * PSTAGE_U4 * 16);
-    const uint32_t sB = sA + TM * 4 * 16;
-    const int64_t koff = kt * PK;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t off = (uint32_t)((32 * wu + 16 * i) * 4 * 16);
-      glds16(ga[i] + koff, __builtin_amdgcn_readfirstlane(sA + off));
-      glds16(gb[i] + koff, __builtin_amdgcn_readfirstlane(sB + off));
-    }
-  };
-
-  const int wm = w >> 2, wn = w & 3;
-  float4_t acc[4][8];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t nk = p.K / PK;
-  for (int64_t s = 0; s < NS - 1 && s < nk; ++s) issue(s);
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const int64_t last_issued = min(nk - 1, kt + NS - 2);
-    vm_wait_stages<NS>(last_issued - kt);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk) issue(kt + NS - 1);   // into the buffer of stage kt-1 (all waves are past it)
-    const uint4* sA = smem + (int)(kt % NS) * PSTAGE_U4;
-    const uint4* sB = sA + TM * 4;
-    short8 fw[4], fx[8];
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      const int r = wn * 64 + jn * 16 + li;
-      uint4 v = sB[r * 4 + (g ^ swz64(r))];
-      fw[jn] = *reinterpret_cast<short8*>(&v);
-    }
-#pragma unroll
-    for (int im = 0; im < 8; ++im) {
-      const int r = wm * 128 + im * 16 + li;
-      uint4 v = sA[r * 4 + (g ^ swz64(r))];
-      fx[im] = *reinterpret_cast<short8*>(&v);
-    }
-#ifndef LLP_ABLATE_NOMFMA
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn)
-#pragma unroll
-      for (int im = 0; im < 8; ++im)
-        acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#else
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
-#pragma unroll
-    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
-#endif
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // ---------------- epilogue: alpha, bias, ReLU, dropout, fused head partials
-  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
-  uint4* stg = smem;
-  float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int jn = 0; jn < 4; ++jn) {
-    const int nl = wn * 64 + jn * 16 + g * 4;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    float hw[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = (n0 + nl + r < p.N) ? p.bias[n0 + nl + r] : 0.f;
-    }
-    if (p.head_w) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) hw[r] = (n0 + nl + r < p.N) ? p.head_w[n0 + nl + r] : 0.f;
-    }
-#pragma unroll
-    for (int im = 0; im < 8; ++im) {
-      const int ml = wm * 128 + im * 16 + li;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = p.alpha * acc[jn][im][r] + bv[r];
-        if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
-      }
-      if (p.drop_p > 0.f) {
-        // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
-        // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
-        const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
-        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
-      }
-      hp[im] = head_dot4(hp[im], v, hw);
-      const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      uint2* dst = reinterpret_cast<uint2*>(stg + ml * EPI_ROW_U4) + (nl >> 2);
-      *dst = make_uint2(lo, hi);
-    }
-  }
-  if (p.head_w) {
-    // rows ml = wm*128 + im*16 + li: sum the 4 lane groups, then the 4 waves (wn) in LDS
-    float* part = reinterpret_cast<float*>(smem + SM_U4);   // [4 wn][256 rows]
-#pragma unroll
-    for (int im = 0; im < 8; ++im) {
-      float v = hp[im];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (g == 0) part[wn * 256 + wm * 128 + im * 16 + li] = v;
-    }
-  }
-  __syncthreads();
-  if (p.head_w && tid < TM && m0 + tid < p.M) {
-    const float* part = reinterpret_cast<const float*>(smem + SM_U4);
-    const float s = part[tid] + part[256 + tid] + part[512 + tid] + part[768 + tid];
-    p.head_part[(n0 / TN) * p.head_ld + m0 + tid] = s;
-  }
-  if (!p.C) return;
-  const int chunks_per_row = TN / 8;
-#pragma unroll 4
-  for (int q = tid; q < TM * chunks_per_row; q += NT2) {
-    const int rl = q / chunks_per_row, c = q % chunks_per_row;
-    const int64_t row = m0 + rl, col = n0 + c * 8;
-    const bool ok = row < p.M && col < p.N;
-    uint4 v = stg[rl * EPI_ROW_U4 + c];
-    if (p.act == LLP_ACT_RELU_BWD) {
-      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-      if (p.mask_in) {
-        const uint32_t bits = ok ? (uint32_t)p.mask_in[row * p.ld_mask + (col >> 3)] : 0u;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          vv[e] = ((bits >> (2 * e)) & 1u ? (vv[e] & 0xFFFFu) : 0u) | ((bits >> (2 * e + 1)) & 1u ? (vv[e] & 0xFFFF0000u) : 0u);
-      } else if (ok) {
-        const uint4 a = *reinterpret_cast<const uint4*>(p.aux + row * p.ld_aux + col);
-        const uint32_t av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool k0 = __uint_as_float(av[e] << 16) > 0.f;
-          const bool k1 = __uint_as_float(av[e] & 0xFFFF0000u) > 0.f;
-          vv[e] = (k0 ? (vv[e] & 0xFFFFu) : 0u) | (k1 ? (vv[e] & 0xFFFF0000u) : 0u);
-        }
-      }
-      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-    }
-    if (ok) {
-      if (p.nt_store) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 vv = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p.C + row * p.ldc + col));
-      } else {
-        *reinterpret_cast<uint4*>(p.C + row * p.ldc + col) = v;
-      }
-    }
-    if (p.mask_out) {
-      // bit e of this chunk's byte = (bf16 output e > 0), the test RELU_BWD applies;
-      // four consecutive lanes (one row, 32 columns) pack one 32-bit word
-      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-      uint32_t byte = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        byte |= (__uint_as_float(vw[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
-        byte |= (__uint_as_float(vw[e] & 0xFFFF0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
-      }
-      const uint32_t word = quad_pack_bytes(byte);
-      if ((q & 3) == 0 && ok) *reinterpret_cast<uint32_t*>(p.mask_out + row * p.ld_mask + (col >> 3)) = word;
-    }
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// Half-height tiles, two workgroups per CU (LLP_GEMM_H128): 128 (m) x 256 (n)
-// per 256-thread workgroup; wave w owns columns [64w, 64w+64) of all 128 rows
-// (the 128 x 64 wave tile of the 256 kernels, same MFMA roles and epilogue).
-// K32 stages of 64-B lines (the pp images and swizzle) in a 3-stage ring,
-// two stages in flight, one barrier per stage: 24 KiB per stage, 72 KiB per
-// workgroup, so two workgroups share a CU (<= 256 VGPRs at two waves per SIMD).
-// They run unsynchronised: one workgroup's epilogue store issue and prologue
-// overlap the other's MFMA main loop -- the per-tile constant that the 256 x
-// 256 kernels (one workgroup per CU) serialise.  Row tiles of 128 also halve
-// the last-wave tail at the teacher's N = 256.
-constexpr int HTM = 128;
-constexpr int HNT = 256;
-constexpr int HNS = 3;
-constexpr int HSTAGE_U4 = (HTM + TN) * 4;     // 24 KiB: A [128][64 B] then B [256][64 B]
-constexpr int HEPI_U4 = HTM * EPI_ROW_U4;     // staged C tile, 66 KiB
-
-template <int TMv>
-__device__ __forceinline__ bool tile_live(P256& p, int64_t& m0, int64_t& n0) {
-  if (p.m_dev) {
-    const int64_t c = *p.m_dev;
-    p.M = c < p.M ? (c > 0 ? c : 0) : p.M;
-  }
-  const int64_t tilesN = (p.N + TN - 1) / TN;
-  const int64_t tilesM = (p.M + TMv - 1) / TMv;
-  const int64_t nt = tilesM * tilesN;
-  if ((int64_t)blockIdx.x >= nt) return false;
-  const int64_t lt = xcd_remap2(blockIdx.x, nt);
-  m0 = (lt / tilesN) * TMv;
-  n0 = (lt % tilesN) * TN;
-  return true;
-}
-
-template <int TMv>
-__device__ __forceinline__ bool tile_host_interleaved(const P256& p, int64_t& m0, int64_t& n0) {
-  const int64_t tilesN = (p.N + TN - 1) / TN;
-  const int64_t tilesM = (p.M + TMv - 1) / TMv;
-  const int64_t xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
-  const int64_t mt = (loc / tilesN) * 8 + xcd;
-  m0 = mt * TMv;
-  n0 = (loc % tilesN) * TN;
-  return mt < tilesM;
-}
-
-__global__ __launch_bounds__(HNT, 2) void gemm_nt_bf16_h128(P256 p) {
-  constexpr int LOOP_U4 = HNS * HSTAGE_U4;
-  constexpr int SM_U4 = LOOP_U4 > HEPI_U4 + 128 ? LOOP_U4 : HEPI_U4 + 128;   // + 2 KiB head partials
-  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  int64_t m0, n0;
-  const bool dyn = p.m_dev != nullptr;
-  const int32_t mlive = dyn ? *p.m_dev : 0;
-  if (dyn ? !tile_host_interleaved<HTM>(p, m0, n0) : !tile_live<HTM>(p, m0, n0)) return;
-
-  // DMA pieces (1 KiB = 16 rows x 64 B): A rows 32w + 16i + (lane>>2), i < 2;
-  // B rows 64w + 16i + (lane>>2), i < 4; physical chunk lane & 3
-  const bf16_t* ga[2];
-  const bf16_t* gb[4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = 32 * w + 16 * i + (lane >> 2);
-    const int lc = (lane & 3) ^ swz64(r);
-    int64_t m = m0 + r;
-    m = m < p.M ? m : p.M - 1;
-    ga[i] = p.A + (p.ia ? (int64_t)p.ia[m] : m) * p.lda + lc * 8;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 64 * w + 16 * i + (lane >> 2);
-    const int lc = (lane & 3) ^ swz64(r);
-    int64_t n = n0 + r;
-    n = n < p.N ? n : p.N - 1;
-    gb[i] = p.B + (p.ib ? (int64_t)p.ib[n] : n) * p.ldb + lc * 8;
-  }
-  const uint32_t lds0 = lds_u32(smem);
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto issue = [&](int64_t kt) {   // 6 LDS-DMA pieces per wave per stage
-    const uint32_t sA = lds0 + (uint32_t)((kt % HNS) * HSTAGE_U4 * 16);
-    const uint32_t sB = sA + HTM * 4 * 16;
-    const int64_t koff = kt * PK;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      glds16(ga[i] + koff, __builtin_amdgcn_readfirstlane(sA + (uint32_t)((32 * wu + 16 * i) * 4 * 16)));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      glds16(gb[i] + koff, __builtin_amdgcn_readfirstlane(sB + (uint32_t)((64 * wu + 16 * i) * 4 * 16)));
-  };
-
-  float4_t acc[4][8];   // [n-tile jn][m-tile im]
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int64_t nk = p.K / PK;
-  issue(0);
-  if (nk > 1) issue(1);
-  if (dyn) {   // the device row count, waited on only now (rows up to the host M are addressable)
-    p.M = mlive < p.M ? (mlive > 0 ? mlive : 0) : p.M;
-    if (m0 >= p.M) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      return;
-    }
-  }
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    // RAW: this wave's pieces of stage kt landed (stage kt+1's 6 may still fly), then visible to all.
-    // WAR: the barrier also orders the refill of stage kt+2's buffer (= stage kt-1's) after every
-    // wave's fragment reads of stage kt-1 (consumed by its MFMAs before it got here).
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#ifndef LLP_ABLATE_NOLOAD
-    if (kt + 2 < nk) issue(kt + 2);
-#endif
-    const uint4* sA = smem + (int)(kt % HNS) * HSTAGE_U4;
-    const uint4* sB = sA + HTM * 4;
-    short8 fw[4], fx[8];
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      const int r = w * 64 + jn * 16 + li;
-      uint4 v = sB[r * 4 + (g ^ swz64(r))];
-      fw[jn] = *reinterpret_cast<short8*>(&v);
-    }
-#pragma unroll
-    for (int im = 0; im < 8; ++im) {
-      const int r = im * 16 + li;
-      uint4 v = sA[r * 4 + (g ^ swz64(r))];
-      fx[im] = *reinterpret_cast<short8*>(&v);
-    }
-#ifndef LLP_ABLATE_NOMFMA
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn)
-#pragma unroll
-      for (int im = 0; im < 8; ++im)
-        acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#else
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
-#pragma unroll
-    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
-#endif
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  epilogue_t<HTM, HNT>(p, acc, smem, HEPI_U4, m0, n0, tid, 0, w, g, li);
-}
-
-int g_gemm_variant = -1;
+namespace {
 
 // the epilogue specialisation a call can use (epilogue_t)
 int epi_mode_of(const P256& p) {
@@ -1797,34 +974,6 @@ int epi_mode_of(const P256& p) {
 }
 
 }  // namespace
-
-// NT main-loop variant for the large-tile bf16 path (tuning / A-B in one
-// process): LLP_GEMM_Q64S1 (default: q64 lean with waves 4-7 staggered by one
-// phase), LLP_GEMM_Q64L, LLP_GEMM_Q64, LLP_GEMM_PP53, LLP_GEMM_PP42,
-// LLP_GEMM_PIPE, LLP_GEMM_H128, LLP_GEMM_Q64S2.  Env LLP_GEMM_VARIANT sets the
-// initial value.
-int llp_gemm_variant() {
-  if (g_gemm_variant < 0) {
-    const char* e = getenv("LLP_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : LLP_GEMM_PP8M;
-  }
-  return g_gemm_variant;
-}
-extern "C" const char* llp_gemm_variant_name(void) {
-  static const char* names[] = {"gemm_nt_bf16_256p<4>", "gemm_nt_bf16_pp<4, 2>", "gemm_nt_bf16_pp<5, 3>",
-                                "gemm_nt_bf16_q64<false, 0>", "gemm_nt_bf16_q64<true, 0>", "gemm_nt_bf16_h128",
-                                "gemm_nt_bf16_q64<true, 1>", "gemm_nt_bf16_q64<true, 2>", "gemm_nt_bf16_pp8<0, 0>",
-                                "gemm_nt_bf16_pp8<1, 0>", "gemm_nt_bf16_pp8<2, 0>", "gemm_nt_bf16_pp8<0, mode>"};
-  const int v = llp_gemm_variant();
-  return v >= 0 && v < (int)(sizeof(names) / sizeof(names[0])) ? names[v] : "?";
-}
-
-extern "C" int llp_set_gemm_variant(int v) {
-  LLP_CHECK_ARG(v >= LLP_GEMM_PIPE && v <= LLP_GEMM_PP8M, "llp_set_gemm_variant: %d", v);
-  const int old = llp_gemm_variant();
-  g_gemm_variant = v;
-  return old;
-}
 
 // Called from llp_gemm_nt when the shapes allow it (gemm.hip).
 int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
@@ -1845,69 +994,35 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.M = M; p.N = N; p.K = K;
   p.m_dev = A->rows_dev;
   p.head_ld = M;
-  static const int nt_store_env = getenv("LLP_GEMM_NT_STORE") ? atoi(getenv("LLP_GEMM_NT_STORE")) : 1;
-  p.nt_store = nt_store_env;
-  static const int lean_env = getenv("LLP_GEMM_LEAN_EPI") ? atoi(getenv("LLP_GEMM_LEAN_EPI")) : 1;
-  p.lean_epi = lean_env;
-  // opt-in until measured: the head dot over the staged bf16 outputs (epilogue_lean_head);
-  // read per call (a few head calls per step, captured once) so one process can A/B it
-  const char* head_lean_s = head_w ? getenv("LLP_GEMM_HEAD_LEAN") : nullptr;
-  const int head_lean_env = head_lean_s ? atoi(head_lean_s) : 0;
+  p.nt_store = 1;   // non-temporal epilogue stores: +20 % on the write-bound K=128 layer, level at K=1024
+  p.lean_epi = 1;
   p.C = (bf16_t*)C; p.ldc = ldc;
   p.bias = bias; p.act = act; p.aux = (const bf16_t*)aux; p.ld_aux = ld_aux; p.alpha = alpha;
   p.drop_p = drop_p; p.drop_thresh = drop_thresh; p.drop_scale = drop_scale; p.drop_seed = drop_seed;
   p.drop_ctr = drop_ctr; p.drop_stream = drop_stream;
-  // with a device row count the q64 kernel maps the host grid interleaved over
-  // the XCDs (tile_256_host_interleaved): m-tiles padded to a multiple of 8;
-  // the other variants map the live tiles and let the surplus blocks exit
-  const int variant = llp_gemm_variant();
-  const int64_t tmr = (variant == LLP_GEMM_H128 && !A->ptr2) ? HTM : TM;   // rows per tile
-  const int64_t tiles = (A->rows_dev ? ((M + 8 * tmr - 1) / (8 * tmr)) * 8 : (M + tmr - 1) / tmr) * ((N + TN - 1) / TN);
-  static const int pipe_env = getenv("LLP_GEMM_STAGES") ? atoi(getenv("LLP_GEMM_STAGES")) : 4;
-  const int pipe = ((head_w || !C) && (pipe_env < 3 || pipe_env > 5)) ? 4 : pipe_env;
-  if (A->ptr2)
-    hipLaunchKernelGGL(gemm_nt_bf16_256<true>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_PP53)
-    hipLaunchKernelGGL((gemm_nt_bf16_pp<5, 3>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_PP42)
-    hipLaunchKernelGGL((gemm_nt_bf16_pp<4, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_Q64)
-    hipLaunchKernelGGL((gemm_nt_bf16_q64<false, 0>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_Q64L)
-    hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 0>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_Q64S1)
-    hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 1>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_Q64S2)
-    hipLaunchKernelGGL((gemm_nt_bf16_q64<true, 2>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_PP8)
-    hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_PP8M) {
-    const int mode = epi_mode_of(p);
-    if (mode == EPI_FWD_RELU)
-      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_FWD_RELU>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-    else if (mode == EPI_FWD_NONE)
-      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_FWD_NONE>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-    else if (mode == EPI_BWD_MASK)
-      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_BWD_MASK>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-    else if (mode == EPI_HEAD_RELU && head_lean_env && lean_env && N % TN == 0 && !((uintptr_t)head_w & 15) &&
-             (!C || (!(ldc & 7) && !((uintptr_t)C & 15))))
-      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_HEAD_LEAN>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-    else if (mode == EPI_HEAD_RELU)
-      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_HEAD_RELU>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-    else
-      hipLaunchKernelGGL((gemm_nt_bf16_pp8<0, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  } else if (variant == LLP_GEMM_PP8D)
-    hipLaunchKernelGGL((gemm_nt_bf16_pp8<1, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (variant == LLP_GEMM_PP8L)
-    hipLaunchKernelGGL((gemm_nt_bf16_pp8<2, EPI_ANY>), dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-
-  else if (variant == LLP_GEMM_H128)
-    hipLaunchKernelGGL(gemm_nt_bf16_h128, dim3((unsigned)tiles), dim3(HNT), 0, s, p);
-  else if (pipe == 4 || pipe == 5)
-    hipLaunchKernelGGL(gemm_nt_bf16_256p<4>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else if (pipe == 3)
-    hipLaunchKernelGGL(gemm_nt_bf16_256p<3>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
-  else
-    hipLaunchKernelGGL(gemm_nt_bf16_256<false>, dim3((unsigned)tiles), dim3(NT2), 0, s, p);
+  // with a device row count pp8 maps the host grid interleaved over the XCDs
+  // (tile_256_host_interleaved): m-tiles padded to a multiple of 8; the Hadamard-operand
+  // kernel maps the live tiles and lets the surplus blocks exit
+  const int64_t tiles = (A->rows_dev ? ((M + 8 * TM - 1) / (8 * TM)) * 8 : (M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  const dim3 grid((unsigned)tiles), block(NT2);
+  if (A->ptr2) {   // A = A1[ia] * A2[ia2] formed on load (rows whose width is not a multiple of 8)
+    hipLaunchKernelGGL(gemm_nt_bf16_256<true>, grid, block, 0, s, p);
+    return (int)hipGetLastError();
+  }
+  switch (epi_mode_of(p)) {
+    case EPI_FWD_RELU: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_RELU>), grid, block, 0, s, p); break;
+    case EPI_FWD_NONE: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_NONE>), grid, block, 0, s, p); break;
+    case EPI_BWD_MASK: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_BWD_MASK>), grid, block, 0, s, p); break;
+    case EPI_HEAD_RELU:
+      // the head dot over the staged bf16 outputs (epilogue_lean_head) on every tile when
+      // the shapes allow: 650 -> 643 us per predictor-layer launch, collab step -0.3 %
+      // (3 interleaved rounds, profiles/r03_head_lean_ab.txt)
+      if (N % TN == 0 && !((uintptr_t)head_w & 15) && (!C || (!(ldc & 7) && !((uintptr_t)C & 15))))
+        hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_HEAD_LEAN>), grid, block, 0, s, p);
+      else
+        hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_HEAD_RELU>), grid, block, 0, s, p);
+      break;
+    default: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_ANY>), grid, block, 0, s, p);
+  }
   return (int)hipGetLastError();
 }

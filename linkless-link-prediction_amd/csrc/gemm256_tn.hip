@@ -79,7 +79,7 @@ __device__ __forceinline__ void vm_wait(int64_t ahead) {   // 4 glds per wave pe
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
-// STAG (2 = LLP_TN_STAG 2; the default is its lean form, gemm_tn_bf16_256c): 1 = waves 4-7 run each stage's MFMAs one stage
+// STAG (2 for gathered operands; plain ones take its lean form, gemm_tn_bf16_256c): 1 = waves 4-7 run each stage's MFMAs one stage
 // late (after the next barrier, before that stage's reads); 2 = as 1 with their
 // DMA issued after those MFMAs.  Bit-identical (same per-accumulator order).
 template <int STAG>
@@ -286,209 +286,7 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256(PTN p) {
 }
 
 
-// Ping-pong form (LLP_TN_STAG=3, 4; measured 10-16 % SLOWER than the staggered
-// lockstep loop on the collab shapes, kept as an A/B knob): every stage is a LOAD segment (counted vmcnt
-// for the NEXT stage, this stage's ds_read_b64_tr_b16 fragment reads, the DMA of stage
-// s + TD) and an MFMA segment (32 MFMAs at s_setprio 1), each closed by a barrier, with
-// waves 4-7 one barrier behind waves 0-3 (cdna_hip_programming.md §5, 256² 8-phase
-// template), so on every SIMD one wave computes while its partner reads.  RAW: stage
-// s+1 is waited for in LOAD_s, before the barriers that precede both groups' LOAD_{s+1}.
-// WAR: the DMA of stage s+TD in LOAD_s overwrites stage s+TD-TNS, whose last reads
-// (group 1's LOAD) drained two barriers earlier: TNS >= TD + 2.  5 stages x 32 KiB =
-// the whole 160 KiB of LDS.  Same MFMA operands and per-accumulator k order as the
-// lockstep kernel: bit-identical slabs.
-constexpr int TNS = 5, TD = 3;
-static_assert(TNS >= TD + 2, "TN ping-pong ring too short for its DMA distance");
-
-// SPLIT: each stage as two LOAD/MFMA pairs (fragments p + q 0-3 then q 4-7, 16 MFMAs
-// each, half the stage's DMA in each LOAD), four barriers per stage.
-template <bool SPLIT>
-__global__ __launch_bounds__(NTT) void gemm_tn_bf16_pp(PTN p) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[TNS * STAGE_T];   // 160 KiB
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int64_t tilesQ = (p.Q + TQ - 1) / TQ;
-  const int64_t tilesP = (p.P + TP - 1) / TP;
-  int64_t tile, z;
-  tn_block(p.zmajor, (int)(tilesP * tilesQ), (int)p.splits, tile, z);
-  const int64_t p0 = (tile / tilesQ) * TP, q0 = (tile % tilesQ) * TQ;
-  if (p.m_dev) {
-    const int64_t c = *p.m_dev;
-    p.M = c < p.M ? (c > 0 ? c : 0) : p.M;
-    const int64_t mc = (p.M + p.splits - 1) / p.splits;
-    p.mchunk = mc > 0 ? (mc + TKM - 1) / TKM * TKM : TKM;
-  }
-  const int64_t mbeg = z * p.mchunk;
-  const int64_t mend = min(p.M, mbeg + p.mchunk);
-
-  const int pc = lane & 31;
-  const int rbase = 4 * w + (lane >> 5);
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const int capA = (int)max((int64_t)0, (p.P - p0) - 8), capB = (int)max((int64_t)0, (p.Q - q0) - 8);
-  const bf16_t* zrow = reinterpret_cast<const bf16_t*>(g_zero_row);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)smem);
-  const int64_t nfull = (p.ia || p.ib) ? 0 : (mend - mbeg) / TKM;
-  const bf16_t* pa[2];
-  const bf16_t* pb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = rbase + 2 * i;
-    const int lc8 = (pc ^ swz(r)) * 8;
-    pa[i] = p.A + (mbeg + r) * p.lda + p0 + min(lc8, capA);
-    pb[i] = p.B + (mbeg + r) * p.ldb + q0 + min(lc8, capB);
-  }
-  const int64_t strideA = (int64_t)TKM * p.lda, strideB = (int64_t)TKM * p.ldb;
-  // half h of stage st's DMA (h = -1: both halves): piece i = h of each operand
-  auto issue = [&](int64_t st, int h = -1) {
-    const int64_t mt = mbeg + st * TKM;
-    const uint32_t sA = lds0 + (uint32_t)((st % TNS) * STAGE_T * 16);
-    const uint32_t sB = sA + IMG_U4 * 16;
-    if (st < nfull) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (h >= 0 && i != h) continue;
-        const uint32_t off = (uint32_t)((4 * wu + 2 * i) * 32 * 16);
-        glds16(pa[i] + st * strideA, __builtin_amdgcn_readfirstlane(sA + off));
-        glds16(pb[i] + st * strideB, __builtin_amdgcn_readfirstlane(sB + off));
-      }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (h >= 0 && i != h) continue;
-      const int r = rbase + 2 * i;
-      const int lc8 = (pc ^ swz(r)) * 8;
-      const int ca = min(lc8, capA), cb = min(lc8, capB);
-      const int64_t m = mt + r;
-      const bool v = m < mend;
-      const int64_t mm = v ? m : mbeg;
-      const int64_t ra = p.ia ? (int64_t)p.ia[mm] : mm;
-      const int64_t rb = p.ib ? (int64_t)p.ib[mm] : mm;
-      const bf16_t* srcA = v ? p.A + ra * p.lda + p0 + ca : zrow + ca;
-      const bf16_t* srcB = v ? p.B + rb * p.ldb + q0 + cb : zrow + cb;
-      const uint32_t off = (uint32_t)((4 * wu + 2 * i) * 32 * 16);
-      glds16(srcA, __builtin_amdgcn_readfirstlane(sA + off));
-      glds16(srcB, __builtin_amdgcn_readfirstlane(sB + off));
-    }
-  };
-
-  const int wq = w >> 2, wp = w & 3;
-  float4_t acc[8][4];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
-  const int q4 = li >> 2, pp = li & 3;
-  const bool do_cs = p.ws_colsum != nullptr && q0 == 0 && wq == 0;
-  float4_t accb[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b) accb[b] = float4_t{0.f, 0.f, 0.f, 0.f};
-  short8 ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
-  auto tr_read = [&](const char* img, int row, int col) -> short4_t {
-    const int off = row * 512 + 16 * ((col >> 3) ^ swz(row)) + 8 * ((col >> 2) & 1);
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s4*)((lds_char*)((__attribute__((address_space(3))) uint4*)img) + off));
-  };
-  auto barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  short8 fp[4];
-  short8 fq[8];
-  const bool grp1 = wu >= 4;
-  if (mbeg < mend) {
-    const int64_t nsteps = (mend - mbeg + TKM - 1) / TKM;
-    for (int64_t s = 0; s < TD && s < nsteps; ++s) issue(s);
-    vm_wait(min(nsteps, (int64_t)TD) - 1);   // stage 0 landed
-    barrier();
-    if (grp1) barrier();
-    for (int64_t st = 0; st < nsteps; ++st) {
-      // LOAD: stage st+1 landed (younger: up to st+TD-1), this stage's fragments, DMA of st+TD
-      if (st + 1 < nsteps) vm_wait(min(nsteps - 1, st + TD - 1) - (st + 1));
-      const char* sA = reinterpret_cast<const char*>(smem + (int)(st % TNS) * STAGE_T);
-      const char* sB = sA + IMG_U4 * 16;
-      const int row0 = 8 * g + q4;
-#pragma unroll
-      for (int ip = 0; ip < 4; ++ip) {
-        const int col = wp * 64 + ip * 16 + 4 * pp;
-        const short4_t t0 = tr_read(sA, row0, col), t1 = tr_read(sA, row0 + 4, col);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { fp[ip][e] = t0[e]; fp[ip][4 + e] = t1[e]; }
-      }
-      auto read_q = [&](int j0, int j1) {
-#pragma unroll
-        for (int jq = j0; jq < j1; ++jq) {
-          const int col = wq * 128 + jq * 16 + 4 * pp;
-          const short4_t t0 = tr_read(sB, row0, col), t1 = tr_read(sB, row0 + 4, col);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { fq[jq][e] = t0[e]; fq[jq][4 + e] = t1[e]; }
-        }
-      };
-      auto mfma_q = [&](int j0, int j1, bool cs) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        if (cs) {
-#pragma unroll
-          for (int ip = 0; ip < 4; ++ip)
-            accb[ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fp[ip], accb[ip], 0, 0, 0);
-        }
-#pragma unroll
-        for (int jq = j0; jq < j1; ++jq)
-#pragma unroll
-          for (int ip = 0; ip < 4; ++ip)
-            acc[jq][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[jq], fp[ip], acc[jq][ip], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      };
-      if (SPLIT) {
-        read_q(0, 4);
-        if (st + TD < nsteps) issue(st + TD, 0);
-        barrier();
-        mfma_q(0, 4, do_cs);
-        barrier();
-        read_q(4, 8);
-        if (st + TD < nsteps) issue(st + TD, 1);
-        barrier();
-        mfma_q(4, 8, false);
-        barrier();
-      } else {
-        read_q(0, 8);
-        if (st + TD < nsteps) issue(st + TD);
-        barrier();
-        mfma_q(0, 8, do_cs);
-        barrier();
-      }
-    }
-    if (!grp1) barrier();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (do_cs && g == 0) {
-#pragma unroll
-    for (int ip = 0; ip < 4; ++ip) {
-      const int64_t pr = p0 + wp * 64 + ip * 16 + li;
-      if (pr < p.P) p.ws_colsum[z * p.P + pr] = accb[ip][0];
-    }
-  }
-  float* out = p.ws + z * p.P * p.Q;
-#pragma unroll
-  for (int ip = 0; ip < 4; ++ip) {
-    const int64_t pr = p0 + wp * 64 + ip * 16 + li;
-    if (pr >= p.P) continue;
-#pragma unroll
-    for (int jq = 0; jq < 8; ++jq) {
-      const int64_t qc = q0 + wq * 128 + jq * 16 + 4 * g;
-      if (qc >= p.Q) continue;
-      *reinterpret_cast<float4_t*>(out + pr * p.Q + qc) = acc[jq][ip];
-    }
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// Lean form of the staggered loop (LLP_TN_STAG 5 = lean STAG 2, 6 = lean STAG 1),
+// Lean form of the staggered loop (STAG 2; plain operands),
 // plain (non-gathered) operands only.  Same stages, DMA pieces, fragments, MFMA
 // operands and per-accumulator order as gemm_tn_bf16_256 (bit-identical slabs),
 // without its per-stage VALU work, which at two waves per SIMD competed with the
@@ -730,27 +528,9 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
 
 }  // namespace
 
-namespace {
-int g_tn_variant = -1;   // main-loop variant of the TN kernel (LLP_TN_STAG; llp_set_gemm_tn_variant)
-}
-
-// 0 lockstep, 1 waves 4-7 staggered by one stage, 2 = 1 with late DMA,
-// 3 ping-pong, 4 ping-pong with two LOAD/MFMA pairs per stage (3, 4: measured slower),
-// 5 = 2 as the lean loop (default; gathered operands fall back to 2), 6 = 1 as the lean loop;
-// + 8: tile-major block order (the round-1 placement) instead of split-major
-extern "C" int llp_set_gemm_tn_variant(int v) {
-  LLP_CHECK_ARG(v >= 0 && v <= 14 && (v & 7) <= 6, "llp_set_gemm_tn_variant: %d", v);
-  const int old = g_tn_variant >= 0 ? g_tn_variant : 5;
-  g_tn_variant = v;
-  return old;
-}
-
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  static const int64_t target = [] {
-    const char* e = getenv("LLP_TN_BLOCKS");   // tuning knob: blocks per launch
-    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)256;
-  }();
+  const int64_t target = 256;   // one wave of workgroups over the 256 CUs
   int64_t splits = (target + tiles - 1) / tiles;
   const int64_t maxs = (M + TKM * 16 - 1) / (TKM * 16);   // >= 16 m-steps per split
   if (splits > maxs) splits = maxs;
@@ -771,23 +551,11 @@ int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   p.splits = splits;
   p.ws = ws;
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  const int var = g_tn_variant >= 0 ? g_tn_variant : (g_tn_variant = getenv("LLP_TN_STAG") ? atoi(getenv("LLP_TN_STAG")) : 5);
-  const int stag = var & 7;
-  p.zmajor = (var & 8) ? 0 : 1;
-  const bool lean_ok = !A->idx && !B->idx;   // the lean loop stages plain operands only
-  if (stag == 5 && lean_ok)
+  p.zmajor = 1;
+  // the lean loop stages plain operands only; a gathered operand takes the staggered loop
+  if (!A->idx && !B->idx)
     hipLaunchKernelGGL(gemm_tn_bf16_256c<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
-  else if (stag == 6 && lean_ok)
-    hipLaunchKernelGGL(gemm_tn_bf16_256c<1>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
-  else if (stag == 3)
-    hipLaunchKernelGGL(gemm_tn_bf16_pp<false>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
-  else if (stag == 4)
-    hipLaunchKernelGGL(gemm_tn_bf16_pp<true>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
-  else if (stag == 1)
-    hipLaunchKernelGGL(gemm_tn_bf16_256<1>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
-  else if (stag == 2 || stag >= 5)
-    hipLaunchKernelGGL(gemm_tn_bf16_256<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   else
-    hipLaunchKernelGGL(gemm_tn_bf16_256<0>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+    hipLaunchKernelGGL(gemm_tn_bf16_256<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   return (int)hipGetLastError();
 }

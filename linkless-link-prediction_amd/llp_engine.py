@@ -31,27 +31,26 @@ from contextlib import nullcontext as _nullctx
 
 # unique-node path: the Hadamard backward is reduced straight onto the unique nodes
 # (llp_hadamard_bwd_segments: the anchors' context sums, then one pass per node over its rows),
-# bit-identical to the row gradients + segment sum (LLP_SEGMENT_FUSED=0) without their [R1, H]
+# bit-identical to the row gradients + segment sum (False: the A/B path) without their [R1, H]
 # buffer: collab step 12.87 -> 12.66 ms (same-box A/B)
-_SEGMENT_FUSED = os.environ.get("LLP_SEGMENT_FUSED", "1") == "1"
+_SEGMENT_FUSED = True
 # unique-node path: the unique count stays on the device (GEMM grids sized by the bound min(R1, N));
-# LLP_DEVICE_COUNT=0 reads it on the host instead (a sync per step, not capturable; A/B knob)
-_DEVICE_COUNT = os.environ.get("LLP_DEVICE_COUNT", "1") != "0"
+# False reads it on the host instead (a sync per step, not capturable; A/B switch)
+_DEVICE_COUNT = True
 # minibatch step: weight-gradient (TN) GEMMs and the frozen teacher predictor run on a second HIP
 # stream beside the data-gradient GEMMs / Hadamard backward / student forward of the main stream
-# (fork/join by events, hipGraph-capturable); LLP_OVERLAP=0 runs everything on one stream (A/B knob)
+# (fork/join by events, hipGraph-capturable), measured slower, so 0: one stream;
 # bit mask: 1 teacher predictor beside the student forward; 2 the predictor's first-layer weight
 # gradient beside the Hadamard backward; 4 every other weight gradient beside its data gradient
-_OVERLAP = int(os.environ.get("LLP_OVERLAP", "0"))
+_OVERLAP = 0
 # minibatch step, bf16: x[this_target] (src/main.py:95) is gathered once into a plain buffer
 # (llp_gather_rows) that the first student layer's forward and weight-gradient GEMMs read, so the
-# weight gradient runs the lean TN loop (gathered operands fall back to the staggered one);
-# LLP_GATHER_X=0 keeps the gathered GEMM operands (A/B knob)
-_GATHER_X = os.environ.get("LLP_GATHER_X", "1") != "0"
+# weight gradient runs the lean TN loop (gathered operands fall back to the staggered one)
+_GATHER_X = True
 # minibatch step with device sampling and randint negatives (collab): one launch builds the
 # samples, negatives, target rows and teacher pair index (llp_minibatch_sample, bit-identical
-# to the five separate kernels); LLP_FUSED_SAMPLE=0 runs them separately (A/B knob)
-_FUSED_SAMPLE = os.environ.get("LLP_FUSED_SAMPLE", "1") != "0"
+# to the five separate kernels; False runs them separately)
+_FUSED_SAMPLE = True
 
 # dropout Philox keys (EngineBase._dropout): one per module, one stream per layer and step
 DROP_ENCODER, DROP_PREDICTOR, DROP_TEACHER_PRED = 0, 1, 2
@@ -494,7 +493,7 @@ class EngineBase:
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
     def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
-        """d(loss)/dh of the predictor input h[ia] * h[ib] into ``out`` [N, H] (compute dtype),
+        """d(loss)/dh of the predictor input h[ia] * h[ib] into ``out`` [N, H] (compute dtype, or f32),
         deterministically: the 2R endpoint rows tgt = [ia | ib] are grouped by node
         (llp_dedup_rows), each row's gradient dZ[r] * h[partner] is formed once
         (llp_hadamard_bwd_blocks, label-row layout; drow: the 'inner' predictor's scalar) and
@@ -631,11 +630,15 @@ class DistillEngine(EngineBase):
     """
 
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
-                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, overlap=True):
+                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, overlap=True,
+                 shard_student=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
         # run the dropout-free student on unique nodes (step_minibatch); the unique
         # count stays on the device, so this path is hipGraph-capturable too
-        self.dedup = bool(dedup) and os.environ.get("LLP_DEDUP", "1") != "0"
+        self.dedup = bool(dedup)
+        # multi-rank full-batch step: each rank runs the student on its slice of the nodes
+        # (_fb_shard); rank 0 of 4 on coauthor-physics 0.94 -> 0.80 ms (profiles/r03_fb_shard_ab.txt)
+        self.shard_student = bool(shard_student)
         self.overlap = bool(overlap)   # second stream for the TN GEMMs / teacher predictor (step_minibatch)
         self._rows_dev = None      # int32 device count of the unique-node student (last step), or None
         self._rows_host = 0
@@ -947,7 +950,7 @@ class DistillEngine(EngineBase):
         ia, ib = ia_ib[:R2], ia_ib[R2:]
         K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
 
-        # ---- a4: student MLP over all nodes (src/main.py:173); with LLP_FB_SHARD=1 each rank
+        # ---- a4: student MLP over all nodes (src/main.py:173); at several ranks each rank
         # runs it on its own slice of the nodes and the slices are all-gathered (_fb_shard)
         shard = self._fb_shard(p_drop, float(a.KD_RM) == 0.0 and self._grouped_ok(H))
         r0, n_rows, n_loc, s_world, s_rank = (0, N, N, 1, 0) if shard is None else shard
@@ -1011,13 +1014,20 @@ class DistillEngine(EngineBase):
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
         mlp = self.predictor_kind == "mlp"
         if grouped and shard is not None:
-            # every rank's d(h) over all nodes, summed onto the owners' slices (reduce-scatter)
-            dh_full = self._buf("fb_dhfull", (s_world * n_loc, H), dt)
+            # every rank's d(h) over all nodes as unrounded f32 per-node sums, summed in f32
+            # onto the owners' slices (reduce-scatter), then rounded once to the compute dtype
+            dh_full = self._buf("fb_dhfull", (s_world * n_loc, H), torch.float32)
             self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh_full[:N])
             if s_world * n_loc > N:
                 dh_full[N:].zero_()
-            dh = self._buf("gS0", (n_loc, H), dt)
-            self._collective(lambda: self._reduce_scatter_rows(dh, dh_full, s_world, s_rank))
+            if dt == torch.float32:
+                dh = self._buf("gS0", (n_loc, H), dt)
+                self._collective(lambda: self._reduce_scatter_rows(dh, dh_full, s_world, s_rank))
+            else:
+                dh32 = self._buf("fb_dh32", (n_loc, H), torch.float32)
+                self._collective(lambda: self._reduce_scatter_rows(dh32, dh_full, s_world, s_rank))
+                dh = self._buf("gS0", (n_loc, H), dt)
+                K.convert(dh32, dh)
         elif grouped:
             dh = self._buf("gS0", (N, H), dt)
             self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh)
@@ -1039,8 +1049,8 @@ class DistillEngine(EngineBase):
     def _fb_shard(self, p_drop, grouped):
         """(first row, rows, rows per rank, world, rank) of this rank's slice of the full-batch student,
         or None: the student over all N nodes on every rank, as in the reference
-        (src/main.py:173).  Opt-in (LLP_FB_SHARD=1) until measured on the GPU: several
-        ranks, no dropout (the GEMM's dropout draws are keyed by the row within the call)
+        (src/main.py:173).  On (``shard_student``, default) with several ranks, no dropout
+        (the GEMM's dropout draws are keyed by the row within the call)
         and the node-grouped d(h) (``grouped``: no KD_RM, whose f32 scatter target covers
         all rows, and rows the grouping kernels take).  The slices are all-gathered
         after the forward; d(h) of all nodes is reduce-scattered onto them before the
@@ -1050,7 +1060,7 @@ class DistillEngine(EngineBase):
         world, rank = self.world, self.rank
         if world <= 1 and self.emulate_shard is not None:
             rank, world = self.emulate_shard
-        if world <= 1 or os.environ.get("LLP_FB_SHARD") != "1" or p_drop > 0.0 or not grouped:
+        if world <= 1 or not self.shard_student or p_drop > 0.0 or not grouped:
             return None
         n_loc = -(-self.N // world)
         if self.N - (world - 1) * n_loc <= 0:   # a rank without rows: off on every rank alike

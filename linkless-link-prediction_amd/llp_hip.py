@@ -50,9 +50,6 @@ _SIGS = {
     "llp_gemm_nt_head": (c_int, [c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_vp, c_int,
                                  c_f32, C.POINTER(Dropout), c_vp, c_vp, c_vp]),
     "llp_head_finish": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "llp_set_gemm_variant": (c_int, [c_int]),
-    "llp_gemm_variant_name": (C.c_char_p, []),
-    "llp_set_gemm_tn_variant": (c_int, [c_int]),
     "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
     "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_vp, c_i64, c_vp]),
@@ -68,7 +65,8 @@ _SIGS = {
     "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_dedup_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_int, c_vp, c_vp,
+                                     c_vp]),
     "llp_hadamard_bwd_segments": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_i64, c_vp, c_vp]),
     "llp_gather_i32": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
@@ -281,11 +279,12 @@ def dedup_rows(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, ws)
 
 def segment_sum_rows(U, seg_ptr, rows, src, out, count=None, out_rows=None):
     """out[u] (out[out_rows[u]] with ``out_rows``) = sum of src[rows[seg_ptr[u]:seg_ptr[u+1]]]
-    for u < U (u < min(U, count) with an int32 device ``count``)."""
+    for u < U (u < min(U, count) with an int32 device ``count``); ``out`` in src's dtype
+    or f32 (unrounded sums)."""
     L = lib()
     check(L.llp_segment_sum_rows(dtype_code(src.dtype), U, src.shape[1], seg_ptr.data_ptr(), rows.data_ptr(),
-                                 src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), ptr(out_rows),
-                                 ptr(count), stream_ptr()), "llp_segment_sum_rows")
+                                 src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), dtype_code(out.dtype),
+                                 ptr(out_rows), ptr(count), stream_ptr()), "llp_segment_sum_rows")
 
 
 def hadamard_bwd_segments(U, B, C, L2, H, seg_ptr, rows, pos, dZ, h, dh, anchor_rows, drow=None, count=None):

@@ -1,4 +1,4 @@
-"""The node-sharded full-batch student (opt-in LLP_FB_SHARD, DistillEngine._fb_shard),
+"""The node-sharded full-batch student (DistillEngine._fb_shard, default at several ranks),
 checked on CPU over 2 and 3 gloo ranks with the oracle as the model: each rank runs the
 student MLP on its slice of the nodes, the slices are all-gathered with the engine's
 own `_all_gather_rows`, the rank's shard of the anchors / label edges gives d(loss)/dh
@@ -77,8 +77,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     prob = _problem()
     N, x, t_h, samples, edge, neg, (sw, sb, pw, pb, tw, tb), args = prob
-    fake = types.SimpleNamespace(world=world, rank=rank, group=None, N=N, emulate_shard=None)
-    os.environ["LLP_FB_SHARD"] = "1"
+    fake = types.SimpleNamespace(world=world, rank=rank, group=None, N=N, emulate_shard=None, shard_student=True)
     r0, n_rows, n_loc, s_world, s_rank = llp_engine.DistillEngine._fb_shard(fake, 0.0, True)
     assert (s_world, s_rank, n_loc) == (world, rank, -(-N // world))
     lw = [w.clone().requires_grad_() for w in sw]
@@ -141,22 +140,23 @@ def test_node_sharded_student_sums_to_the_batch_gradient(world):
     np.testing.assert_allclose(flat, full, rtol=1e-10, atol=1e-13)
 
 
-def test_fb_shard_gating(monkeypatch):
-    """_fb_shard is off unless LLP_FB_SHARD=1 with several (or emulated) ranks, no dropout
+def test_fb_shard_gating():
+    """_fb_shard is on (shard_student, default) with several (or emulated) ranks, no dropout
     and no KD_RM; slices cover the nodes with ceil(N / world) rows, the last one ragged."""
     sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
     import llp_engine
     f = llp_engine.DistillEngine._fb_shard
-    eng = types.SimpleNamespace(world=4, rank=3, N=10, emulate_shard=None)
-    monkeypatch.delenv("LLP_FB_SHARD", raising=False)
-    assert f(eng, 0.0, True) is None
-    monkeypatch.setenv("LLP_FB_SHARD", "1")
+    ns = lambda **kw: types.SimpleNamespace(**{"emulate_shard": None, "shard_student": True, **kw})
+    eng = ns(world=4, rank=3, N=10)
     assert f(eng, 0.0, True) == (9, 1, 3, 4, 3)
+    eng.shard_student = False
+    assert f(eng, 0.0, True) is None
+    eng.shard_student = True
     assert f(eng, 0.5, True) is None and f(eng, 0.0, False) is None
-    one = types.SimpleNamespace(world=1, rank=0, N=10, emulate_shard=None)
+    one = ns(world=1, rank=0, N=10)
     assert f(one, 0.0, True) is None
     one.emulate_shard = (1, 4)
     assert f(one, 0.0, True) == (3, 3, 3, 4, 1)
     for r in range(4):   # N=7 over 4 ranks: 2, 2, 2, 1 rows; N=6: rank 3 would have none -> off on every rank
-        assert f(types.SimpleNamespace(world=4, rank=r, N=7, emulate_shard=None), 0.0, True)[1] == (1 if r == 3 else 2)
-        assert f(types.SimpleNamespace(world=4, rank=r, N=6, emulate_shard=None), 0.0, True) is None
+        assert f(ns(world=4, rank=r, N=7), 0.0, True)[1] == (1 if r == 3 else 2)
+        assert f(ns(world=4, rank=r, N=6), 0.0, True) is None

@@ -178,7 +178,7 @@ def test_two_ranks_segmented_graph_matches_eager(size):
         assert np.array_equal(a, b)
 
 
-def _run_fullbatch(rank, world, port, out):
+def _run_fullbatch(rank, world, port, out, shard=True):
     """Two full-batch steps (train(), src/main.py:167-235: the student over all
     nodes, PyG-dense negatives) of this rank's shard: the BASELINE configs[3] path."""
     import sys
@@ -203,7 +203,7 @@ def _run_fullbatch(rank, world, port, out):
         p.requires_grad = False
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
     eng = llp_engine.DistillEngine(model, pred, tpred, x.to(dev), t_h.to(dev), ei[0].numpy(), ei[1].numpy(), N, args,
-                                   opt, dtype="fp32", seed=13)
+                                   opt, dtype="fp32", seed=13, shard_student=shard)
     B, P = anchors.numel(), links.numel()
     b0, b1 = rank * B // world, (rank + 1) * B // world
     p0, p1 = rank * P // world, (rank + 1) * P // world
@@ -224,44 +224,38 @@ def _run_fullbatch(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def _fullbatch_worker(rank, world, port, q):
+def _fullbatch_worker(rank, world, port, q, shard):
     out = {}
-    _run_fullbatch(rank, world, port, out)
+    _run_fullbatch(rank, world, port, out, shard)
     if rank == 0:
         q.put(out)
 
 
 def test_two_ranks_fullbatch_equal_one_rank():
     """Anchor / link batches of the full-batch step sharded over 2 ranks (every rank
-    draws the same dense negatives and keeps its columns) == the whole batch on one."""
+    draws the same dense negatives and keeps its columns) == the whole batch on one.
+    Default engine: each rank runs the student on half of the nodes, the halves are
+    all-gathered and d(h) is reduce-scattered back in f32 (DistillEngine._fb_shard)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _fullbatch_compare()
 
 
-@pytest.mark.skipif(os.environ.get("LLP_TEST_FB_SHARD") != "1",
-                    reason="opt-in node-sharded full-batch student (LLP_FB_SHARD) not yet run on the GPU; "
-                           "LLP_TEST_FB_SHARD=1")
-def test_two_ranks_fullbatch_sharded_student_equal_one_rank():
-    """LLP_FB_SHARD=1: each rank runs the student on half of the nodes, the halves are
-    all-gathered and d(h) is reduce-scattered back (DistillEngine._fb_shard); same bar
-    as the replicated student."""
+def test_two_ranks_fullbatch_replicated_student_equal_one_rank():
+    """shard_student=False: every rank runs the student over all nodes, as the reference
+    (src/main.py:173); same bar as the node-sharded default."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    os.environ["LLP_FB_SHARD"] = "1"
-    try:
-        _fullbatch_compare()
-    finally:
-        del os.environ["LLP_FB_SHARD"]
+    _fullbatch_compare(shard=False)
 
 
-def _fullbatch_compare():
+def _fullbatch_compare(shard=True):
     single = {}
-    _run_fullbatch(0, 1, 0, single)
+    _run_fullbatch(0, 1, 0, single, shard)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fullbatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_fullbatch_worker, args=(r, 2, port, q, shard)) for r in range(2)]
     for p in procs:
         p.start()
     multi = q.get(timeout=300)

@@ -7,7 +7,7 @@ LLP_D=10 LLP_R=0.01 True_label=0.1, rw_step=2 hops=2 ns_rate=4 (C=20), PyG
 dense negatives.  Prints one JSON line: ms per link batch and edges/s, per
 dtype; --emulate-ranks R times rank 0's shard of each batch (no collective).
 
-    python tools/physics_bench.py [--steps 10] [--dtype bf16] [--emulate-ranks 4]
+    python tools/physics_bench.py [--steps 10] [--dtype bf16] [--emulate-ranks 4 [--replicated]]
 """
 import argparse
 import json
@@ -35,7 +35,7 @@ def physics_args():
                                  hidden_channels=256, num_layers=2, link_batch_size=64 * 1024, predictor="mlp")
 
 
-def run(dtype, steps, warmup, emulate, split):
+def run(dtype, steps, warmup, emulate, split, shard_student=True):
     dev = torch.device("cuda", 0)
     a = physics_args()
     td = split[0]                                     # training_data: old nodes, old-old edges
@@ -53,9 +53,9 @@ def run(dtype, steps, warmup, emulate, split):
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
     row, col = td.edge_index
     eng = llp_engine.DistillEngine(model, pred, tpred, td.x.to(dev), t_h.to(dev), row.numpy(), col.numpy(), N, a,
-                                   opt, dtype=dtype, seed=11)
-    if emulate and os.environ.get("LLP_FB_SHARD") == "1":
-        eng.emulate_shard = (0, emulate)      # rank 0's slice of the node-sharded student (opt-in)
+                                   opt, dtype=dtype, seed=11, shard_student=shard_student)
+    if emulate and shard_student:
+        eng.emulate_shard = (0, emulate)      # rank 0's slice of the node-sharded student (default)
     pairs = td.edge_index.t().to(torch.int32).to(dev).contiguous()      # pos_train_edge (src/main.py:153)
     g = torch.Generator(device=dev)
     g.manual_seed(3)
@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--dtype", default="bf16,fp32")
     ap.add_argument("--emulate-ranks", type=int, default=0)
+    ap.add_argument("--replicated", action="store_true", help="every rank runs the student over all nodes")
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "llp_physics"))
     opt = ap.parse_args()
     t0 = time.perf_counter()
@@ -101,7 +102,7 @@ def main():
     out = {"workload": "coauthor-physics production LLP distillation (train, full-batch student)",
            "split_s": prep, "runs": []}
     for dt in opt.dtype.split(","):
-        out["runs"].append(run(dt, opt.steps, opt.warmup, opt.emulate_ranks, split))
+        out["runs"].append(run(dt, opt.steps, opt.warmup, opt.emulate_ranks, split, not opt.replicated))
         print(json.dumps(out["runs"][-1]), flush=True)
     print(json.dumps(out), flush=True)
 
