@@ -90,11 +90,11 @@ def cpu_baseline(data, a, t_h, init_params, B_full, P_full, sample_P=8192, steps
     for s in range(steps):
         anchors = rng.permutation(data.N)[:B]
         pos, neg = O.neighbor_samplers(rowptr, colv, anchors, data.N, a.rw_step, a.ps_method, a.ns_rate, a.hops,
-                                       seed=5, stream_base=16 * s)
+                                       seed=5, stream_base=O.STREAMS_PER_STEP * s)
         samples = torch.from_numpy(np.concatenate([pos, neg], 1))
         link = rng.integers(0, data.train_pairs.shape[0], P)
         edge = data.train_pairs[link].t()
-        negE = torch.from_numpy(O.randint_edges(data.N, P, seed=5, stream=16 * s + 15))
+        negE = torch.from_numpy(O.randint_edges(data.N, P, seed=5, stream=O.STREAMS_PER_STEP * s + O.RANDINT_STREAM))
         r = O.distill_losses_minibatch(x, t_h, samples, edge, negE, stu[0::2], stu[1::2], prd[0::2], prd[1::2],
                                        tp[0::2], tp[1::2], a)
         new, _, _ = O.distill_step(stu, prd, adam, r["loss"])

@@ -53,7 +53,7 @@ __global__ void neg_candidates(int64_t M, int enumerate_all, uint64_t population
   if (enumerate_all) {
     c = (uint64_t)(i % (int64_t)population);
   } else {
-    const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_offset);
+    const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * (*step_ctr) + stream_offset);
     const uint64_t lo = philox_u32(seed, stream, 2 * (uint64_t)i);
     const uint64_t hi = philox_u32(seed, stream, 2 * (uint64_t)i + 1);
     c = __umul64hi((hi << 32) | lo, population);

@@ -289,7 +289,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
   }
 
   // epilogue: acc[i][j][r] -> row m0 + wm*64 + i*16 + g*4 + r, col n0 + wn*64 + j*16 + li
-  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t col = n0 + wn * 64 + j * 16 + li;

@@ -257,7 +257,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
   }
 
   // ---------------- epilogue in registers: alpha, bias, ReLU, dropout
-  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
   uint4* stg = smem;   // staged C tile: row-major [256][EPI_ROW_U4] uint4
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn) {
@@ -366,7 +366,7 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
     for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(acc[jn][im]));
   return;
 #endif
-  const uint64_t dstream = drop ? (uint64_t)(16 * (*p.drop_ctr) + p.drop_stream) : 0;
+  const uint64_t dstream = drop ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
   // ReLU-backward bit mask: this thread's 16 bytes (one per store below) are loaded
   // first, so their latency hides under the staging work instead of under each store
   constexpr int chunks_per_row = TN / 8;
@@ -427,7 +427,9 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         v[r] = fwd ? acc[jn][im][r] + bv[r] : alpha * acc[jn][im][r] + bv[r];
-        if (relu) v[r] = fmaxf(v[r], 0.f);
+        // sign-bit ReLU, the lean epilogue's packed int16 max on the rounded pair: x if its sign
+        // bit is clear (a +NaN stays NaN), else 0 (-0 and -NaN too), so the two agree on every input
+        if (relu) v[r] = __float_as_int(v[r]) < 0 ? 0.f : v[r];
       }
       if (drop) {
         // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
@@ -570,8 +572,9 @@ __device__ __forceinline__ void load_cols16(const float* v, int64_t N, int64_t c
 // per-bit mask compares); here:
 //  * bias from registers loaded before the main loop, packed f32 adds (v_pk_add /
 //    v_pk_fma as before), ReLU AFTER rounding as a packed int16 max on the bf16
-//    pair (identical bits for every non-NaN value: a negative bf16 is a negative
-//    int16; a NaN now propagates like torch.relu instead of becoming 0);
+//    pair: the sign-bit rule of epilogue_t (x if the sign bit is clear, else 0), so
+//    the two epilogues agree on every input, NaNs included (+NaN stays NaN; -NaN
+//    becomes 0 where torch.relu would keep it);
 //  * LDS staging at per-thread bases + compile-time offsets;
 //  * stores from a uniform tile-corner base (SGPRs, advanced per 16 rows) plus one
 //    32-bit lane offset, no bounds tests;

@@ -43,6 +43,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+// Philox streams per training step: a draw of step s at offset o uses stream
+// LLP_STREAMS_PER_STEP * s + o (walks 0 .. rw_step-1, context negatives rw_step, PyG-dense
+// negatives STREAMS-2 under their own key, randint negatives STREAMS-1; dropout layers 1 + l
+// under per-module keys).  Must match oracle/llp_oracle.py:STREAMS_PER_STEP.
+constexpr int64_t LLP_STREAMS_PER_STEP = 64;
+
 // ---------------------------------------------------------------- Philox4x32-10
 // Counter = (idx>>2 lo, idx>>2 hi, stream lo, stream hi), key = seed; word idx&3.
 // Must match oracle/llp_oracle.py:philox_u32 bit for bit.

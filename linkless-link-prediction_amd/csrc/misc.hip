@@ -64,13 +64,13 @@ __global__ void sigmoid_bwd_kernel(int64_t n, const float* __restrict__ gprob, c
 unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384)); }
 
 // y = dropout(relu(x)) on a strided [rows, cols] view; draw #(r*cols + c) of
-// Philox stream 16*(*ctr) + stream_off, as the GEMM epilogue draws.
+// Philox stream LLP_STREAMS_PER_STEP*(*ctr) + stream_off, as the GEMM epilogue draws.
 template <typename T>
 __global__ void act_2d_kernel(int64_t rows, int64_t cols, const T* __restrict__ x, int64_t ldx, T* __restrict__ y,
                               int64_t ldy, int relu, uint32_t thr, float scale, uint64_t seed,
                               const int64_t* __restrict__ ctr, int64_t stream_off) {
   const int64_t n = rows * cols;
-  const uint64_t stream = ctr ? (uint64_t)(16 * (*ctr) + stream_off) : 0;
+  const uint64_t stream = ctr ? (uint64_t)(LLP_STREAMS_PER_STEP * (*ctr) + stream_off) : 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cols, c = i % cols;
     float v = ldv<T>(x, r * ldx + c);

@@ -22,7 +22,7 @@ __global__ void context_walk_kernel(const int32_t* __restrict__ rowptr, const in
   if (t >= B * n_walks) return;
   const int64_t b = t % B;
   const int w = (int)(t / B);
-  const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_offset + w);
+  const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * (*step_ctr) + stream_offset + w);
   const int64_t bg = b + b_offset;
   int32_t cur = start[b];
   int32_t* out = samples + b * C1;
@@ -43,7 +43,7 @@ __global__ void context_neg_kernel(int64_t B, int64_t b_offset, int64_t nneg, in
                                    int64_t stream_rel, int32_t* __restrict__ samples) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= B * nneg) return;
-  const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_rel);
+  const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * (*step_ctr) + stream_rel);
   const int64_t b = t / nneg, q = t % nneg;
   const uint32_t x = philox_u32(seed, stream, (uint64_t)((b + b_offset) * nneg + q));
   samples[b * C1 + col0 + q] = (int32_t)randint_index(x, num_nodes);
@@ -54,7 +54,7 @@ __global__ void randint_pairs_kernel(int64_t num_nodes, int64_t n, int64_t n_tot
                                      int32_t* __restrict__ out) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= 2 * n) return;
-  const uint64_t stream = (uint64_t)(16 * (*step_ctr) + stream_offset);
+  const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * (*step_ctr) + stream_offset);
   const int64_t side = t / n, i = t % n;
   const uint64_t draw = (uint64_t)(side * n_total + offset + i);
   out[t] = (int32_t)randint_index(philox_u32(seed, stream, draw), num_nodes);
@@ -115,7 +115,7 @@ __global__ void minibatch_sample_kernel(MbSample a) {
   if (t < nw) {   // walk w of anchor b (context_walk_kernel)
     const int64_t b = t % a.B;
     const int w = (int)(t / a.B);
-    const uint64_t stream = (uint64_t)(16 * step + a.stream_offset + w);
+    const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * step + a.stream_offset + w);
     const int64_t bg = b + a.b_offset;
     const int32_t anchor = a.start[b];
     int32_t cur = anchor;
@@ -136,7 +136,7 @@ __global__ void minibatch_sample_kernel(MbSample a) {
   }
   int64_t u = t - nw;
   if (u < nn) {   // context negative q of anchor b (context_neg_kernel)
-    const uint64_t stream = (uint64_t)(16 * step + a.stream_offset + a.rw_step);
+    const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * step + a.stream_offset + a.rw_step);
     const int64_t b = u / a.nneg, q = u % a.nneg;
     const uint32_t x = philox_u32(a.seed, stream, (uint64_t)((b + a.b_offset) * a.nneg + q));
     const int32_t v = (int32_t)randint_index(x, a.num_nodes);
@@ -149,7 +149,7 @@ __global__ void minibatch_sample_kernel(MbSample a) {
   }
   u -= nn;
   if (u < 2 * a.P) {   // label negative (randint_pairs_kernel) -> neg[side][i], target
-    const uint64_t stream = (uint64_t)(16 * step + a.neg_stream);
+    const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * step + a.neg_stream);
     const int64_t side = u / a.P, i = u % a.P;
     const uint64_t draw = (uint64_t)(side * a.P_total + a.p_offset + i);
     const int32_t v = (int32_t)randint_index(philox_u32(a.seed, stream, draw), a.num_nodes);

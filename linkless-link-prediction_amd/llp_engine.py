@@ -52,9 +52,17 @@ _GATHER_X = True
 # to the five separate kernels; False runs them separately)
 _FUSED_SAMPLE = True
 
+# Philox streams per step (csrc/llp_common.h LLP_STREAMS_PER_STEP): a draw of step s at
+# offset o uses stream STREAMS_PER_STEP * s + o.  Offsets under self.seed: the context
+# sampler's walks 0 .. rw_step-1 and its negatives rw_step; randint negatives S-1; PyG-dense
+# negatives S-2 under their own key; dropout 1 + layer under per-module keys.
+STREAMS_PER_STEP = 64
+RANDINT_STREAM = STREAMS_PER_STEP - 1
+DENSE_NEG_STREAM = STREAMS_PER_STEP - 2
+MAX_RW_STEP = STREAMS_PER_STEP - 3          # walks + negatives below DENSE_NEG_STREAM
 # dropout Philox keys (EngineBase._dropout): one per module, one stream per layer and step
 DROP_ENCODER, DROP_PREDICTOR, DROP_TEACHER_PRED = 0, 1, 2
-_MAX_DROPOUT_LAYERS = 15
+_MAX_DROPOUT_LAYERS = STREAMS_PER_STEP - 1
 
 _DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
 
@@ -325,7 +333,7 @@ class EngineBase:
         """Dropout draws of ``layer`` of ``module`` (DROP_ENCODER: the student MLP / the
         teacher's GNN, DROP_PREDICTOR: the trained LinkPredictor, DROP_TEACHER_PRED: the
         frozen teacher predictor).  Each module has its own Philox key and each layer its
-        own stream 16 * step_ctr + 1 + layer, so no two (module, layer) pairs and no two
+        own stream STREAMS_PER_STEP * step_ctr + 1 + layer, so no two (module, layer) pairs and no two
         steps share draws; the other seeds' streams (sampler, negatives) never meet them."""
         if p <= 0.0:
             return None
@@ -382,13 +390,14 @@ class EngineBase:
             negg = self._buf("neg_all", (2, max(P_total, 1)), torch.int32)
             cnt = self._buf("neg_count", (1,), torch.int32)
             ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
-            K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, 14, negg, cnt, ws)
+            K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
+                               cnt, ws)
             n_neg_total = int(cnt.item())
             lo = min(p_offset, n_neg_total)         # this shard's columns (all of them unsharded)
             hi = min(p_offset + P, n_neg_total)
             return negg[:, lo:hi], hi - lo, n_neg_total
         negb = self._buf("neg", (2, max(P, 1)), torch.int32)
-        K.randint_pairs(N, P, self.seed, self.step_ctr, 15, negb, n_total=P_total, offset=p_offset)
+        K.randint_pairs(N, P, self.seed, self.step_ctr, RANDINT_STREAM, negb, n_total=P_total, offset=p_offset)
         return negb, P, P_total
 
     def _predictor_forward(self, h, ia, ib, R2, logit, p_drop):
@@ -645,9 +654,10 @@ class DistillEngine(EngineBase):
         self.args = args
         self.N = int(num_nodes)
         # Philox streams per step under self.seed: the context sampler's walks 0..rw_step-1 and its
-        # negatives rw_step, randint negatives 15 (16 * step_ctr + offset)
-        if not 1 <= int(args.rw_step) < 15:
-            raise ValueError(f"rw_step={args.rw_step}: the context sampler has streams 0..14 per step (1 <= rw_step <= 14)")
+        # negatives rw_step (STREAMS_PER_STEP * step_ctr + offset)
+        if not 1 <= int(args.rw_step) <= MAX_RW_STEP:
+            raise ValueError(f"rw_step={args.rw_step}: the context sampler has {MAX_RW_STEP + 1} Philox streams per "
+                             f"step (1 <= rw_step <= {MAX_RW_STEP})")
 
         # ---------------- parameters
         self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
@@ -763,7 +773,8 @@ class DistillEngine(EngineBase):
             R2 = B * C + n_lab
             target = self._buf("target", (R1,), torch.int32)
             K.minibatch_sample(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
-                               self.seed, self.step_ctr, 0, pairs, link_ids, P, P_total, p_offset, 15, samp, negb,
+                               self.seed, self.step_ctr, 0, pairs, link_ids, P, P_total, p_offset, RANDINT_STREAM,
+                               samp, negb,
                                target, t_ia, t_ib, b_offset=b_offset)
             self._dbg_cut("sample")
         else:
@@ -1098,7 +1109,7 @@ class DistillEngine(EngineBase):
 
         ``anchors`` / ``link_ids`` must be persistent device buffers: refill them
         (e.g. ``anchors.copy_(node_perm[i*B:(i+1)*B])``) before each ``replay()``.
-        Every random draw is keyed by device counters (Philox stream = 16 *
+        Every random draw is keyed by device counters (Philox stream = STREAMS_PER_STEP *
         step_ctr + offset; Adam's step), so each replay is a fresh step.  Call
         after at least one eager step (kernels and buffers already loaded).
         With several ranks the step is captured as segments cut at the gradient

@@ -35,7 +35,7 @@ def test_neg_sample_dense_bit_exact(N, n_und, num_neg):
     keys, n_idx = O.dense_neg_keys(ei, N)
     ss = O.dense_neg_sample_size(n_idx, N, num_neg)
     seed, step, off = 77, 3, 14
-    exp = O.negative_sampling_dense_philox(ei, N, num_neg, seed, 16 * step + off)
+    exp = O.negative_sampling_dense_philox(ei, N, num_neg, seed, O.STREAMS_PER_STEP * step + off)
     pop = N * (N - 1)
     M = pop if pop <= ss else 3 * ss
     out = torch.full((2, num_neg), -1, dtype=torch.int32, device=DEV)

@@ -136,13 +136,13 @@ def test_gemm_nt_head_fused(M, N, Kd):
     assert torch.equal(hpart, hpart2)
 
 
-@pytest.mark.skipif(os.environ.get("LLP_TEST_HEAD_LEAN") != "1",
-                    reason="opt-in head epilogue (LLP_GEMM_HEAD_LEAN) not yet run on the GPU; LLP_TEST_HEAD_LEAN=1")
 @pytest.mark.parametrize("M,N,Kd", [(1000, 1024, 128), (513, 256, 256), (4096, 1024, 1024)])
 def test_gemm_nt_head_lean(M, N, Kd):
-    """The opt-in lean head epilogue (gemm256.hip epilogue_lean_head): C bit-identical
-    to the default head epilogue; the head dot over the ROUNDED bf16 outputs, within
-    f32 summation-order tolerance of bf16(y) @ hw; deterministic with and without C."""
+    """The head epilogue over the staged bf16 outputs (gemm256.hip epilogue_lean_head, taken
+    when N % 256 == 0 and C is 16-B aligned with ldc % 8 == 0): C bit-identical to the
+    generic head epilogue (forced here by a C row stride of N + 4); the head dot over the
+    ROUNDED bf16 outputs, within f32 summation-order tolerance of bf16(y) @ hw;
+    deterministic with and without C."""
     k = K()
     g = torch.Generator().manual_seed(M + 1)
     A = (torch.randn(M, Kd, generator=g) * 0.5).to(DEV, torch.bfloat16)
@@ -150,24 +150,48 @@ def test_gemm_nt_head_lean(M, N, Kd):
     b = torch.randn(N, generator=g).to(DEV)
     hw = torch.randn(N, generator=g).to(DEV)
     parts = k.head_parts(N)
-    C0 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C0 = torch.empty(M, N + 4, device=DEV, dtype=torch.bfloat16)[:, :N]      # generic epilogue
     k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C0, hw, torch.empty(parts, M, device=DEV), bias=b,
                    act=k.ACT_RELU)
-    os.environ["LLP_GEMM_HEAD_LEAN"] = "1"
-    try:
-        C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        h1 = torch.empty(parts, M, device=DEV)
-        k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C1, hw, h1, bias=b, act=k.ACT_RELU)
-        h2 = torch.empty(parts, M, device=DEV)
-        k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, None, hw, h2, bias=b, act=k.ACT_RELU)
-        torch.cuda.synchronize()
-    finally:
-        del os.environ["LLP_GEMM_HEAD_LEAN"]
+    C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)                  # lean head epilogue
+    h1 = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C1, hw, h1, bias=b, act=k.ACT_RELU)
+    h2 = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, None, hw, h2, bias=b, act=k.ACT_RELU)
+    torch.cuda.synchronize()
     assert torch.equal(C1, C0)
     assert torch.equal(h1, h2)
     ref = C0.float() @ hw
     got = h1.sum(0)
     assert torch.allclose(got, ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item())), (got - ref).abs().max()
+
+
+def test_gemm_nt_relu_lean_and_generic_agree_with_nan():
+    """ReLU forward: full 256 x 256 tiles take the lean epilogue (int16 max on the rounded
+    pair), partial tiles the generic one (f32); both follow the sign-bit rule, so the same
+    rows give the same outputs in a full and in a partial tile, NaN rows included."""
+    k = K()
+    g = torch.Generator().manual_seed(7)
+    M, N, Kd = 256, 256, 128
+    A = (torch.randn(M, Kd, generator=g) * 0.5)
+    A[3, 5] = float("nan")
+    A[77, 0] = -float("nan")
+    A[130, :] = float("inf")
+    A = A.to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    full = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, full, k.LLP_BF16, bias=b, act=k.ACT_RELU)
+    Mp = 200
+    part = torch.empty(Mp, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt(k.operand(A[:Mp]), k.operand(W), Mp, N, Kd, part, k.LLP_BF16, bias=b, act=k.ACT_RELU)
+    torch.cuda.synchronize()
+    f, p_ = full[:Mp].float().cpu(), part.float().cpu()
+    assert torch.equal(torch.isnan(f), torch.isnan(p_))
+    ok = ~torch.isnan(f)
+    assert torch.equal(f[ok], p_[ok])
+    assert bool((f[ok] >= 0).all())
+    assert bool(torch.isnan(f[3]).any() or (f[3] == 0).all())
 
 
 def test_gemm_nt_bf16_dropout_matches_fp32_mask():
@@ -364,7 +388,7 @@ def test_context_sampler_bit_exact(ps, rw_step, hops, ns_rate, sorted_):
     k.context_sampler(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(col).to(DEV), N,
                       torch.from_numpy(start).to(DEV), 123, ps, rw_step, hops, ns_rate, 99, ctr, 0, out, b_offset=0)
     pos, neg = O.neighbor_samplers(rowptr.astype(np.int64), col.astype(np.int64), start, N, rw_step, ps, ns_rate,
-                                   hops, seed=99, stream_base=16 * 7)
+                                   hops, seed=99, stream_base=O.STREAMS_PER_STEP * 7)
     ref = np.concatenate([pos, neg], 1)
     assert np.array_equal(out.cpu().numpy(), ref)
     # shard invariance: anchors [60, 123) drawn by a second "rank" match
@@ -399,11 +423,11 @@ def test_minibatch_sample_equals_separate_kernels(ps, rw_step, hops, ns_rate, b_
     t1, t2 = (torch.full((R1,), -1, dtype=torch.int32, device=DEV) for _ in range(2))
     a1, a2, b1, b2 = (torch.full((B * C,), -1, dtype=torch.int32, device=DEV) for _ in range(4))
     k.context_sampler(rowptr, col, N, start, B, ps, rw_step, hops, ns_rate, 31, ctr, 0, s1, b_offset=b_off)
-    k.randint_pairs(N, P, 31, ctr, 15, n1, n_total=P_total, offset=p_off)
+    k.randint_pairs(N, P, 31, ctr, O.RANDINT_STREAM, n1, n_total=P_total, offset=p_off)
     k.build_targets(B, C1, s1, pairs, perm, None, 0, P, n1, t1)
     k.pair_index_from_samples(B, C, s1, a1, b1)
     k.minibatch_sample(rowptr, col, N, start, B, ps, rw_step, hops, ns_rate, 31, ctr, 0, pairs, perm, P, P_total,
-                       p_off, 15, s2, n2, t2, a2, b2, b_offset=b_off)
+                       p_off, O.RANDINT_STREAM, s2, n2, t2, a2, b2, b_offset=b_off)
     for x, y in ((s1, s2), (n1, n2), (t1, t2), (a1, a2), (b1, b2)):
         assert torch.equal(x, y)
 
@@ -422,11 +446,11 @@ def test_randint_pairs_bit_exact_and_sharded():
     k = K()
     ctr = torch.tensor([3], dtype=torch.int64, device=DEV)
     out = torch.empty(2, 1000, dtype=torch.int32, device=DEV)
-    k.randint_pairs(12345, 1000, 77, ctr, 15, out)
-    ref = O.randint_edges(12345, 1000, seed=77, stream=16 * 3 + 15)
+    k.randint_pairs(12345, 1000, 77, ctr, O.RANDINT_STREAM, out)
+    ref = O.randint_edges(12345, 1000, seed=77, stream=O.STREAMS_PER_STEP * 3 + O.RANDINT_STREAM)
     assert np.array_equal(out.cpu().numpy(), ref)
     part = torch.empty(2, 300, dtype=torch.int32, device=DEV)
-    k.randint_pairs(12345, 300, 77, ctr, 15, part, n_total=1000, offset=500)
+    k.randint_pairs(12345, 300, 77, ctr, O.RANDINT_STREAM, part, n_total=1000, offset=500)
     assert np.array_equal(part.cpu().numpy(), ref[:, 500:800])
 
 

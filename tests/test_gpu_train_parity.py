@@ -86,7 +86,7 @@ def test_cora_training_tracks_oracle_on_logits_and_hits():
         node_perm = torch.randperm(N, generator=g)[:B]
         link_perm = torch.randperm(E, generator=g)[:P]
         pos, negs = O.neighbor_samplers(rowptr, colc, node_perm.numpy(), N, args.rw_step, "nb", args.ns_rate,
-                                        args.hops, 99, 16 * epoch)
+                                        args.hops, 99, O.STREAMS_PER_STEP * epoch)
         samples = torch.from_numpy(np.concatenate([pos, negs], 1)).long()
         neg = torch.randint(0, N, (2, P), generator=g)
         # oracle step

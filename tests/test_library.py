@@ -57,3 +57,17 @@ def test_binding_loads_without_gpu():
     # argument validation happens before any device call
     assert L.llp_llp_loss_workspace_bytes(10, 20) > 0
     assert L.llp_gemm_tn_workspace_bytes(1, 1000, 64, 64) >= 64 * 64 * 4
+
+
+def test_philox_stream_layout_agrees():
+    """One stream layout per step in the kernels, the engine and the oracle, wide enough
+    for the reference CLI's rw_step (any int; its scripts use up to 3) well past 14."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
+    import llp_engine
+    from oracle import llp_oracle as O
+    txt = open(os.path.join(REPO, "linkless-link-prediction_amd", "csrc", "llp_common.h")).read()
+    m = re.search(r"LLP_STREAMS_PER_STEP\s*=\s*(\d+)", txt)
+    assert m and int(m.group(1)) == llp_engine.STREAMS_PER_STEP == O.STREAMS_PER_STEP
+    assert llp_engine.RANDINT_STREAM == O.RANDINT_STREAM and llp_engine.DENSE_NEG_STREAM == O.DENSE_NEG_STREAM
+    assert llp_engine.MAX_RW_STEP + 1 < llp_engine.DENSE_NEG_STREAM and llp_engine.MAX_RW_STEP >= 60

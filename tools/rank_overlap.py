@@ -29,7 +29,7 @@ links = rng.permutation(E_train)[:P]
 pairs = data.train_pairs.numpy()
 pos_s, neg_s = O.neighbor_samplers(rowptr, col, anchors, N, 3, "nb", 3, 3, seed=123, stream_base=0)
 samples = np.concatenate([pos_s, neg_s], 1)                                                        # [B, 1 + 36]
-neg = O.randint_edges(N, P, seed=123, stream=15)                                                   # [2, P]
+neg = O.randint_edges(N, P, seed=123, stream=O.RANDINT_STREAM)                                                   # [2, P]
 
 
 def target_rows(b0, b1, p0, p1):
