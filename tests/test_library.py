@@ -70,4 +70,4 @@ def test_philox_stream_layout_agrees():
     m = re.search(r"LLP_STREAMS_PER_STEP\s*=\s*(\d+)", txt)
     assert m and int(m.group(1)) == llp_engine.STREAMS_PER_STEP == O.STREAMS_PER_STEP
     assert llp_engine.RANDINT_STREAM == O.RANDINT_STREAM and llp_engine.DENSE_NEG_STREAM == O.DENSE_NEG_STREAM
-    assert llp_engine.MAX_RW_STEP + 1 < llp_engine.DENSE_NEG_STREAM and llp_engine.MAX_RW_STEP >= 60
+    assert llp_engine.MAX_RW_STEP < llp_engine.DENSE_NEG_STREAM and llp_engine.MAX_RW_STEP >= 60   # negatives at rw_step
