@@ -9,6 +9,8 @@
 // once: HBM traffic = E*F*s (neighbours) + 4E (col) + 4(N+1) (rowptr) + N*F*s.
 #include "llp_common.h"
 
+#include <type_traits>
+
 namespace {
 
 template <typename T>
@@ -130,6 +132,63 @@ __global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_
   }
 }
 
+// Rows of NCH <= 64 16-B chunks: RPW = 64 / NCH destination rows per wave, one lane per
+// chunk of its row, each lane walking the row's neighbours in order with UNR row loads in
+// flight (the last round predicated).  Against csr_agg_vec_kernel (one row per wave, its
+// neighbours dealt to lane groups and the groups summed through LDS) a wave keeps RPW rows'
+// neighbour loads in flight and needs no reduction: bf16 F=128 (256-B rows) takes 4 rows
+// per wave.  Per-row accumulation in neighbour order (deterministic).
+template <typename T, int NCH, int UNR>
+__global__ __launch_bounds__(256) void csr_agg_rows_kernel(int64_t n_rows, const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ col, const T* __restrict__ x,
+                                                           int64_t ldx, const float* __restrict__ inv_deg, int mode,
+                                                           const float* __restrict__ bias, T* __restrict__ out,
+                                                           int64_t ldo, int accumulate) {
+  constexpr int E = V16<T>::E;
+  constexpr int RPW = 64 / NCH;
+  const int lane = threadIdx.x & 63;
+  const int rl = lane / NCH, ch = lane % NCH;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + rl;
+  if (row >= n_rows) return;
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  const T* xc = x + ch * E;
+  for (int64_t e = beg; e < end; e += UNR) {
+    int32_t j[UNR];
+    bool v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      v[k] = e + k < end;
+      j[k] = v[k] ? col[e + k] : 0;
+    }
+    uint4 r[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k)
+      r[k] = v[k] ? *reinterpret_cast<const uint4*>(xc + (int64_t)j[k] * ldx) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < UNR; ++k)
+      if (v[k]) V16<T>::add(acc, r[k], mode ? inv_deg[j[k]] : 1.f);
+  }
+  const float sc = mode == 0 ? 1.f / (float)max(end - beg, (int64_t)1) : (mode == 2 ? inv_deg[row] : 1.f);
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] *= sc;
+  if (bias)
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += bias[ch * E + i];
+  uint4* dst = reinterpret_cast<uint4*>(out + row * ldo + ch * E);
+  if (accumulate) {
+    float prev[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) prev[i] = 0.f;
+    V16<T>::add(prev, *dst, 1.f);
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += prev[i];
+  }
+  *dst = V16<T>::pack(acc);
+}
+
 // Scalar fallback for feature widths that are not a multiple of the vector.
 template <typename T>
 __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int64_t F,
@@ -175,6 +234,29 @@ static int csr_aggregate_launch(int dtype, int64_t n_rows, int64_t F, const int3
   const bool vec = (F % E == 0) && (ldx % E == 0) && (ldo % E == 0) && ((uintptr_t)x % 16 == 0) &&
                    ((uintptr_t)out % 16 == 0);
   dim3 grid(ceil_div_u(n_rows, 4));
+#ifdef LLP_AGG_GROUPS   // A/B build: csr_agg_vec_kernel for every width
+  const int64_t nch = 0;
+#else
+  const int64_t nch = vec ? F / E : 0;
+#endif
+  if (nch == 8 || nch == 16 || nch == 32 || nch == 64) {   // rows of 8..64 chunks: rows per wave
+    const dim3 g2(ceil_div_u(n_rows, 4 * (64 / nch)));
+    auto go = [&](auto kern, auto* xx, auto* oo) {
+      hipLaunchKernelGGL(kern, g2, dim3(256), 0, s, n_rows, rowptr, col, xx, ldx, inv_deg, mode, bias, oo, ldo,
+                         accumulate);
+    };
+    auto pick = [&](auto* xx, auto* oo) {
+      using TT = std::remove_const_t<std::remove_pointer_t<decltype(xx)>>;
+      if (nch == 8) go(csr_agg_rows_kernel<TT, 8, 4>, xx, oo);
+      else if (nch == 16) go(csr_agg_rows_kernel<TT, 16, 4>, xx, oo);
+      else if (nch == 32) go(csr_agg_rows_kernel<TT, 32, 4>, xx, oo);
+      else go(csr_agg_rows_kernel<TT, 64, 4>, xx, oo);
+    };
+    if (dtype == LLP_BF16) pick((const bf16_t*)x, (bf16_t*)out);
+    else pick((const float*)x, (float*)out);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
   if (dtype == LLP_BF16) {
     if (vec)
       hipLaunchKernelGGL(csr_agg_vec_kernel<bf16_t>, grid, dim3(256), 0, s, n_rows, F, rowptr, col, (const bf16_t*)x,

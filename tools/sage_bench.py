@@ -22,12 +22,50 @@ import llp_teacher  # noqa: E402
 import models  # noqa: E402
 
 
+def agg_only(iters):
+    """Each configuration's launches in a fixed order: tools/pmc_kernels.py matches the
+    csr_agg dispatches of a PMC pass to it by position."""
+    dev = torch.device("cuda", 0)
+    data = llp_data.synthetic_collab(seed=0, with_eval=False)
+    N = data.N
+    g = llp_sage.Graph(data.edge_index, N, dev)
+    E = g.num_edges
+    plan = []
+    for dts in ("fp32", "bf16"):
+        dt = torch.float32 if dts == "fp32" else torch.bfloat16
+        es = 4 if dts == "fp32" else 2
+        for F_ in (128, 256):
+            x = torch.randn(N, F_, device=dev).to(dt)
+            out = torch.empty(N, F_, device=dev, dtype=dt)
+            for mode, (rp, cl, w) in (("fwd", (g.rowptr, g.col, None)), ("bwd", (g.rowptr_t, g.col_t, g.inv_deg))):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for _ in range(3):
+                    K.csr_aggregate(N, F_, rp, cl, x, w, 0 if mode == "fwd" else 1, out)
+                s.record()
+                for _ in range(iters):
+                    K.csr_aggregate(N, F_, rp, cl, x, w, 0 if mode == "fwd" else 1, out)
+                e.record()
+                torch.cuda.synchronize()
+                ms = s.elapsed_time(e) / iters
+                nbytes = E * F_ * es + 4 * E + 4 * (N + 1) + N * F_ * es + (4 * E if mode == "bwd" else 0)
+                compulsory = N * F_ * es + 4 * E + 4 * (N + 1) + N * F_ * es + (4 * N if mode == "bwd" else 0)
+                plan.append({"dtype": dts, "F": F_, "mode": mode, "launches": 3 + iters, "ms": ms,
+                             "algorithmic_bytes": nbytes, "compulsory_bytes": compulsory,
+                             "algorithmic_GBs": nbytes / (ms * 1e-3) / 1e9})
+    print(json.dumps({"N": N, "E": E, "plan": plan}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--agg-only", action="store_true",
+                    help="every aggregate configuration (fp32 / bf16, F 128 / 256, fwd / bwd), 3 warm-up + --iters "
+                         "launches each, in the printed order (rocprofv3 --pmc passes), then exit")
     opt = ap.parse_args()
+    if opt.agg_only:
+        return agg_only(opt.iters)
     dev = torch.device("cuda", 0)
     dt = torch.float32 if opt.dtype == "fp32" else torch.bfloat16
     data = llp_data.synthetic_collab(seed=0, with_eval=False)
