@@ -141,8 +141,9 @@ def test_gemm_nt_head_fused(M, N, Kd):
 @pytest.mark.parametrize("M,N,Kd", [(1000, 1024, 128), (513, 256, 256), (4096, 1024, 1024)])
 def test_gemm_nt_head_lean(M, N, Kd):
     """The head epilogue over the staged bf16 outputs (gemm256.hip epilogue_lean_head, taken
-    when N % 256 == 0 and C is 16-B aligned with ldc % 8 == 0): C bit-identical to the
-    generic head epilogue (forced here by a C row stride of N + 4); the head dot over the
+    when N % 256 == 0, the head weights are 16-B aligned and C is 16-B aligned with ldc % 8
+    == 0): C bit-identical to the generic head epilogue (forced here by misaligned head
+    weights); the head dot over the
     ROUNDED bf16 outputs, within f32 summation-order tolerance of bf16(y) @ hw;
     deterministic with and without C."""
     k = K()
@@ -152,8 +153,10 @@ def test_gemm_nt_head_lean(M, N, Kd):
     b = torch.randn(N, generator=g).to(DEV)
     hw = torch.randn(N, generator=g).to(DEV)
     parts = k.head_parts(N)
-    C0 = torch.empty(M, N + 4, device=DEV, dtype=torch.bfloat16)[:, :N]      # generic epilogue
-    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C0, hw, torch.empty(parts, M, device=DEV), bias=b,
+    hw_odd = torch.empty(N + 1, device=DEV)[1:]          # head weights off 16-B alignment: generic epilogue
+    hw_odd.copy_(hw)
+    C0 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C0, hw_odd, torch.empty(parts, M, device=DEV), bias=b,
                    act=k.ACT_RELU)
     C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)                  # lean head epilogue
     h1 = torch.empty(parts, M, device=DEV)
