@@ -170,31 +170,52 @@ def evaluate(model, pred, data, dev):
             "hits_note": "after the timed steps from random init on synthetic data (not a converged model)"}
 
 
+SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_sage.json")
+
+
 def sage_aggregate(data, dev):
-    """SAGE teacher's CSR mean aggregate (a11) at the collab shape, F=128 f32,
-    event-timed: algorithmic bytes E*F*4 + 4E + 4(N+1) + N*F*4 per launch."""
+    """SAGE teacher's CSR mean aggregate (a11, src/sageconv_updated.py:65-81 / PyG SAGEConv mean)
+    at the collab shape, forward, F = 128 and 256, fp32 and bf16, event-timed live.
+    algorithmic bytes E*F*s + 4E + 4(N+1) + N*F*s (every neighbour row from memory, SURVEY
+    §8d); compulsory bytes: x, col, rowptr read once, out written once; traffic: beyond-L2
+    counter bytes per launch from the committed PMC passes (profiles/r03_pmc_sage.json:
+    2 x FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits included, so an upper bound on HBM
+    bytes).  frac = traffic / time / 8 TB/s."""
     import llp_hip as K
     import llp_sage
     g = llp_sage.Graph(data.edge_index, data.N, dev)
-    x = data.x.to(dev)
-    out = torch.empty_like(x)
-    F_ = x.shape[1]
-    for _ in range(3):
-        K.csr_aggregate(data.N, F_, g.rowptr, g.col, x, None, 0, out)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n = 20
-    s.record()
-    for _ in range(n):
-        K.csr_aggregate(data.N, F_, g.rowptr, g.col, x, None, 0, out)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / n
-    nbytes = g.num_edges * F_ * 4 + 4 * g.num_edges + 4 * (data.N + 1) + data.N * F_ * 4
-    gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"kernel": "csr_agg_vec_kernel<float> fwd", "N": data.N, "E": g.num_edges, "F": F_, "ms": ms,
-            "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-            "algorithmic_bytes": nbytes,
-            "note": "x (121 MB) stays resident in the 256 MiB Infinity Cache across the ~10 neighbour re-reads"}
+    try:
+        with open(SAGE_PMC_FILE) as f:
+            pmc = {(c["dtype"], c["F"], c["mode"]): c["counter_bytes"] for c in json.load(f)["configs"]}
+    except (OSError, ValueError, KeyError):
+        pmc = {}
+    out = []
+    for dts, dt, es in (("fp32", torch.float32, 4), ("bf16", torch.bfloat16, 2)):
+        for F_ in (128, 256):
+            x = torch.randn(data.N, F_, device=dev).to(dt)
+            y = torch.empty_like(x)
+            for _ in range(3):
+                K.csr_aggregate(data.N, F_, g.rowptr, g.col, x, None, 0, y)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 20
+            s.record()
+            for _ in range(n):
+                K.csr_aggregate(data.N, F_, g.rowptr, g.col, x, None, 0, y)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / n
+            algo = g.num_edges * F_ * es + 4 * g.num_edges + 4 * (data.N + 1) + data.N * F_ * es
+            comp = 2 * data.N * F_ * es + 4 * g.num_edges + 4 * (data.N + 1)
+            traffic = pmc.get((dts, F_, "fwd"))
+            tb = (traffic if traffic else algo) / (ms * 1e-3)
+            out.append({"kernel": "csr_agg_rows_kernel fwd", "dtype": dts, "F": F_, "N": data.N, "E": g.num_edges,
+                        "ms": ms, "achieved": tb / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": tb / 1e9 / PEAK_HBM_GBS, "traffic": traffic, "algorithmic_bytes": algo,
+                        "algorithmic_frac": algo / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "compulsory_bytes": comp,
+                        "compulsory_frac": comp / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                        "note": "achieved/frac on PMC beyond-L2 bytes (Infinity-Cache hits counted: x fits the "
+                                "256 MiB cache, so most neighbour re-reads are cache hits, not HBM reads)"})
+    return out
 
 
 def sage_teacher_step(data, dev, dtype, steps=5):

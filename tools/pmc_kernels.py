@@ -53,9 +53,14 @@ def trace(root):
 
 
 def per_kernel(fetch, write, match):
-    """Counter bytes per dispatch of kernels whose name contains ``match``, in dispatch order."""
+    """Counter bytes per dispatch of kernels whose name contains ``match``, in dispatch order
+    (FETCH_SIZE / WRITE_SIZE are reported in KiB)."""
     ids = sorted(k for k, v in fetch.items() if match in v[0])
-    return [(fetch[k][0], 2 * fetch[k][1] + write.get(k, ("", 0.0, 0))[1], fetch[k][2]) for k in ids]
+    return [(fetch[k][0], 1024.0 * (2 * fetch[k][1] + write.get(k, ("", 0.0, 0))[1]), fetch[k][2]) for k in ids]
+
+
+def short(name):
+    return name.split("(")[0].split("::")[-1] if "::" in name.split("(")[0] else name.split("(")[0]
 
 
 def entry(name, algo, cbytes, ns, note=""):
@@ -94,7 +99,7 @@ def step(a):
         if not cb:
             continue
         durs = [d for n, d in tr if frag in n][a.skip:] or [x[2] for x in cb]
-        res.append(entry(cb[0][0].split("(")[0], algo, [x[1] for x in cb], sum(durs) / len(durs), what))
+        res.append(entry(short(cb[0][0]) + "<" + cb[0][0].split("<", 1)[1].split(">")[0] + ">", algo, [x[1] for x in cb], sum(durs) / len(durs), what))
     out = {"workload": "ogbl-collab LLP step, bf16", "B": B, "C": C, "P": P, "H": H, "unique_nodes": U,
            "bytes": "counter = 2 x FETCH_SIZE + WRITE_SIZE per dispatch (beyond-L2, MALL hits included)",
            "durations": "kernel trace of the same command (eager steps)" if tr else "PMC pass timestamps",
@@ -117,7 +122,7 @@ def sage(a):
     for p in plan["plan"]:
         seg = cb[i:i + p["launches"]][3:]     # the 3 warm-up launches of each configuration excluded
         i += p["launches"]
-        name = seg[0][0].split("(")[0] if seg else "?"
+        name = short(seg[0][0]) + "<" + seg[0][0].split("<", 1)[1].split(">")[0] + ">" if seg else "?"
         e = entry(name, p["algorithmic_bytes"], [x[1] for x in seg], p["ms"] * 1e6,
                   "x rows re-read ~E/N times; the Infinity Cache serves most of them")
         e.update({"dtype": p["dtype"], "F": p["F"], "mode": p["mode"], "compulsory_bytes": p["compulsory_bytes"],
