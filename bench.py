@@ -248,6 +248,45 @@ def sage_teacher_step(data, dev, dtype, steps=5):
                       "65,536 positives"}
 
 
+def fp32_step(data, a, t_h, init, dev, steps=3):
+    """The same collab step in fp32, the reference's arithmetic (fp32 GEMMs on the f32
+    MFMA path, gemm.hip): a fresh engine from the same initial weights, one warm-up and
+    ``steps`` timed eager steps."""
+    import llp_engine
+    import models
+    N, F, H, L = data.N, data.F, a.hidden_channels, a.num_layers
+    model = models.MLP(L, F, H, H, a.dropout).to(dev)
+    pred = models.LinkPredictor("mlp", H, H, 1, L, a.dropout).to(dev)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, a.dropout).to(dev)
+    for p, p0 in zip(list(model.parameters()) + list(pred.parameters()) + list(tpred.parameters()),
+                     init[0] + init[1] + init[2]):
+        p.data.copy_(p0)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    optim = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
+    eng = llp_engine.DistillEngine(model, pred, tpred, data.x.to(dev), t_h.to(dev), data.edge_index[0].numpy(),
+                                   data.edge_index[1].numpy(), N, a, optim, dtype="fp32", seed=123)
+    pairs = data.train_pairs.to(torch.int32).to(dev).contiguous()
+    E = data.train_pairs.shape[0]
+    P = a.link_batch_size
+    B = int(N / (E / P))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2)
+    link_perm = torch.randperm(E, generator=gen, device=dev).to(torch.int32)
+    node_perm = torch.randperm(N, generator=gen, device=dev).to(torch.int32)
+    eng.step_minibatch(node_perm[:B], link_perm[:P], pairs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(1, steps + 1):
+        eng.step_minibatch(node_perm[s * B:(s + 1) * B], link_perm[s * P:(s + 1) * P], pairs)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    del eng
+    torch.cuda.empty_cache()
+    return {"dtype": "fp32", "ms_per_step": dt * 1e3, "edges_per_s": P / dt, "steps": steps,
+            "note": "the reference's arithmetic; same configuration, eager steps"}
+
+
 def physics_production_step(dtype):
     """BASELINE configs[3] at one GPU: the full-batch train() step at the
     coauthor-physics production shape (tools/physics_bench.py), plus rank 0's
@@ -285,6 +324,7 @@ def main():
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-sage", action="store_true")
     ap.add_argument("--no-physics", action="store_true")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 collab step leg")
     ap.add_argument("--no-shard8", action="store_true", help="skip the 8-rank per-rank shard leg")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single GPU: run only rank 0's shard of an R-rank job (no collective) and report "
@@ -477,6 +517,8 @@ def main():
                 shard(3 + s)
             torch.cuda.synchronize()
             res["rank0_ms_per_step_at_8_ranks"] = (time.perf_counter() - t1) / 20 * 1e3
+        if world == 1 and opt.dtype == "bf16" and not opt.no_fp32:
+            res["fp32_step"] = fp32_step(data, a, t_h, init, dev)
         if not opt.no_sage:
             res["sage_aggregate"] = sage_aggregate(data, dev)
             res["sage_teacher_step"] = sage_teacher_step(data, dev, opt.dtype)
