@@ -89,10 +89,11 @@ def train(dtype, data, epochs, link_batch, seed=0, hidden=1024, eval_every=1):
     return {"dtype": dtype, "seconds": time.perf_counter() - t0, "B": B, "P": P, "history": hist}
 
 
-def compare(scale=0.1, link_batch=8192, epochs=8, seed=0, hidden=1024):
+def compare(scale=0.1, link_batch=8192, epochs=8, seed=0, hidden=1024, eval_every=1):
     import llp_data
     data = llp_data.synthetic_collab(seed=0, scale=scale, with_eval=True)
-    runs = {dt: train(dt, data, epochs, link_batch, seed=seed, hidden=hidden) for dt in ("fp32", "bf16")}
+    runs = {dt: train(dt, data, epochs, link_batch, seed=seed, hidden=hidden, eval_every=eval_every)
+            for dt in ("fp32", "bf16")}
     last = {dt: runs[dt]["history"][-1]["hits"] for dt in runs}
     diff = {f"Hits@{k}": {s: last["bf16"][f"Hits@{k}"][s] - last["fp32"][f"Hits@{k}"][s] for s in ("valid", "test")}
             for k in KS}
@@ -108,9 +109,10 @@ def main():
     ap.add_argument("--epochs", type=int, default=8)
     ap.add_argument("--seeds", type=int, default=1)
     ap.add_argument("--hidden", type=int, default=1024)
+    ap.add_argument("--eval-every", type=int, default=1)
     opt = ap.parse_args()
     for s in range(opt.seeds):
-        r = compare(opt.scale, opt.link_batch, opt.epochs, seed=s, hidden=opt.hidden)
+        r = compare(opt.scale, opt.link_batch, opt.epochs, seed=s, hidden=opt.hidden, eval_every=opt.eval_every)
         print(json.dumps(r), flush=True)
 
 
