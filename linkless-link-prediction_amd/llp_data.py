@@ -51,18 +51,19 @@ def interleave(pairs: np.ndarray) -> np.ndarray:
     return np.stack([pairs, pairs[:, ::-1]], 1).reshape(-1, 2).T.copy()
 
 
-def synthetic_collab(seed: int = 0, scale: float = 1.0, with_eval: bool = True, F: int = None):
+def synthetic_collab(seed: int = 0, scale: float = 1.0, with_eval: bool = True, F: int = None, n_comm: int = None):
     """Returns a namespace with x (f32 [N,F]), edge_index (int64 [2,E]),
-    train pairs (int64 [E_train,2]) and split_edge-style valid/test dicts."""
+    train pairs (int64 [E_train,2]) and split_edge-style valid/test dicts.
+    n_comm: planted communities (default 1,000 x scale, at least 10)."""
     rng = np.random.default_rng(seed)
     N = int(COLLAB["N"] * scale)
     Fd = COLLAB["F"] if F is None else F
     E = int(COLLAB["E_train"] * scale)
-    pairs = planted_pairs(N, E, max(10, int(1000 * scale)), 0.9, 0.05, rng)
+    n_comm = max(10, int(1000 * scale)) if n_comm is None else int(n_comm)
+    pairs = planted_pairs(N, E, n_comm, 0.9, 0.05, rng)
     comm = planted_pairs.last_comm
     # features carry the planted community (centroid + noise), so the student
     # MLP can learn the link structure from x as it does from real features
-    n_comm = max(10, int(1000 * scale))
     cent = rng.standard_normal((n_comm, Fd), dtype=np.float32)
     x = (0.07 * (cent[comm] + rng.standard_normal((N, Fd), dtype=np.float32))).astype(np.float32)
     d = types.SimpleNamespace(N=N, F=Fd, x=torch.from_numpy(x), train_pairs=torch.from_numpy(pairs),
@@ -70,7 +71,7 @@ def synthetic_collab(seed: int = 0, scale: float = 1.0, with_eval: bool = True, 
     if with_eval:
         nv, nt, nn_ = (int(COLLAB[k] * scale) for k in ("n_valid", "n_test", "n_neg"))
         # held-out positives from the SAME planted communities as the training graph
-        held = planted_pairs(N, nv + nt, max(10, int(1000 * scale)), 0.9, 0.0, rng, comm=comm)
+        held = planted_pairs(N, nv + nt, n_comm, 0.9, 0.0, rng, comm=comm)
         d.split_edge = {
             "train": {"edge": d.train_pairs},
             "valid": {"edge": torch.from_numpy(held[:nv]),

@@ -89,9 +89,9 @@ def train(dtype, data, epochs, link_batch, seed=0, hidden=1024, eval_every=1):
     return {"dtype": dtype, "seconds": time.perf_counter() - t0, "B": B, "P": P, "history": hist}
 
 
-def compare(scale=0.1, link_batch=8192, epochs=8, seed=0, hidden=1024, eval_every=1):
+def compare(scale=0.1, link_batch=8192, epochs=8, seed=0, hidden=1024, eval_every=1, communities=None):
     import llp_data
-    data = llp_data.synthetic_collab(seed=0, scale=scale, with_eval=True)
+    data = llp_data.synthetic_collab(seed=0, scale=scale, with_eval=True, n_comm=communities)
     runs = {dt: train(dt, data, epochs, link_batch, seed=seed, hidden=hidden, eval_every=eval_every)
             for dt in ("fp32", "bf16")}
     last = {dt: runs[dt]["history"][-1]["hits"] for dt in runs}
@@ -110,9 +110,11 @@ def main():
     ap.add_argument("--seeds", type=int, default=1)
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--eval-every", type=int, default=1)
+    ap.add_argument("--communities", type=int, default=None)
     opt = ap.parse_args()
     for s in range(opt.seeds):
-        r = compare(opt.scale, opt.link_batch, opt.epochs, seed=s, hidden=opt.hidden, eval_every=opt.eval_every)
+        r = compare(opt.scale, opt.link_batch, opt.epochs, seed=s, hidden=opt.hidden, eval_every=opt.eval_every,
+                    communities=opt.communities)
         print(json.dumps(r), flush=True)
 
 
