@@ -2,7 +2,7 @@
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -u tools/bf16_accuracy.py --seeds 3 --epochs 24 --eval-every 4 --communities 2000 > gpurun_out/c6_bf16_acc.json 2> gpurun_out/c6_bf16_acc.err || { echo "failed"; tail -20 gpurun_out/c6_bf16_acc.err; exit 1; }
+timeout -k 10 900 python -u tools/bf16_accuracy.py --seeds 3 --epochs 48 --eval-every 8 --communities 2000 > gpurun_out/c6_bf16_acc.json 2> gpurun_out/c6_bf16_acc.err || { echo "failed"; tail -20 gpurun_out/c6_bf16_acc.err; exit 1; }
 python -c "
 import json
 for l in open('gpurun_out/c6_bf16_acc.json'):
