@@ -172,6 +172,66 @@ __global__ __launch_bounds__(256) void hadamard_anchor_rows_kernel(int64_t B, in
   *reinterpret_cast<uint4*>(arow + b * H + col) = V8<T>::pack(acc);
 }
 
+// Same sums, one wave per anchor: lane l owns the 16-B chunks l, l + 64, ... (NCH of them,
+// H / E = 64 * NCH).  The anchor is wave-uniform, so its C context slots are scalar loads,
+// and the dZ and h[ctx] loads of G contexts issue together before their fmas, which run
+// in context order per element (bit-identical to the kernel above).
+template <typename T, int NCH, int G>
+__global__ __launch_bounds__(256) void hadamard_anchor_rows_wave_kernel(int64_t B, int64_t C, int64_t H,
+                                                                        const T* __restrict__ dZ,
+                                                                        const float* __restrict__ drow,
+                                                                        const T* __restrict__ h,
+                                                                        const int32_t* __restrict__ pos,
+                                                                        T* __restrict__ arow) {
+  constexpr int E = V8<T>::E;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (b >= B) return;
+  const int32_t* pc = pos + b * (C + 1) + 1;
+  float acc[NCH][E];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[j][i] = 0.f;
+  for (int64_t c0 = 0; c0 < C; c0 += G) {
+    uint4 rd[G][NCH], rh[G][NCH];
+    float s[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t cc = c0 + g < C ? c0 + g : C - 1;
+      const int64_t z = b * C + cc;
+      const T* ph = h + (int64_t)pc[cc] * H;
+      s[g] = drow ? drow[z] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int64_t col = (int64_t)(lane + 64 * j) * E;
+        if (!drow) rd[g][j] = *reinterpret_cast<const uint4*>(dZ + z * H + col);
+        rh[g][j] = *reinterpret_cast<const uint4*>(ph + col);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (c0 + g >= C) break;   // (wave-uniform)
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        float d[E], hc[E];
+        if (drow) {
+#pragma unroll
+          for (int i = 0; i < E; ++i) d[i] = s[g];
+        } else {
+          unpack16<T>(rd[g][j], d);
+        }
+        unpack16<T>(rh[g][j], hc);
+#pragma unroll
+        for (int i = 0; i < E; ++i) acc[j][i] = fmaf(d[i], hc[i], acc[j][i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+    *reinterpret_cast<uint4*>(arow + b * H + (int64_t)(lane + 64 * j) * E) = V8<T>::pack(acc[j]);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
     int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
@@ -770,12 +830,30 @@ extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_
   const int64_t cpr = H / E, spb = 256 / cpr;
   hipStream_t s = (hipStream_t)stream;
   if (B > 0) {
-    if (dtype == LLP_BF16)
+    const int anch = (cpr % 64 == 0) ? (int)(cpr / 64) : 0;   // chunks per lane, one wave per anchor
+#ifdef LLP_ANCHOR_THREADS   // A/B build: the thread-per-chunk kernel
+    if (false) {
+#else
+    if (anch == 1 || anch == 2 || anch == 4) {
+#endif
+      auto go = [&](auto kern, auto* dz, auto* hh, auto* ar) {
+        hipLaunchKernelGGL(kern, dim3(ceil_div_u(B, 4)), dim3(256), 0, s, B, C, H, dz, drow, hh, pos, ar);
+      };
+      auto pick = [&](auto* dz, auto* hh, auto* ar) {
+        using TT = std::remove_const_t<std::remove_pointer_t<decltype(dz)>>;
+        if (anch == 1) go(hadamard_anchor_rows_wave_kernel<TT, 1, 8>, dz, hh, ar);
+        else if (anch == 2) go(hadamard_anchor_rows_wave_kernel<TT, 2, 4>, dz, hh, ar);
+        else go(hadamard_anchor_rows_wave_kernel<TT, 4, 2>, dz, hh, ar);
+      };
+      if (dtype == LLP_BF16) pick((const bf16_t*)dZ, (const bf16_t*)h, (bf16_t*)anchor_rows);
+      else pick((const float*)dZ, (const float*)h, (float*)anchor_rows);
+    } else if (dtype == LLP_BF16) {
       hipLaunchKernelGGL(hadamard_anchor_rows_kernel<bf16_t>, dim3(ceil_div_u(B, spb)), dim3(256), 0, s, B, C, H,
                          (const bf16_t*)dZ, drow, (const bf16_t*)h, pos, (bf16_t*)anchor_rows);
-    else
+    } else {
       hipLaunchKernelGGL(hadamard_anchor_rows_kernel<float>, dim3(ceil_div_u(B, spb)), dim3(256), 0, s, B, C, H,
                          (const float*)dZ, drow, (const float*)h, pos, (float*)anchor_rows);
+    }
     LLP_LAUNCH_CHECK();
   }
   // one wave per node when a row is 64 * NCH 16-B chunks (1, 2, 4 or 8 per lane): 487 us at the

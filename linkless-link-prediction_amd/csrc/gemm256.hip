@@ -19,6 +19,25 @@
 
 #include <type_traits>
 
+#ifdef LLP_GEMM_STAMPS
+// Diagnostic build (tools/gemm_stamps.py): per workgroup of the pp8 kernel, lane 0 of wave 0
+// records s_memtime (shader clock) and s_memrealtime (100 MHz) at entry, after the prologue's
+// first K-tile, after the main loop and at exit; read back by llp_debug_gemm_stamps.
+constexpr int STAMP_MAX = 1 << 16;
+__device__ unsigned long long g_llp_stamps[STAMP_MAX * 8];
+#define LLP_STAMP(slot)                                                                          \
+  do {                                                                                           \
+    if (tid == 0 && blockIdx.x < STAMP_MAX) {                                                    \
+      g_llp_stamps[blockIdx.x * 8 + 2 * (slot)] = __builtin_amdgcn_s_memtime();                  \
+      g_llp_stamps[blockIdx.x * 8 + 2 * (slot) + 1] = __builtin_amdgcn_s_memrealtime();          \
+    }                                                                                            \
+  } while (0)
+#else
+#define LLP_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int TM = 256, TN = 256, TK = 64;
@@ -802,6 +821,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
+  LLP_STAMP(0);
   int64_t m0, n0;
   const bool dyn = p.m_dev != nullptr;
   const int32_t mlive = dyn ? *p.m_dev : 0;
@@ -906,6 +926,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   }
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   barrier();
+  LLP_STAMP(1);
   const bool grp1 = wu >= 4;
   if (grp1) barrier();          // waves 4-7: one barrier behind from here on
   for (int64_t kt = 0; kt < nk; ++kt) {
@@ -942,6 +963,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
     barrier();
   }
   if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
+  LLP_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if constexpr (MODE == EPI_HEAD_LEAN) {   // every tile (the host checked the shapes)
     __syncthreads();
@@ -952,6 +974,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
       if (lean_tile_ok<MODE>(p, m0, n0)) {
         __syncthreads();
         epilogue_lean<MODE>(p, acc, bvec, smem, m0, n0, tid, wm, wn, g, li);
+        LLP_STAMP(3);
         return;
       }
     }
@@ -1029,3 +1052,11 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   }
   return (int)hipGetLastError();
 }
+
+#ifdef LLP_GEMM_STAMPS
+extern "C" int llp_debug_gemm_stamps(unsigned long long* host, int64_t n_blocks) {
+  const int64_t n = n_blocks < STAMP_MAX ? n_blocks : STAMP_MAX;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_llp_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
