@@ -347,6 +347,12 @@ __device__ __forceinline__ void glds16(const void* gptr, uint32_t lds_addr_unifo
                "s"(lds_addr_uniform)
                : "memory", "m0");
 }
+// SADDR form: a wave-uniform 64-bit base in SGPRs plus a per-lane 32-bit byte offset
+__device__ __forceinline__ void glds16_s(uint32_t voff, const void* sbase, uint32_t lds_addr_uniform) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase),
+               "s"(lds_addr_uniform)
+               : "memory", "m0");
+}
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)p);
 }
@@ -987,6 +993,287 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
 
 namespace {
 
+// ---------------------------------------------------------------------------
+// Persistent form of pp8 for the lean modes (EPI_FWD_RELU / EPI_FWD_NONE / EPI_BWD_MASK,
+// plain operands, K % 128 == 0).  In pp8 every 256 x 256 tile pays a prologue (its first
+// K-tile's DMA, nothing to overlap it with) and an epilogue (LDS staging + 128 KB of
+// stores) on top of the main loop: tools/gemm_stamps.py measured 6.6k + 8.4k of 58.8k
+// cycles per tile at the dominant shape (26 %).  Here one workgroup per CU walks its
+// tiles (t = blockIdx.x, + gridDim.x, ...; the tile map of tile_256_host_interleaved),
+// and the last K-tile of a tile issues the NEXT tile's first K-tile into buffer 0, exactly
+// as it would issue its own next K-tile (same phases, same counted waits: WAR-safe for
+// the same reason), so that DMA lands during the epilogue.  The epilogue (the lean one of
+// pp8, with row guards for a partial last m-tile; the host admits only shapes it takes)
+// therefore must not touch buffer 0: it stages the C tile in two 128-row halves in
+// [64 KB, 131 KB), and
+// the bias and the ReLU-backward mask tile come into LDS by DMA at the tile's start (an
+// ordinary load would make hipcc drain every DMA in flight, vmcnt(0), at its first use),
+// and all its barriers are raw s_barrier + lgkmcnt waits (a __syncthreads() would drain
+// the prefetch too).  Before the next tile's loop a counted vmcnt leaves only the
+// epilogue's stores in flight.  Per tile the MFMAs, their operands and their order are
+// pp8's, and the lean epilogue's values are epilogue_t's: outputs are bit-identical.
+constexpr int PP_STAGE_U4 = 128 * EPI_ROW_U4;          // one 128-row half of the staged C tile
+template <int MODE>
+__global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
+  static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK, "lean modes only");
+  constexpr bool RELU = MODE == EPI_FWD_RELU;
+  constexpr bool BWD = MODE == EPI_BWD_MASK;
+  constexpr int IMG_U4 = 256 * 8;
+  constexpr int TILE_U4 = 2 * IMG_U4;
+  constexpr int STG = TILE_U4;                          // staging half: [64 KB, 64 KB + 66 KB)
+  constexpr int MLDS = STG + PP_STAGE_U4;               // ReLU-backward mask tile: 256 x 32 B
+  constexpr int BLDS = MLDS + 512;                      // bias of the tile's 256 columns: 1 KB
+  constexpr int SM_A = BLDS + 64;
+  constexpr int SM_B = SMEM_U4_EPI + 768;               // epilogue_256 (partial tiles)
+  constexpr int SM_U4 = SM_A > SM_B ? SM_A : SM_B;
+  static_assert(SM_U4 * 16 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM_U4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int wm = w >> 2, wn = w & 3;
+  const bool grp1 = wu >= 4;
+  const int64_t tilesN = (p.N + TN - 1) / TN;
+  const int64_t tilesM_host = (p.M + TM - 1) / TM;
+  const int64_t n_tiles = (p.m_dev ? (tilesM_host + 7) / 8 * 8 : tilesM_host) * tilesN;
+  int64_t M_live = p.M;
+  if (p.m_dev) {
+    const int64_t c = *p.m_dev;
+    M_live = c < p.M ? (c > 0 ? c : 0) : p.M;
+  }
+  p.M = M_live;
+  const int64_t tilesM = (M_live + TM - 1) / TM;
+  // tile t -> (m0, n0): XCD t % 8 takes m-tiles t % 8, + 8, ..., each with its n-tiles
+  auto tile_of = [&](int64_t t, int64_t& m0, int64_t& n0) -> bool {
+    const int64_t xcd = t % 8, loc = t / 8;
+    const int64_t mt = (loc / tilesN) * 8 + xcd;
+    m0 = mt * TM;
+    n0 = (loc % tilesN) * TN;
+    return t < n_tiles && mt < tilesM;
+  };
+  int64_t t = blockIdx.x, m0, n0;
+  if (!tile_of(t, m0, n0)) return;
+
+  // DMA in SADDR form: a wave-uniform base (the tile's row panel at the K-tile) and a per-lane
+  // 32-bit byte offset computed per piece: row q64_row(..) + lane / 8 of the tile, clamped to
+  // the tile's last live row (lim), and 16-B chunk (lane % 8) ^ (lane / 8) -- the row's
+  // swizzle, as q64_row(..) is a multiple of 8 (no offsets held across the loop)
+  const int lr = lane >> 3, lc8 = ((lane & 7) ^ (lane >> 3)) * 8;
+  const uint32_t lds0 = lds_u32(smem);
+  auto issue_chunk = [&](int j, int buf, int64_t tm0, int64_t tn0, int64_t koff) {
+    const bool isA = j == 0 || j == 3;
+    const uint32_t base = lds0 + (uint32_t)(buf * TILE_U4 * 16) + (isA ? 0u : IMG_U4 * 16u);
+    const bf16_t* sb = isA ? p.A + tm0 * p.lda + koff : p.B + tn0 * p.ldb + koff;
+    const int lim = (int)(isA ? min((int64_t)255, p.M - 1 - tm0) : min((int64_t)255, p.N - 1 - tn0));
+    const int64_t ld = isA ? p.lda : p.ldb;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row0 = q64_row(j, 16 * wu + 8 * i);
+      const uint32_t voff = (uint32_t)((min(row0 + lr, lim) * (int)ld + lc8) * 2);
+      glds16_s(voff, sb, __builtin_amdgcn_readfirstlane(base + (uint32_t)(row0 * 128)));
+    }
+  };
+  short8 fa[2][4];
+  short8 fb[2][2][2];
+  float4_t acc[4][8];
+  auto read_a = [&](const uint4* sA, int mh) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int im = 0; im < 4; ++im) {
+        const int r = wm * 128 + mh * 64 + im * 16 + li;
+        uint4 v = sA[r * 8 + ((kh * 4 + g) ^ (r & 7))];
+        fa[kh][im] = *reinterpret_cast<short8*>(&v);
+      }
+  };
+  auto read_b = [&](const uint4* sB, int nh) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) {
+        const int r = wn * 64 + nh * 32 + jn * 16 + li;
+        uint4 v = sB[r * 8 + ((kh * 4 + g) ^ (r & 7))];
+        fb[nh][kh][jn] = *reinterpret_cast<short8*>(&v);
+      }
+  };
+  auto mfma_q = [&](int mh, int nh) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int im = 0; im < 4; ++im)
+          acc[nh * 2 + jn][mh * 4 + im] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][kh][jn], fa[kh][im], acc[nh * 2 + jn][mh * 4 + im], 0,
+                                                      0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int64_t nk = p.K / TK;
+  const uint32_t ones = 0x00010001u;
+  const uint32_t lo16 = __builtin_amdgcn_readfirstlane(0xFFFFu);
+  float* blds = reinterpret_cast<float*>(smem + BLDS);
+  uint8_t* mlds = reinterpret_cast<uint8_t*>(smem + MLDS);
+
+  // first tile: its K-tile 0 (all four chunks) into buffer 0
+#pragma unroll
+  for (int j = 0; j < 4; ++j) issue_chunk(j, 0, m0, n0, 0);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // chunks 0, 1 landed
+  for (;;) {
+    int64_t t_next = t + gridDim.x, m1 = 0, n1 = 0;
+    const bool pf = tile_of(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
+    const int64_t rows = min((int64_t)TM, p.M - m0);  // live rows (the last m-tile may be partial)
+    // this tile's bias and (ReLU backward) mask tile into LDS by DMA; older than its K-tile 1
+    if (BWD) {
+      const uint8_t* ms = p.mask_in + (m0 + min((int64_t)(tid >> 1), rows - 1)) * p.ld_mask + (n0 >> 3) + 16 * (tid & 1);
+      glds16(ms, __builtin_amdgcn_readfirstlane(lds_u32(smem + MLDS) + (uint32_t)(wu * 1024)));
+    } else if (p.bias && wu == 0) {
+      glds16(p.bias + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + BLDS)));
+    }
+    barrier();
+    if (grp1) barrier();          // waves 4-7: one barrier behind from here on
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
+    // one K-tile: 4 quadrant phases; `issue`: DMA chunk j of the K-tile at (tm0, tn0, koff)
+    // into buffer nbuf in phase j (the next K-tile, or the next tile's K-tile 0)
+    auto ktile = [&](int64_t kt, bool issue, int nbuf, int64_t tm0, int64_t tn0, int64_t koff) {
+      const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
+      const uint4* sB = sA + IMG_U4;
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      read_a(sA, 0);
+      read_b(sB, 0);
+      if (issue) issue_chunk(0, nbuf, tm0, tn0, koff);
+      barrier();
+      mfma_q(0, 0);
+      barrier();
+      if (issue) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      read_b(sB, 1);
+      if (issue) issue_chunk(1, nbuf, tm0, tn0, koff);
+      barrier();
+      mfma_q(0, 1);
+      barrier();
+      read_a(sA, 1);
+      if (issue) issue_chunk(2, nbuf, tm0, tn0, koff);
+      barrier();
+      mfma_q(1, 1);
+      barrier();
+      if (issue) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if (issue) issue_chunk(3, nbuf, tm0, tn0, koff);
+      barrier();
+      mfma_q(1, 0);
+      barrier();
+    };
+    for (int64_t kt = 0; kt + 1 < nk; ++kt) ktile(kt, true, (int)((kt + 1) & 1), m0, n0, (kt + 1) * TK);
+    // the last K-tile: the next tile's K-tile 0 into buffer 0 (nk is even) when prefetching
+    ktile(nk - 1, pf, 0, m1, n1, 0);
+    if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
+    // ---- lean epilogue in two 128-row halves, staged in [64 KB, 130 KB): buffer 0 receives
+    // the next tile's K-tile 0 meanwhile.  Its per-thread addresses derive from an opaque
+    // copy of the thread id, so hipcc cannot hoist them above the main loop (where they
+    // would hold ~12 VGPRs across it and push the kernel into scratch).
+    int etid = tid;
+    asm volatile("" : "+v"(etid));
+    const int elane = etid & 63, ew = etid >> 6;
+    const int eg = elane >> 4, eli = elane & 15, ewm = ew >> 2, ewn = ew & 3;
+    constexpr int ROWB = EPI_ROW_U4 * 16;
+    float4_t bl[4];
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn)
+      bl[jn] = (!BWD && p.bias) ? *reinterpret_cast<const float4_t*>(blds + ewn * 64 + jn * 16 + eg * 4)
+                                : float4_t{0.f, 0.f, 0.f, 0.f};
+    const float2_t al = {p.alpha, p.alpha}, z2 = {0.f, 0.f};
+    const int rl0 = etid >> 5, c = etid & 31;
+    char* stg = reinterpret_cast<char*>(smem + STG);
+    char* cbase = reinterpret_cast<char*>(p.C + m0 * p.ldc + n0);
+    const uint32_t toff = (uint32_t)((rl0 * p.ldc + c * 8) * 2);
+    const int64_t cstep = 16 * p.ldc * 2;
+    const bool mo = RELU && p.mask_out;
+    char* mbase = mo ? reinterpret_cast<char*>(p.mask_out + m0 * p.ld_mask + (n0 >> 3)) : nullptr;
+    const uint32_t moff = (uint32_t)(rl0 * p.ld_mask + c);
+    const int64_t mstep = 16 * p.ld_mask;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (ewm == h) {   // phase 1: this wave group's 128 rows (local row im*16 + li)
+        char* sb = stg + eli * ROWB + (ewn * 64 + eg * 4) * 2;
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) {
+          const float2_t b01 = {bl[jn][0], bl[jn][1]}, b23 = {bl[jn][2], bl[jn][3]};
+#pragma unroll
+          for (int im = 0; im < 8; ++im) {
+            float2_t v01 = {acc[jn][im][0], acc[jn][im][1]}, v23 = {acc[jn][im][2], acc[jn][im][3]};
+            if (BWD) {
+              v01 = __builtin_elementwise_fma(v01, al, z2);
+              v23 = __builtin_elementwise_fma(v23, al, z2);
+            } else {
+              v01 = v01 + b01;
+              v23 = v23 + b23;
+            }
+            uint32_t lo = pk_bf16(v01), hi = pk_bf16(v23);
+            if (RELU) { lo = relu_pk_bf16(lo); hi = relu_pk_bf16(hi); }
+            *reinterpret_cast<uint2*>(sb + im * 16 * ROWB + jn * 32) = make_uint2(lo, hi);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+      // phase 2: all threads, rows rl0 + 16 i (i < 8) of this half
+      const char* rb = stg + rl0 * ROWB + c * 16;
+      auto run = [&](auto NTS) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          uint4 v = *reinterpret_cast<const uint4*>(rb + i * 16 * ROWB);
+          const int ii = 8 * h + i;   // 16-row group of the tile
+          if (BWD) {
+            const uint32_t bits = mlds[(rl0 + 16 * ii) * 32 + c];
+            v.x &= half_mask<0>(bits, lo16);
+            v.y &= half_mask<2>(bits, lo16);
+            v.z &= half_mask<4>(bits, lo16);
+            v.w &= half_mask<6>(bits, lo16);
+          }
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 sv = {v.x, v.y, v.z, v.w};
+          u32x4* dst = reinterpret_cast<u32x4*>(cbase + ii * cstep + toff);
+          const bool live = rl0 + 16 * ii < rows;
+          if (live) {
+            if constexpr (decltype(NTS)::value) __builtin_nontemporal_store(sv, dst);
+            else *dst = sv;
+          }
+          if (RELU) {
+            if (mo) {
+              const uint32_t u = nz_pk_u16(v.x, ones) | (nz_pk_u16(v.y, ones) << 2) | (nz_pk_u16(v.z, ones) << 4) |
+                                 (nz_pk_u16(v.w, ones) << 6);
+              const uint32_t word = quad_pack_bytes((u | (u >> 15)) & 0xFFu);
+              if ((c & 3) == 0 && live) *reinterpret_cast<uint32_t*>(mbase + ii * mstep + moff) = word;
+            }
+          }
+        }
+      };
+      if (p.nt_store) run(std::true_type{});
+      else run(std::false_type{});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+    }
+    if (!pf) return;
+    // the next tile: its K-tile 0 was issued by this tile's last K-tile; all but the
+    // epilogue's stores (16 per wave, 32 with the ReLU mask) have landed after this wait
+    // the stores of the last 16-row groups may be predicated off on a partial tile, but every
+    // full tile issues >= 16 store instructions per wave after the last DMA piece (8 per
+    // half), and a partial tile is the last of its workgroup (the largest m-tile)
+    t = t_next; m0 = m1; n0 = n1;
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
+}
+
 // the epilogue specialisation a call can use (epilogue_t)
 int epi_mode_of(const P256& p) {
   if (p.drop_p > 0.f) return EPI_ANY;
@@ -1035,7 +1322,26 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
     hipLaunchKernelGGL(gemm_nt_bf16_256<true>, grid, block, 0, s, p);
     return (int)hipGetLastError();
   }
-  switch (epi_mode_of(p)) {
+  const int mode = epi_mode_of(p);
+#ifndef LLP_GEMM_NO_PERSISTENT
+  // persistent form for the lean modes (plain operands, an even number of K-tiles): one
+  // workgroup per CU walks its tiles with the next tile's first K-tile prefetched
+  const bool lean_shapes = N % TN == 0 && !(ldc & 7) && !((uintptr_t)C & 15) &&
+                           (mode != EPI_FWD_RELU || !mask_out || (!(ld_mask & 3) && !((uintptr_t)mask_out & 3))) &&
+                           (mode != EPI_BWD_MASK || (!(ld_mask & 15) && !((uintptr_t)mask_in & 15))) &&
+                           (!bias || !((uintptr_t)bias & 15));
+  if ((mode == EPI_FWD_RELU || mode == EPI_FWD_NONE || mode == EPI_BWD_MASK) && lean_shapes && !A->idx && !B->idx &&
+      (K / TK) % 2 == 0 && tiles > 256) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
+    const dim3 pgrid((unsigned)(tiles < cus ? tiles : cus));
+    if (mode == EPI_FWD_RELU) hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_RELU>), pgrid, block, 0, s, p);
+    else if (mode == EPI_FWD_NONE) hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_NONE>), pgrid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_BWD_MASK>), pgrid, block, 0, s, p);
+    return (int)hipGetLastError();
+  }
+#endif
+  switch (mode) {
     case EPI_FWD_RELU: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_RELU>), grid, block, 0, s, p); break;
     case EPI_FWD_NONE: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_NONE>), grid, block, 0, s, p); break;
     case EPI_BWD_MASK: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_BWD_MASK>), grid, block, 0, s, p); break;

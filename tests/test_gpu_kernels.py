@@ -819,3 +819,81 @@ def test_zero_bytes_exact_region(off, nbytes):
     h = buf.cpu()
     assert int((h[off:off + nbytes] != 0).sum()) == 0
     assert int((h[:off] != 0xAB).sum()) == 0 and int((h[off + nbytes:] != 0xAB).sum()) == 0
+
+
+def _nt_sliced(k, A, W, M, N, Kd, dtype_code, slice_rows, **kw):
+    """The same GEMM in row slices of <= 256 tiles each (the non-persistent pp8 kernel)."""
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    mask = kw.pop("mask", None)
+    aux = kw.pop("aux", None)
+    for s in range(0, M, slice_rows):
+        e = min(M, s + slice_rows)
+        k.gemm_nt(k.operand(A[s:e]), k.operand(W), e - s, N, Kd, C[s:e], dtype_code,
+                  aux=(mask[s:e] if mask is not None else (aux[s:e] if aux is not None else None)), **kw)
+    return C
+
+
+@pytest.mark.parametrize("mode,M,N,Kd", [("relu_mask", 70_000, 1024, 1024), ("relu_mask", 70_000, 1024, 128),
+                                          ("none", 70_001, 512, 256), ("bwd_mask", 70_000, 1024, 1024),
+                                          ("relu", 70_000, 256, 1024)])
+def test_gemm_nt_persistent_bit_identical(mode, M, N, Kd):
+    """gemm_nt_bf16_pp8p (one workgroup per CU, the next tile's first K-tile prefetched under
+    the epilogue; launched above 256 tiles) against pp8 on row slices of 64 m-tiles (<= 256
+    tiles): C and the ReLU bit masks bit for bit, including a partial last m-tile."""
+    k = K()
+    g = torch.Generator().manual_seed(M + Kd)
+    A = torch.relu(torch.randn(M, Kd, generator=g)).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV) * 0.1
+    sl = 64 * 256
+    if mode in ("relu_mask", "relu"):
+        C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        m1 = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8) if mode == "relu_mask" else None
+        k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C1, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=m1)
+        m2 = torch.empty_like(m1) if m1 is not None else None
+        C2 = _nt_sliced(k, A, W, M, N, Kd, k.LLP_BF16, sl, bias=b, act=k.ACT_RELU, mask=m2)
+        torch.cuda.synchronize()
+        assert torch.equal(C1, C2)
+        if m1 is not None:
+            assert torch.equal(m1, m2)
+    elif mode == "none":
+        C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C1, k.LLP_BF16)
+        C2 = _nt_sliced(k, A, W, M, N, Kd, k.LLP_BF16, sl)
+        torch.cuda.synchronize()
+        assert torch.equal(C1, C2)
+    else:
+        Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        mask = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8)
+        k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, Y, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=mask)
+        G = (torch.randn(M, Kd, generator=g)).to(DEV, torch.bfloat16)
+        Wt = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+        # dX [M, N] = (G @ Wt^T) * (mask bits), alpha 2
+        C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        k.gemm_nt(k.operand(G), k.operand(Wt), M, N, Kd, C1, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=mask, alpha=2.0)
+        C2 = _nt_sliced(k, G, Wt, M, N, Kd, k.LLP_BF16, sl, act=k.ACT_RELU_BWD, aux=mask, alpha=2.0)
+        torch.cuda.synchronize()
+        assert torch.equal(C1, C2)
+        ref = 2.0 * (G.float() @ Wt.float().t()) * (Y.float() > 0)
+        assert torch.allclose(C1.float(), ref, rtol=2e-2, atol=2e-2 * (1 + ref.abs().max().item()))
+
+
+def test_gemm_nt_persistent_device_row_count():
+    """The persistent kernel with a device row count (the unique-node student): rows past the
+    count are neither computed nor stored, the live rows equal the exact-M launch."""
+    k = K()
+    g = torch.Generator().manual_seed(11)
+    Mh, Ml, N, Kd = 80_000, 71_333, 1024, 1024
+    A = torch.relu(torch.randn(Mh, Kd, generator=g)).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV) * 0.1
+    cnt = torch.tensor([Ml], dtype=torch.int32, device=DEV)
+    C1 = torch.full((Mh, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    m1 = torch.zeros(Mh, N // 8, device=DEV, dtype=torch.uint8)
+    k.gemm_nt(k.operand(A, count=cnt), k.operand(W), Mh, N, Kd, C1, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=m1)
+    C2 = torch.empty(Ml, N, device=DEV, dtype=torch.bfloat16)
+    m2 = torch.zeros(Ml, N // 8, device=DEV, dtype=torch.uint8)
+    k.gemm_nt(k.operand(A[:Ml]), k.operand(W), Ml, N, Kd, C2, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=m2)
+    torch.cuda.synchronize()
+    assert torch.equal(C1[:Ml], C2) and torch.equal(m1[:Ml], m2)
+    assert bool((C1[Ml:].float() == 7.0).all()) and int(m1[Ml:].sum()) == 0
