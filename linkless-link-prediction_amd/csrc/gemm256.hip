@@ -1035,7 +1035,10 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   const bool grp1 = wu >= 4;
   const int64_t tilesN = (p.N + TN - 1) / TN;
   const int64_t tilesM_host = (p.M + TM - 1) / TM;
-  const int64_t n_tiles = (p.m_dev ? (tilesM_host + 7) / 8 * 8 : tilesM_host) * tilesN;
+  // the map below deals m-tiles to XCDs in groups of 8, so its index space is the m-tile
+  // count padded to a multiple of 8 (the padding's tiles are skipped) -- also without a
+  // device row count
+  const int64_t n_tiles = (tilesM_host + 7) / 8 * 8 * tilesN;
   int64_t M_live = p.M;
   if (p.m_dev) {
     const int64_t c = *p.m_dev;
@@ -1051,8 +1054,13 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     n0 = (loc % tilesN) * TN;
     return t < n_tiles && mt < tilesM;
   };
-  int64_t t = blockIdx.x, m0, n0;
-  if (!tile_of(t, m0, n0)) return;
+  // the first live tile at or after t on this workgroup's walk (t += gridDim.x); false past the end
+  auto next_tile = [&](int64_t& t, int64_t& m0, int64_t& n0) -> bool {
+    while (t < n_tiles && !tile_of(t, m0, n0)) t += gridDim.x;
+    return t < n_tiles;
+  };
+  int64_t t = blockIdx.x, m0 = 0, n0 = 0;
+  if (!next_tile(t, m0, n0)) return;
 
   // DMA in SADDR form: a wave-uniform base (the tile's row panel at the K-tile) and a per-lane
   // 32-bit byte offset computed per piece: row q64_row(..) + lane / 8 of the tile, clamped to
@@ -1128,7 +1136,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // chunks 0, 1 landed
   for (;;) {
     int64_t t_next = t + gridDim.x, m1 = 0, n1 = 0;
-    const bool pf = tile_of(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
+    const bool pf = next_tile(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
     const int64_t rows = min((int64_t)TM, p.M - m0);  // live rows (the last m-tile may be partial)
     // this tile's bias and (ReLU backward) mask tile into LDS by DMA; older than its K-tile 1
     if (BWD) {
@@ -1264,11 +1272,10 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
       barrier();
     }
     if (!pf) return;
-    // the next tile: its K-tile 0 was issued by this tile's last K-tile; all but the
-    // epilogue's stores (16 per wave, 32 with the ReLU mask) have landed after this wait
-    // the stores of the last 16-row groups may be predicated off on a partial tile, but every
-    // full tile issues >= 16 store instructions per wave after the last DMA piece (8 per
-    // half), and a partial tile is the last of its workgroup (the largest m-tile)
+    // the next tile: its K-tile 0 was issued by this tile's last K-tile.  This wait only
+    // bounds the stores in flight; correctness rests on the next tile's first K-tile wait
+    // (vmcnt(2)), which the epilogue's stores and the bias / mask DMA, all younger than the
+    // prefetch, can only make wait longer
     t = t_next; m0 = m1; n0 = n1;
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   }

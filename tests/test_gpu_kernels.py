@@ -835,17 +835,18 @@ def _nt_sliced(k, A, W, M, N, Kd, dtype_code, slice_rows, **kw):
 
 @pytest.mark.parametrize("mode,M,N,Kd", [("relu_mask", 70_000, 1024, 1024), ("relu_mask", 70_000, 1024, 128),
                                           ("none", 70_001, 512, 256), ("bwd_mask", 70_000, 1024, 1024),
-                                          ("relu", 70_000, 256, 1024)])
+                                          ("relu", 70_000, 256, 1024), ("none", 2_000, 9216, 256)])
 def test_gemm_nt_persistent_bit_identical(mode, M, N, Kd):
     """gemm_nt_bf16_pp8p (one workgroup per CU, the next tile's first K-tile prefetched under
     the epilogue; launched above 256 tiles) against pp8 on row slices of 64 m-tiles (<= 256
-    tiles): C and the ReLU bit masks bit for bit, including a partial last m-tile."""
+    tiles): C and the ReLU bit masks bit for bit, including a partial last m-tile, m-tile
+    counts that are not a multiple of 8 and a walk along one m-tile's n-tiles (N = 9216)."""
     k = K()
     g = torch.Generator().manual_seed(M + Kd)
     A = torch.relu(torch.randn(M, Kd, generator=g)).to(DEV, torch.bfloat16)
     W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
     b = torch.randn(N, generator=g).to(DEV) * 0.1
-    sl = 64 * 256
+    sl = min(64, 256 // (N // 256)) * 256
     if mode in ("relu_mask", "relu"):
         C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         m1 = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8) if mode == "relu_mask" else None
@@ -880,7 +881,7 @@ def test_gemm_nt_persistent_bit_identical(mode, M, N, Kd):
 
 def test_gemm_nt_persistent_device_row_count():
     """The persistent kernel with a device row count (the unique-node student): rows past the
-    count are neither computed nor stored, the live rows equal the exact-M launch."""
+    count are neither computed nor stored, the live rows equal pp8 on row slices."""
     k = K()
     g = torch.Generator().manual_seed(11)
     Mh, Ml, N, Kd = 80_000, 71_333, 1024, 1024
@@ -891,9 +892,8 @@ def test_gemm_nt_persistent_device_row_count():
     C1 = torch.full((Mh, N), 7.0, device=DEV, dtype=torch.bfloat16)
     m1 = torch.zeros(Mh, N // 8, device=DEV, dtype=torch.uint8)
     k.gemm_nt(k.operand(A, count=cnt), k.operand(W), Mh, N, Kd, C1, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=m1)
-    C2 = torch.empty(Ml, N, device=DEV, dtype=torch.bfloat16)
     m2 = torch.zeros(Ml, N // 8, device=DEV, dtype=torch.uint8)
-    k.gemm_nt(k.operand(A[:Ml]), k.operand(W), Ml, N, Kd, C2, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=m2)
+    C2 = _nt_sliced(k, A[:Ml], W, Ml, N, Kd, k.LLP_BF16, 64 * 256, bias=b, act=k.ACT_RELU, mask=m2)
     torch.cuda.synchronize()
     assert torch.equal(C1[:Ml], C2) and torch.equal(m1[:Ml], m2)
     assert bool((C1[Ml:].float() == 7.0).all()) and int(m1[Ml:].sum()) == 0
