@@ -491,7 +491,7 @@ def main():
                        "student_rows_per_step": {"reference": B_full * (C + 1) + 4 * P_full,
                                                  "unique_nodes": int(rows_all.item())},
                        "mfma_util_step": flop_exec / (dt / opt.steps) / 1e12 / peak / world},
-            "roofline": {"bound": "mfma", "kernel": f"gemm_nt_bf16_pp8<EPI_FWD_RELU> student layer-2 forward "
+            "roofline": {"bound": "mfma", "kernel": f"gemm_nt_bf16_pp8p<EPI_FWD_RELU> (persistent) student layer-2 forward "
                          f"({rows_exec}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": pmc_traffic(rows_exec, H, opt.dtype),
                          "algorithmic_bytes": 2.0 * rows_exec * H * 2 + 2.0 * H * H + rows_exec * H / 8.0,

@@ -1015,15 +1015,18 @@ namespace {
 constexpr int PP_STAGE_U4 = 128 * EPI_ROW_U4;          // one 128-row half of the staged C tile
 template <int MODE>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
-  static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK, "lean modes only");
+  static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK || MODE == EPI_HEAD_LEAN,
+                "lean modes only");
   constexpr bool RELU = MODE == EPI_FWD_RELU;
   constexpr bool BWD = MODE == EPI_BWD_MASK;
+  constexpr bool HEAD = MODE == EPI_HEAD_LEAN;
   constexpr int IMG_U4 = 256 * 8;
   constexpr int TILE_U4 = 2 * IMG_U4;
   constexpr int STG = TILE_U4;                          // staging half: [64 KB, 64 KB + 66 KB)
-  constexpr int MLDS = STG + PP_STAGE_U4;               // ReLU-backward mask tile: 256 x 32 B
+  constexpr int MLDS = STG + PP_STAGE_U4;               // ReLU-backward mask tile: 256 x 32 B (head: quad partials)
   constexpr int BLDS = MLDS + 512;                      // bias of the tile's 256 columns: 1 KB
-  constexpr int SM_A = BLDS + 64;
+  constexpr int HWLDS = BLDS + 64;                      // head weights of the tile's 256 columns: 1 KB
+  constexpr int SM_A = HWLDS + 64;
   constexpr int SM_B = SMEM_U4_EPI + 768;               // epilogue_256 (partial tiles)
   constexpr int SM_U4 = SM_A > SM_B ? SM_A : SM_B;
   static_assert(SM_U4 * 16 <= 160 * 1024, "LDS");
@@ -1142,8 +1145,9 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     if (BWD) {
       const uint8_t* ms = p.mask_in + (m0 + min((int64_t)(tid >> 1), rows - 1)) * p.ld_mask + (n0 >> 3) + 16 * (tid & 1);
       glds16(ms, __builtin_amdgcn_readfirstlane(lds_u32(smem + MLDS) + (uint32_t)(wu * 1024)));
-    } else if (p.bias && wu == 0) {
-      glds16(p.bias + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + BLDS)));
+    } else {
+      if (p.bias && wu == 0) glds16(p.bias + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + BLDS)));
+      if (HEAD && wu == 1) glds16(p.head_w + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + HWLDS)));
     }
     barrier();
     if (grp1) barrier();          // waves 4-7: one barrier behind from here on
@@ -1202,7 +1206,14 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     const float2_t al = {p.alpha, p.alpha}, z2 = {0.f, 0.f};
     const int rl0 = etid >> 5, c = etid & 31;
     char* stg = reinterpret_cast<char*>(smem + STG);
-    char* cbase = reinterpret_cast<char*>(p.C + m0 * p.ldc + n0);
+    const bool st = !HEAD || p.C != nullptr;           // the head GEMM may store no C
+    char* cbase = st ? reinterpret_cast<char*>(p.C + m0 * p.ldc + n0) : nullptr;
+    float* part = reinterpret_cast<float*>(smem + MLDS);   // head: [256 rows][8 quads] partial dots
+    float4_t hw0 = {0.f, 0.f, 0.f, 0.f}, hw1 = hw0;
+    if (HEAD) {   // this thread's 8 head weights (columns n0 + 8c ..) for the head dot
+      hw0 = *reinterpret_cast<const float4_t*>(reinterpret_cast<const float*>(smem + HWLDS) + 8 * (etid & 31));
+      hw1 = *reinterpret_cast<const float4_t*>(reinterpret_cast<const float*>(smem + HWLDS) + 8 * (etid & 31) + 4);
+    }
     const uint32_t toff = (uint32_t)((rl0 * p.ldc + c * 8) * 2);
     const int64_t cstep = 16 * p.ldc * 2;
     const bool mo = RELU && p.mask_out;
@@ -1227,7 +1238,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
               v23 = v23 + b23;
             }
             uint32_t lo = pk_bf16(v01), hi = pk_bf16(v23);
-            if (RELU) { lo = relu_pk_bf16(lo); hi = relu_pk_bf16(hi); }
+            if (RELU || HEAD) { lo = relu_pk_bf16(lo); hi = relu_pk_bf16(hi); }
             *reinterpret_cast<uint2*>(sb + im * 16 * ROWB + jn * 32) = make_uint2(lo, hi);
           }
         }
@@ -1252,7 +1263,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
           const u32x4 sv = {v.x, v.y, v.z, v.w};
           u32x4* dst = reinterpret_cast<u32x4*>(cbase + ii * cstep + toff);
           const bool live = rl0 + 16 * ii < rows;
-          if (live) {
+          if (live && st) {
             if constexpr (decltype(NTS)::value) __builtin_nontemporal_store(sv, dst);
             else *dst = sv;
           }
@@ -1264,12 +1275,29 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
               if ((c & 3) == 0 && live) *reinterpret_cast<uint32_t*>(mbase + ii * mstep + moff) = word;
             }
           }
+          if (HEAD) {   // epilogue_lean_head's dot of the 8 rounded outputs, same order
+            float d = __uint_as_float(v.x << 16) * hw0[0];
+            d = fmaf(__uint_as_float(v.x & 0xFFFF0000u), hw0[1], d);
+            d = fmaf(__uint_as_float(v.y << 16), hw0[2], d);
+            d = fmaf(__uint_as_float(v.y & 0xFFFF0000u), hw0[3], d);
+            d = fmaf(__uint_as_float(v.z << 16), hw1[0], d);
+            d = fmaf(__uint_as_float(v.z & 0xFFFF0000u), hw1[1], d);
+            d = fmaf(__uint_as_float(v.w << 16), hw1[2], d);
+            d = fmaf(__uint_as_float(v.w & 0xFFFF0000u), hw1[3], d);
+            d = dpp_quad_sum(d);
+            if ((c & 3) == 0) part[(rl0 + 16 * ii) * 8 + (c >> 2)] = d;
+          }
         }
       };
       if (p.nt_store) run(std::true_type{});
       else run(std::false_type{});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier();
+    }
+    if (HEAD && etid < rows) {   // the row's 8 quad partials in column order (epilogue_lean_head)
+      const float4_t a = *reinterpret_cast<const float4_t*>(part + etid * 8);
+      const float4_t b = *reinterpret_cast<const float4_t*>(part + etid * 8 + 4);
+      p.head_part[(n0 / TN) * p.head_ld + m0 + etid] = ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
     }
     if (!pf) return;
     // the next tile: its K-tile 0 was issued by this tile's last K-tile.  This wait only
@@ -1294,6 +1322,19 @@ int epi_mode_of(const P256& p) {
 }
 
 }  // namespace
+
+// one workgroup per CU (the persistent kernel's grid)
+static dim3 persistent_grid(int64_t tiles) {
+  static int cus_of[64] = {};   // per device, queried once (a race only repeats the query)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int cus = cus_of[dev];
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cus_of[dev] = cus;
+  }
+  return dim3((unsigned)(tiles < cus ? tiles : cus));
+}
 
 // Called from llp_gemm_nt when the shapes allow it (gemm.hip).
 int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
@@ -1339,9 +1380,7 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
                            (!bias || !((uintptr_t)bias & 15));
   if ((mode == EPI_FWD_RELU || mode == EPI_FWD_NONE || mode == EPI_BWD_MASK) && lean_shapes && !A->idx && !B->idx &&
       (K / TK) % 2 == 0 && tiles > 256) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
-    const dim3 pgrid((unsigned)(tiles < cus ? tiles : cus));
+    const dim3 pgrid = persistent_grid(tiles);
     if (mode == EPI_FWD_RELU) hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_RELU>), pgrid, block, 0, s, p);
     else if (mode == EPI_FWD_NONE) hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_NONE>), pgrid, block, 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_BWD_MASK>), pgrid, block, 0, s, p);
@@ -1353,6 +1392,13 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
     case EPI_FWD_NONE: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_NONE>), grid, block, 0, s, p); break;
     case EPI_BWD_MASK: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_BWD_MASK>), grid, block, 0, s, p); break;
     case EPI_HEAD_RELU:
+#ifndef LLP_GEMM_NO_PERSISTENT
+      if (N % TN == 0 && !((uintptr_t)head_w & 15) && (!C || (!(ldc & 7) && !((uintptr_t)C & 15))) &&
+          (!bias || !((uintptr_t)bias & 15)) && !A->idx && !B->idx && (K / TK) % 2 == 0 && tiles > 256) {
+        hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_HEAD_LEAN>), persistent_grid(tiles), block, 0, s, p);
+        break;
+      }
+#endif
       // the head dot over the staged bf16 outputs (epilogue_lean_head) on every tile when
       // the shapes allow: 650 -> 643 us per predictor-layer launch, collab step -0.3 %
       // (3 interleaved rounds, profiles/r03_head_lean_ab.txt)

@@ -897,3 +897,36 @@ def test_gemm_nt_persistent_device_row_count():
     torch.cuda.synchronize()
     assert torch.equal(C1[:Ml], C2) and torch.equal(m1[:Ml], m2)
     assert bool((C1[Ml:].float() == 7.0).all()) and int(m1[Ml:].sum()) == 0
+
+
+@pytest.mark.parametrize("M,N,Kd,with_c", [(70_000, 1024, 1024, True), (70_000, 1024, 1024, False),
+                                           (3_000, 9216, 256, True)])
+def test_gemm_nt_persistent_head_bit_identical(M, N, Kd, with_c):
+    """The fused-head GEMM (predictor's last hidden layer + Linear(N,1)) in the persistent
+    kernel (gemm_nt_bf16_pp8p<EPI_HEAD_LEAN>: bias and head weights DMA'd into LDS per tile,
+    the quad partials in the mask region) against pp8<EPI_HEAD_LEAN> on row slices of
+    <= 256 tiles: C and every head partial bit for bit, with and without C."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.relu(torch.randn(M, Kd, generator=g)).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV) * 0.1
+    hw = torch.randn(N, generator=g).to(DEV)
+    parts = k.head_parts(N)
+    C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if with_c else None
+    h1 = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, C1, hw, h1, bias=b, act=k.ACT_RELU)
+    sl = min(64, 256 // (N // 256)) * 256
+    C2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    h2 = torch.empty(parts, M, device=DEV)
+    for s in range(0, M, sl):
+        e = min(M, s + sl)
+        hs = torch.empty(parts, e - s, device=DEV)
+        k.gemm_nt_head(k.operand(A[s:e]), k.operand(W), e - s, N, Kd, C2[s:e], hw, hs, bias=b, act=k.ACT_RELU)
+        h2[:, s:e] = hs
+    torch.cuda.synchronize()
+    if with_c:
+        assert torch.equal(C1, C2)
+    assert torch.equal(h1, h2)
+    ref = C2.float() @ hw
+    assert torch.allclose(h1.sum(0), ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item()))
