@@ -1013,7 +1013,6 @@ namespace {
 // epilogue's stores in flight.  Per tile the MFMAs, their operands and their order are
 // pp8's, and the lean epilogue's values are epilogue_t's: outputs are bit-identical.
 constexpr int PP_STAGE_U4 = 128 * EPI_ROW_U4;          // one 128-row half of the staged C tile
-constexpr int PP_STORES_BEHIND = 16;                    // C stores per wave of a full tile (2 halves x 8)
 template <int MODE>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK || MODE == EPI_HEAD_LEAN,
@@ -1138,7 +1137,6 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) issue_chunk(j, 0, m0, n0, 0);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // chunks 0, 1 landed
-  bool behind = false;
   for (;;) {
     int64_t t_next = t + gridDim.x, m1 = 0, n1 = 0;
     const bool pf = next_tile(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
@@ -1159,32 +1157,17 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
       for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
     // one K-tile: 4 quadrant phases; `issue`: DMA chunk j of the K-tile at (tm0, tn0, koff)
     // into buffer nbuf in phase j (the next K-tile, or the next tile's K-tile 0)
-    // `behind`: the previous tile's epilogue issued >= PP_STORES_BEHIND vector-memory
-    // operations after this K-tile's DMA (its stores), which the first two waits then
-    // leave in flight (a lower bound: fewer only makes a wait stricter)
-    // (the choice is a scalar branch inside one asm statement: a branch in the C++ control
-    // flow splits the loop body's scheduling regions and costs ~15 VGPRs)
-    auto wait_behind = [&](bool b) {
-      asm volatile(
-          "s_cmp_eq_u32 %0, 0\n\t"
-          "s_cbranch_scc1 .Lpp8p_near%=\n\t"
-          "s_waitcnt vmcnt(%1)\n\t"
-          "s_branch .Lpp8p_done%=\n"
-          ".Lpp8p_near%=:\n\t"
-          "s_waitcnt vmcnt(2)\n"
-          ".Lpp8p_done%=:" ::"s"(__builtin_amdgcn_readfirstlane((int)b)), "n"(2 + PP_STORES_BEHIND) : "memory", "scc");
-    };
-    auto ktile = [&](int64_t kt, bool issue, int nbuf, int64_t tm0, int64_t tn0, int64_t koff, bool behind) {
+    auto ktile = [&](int64_t kt, bool issue, int nbuf, int64_t tm0, int64_t tn0, int64_t koff) {
       const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
       const uint4* sB = sA + IMG_U4;
-      wait_behind(behind);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       read_a(sA, 0);
       read_b(sB, 0);
       if (issue) issue_chunk(0, nbuf, tm0, tn0, koff);
       barrier();
       mfma_q(0, 0);
       barrier();
-      if (issue) wait_behind(behind);
+      if (issue) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       read_b(sB, 1);
       if (issue) issue_chunk(1, nbuf, tm0, tn0, koff);
@@ -1202,10 +1185,9 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
       mfma_q(1, 0);
       barrier();
     };
-    for (int64_t kt = 0; kt + 1 < nk; ++kt)
-      ktile(kt, true, (int)((kt + 1) & 1), m0, n0, (kt + 1) * TK, behind && kt == 0);
+    for (int64_t kt = 0; kt + 1 < nk; ++kt) ktile(kt, true, (int)((kt + 1) & 1), m0, n0, (kt + 1) * TK);
     // the last K-tile: the next tile's K-tile 0 into buffer 0 (nk is even) when prefetching
-    ktile(nk - 1, pf, 0, m1, n1, 0, false);
+    ktile(nk - 1, pf, 0, m1, n1, 0);
     if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
     // ---- lean epilogue in two 128-row halves, staged in [64 KB, 130 KB): buffer 0 receives
     // the next tile's K-tile 0 meanwhile.  Its per-thread addresses derive from an opaque
@@ -1318,13 +1300,14 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
       p.head_part[(n0 / TN) * p.head_ld + m0 + etid] = ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
     }
     if (!pf) return;
-    // the next tile: its K-tile 0 was issued by this tile's last K-tile, and this tile's
-    // stores drain under the next tile's first K-tile: a full tile that stored C issued 8
-    // C stores per wave and half (plus the ReLU mask's), all younger than that DMA
-#ifndef LLP_PP8P_DRAIN
-    behind = __builtin_amdgcn_readfirstlane((int)(rows == TM && st)) != 0;
-#endif
+    // the next tile: its K-tile 0 was issued by this tile's last K-tile.  This wait only
+    // bounds the stores in flight; correctness rests on the next tile's first K-tile wait
+    // (vmcnt(2)), which the epilogue's stores and the bias / mask DMA, all younger than the
+    // prefetch, can only make wait longer.  (Leaving a full tile's 16 stores per wave in
+    // flight through the next tile's first two waits measured 1 % SLOWER on the collab
+    // step, 3 interleaved rounds each: the stores then compete with that K-tile's DMA.)
     t = t_next; m0 = m1; n0 = n1;
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   }
 }
 
