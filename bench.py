@@ -128,12 +128,12 @@ def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, 
     print(json.dumps({"dominant_rows": R1, "H": lin.out_f, "launches": n}), flush=True)
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r02_pmc_dominant.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_dominant.json")
 
 
 def pmc_traffic(rows, H, dtype):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC passes (profiles/r02_pmc_dominant.json, tools/pmc_summary.py):
+    PMC passes (profiles/r03_pmc_dominant.json, tools/pmc_summary.py):
     2 x FETCH_SIZE (gfx950 reports half of a wide streaming read) + WRITE_SIZE,
     per dispatch.  None when the profile is absent or for another shape."""
     try:

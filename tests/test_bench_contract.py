@@ -28,7 +28,7 @@ def test_step_flops_matches_survey():
 
 
 def test_pmc_traffic_reads_committed_profile():
-    prof = os.path.join(REPO, "profiles", "r02_pmc_dominant.json")
+    prof = bench.PMC_FILE
     p = json.load(open(prof))
     t = bench.pmc_traffic(p["rows"], p["H"], p["dtype"])
     assert t == pytest.approx(p["traffic_bytes_per_launch"], rel=1e-9)

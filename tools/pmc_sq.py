@@ -50,7 +50,7 @@ def main():
     ns = sum(dur[d] for d in ids) / len(ids)
     clk = raw["GRBM_GUI_ACTIVE"] / 8 / (ns * 1e-9)
     wc = raw["SQ_WAVE_CYCLES"]
-    out = {"kernel": name[ids[-1]].split("(")[0], "dispatches": len(ids),
+    out = {"kernel": name[ids[-1]].replace("void (anonymous namespace)::", "").split("((")[0], "dispatches": len(ids),
            "method": "rocprofv3 --pmc " + " ".join(sorted(raw)) + " (one pass), last %d dispatches" % len(ids),
            "duration_ms_profiled": ns / 1e6, "clock_ghz": clk / 1e9,
            "mfma_busy": raw["SQ_VALU_MFMA_BUSY_CYCLES"] / (raw["GRBM_GUI_ACTIVE"] / 8 * 1024),
