@@ -60,7 +60,8 @@ def per_kernel(fetch, write, match):
 
 
 def short(name):
-    return name.split("(")[0].split("::")[-1] if "::" in name.split("(")[0] else name.split("(")[0]
+    """kernel name without the return type, namespace and parameter list"""
+    return name.replace("void (anonymous namespace)::", "").split("(")[0]
 
 
 def entry(name, algo, cbytes, ns, note=""):
@@ -85,7 +86,7 @@ def step(a):
             "teacher predictor input t_h[a] * t_h[c] (256 wide)"),
         "colsum_vec_kernel": (2 * R2 * H * s + 4 * R2,
             "head backward: read Z1, write dZ1, dw / db partials"),
-        "hadamard_anchor_rows_kernel": (2 * BC * H * s + 4 * BC + B * H * s,
+        "hadamard_anchor_rows": (2 * BC * H * s + 4 * BC + B * H * s,
             "anchors' sum over contexts of dZ * h[ctx]: dZ context rows + h[ctx] rows, write B rows"),
         "hadamard_bwd_segments_wave_kernel": ((2 * BC + B + 2 * L) * H * s + U * H * s + 12 * (B * (C + 1) + L),
             "per unique node, its target rows in order: dZ row + partner h row (anchor rows: their sum), "
@@ -99,7 +100,7 @@ def step(a):
         if not cb:
             continue
         durs = [d for n, d in tr if frag in n][a.skip:] or [x[2] for x in cb]
-        res.append(entry(short(cb[0][0]) + "<" + cb[0][0].split("<", 1)[1].split(">")[0] + ">", algo, [x[1] for x in cb], sum(durs) / len(durs), what))
+        res.append(entry(short(cb[0][0]), algo, [x[1] for x in cb], sum(durs) / len(durs), what))
     out = {"workload": "ogbl-collab LLP step, bf16", "B": B, "C": C, "P": P, "H": H, "unique_nodes": U,
            "bytes": "counter = 2 x FETCH_SIZE + WRITE_SIZE per dispatch (beyond-L2, MALL hits included)",
            "durations": "kernel trace of the same command (eager steps)" if tr else "PMC pass timestamps",
@@ -122,7 +123,7 @@ def sage(a):
     for p in plan["plan"]:
         seg = cb[i:i + p["launches"]][3:]     # the 3 warm-up launches of each configuration excluded
         i += p["launches"]
-        name = short(seg[0][0]) + "<" + seg[0][0].split("<", 1)[1].split(">")[0] + ">" if seg else "?"
+        name = short(seg[0][0]) if seg else "?"
         e = entry(name, p["algorithmic_bytes"], [x[1] for x in seg], p["ms"] * 1e6,
                   "x rows re-read ~E/N times; the Infinity Cache serves most of them")
         e.update({"dtype": p["dtype"], "F": p["F"], "mode": p["mode"], "compulsory_bytes": p["compulsory_bytes"],
