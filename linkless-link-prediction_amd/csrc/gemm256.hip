@@ -236,9 +236,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
     const bool more = kt + 1 < nk;
     if (more) {
       if (HADA) hada_load(kt + 1);
-#ifndef LLP_ABLATE_NOLOAD   // tools/gemm_ablate.cpp: time the loop without its staging loads
       stage_glds(buf ^ 1, kt + 1);
-#endif
     }
     const uint4* sA = smem + buf * STAGE_U4;
     const uint4* sB = sA + TM * 8;
@@ -257,18 +255,11 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
         uint4 v = sA[r * 8 + ((g + 4 * s) ^ (r & 7))];
         fx[im] = *reinterpret_cast<short8*>(&v);
       }
-#ifndef LLP_ABLATE_NOMFMA
 #pragma unroll
       for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
         for (int im = 0; im < 8; ++im)
           acc[jn][im] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[jn], fx[im], acc[jn][im], 0, 0, 0);
-#else
-#pragma unroll
-      for (int jn = 0; jn < 4; ++jn) asm volatile("" ::"v"(fw[jn]));
-#pragma unroll
-      for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(fx[im]));
-#endif
     }
     if (more && HADA) hada_store(buf ^ 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -384,13 +375,6 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
   const bool fwd = MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_HEAD_RELU;
   const float alpha = fwd ? 1.f : p.alpha;
   const float* bias = MODE == EPI_BWD_MASK ? nullptr : p.bias;
-#ifdef LLP_ABLATE_NOEPI   // tools: time the kernel without its epilogue (outputs garbage)
-#pragma unroll
-  for (int jn = 0; jn < 4; ++jn)
-#pragma unroll
-    for (int im = 0; im < 8; ++im) asm volatile("" ::"v"(acc[jn][im]));
-  return;
-#endif
   const uint64_t dstream = drop ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
   // ReLU-backward bit mask: this thread's 16 bytes (one per store below) are loaded
   // first, so their latency hides under the staging work instead of under each store
@@ -515,12 +499,7 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
-#ifdef LLP_ABLATE_NOSTORE   // tools: the epilogue without its global stores
-    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-    if (false) {
-#else
     if (ok) {
-#endif
       if (p.nt_store) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 vv = {v.x, v.y, v.z, v.w};
