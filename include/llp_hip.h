@@ -75,7 +75,7 @@ int llp_device_count(void);
 /* Optional inverted dropout after the activation (F.dropout / nn.Dropout after
  * ReLU, src/models.py:52-53,144-145): element (m, n) is kept iff
  * u >= p with u = uniform draw #(m*N + n) of Philox stream
- * 16*(*step_ctr) + stream_offset; kept values are scaled by 1/(1-p).
+ * 64*(*step_ctr) + stream_offset; kept values are scaled by 1/(1-p).
  * The backward needs no mask: LLP_ACT_RELU_BWD against the stored dropped
  * activation with alpha = 1/(1-p) is exact. */
 typedef struct llp_dropout {
@@ -104,6 +104,22 @@ int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, cons
                      const llp_dropout* dropout, const float* head_w, float* head_part, void* stream);
 int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit,
                     float* prob, void* stream);
+
+/* Split-K bf16 GEMM for few output tiles over a long K: the first Linear of the
+ * full-batch student (src/models.py:48 on x [N_old, 8,415] at the coauthor-physics
+ * production shape, src/main.py:173), where C = act(A.B^T + bias) has fewer
+ * 256x256 tiles than the CUs.  Workgroup (tile, s) sums K-tiles
+ * [nkt*s/S, nkt*(s+1)/S) into an f32 slab of `workspace`
+ * (llp_gemm_nt_splitk_ws_bytes), then one pass sums the S slabs in order, adds the
+ * bias, rounds to bf16 and applies act (NONE or RELU, with an optional ReLU bit
+ * mask as llp_gemm_nt writes it).  Deterministic; equal to llp_gemm_nt up to where
+ * the K-range partial sums are added.  llp_gemm_nt_splitk_plan returns S (1: use
+ * llp_gemm_nt).  bf16 only; plain, 16-B aligned operands; N % 256 == 0. */
+int llp_gemm_nt_splitk_plan(int64_t M, int64_t N, int64_t K);
+int64_t llp_gemm_nt_splitk_ws_bytes(int64_t M, int64_t N, int splits);
+int llp_gemm_nt_splitk(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B,
+                       void* C, int64_t ldc, const float* bias, int act, void* mask_out, int64_t ld_mask,
+                       int splits, void* workspace, int64_t workspace_bytes, void* stream);
 
 
 /* Weight gradient: C[p,q] (+)= sum_m A[m,p] * B[m,q]  (A = dY [M,P], B = X [M,Q]).
@@ -239,7 +255,7 @@ int llp_hadamard_bwd_scatter(int dtype, int64_t R, int64_t H, const void* dZ, co
  * rw_step*hops steps; 1 = 'nb': rw_step walks of `hops` steps, start column
  * dropped after the first); then rw_step*hops*ns_rate uniform negatives.
  * Philox stream of walk i = stream_base + i, negatives stream_base + rw_step,
- * with stream_base = 16*(*step_ctr) + stream_offset (device counter: graph-safe).
+ * with stream_base = 64*(*step_ctr) + stream_offset (device counter: graph-safe).
  * Draw indices use the GLOBAL anchor position b + b_offset, so a rank holding
  * anchors [b_offset, b_offset + B) draws what a single GPU would. */
 int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
@@ -249,7 +265,7 @@ int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_n
 
 /* torch.randint(0, N, [2, n_total]) (src/main.py:84,209) restricted to columns
  * [offset, offset + n): out[0..n) = row 0, out[n..2n) = row 1.  Philox stream
- * 16*(*step_ctr) + stream_offset, draw #(row*n_total + column). */
+ * 64*(*step_ctr) + stream_offset, draw #(row*n_total + column). */
 int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
                       const int64_t* step_ctr, int64_t stream_offset, int32_t* out, void* stream);
 
@@ -289,7 +305,7 @@ int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_
  * int(1.1*num_neg/prob) as PyG computes it (host, with duplicate edges counted).
  * population = N(N-1) <= sample_size: the non-edges in ascending order (bit-exact
  * with PyG).  Otherwise `rounds` * sample_size Philox candidates (stream
- * 16*(*step_ctr)+stream_offset), duplicates and existing edges dropped, first
+ * 64*(*step_ctr)+stream_offset), duplicates and existing edges dropped, first
  * num_neg kept in draw order — the law of PyG's sample-without-replacement
  * rounds.  out = int32[2, ld_out] (row 0 = source); *count = columns written
  * (may be < num_neg, as PyG's may). */

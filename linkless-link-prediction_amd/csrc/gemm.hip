@@ -22,6 +22,10 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
                          float drop_p, uint32_t drop_thresh, float drop_scale, uint64_t drop_seed,
                          const int64_t* drop_ctr, int64_t drop_stream, const float* head_w, float* head_part,
                          uint8_t* mask_out, const uint8_t* mask_in, int64_t ld_mask, hipStream_t s);
+int llp_gemm_nt_bf16_splitk(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
+                            int64_t ldc, const float* bias, int relu, uint8_t* mask_out, int64_t ld_mask, int S,
+                            float* slab, hipStream_t s);
+int llp_cu_count();
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q);
 int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
                          float* ws_colsum, int64_t splits, hipStream_t s);
@@ -674,6 +678,49 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
     else hipLaunchKernelGGL((gemm_nt_kernel<float, false>), grid, dim3(NTHREADS), 0, s, p);
   }
   LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+// Split-K plan: worth it when the 256x256 tiles fill under ~5/8 of the CUs and K is long.
+// S = CUs / tiles (one wave of workgroups), at least 8 K-tiles per split, at most 16 slabs.
+extern "C" int llp_gemm_nt_splitk_plan(int64_t M, int64_t N, int64_t K) {
+#ifdef LLP_NO_SPLITK   // A/B build: never split
+  return 1;
+#endif
+  if (M <= 0 || N <= 0 || N % 256 != 0 || K <= 0 || K % 64 != 0) return 1;
+  const int64_t tiles = ((M + 255) / 256) * (N / 256), nkt = K / 64;
+  const int64_t cus = llp_cu_count();
+  if (tiles * 8 > cus * 5 || nkt < 16) return 1;
+  int64_t S = cus / tiles;
+  if (S > nkt / 8) S = nkt / 8;
+  if (S > 16) S = 16;
+  return S < 2 ? 1 : (int)S;
+}
+
+extern "C" int64_t llp_gemm_nt_splitk_ws_bytes(int64_t M, int64_t N, int splits) {
+  return (int64_t)(splits > 0 ? splits : 0) * M * N * (int64_t)sizeof(float);
+}
+
+extern "C" int llp_gemm_nt_splitk(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B, void* C,
+                                  int64_t ldc, const float* bias, int act, void* mask_out, int64_t ld_mask, int splits,
+                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(A && B && C && workspace, "llp_gemm_nt_splitk: null pointer");
+  LLP_CHECK_ARG(act == LLP_ACT_NONE || act == LLP_ACT_RELU, "llp_gemm_nt_splitk: act must be NONE or RELU");
+  LLP_CHECK_ARG(!mask_out || act == LLP_ACT_RELU, "llp_gemm_nt_splitk: a ReLU mask needs act RELU");
+  LLP_CHECK_ARG(splits >= 1 && splits <= 64, "llp_gemm_nt_splitk: splits %d not in 1..64", splits);
+  LLP_CHECK_ARG(M >= 0 && N % 256 == 0 && N > 0 && K % 64 == 0 && K / 64 >= splits,
+                "llp_gemm_nt_splitk: needs N %% 256 == 0, K %% 64 == 0, K/64 >= splits (M=%lld N=%lld K=%lld S=%d)",
+                (long long)M, (long long)N, (long long)K, splits);
+  auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
+  LLP_CHECK_ARG(!A->idx && !A->ptr2 && !A->rows_dev && !B->idx && !B->ptr2 && a16(A->ptr, A->ld) &&
+                    a16(B->ptr, B->ld) && a16(C, ldc) && (!bias || (uintptr_t)bias % 16 == 0),
+                "llp_gemm_nt_splitk: plain 16-B aligned bf16 operands and C, 16-B aligned bias");
+  LLP_CHECK_ARG(workspace_bytes >= llp_gemm_nt_splitk_ws_bytes(M, N, splits) && (uintptr_t)workspace % 16 == 0,
+                "llp_gemm_nt_splitk: workspace too small or misaligned");
+  if (M == 0) return LLP_OK;
+  const int rc = llp_gemm_nt_bf16_splitk(A, B, M, N, K, C, ldc, bias, act == LLP_ACT_RELU ? 1 : 0, (uint8_t*)mask_out,
+                                         ld_mask, splits, (float*)workspace, (hipStream_t)stream);
+  if (rc != 0) return llp::set_error(rc, "llp_gemm_nt_splitk: %s", hipGetErrorString((hipError_t)rc));
   return LLP_OK;
 }
 

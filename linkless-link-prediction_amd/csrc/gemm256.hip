@@ -356,9 +356,13 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // ReLU mask out, no dropout / head / aux; EPI_BWD_MASK: ReLU backward through a bit mask, alpha,
 // no bias / dropout / head.  The host picks the mode (epi_mode_of).
 constexpr int EPI_ANY = 0, EPI_FWD_RELU = 1, EPI_FWD_NONE = 2, EPI_BWD_MASK = 3, EPI_HEAD_RELU = 4;
-// opt-in (LLP_GEMM_HEAD_LEAN=1): EPI_HEAD_RELU with the head dot taken from the staged
-// bf16 outputs in the lean epilogue's second phase (pp8 only; epilogue_lean_head)
+// EPI_HEAD_RELU with the head dot taken from the staged bf16 outputs in the lean
+// epilogue's second phase (pp8 / pp8p; epilogue_lean_head; the host's default)
 constexpr int EPI_HEAD_LEAN = 5;
+// split-K partial (pp8 only): workgroup (tile, blockIdx.y = s) sums K-tiles
+// [nkt*s/S, nkt*(s+1)/S) and stores its raw f32 accumulators to slab s at
+// head_part + s*M*N (row stride N); splitk_reduce_kernel applies the epilogue
+constexpr int EPI_PARTIAL = 6;
 
 // MASK_LDS (TMv 256, NTHR 512 only): the ReLU-backward bit mask of the tile (256 rows x
 // 32 bytes) is read with ONE 16-byte load per thread into LDS at smem + head_off_u4 + 256
@@ -811,6 +815,14 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   const bool dyn = p.m_dev != nullptr;
   const int32_t mlive = dyn ? *p.m_dev : 0;
   if (dyn ? !tile_256_host_interleaved(p, m0, n0) : !tile_256(p, m0, n0)) return;
+  if constexpr (MODE == EPI_PARTIAL) {   // this workgroup's K range and slab
+    const int64_t nkt = p.K / TK, S = gridDim.y, sk = blockIdx.y;
+    const int64_t k0 = nkt * sk / S, k1 = nkt * (sk + 1) / S;
+    p.A += k0 * TK;
+    p.B += k0 * TK;
+    p.K = (k1 - k0) * TK;
+    p.head_part += sk * p.M * p.N;
+  }
 
   const bf16_t* src[4][2];
   int dst_row[4][2];
@@ -950,7 +962,18 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8(P256 p) {
   if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
   LLP_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if constexpr (MODE == EPI_HEAD_LEAN) {   // every tile (the host checked the shapes)
+  if constexpr (MODE == EPI_PARTIAL) {   // raw accumulators: lane (li, g) holds row im*16 + li, columns jn*16 + g*4 ..
+#pragma unroll
+    for (int im = 0; im < 8; ++im) {
+      const int64_t row = m0 + wm * 128 + im * 16 + li;
+      if (row < p.M) {
+        float* dst = p.head_part + row * p.N + n0 + wn * 64 + g * 4;
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) *reinterpret_cast<float4_t*>(dst + jn * 16) = acc[jn][im];
+      }
+    }
+    return;
+  } else if constexpr (MODE == EPI_HEAD_LEAN) {   // every tile (the host checked the shapes)
     __syncthreads();
     epilogue_lean_head(p, acc, smem, m0, n0, tid, wm, wn, g, li);
     return;
@@ -1302,11 +1325,50 @@ int epi_mode_of(const P256& p) {
   return EPI_ANY;
 }
 
+// Split-K epilogue: thread (row, 8-column chunk) sums the S slabs in order (slab 0
+// first), adds the bias, rounds to bf16 (RNE) and applies the lean epilogue's ReLU
+// (sign-bit rule), stores 16 B of C and, with a mask, the chunk's ReLU bit byte
+// (bit i = column 8c + i is nonzero).  Deterministic; the sum differs from the
+// unsplit kernel's only in where the K-range partial sums are added.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(int64_t M, int64_t N, int S, const float* __restrict__ slab,
+                                                            const float* __restrict__ bias, int relu,
+                                                            bf16_t* __restrict__ C, int64_t ldc,
+                                                            uint8_t* __restrict__ mask_out, int64_t ld_mask) {
+  const int64_t cpr = N / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * cpr) return;
+  const int64_t row = i / cpr, c = i % cpr;
+  const float* src = slab + row * N + c * 8;
+  float4_t a = *reinterpret_cast<const float4_t*>(src), b = *reinterpret_cast<const float4_t*>(src + 4);
+  for (int s = 1; s < S; ++s) {
+    a += *reinterpret_cast<const float4_t*>(src + (int64_t)s * M * N);
+    b += *reinterpret_cast<const float4_t*>(src + (int64_t)s * M * N + 4);
+  }
+  if (bias) {
+    a += *reinterpret_cast<const float4_t*>(bias + c * 8);
+    b += *reinterpret_cast<const float4_t*>(bias + c * 8 + 4);
+  }
+  uint32_t w0 = pk_bf16(float2_t{a[0], a[1]}), w1 = pk_bf16(float2_t{a[2], a[3]});
+  uint32_t w2 = pk_bf16(float2_t{b[0], b[1]}), w3 = pk_bf16(float2_t{b[2], b[3]});
+  if (relu) {
+    w0 = relu_pk_bf16(w0); w1 = relu_pk_bf16(w1); w2 = relu_pk_bf16(w2); w3 = relu_pk_bf16(w3);
+  }
+  *reinterpret_cast<uint4*>(C + row * ldc + c * 8) = make_uint4(w0, w1, w2, w3);
+  if (mask_out) {
+    const uint32_t w[4] = {w0, w1, w2, w3};
+    uint32_t byte = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      byte |= ((w[k] & 0xFFFFu) ? 1u : 0u) << (2 * k) | ((w[k] >> 16) ? 1u : 0u) << (2 * k + 1);
+    mask_out[row * ld_mask + c] = (uint8_t)byte;
+  }
+}
+
 }  // namespace
 
-// one workgroup per CU (the persistent kernel's grid)
-static dim3 persistent_grid(int64_t tiles) {
-  static int cus_of[64] = {};   // per device, queried once (a race only repeats the query)
+// CUs of the current device, queried once per device (a race only repeats the query)
+int llp_cu_count() {
+  static int cus_of[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   int cus = cus_of[dev];
@@ -1314,7 +1376,36 @@ static dim3 persistent_grid(int64_t tiles) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     cus_of[dev] = cus;
   }
+  return cus;
+}
+
+// one workgroup per CU (the persistent kernel's grid)
+static dim3 persistent_grid(int64_t tiles) {
+  const int cus = llp_cu_count();
   return dim3((unsigned)(tiles < cus ? tiles : cus));
+}
+
+// Split-K bf16 GEMM (llp_gemm_nt_splitk, gemm.hip): pp8<EPI_PARTIAL> over (tiles, S)
+// into f32 slabs, then splitk_reduce_kernel.  The caller checked the shapes.
+int llp_gemm_nt_bf16_splitk(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
+                            int64_t ldc, const float* bias, int relu, uint8_t* mask_out, int64_t ld_mask, int S,
+                            float* slab, hipStream_t s) {
+  P256 p = {};
+  p.A = (const bf16_t*)A->ptr; p.lda = A->ld;
+  p.B = (const bf16_t*)B->ptr; p.ldb = B->ld;
+  p.M = M; p.N = N; p.K = K;
+  p.C = (bf16_t*)C; p.ldc = ldc;
+  p.alpha = 1.f;
+  p.head_part = slab;
+  p.head_ld = M;
+  const int64_t tiles = ((M + TM - 1) / TM) * (N / TN);
+  hipLaunchKernelGGL(gemm_nt_bf16_pp8<EPI_PARTIAL>, dim3((unsigned)tiles, (unsigned)S), dim3(NT2), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int64_t n = M * (N / 8);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, N, S, slab, bias,
+                     relu, (bf16_t*)C, ldc, mask_out, ld_mask);
+  return (int)hipGetLastError();
 }
 
 // Called from llp_gemm_nt when the shapes allow it (gemm.hip).

@@ -329,6 +329,16 @@ class EngineBase:
     def _ws(self, name, nbytes):
         return self._buf(name, (nbytes // 4 + 16,), torch.float32)
 
+    def _splitk_plan(self, M, N, Kd):
+        """Split count of the bf16 split-K GEMM for this shape (1: the plain GEMM), cached."""
+        if self.dtype != torch.bfloat16:
+            return 1
+        cache = self.__dict__.setdefault("_splitk", {})
+        key = (int(M), int(N), int(Kd))
+        if key not in cache:
+            cache[key] = int(K.gemm_nt_splitk_plan(*key))
+        return cache[key]
+
     def _dropout(self, p, module, layer):
         """Dropout draws of ``layer`` of ``module`` (DROP_ENCODER: the student MLP / the
         teacher's GNN, DROP_PREDICTOR: the trained LinkPredictor, DROP_TEACHER_PRED: the
@@ -973,9 +983,15 @@ class DistillEngine(EngineBase):
             out = self._buf(f"H{l}", (n_loc, lin.out_f), dt)
             hm = None if last else self._mask(f"Hm{l}", n_rows, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
             self._act_mask[id(out)] = hm
-            K.gemm_nt(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, out, dc, bias=lin.b,
-                      act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
-                      dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
+            act = K.ACT_NONE if last else K.ACT_RELU
+            splits = self._splitk_plan(n_rows, lin.out_f, lin.k_in) if p_drop == 0.0 else 1
+            if splits > 1:   # few output tiles over a long K (the first layer at 8,448 features)
+                ws = self._ws("ws_splitk", K.gemm_nt_splitk_ws_bytes(n_rows, lin.out_f, splits))
+                K.gemm_nt_splitk(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, out, splits, ws, bias=lin.b,
+                                 act=act, mask=hm)
+            else:
+                K.gemm_nt(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, out, dc, bias=lin.b, act=act, aux=hm,
+                          dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
             acts.append(out)
             A = K.operand(out)
         if shard is None:

@@ -50,6 +50,10 @@ _SIGS = {
     "llp_gemm_nt_head": (c_int, [c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_vp, c_int,
                                  c_f32, C.POINTER(Dropout), c_vp, c_vp, c_vp]),
     "llp_head_finish": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_gemm_nt_splitk_plan": (c_int, [c_i64, c_i64, c_i64]),
+    "llp_gemm_nt_splitk_ws_bytes": (c_i64, [c_i64, c_i64, c_int]),
+    "llp_gemm_nt_splitk": (c_int, [c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_vp,
+                                   c_int, c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
     "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
     "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_vp, c_i64, c_vp]),
@@ -191,6 +195,24 @@ def gemm_nt(A: Operand, B: Operand, M, N, K, C_out, dtype, bias=None, act=ACT_NO
 
 def head_parts(N):
     return load().llp_gemm_nt_head_parts(N)
+
+
+def gemm_nt_splitk_plan(M, N, K):
+    """Split count for llp_gemm_nt_splitk (1: the plain llp_gemm_nt is the better launch).
+    Host arithmetic only (the CU count falls back to 256 without a device)."""
+    return load().llp_gemm_nt_splitk_plan(M, N, K)
+
+
+def gemm_nt_splitk_ws_bytes(M, N, splits):
+    return load().llp_gemm_nt_splitk_ws_bytes(M, N, splits)
+
+
+def gemm_nt_splitk(A: Operand, B: Operand, M, N, K, C_out, splits, ws, bias=None, act=ACT_NONE, mask=None):
+    """bf16 split-K GEMM: C = act(A.B^T + bias) with an optional ReLU bit mask [M, N/8]."""
+    L = lib()
+    check(L.llp_gemm_nt_splitk(M, N, K, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0), ptr(bias), act,
+                               ptr(mask), mask.stride(0) if mask is not None else 0, splits, ws.data_ptr(),
+                               ws.numel() * ws.element_size(), stream_ptr()), "llp_gemm_nt_splitk")
 
 
 def gemm_nt_head(A: Operand, B: Operand, M, N, K, C_out, head_w, head_part, bias=None, act=ACT_RELU, alpha=1.0,

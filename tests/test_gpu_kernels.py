@@ -930,3 +930,47 @@ def test_gemm_nt_persistent_head_bit_identical(M, N, Kd, with_c):
     assert torch.equal(h1, h2)
     ref = C2.float() @ hw
     assert torch.allclose(h1.sum(0), ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item()))
+
+
+def _mask_bits(m, N):
+    sh = torch.arange(8, device=m.device, dtype=torch.int32)
+    return ((m.to(torch.int32).unsqueeze(-1) >> sh) & 1).reshape(m.shape[0], N)
+
+
+@pytest.mark.parametrize("M,N,Kd,relu", [(31_044, 256, 8_448, True), (7_761, 256, 8_448, True),
+                                         (1_000, 512, 2_048, False)])
+def test_gemm_nt_splitk(M, N, Kd, relu):
+    """Split-K bf16 GEMM (llp_gemm_nt_splitk: f32 slabs over K ranges, one ordered reduce
+    with bias, bf16 rounding, ReLU and the bit mask) at the physics first-layer shapes:
+    deterministic, within bf16 rounding of the fp32 product, equal to the unsplit GEMM
+    except where the two f32 sums round to neighbouring bf16 values, mask == (C != 0)."""
+    k = K()
+    S = k.gemm_nt_splitk_plan(M, N, Kd)
+    assert S > 1
+    g = torch.Generator().manual_seed(M + Kd)
+    A = (torch.rand(M, Kd, generator=g) < 0.05).to(DEV, torch.bfloat16)      # binary features, as coauthor-physics
+    W = (torch.randn(N, Kd, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    act = k.ACT_RELU if relu else k.ACT_NONE
+    ws = torch.empty(k.gemm_nt_splitk_ws_bytes(M, N, S) // 4, device=DEV)
+    C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    m1 = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8) if relu else None
+    k.gemm_nt_splitk(k.operand(A), k.operand(W), M, N, Kd, C1, S, ws, bias=b, act=act, mask=m1)
+    C2 = torch.empty_like(C1)
+    m2 = torch.empty_like(m1) if relu else None
+    k.gemm_nt_splitk(k.operand(A), k.operand(W), M, N, Kd, C2, S, ws, bias=b, act=act, mask=m2)
+    C0 = torch.empty_like(C1)
+    m0 = torch.empty_like(m1) if relu else None
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C0, k.LLP_BF16, bias=b, act=act, aux=m0)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2) and (not relu or torch.equal(m1, m2))
+    ref = A.float() @ W.float().t() + b
+    if relu:
+        ref = torch.relu(ref)
+    err = (C1.float() - ref).abs()
+    assert bool((err <= 2.0 ** -8 * ref.abs() + 1e-5).all()), err.max()
+    diff = C1 != C0
+    assert diff.float().mean().item() < 0.01
+    assert bool(((C1.float() - C0.float()).abs()[diff] <= 2.0 ** -7 * C0.float().abs()[diff] + 1e-6).all())
+    if relu:
+        assert torch.equal(_mask_bits(m1, N), (C1 != 0).to(torch.int32))

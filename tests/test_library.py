@@ -71,3 +71,20 @@ def test_philox_stream_layout_agrees():
     assert m and int(m.group(1)) == llp_engine.STREAMS_PER_STEP == O.STREAMS_PER_STEP
     assert llp_engine.RANDINT_STREAM == O.RANDINT_STREAM and llp_engine.DENSE_NEG_STREAM == O.DENSE_NEG_STREAM
     assert llp_engine.MAX_RW_STEP < llp_engine.DENSE_NEG_STREAM and llp_engine.MAX_RW_STEP >= 60   # negatives at rw_step
+
+
+def test_splitk_plan_host_arithmetic():
+    """llp_gemm_nt_splitk_plan (host only; 256 CUs without a device): split the first
+    full-batch student layer at the coauthor-physics production shape (122 and, at 4
+    ranks, 31 tiles over 132 K-tiles), never a launch that already fills the chip or has
+    a short K, and the slab workspace is S*M*N floats."""
+    import llp_hip
+    plan = llp_hip.gemm_nt_splitk_plan
+    assert plan(31_044, 256, 8_448) == 2
+    assert plan(7_761, 256, 8_448) == 8
+    assert plan(1_000, 512, 2_048) == 4
+    assert plan(225_334, 1024, 1024) == 1       # thousands of tiles
+    assert plan(31_044, 256, 256) == 1          # 4 K-tiles
+    assert plan(1_000, 500, 2_048) == 1         # N not a multiple of 256
+    assert plan(100, 256, 64 * 1000) == 16      # capped at 16 slabs
+    assert llp_hip.gemm_nt_splitk_ws_bytes(7_761, 256, 8) == 8 * 7_761 * 256 * 4
