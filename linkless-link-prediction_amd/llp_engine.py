@@ -961,17 +961,8 @@ class DistillEngine(EngineBase):
             else:
                 K.context_sampler(self.rowptr, self.col, N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                   self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
-        # ---- negatives (src/main.py:205-209)
-        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
-        n_lab = P + n_neg
-        n_lab_total = P_total + n_neg_total
-        BC = Bc * C
-        R2 = BC + n_lab
-        ia_ib = self._buf("fb_iab", (max(2 * R2, 1),), torch.int32)[:2 * R2]   # [ia | ib]: endpoint rows
-        ia, ib = ia_ib[:R2], ia_ib[R2:]
-        K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
-
-        # ---- a4: student MLP over all nodes (src/main.py:173); at several ranks each rank
+        # ---- a4: student MLP over all nodes (src/main.py:173), queued before the dense negatives'
+        # count is read back (one host sync), so the GPU runs it while the host waits; at several ranks each rank
         # runs it on its own slice of the nodes and the slices are all-gathered (_fb_shard)
         shard = self._fb_shard(p_drop, float(a.KD_RM) == 0.0 and self._grouped_ok(H))
         r0, n_rows, n_loc, s_world, s_rank = (0, N, N, 1, 0) if shard is None else shard
@@ -1001,6 +992,16 @@ class DistillEngine(EngineBase):
             h_loc = acts[-1]
             self._collective(lambda: self._all_gather_rows(h_full, h_loc, s_world, s_rank))
             h = h_full[:N]
+
+        # ---- negatives (src/main.py:205-209)
+        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+        n_lab = P + n_neg
+        n_lab_total = P_total + n_neg_total
+        BC = Bc * C
+        R2 = BC + n_lab
+        ia_ib = self._buf("fb_iab", (max(2 * R2, 1),), torch.int32)[:2 * R2]   # [ia | ib]: endpoint rows
+        ia, ib = ia_ib[:R2], ia_ib[R2:]
+        K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
