@@ -411,7 +411,8 @@ int llp_increment(int64_t* ctr, void* stream);
  * epoch's total_loss += loss.item() * num_examples, src/main.py:140-141) and
  * *step_ctr += 1 (the device step counter that keys every Philox stream). */
 int llp_step_end(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, void* stream);
-/* hipMemsetAsync(p, 0, bytes) on the stream. */
+/* Zero `bytes` bytes at p by a kernel (no memset node: a captured hipMemsetAsync node
+ * was measured not to do its work on replay). */
 int llp_zero(void* p, int64_t bytes, void* stream);
 
 /* Elementwise pieces of the module-level autograd ops (models.py):
@@ -432,6 +433,43 @@ int llp_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* 
 int llp_mul(int dtype, int64_t n, const void* a, const void* b, void* out, void* stream);
 int llp_row_scale(int dtype, int64_t rows, int64_t cols, const void* z, const float* s, void* out, void* stream);
 int llp_sigmoid_bwd(int64_t n, const float* gprob, const float* prob, float* out, void* stream);
+
+/* ---------------------------------------------------------------- norm_type
+ * nn.LayerNorm(H) / nn.BatchNorm1d(H) after a hidden layer, fused with the ReLU and
+ * dropout that follow it: MLP.forward src/models.py:45-54 (norms built at :27-37),
+ * SAGE.forward src/models.py:110-119 (:90-101).  y = the layer's pre-norm output
+ * [M, H], out = dropout(relu(norm(y))) [M, H] (relu 0: no ReLU), leading dimensions
+ * ldy / ldo.  stats (f32): mean and 1/sqrt(var + eps), LayerNorm [2][M] per row,
+ * BatchNorm [2][H] per column.  m_dev: optional device row count (LayerNorm only:
+ * rows past it are not touched).  Dropout draw #(r*H + c) of the layer's stream, as
+ * the GEMM epilogue.  Column sums are f64 [2][H], reduced in a fixed order
+ * (deterministic); a batch split over ranks SUM-all-reduces them between the sum call
+ * and the call that consumes them, and then normalises as the whole batch would. */
+enum llp_norm_kind { LLP_NORM_LAYER = 1, LLP_NORM_BATCH = 2 };
+int64_t llp_norm_workspace_bytes(int64_t M, int64_t H);
+/* BatchNorm statistics: sums[0:H] = sum_r y[r, :], sums[H:2H] = sum_r y[r, :]^2. */
+int llp_norm_colsums(int dtype, int64_t M, int64_t H, const void* y, int64_t ldy, const int32_t* m_dev,
+                     double* sums, void* ws, void* stream);
+/* Forward.  LayerNorm: per-row statistics into stats.  BatchNorm, training: mean and
+ * biased variance from sums over `count` rows, running_mean / running_var updated with
+ * `momentum` (unbiased variance) and *num_batches_tracked += 1, as torch's
+ * BatchNorm1d.train(); eval: the running statistics (sums unused). */
+int llp_norm_fwd(int kind, int dtype, int64_t M, int64_t H, const void* y, int64_t ldy, const float* gamma,
+                 const float* beta, float eps, int training, const double* sums, double count, float momentum,
+                 float* running_mean, float* running_var, int64_t* num_batches_tracked, float* stats,
+                 const int32_t* m_dev, int relu, const llp_dropout* dropout, void* out, int64_t ldo, void* stream);
+/* Backward, step 1: g = alpha * gout * (out > 0) (out NULL: no mask), xhat the
+ * normalised y; sums[0:H] = sum_r g, sums[H:2H] = sum_r g * xhat, also written as
+ * dbeta / dgamma (f32, may be NULL) -- this call's rows' share of them. */
+int llp_norm_bwd_sums(int kind, int dtype, int64_t M, int64_t H, const void* gout, int64_t ldg, const void* out,
+                      int64_t ldo, float alpha, const void* y, int64_t ldy, const float* stats, const int32_t* m_dev,
+                      double* sums, float* dgamma, float* dbeta, void* ws, void* stream);
+/* Backward, step 2: gy = d(loss)/dy.  LayerNorm: rstd * (a - mean_c(a) - xhat * mean_c(a * xhat)),
+ * a = gamma * g, per row (sums unused); BatchNorm (training statistics):
+ * gamma * rstd * (g - sums[c] / count - xhat * sums[H + c] / count). */
+int llp_norm_bwd(int kind, int dtype, int64_t M, int64_t H, const void* gout, int64_t ldg, const void* out,
+                 int64_t ldo, float alpha, const void* y, int64_t ldy, const float* gamma, const float* stats,
+                 const double* sums, double count, const int32_t* m_dev, void* gy, int64_t ldgy, void* stream);
 
 #ifdef __cplusplus
 }

@@ -106,6 +106,53 @@ class _Linear:
         return self.Wc if self.Wc is not None else self.W
 
 
+class _Norm:
+    """Device view of one norm module after a hidden layer (``norm_type`` 'layer' /
+    'batch', src/models.py:27-37,90-101): nn.LayerNorm(H) or nn.BatchNorm1d(H) with
+    the reference's defaults (affine; BatchNorm with running statistics, momentum
+    0.1).  gamma / beta are the module's parameters (their .grad views into the flat
+    gradient); BatchNorm's running_mean / running_var / num_batches_tracked buffers
+    are updated in place by the forward kernel, as torch's train() forward does."""
+
+    def __init__(self, m: torch.nn.Module, width: int):
+        if isinstance(m, torch.nn.LayerNorm):
+            self.kind = K.NORM_LAYER
+            if tuple(m.normalized_shape) != (width,):
+                raise NotImplementedError(f"LayerNorm over {tuple(m.normalized_shape)} (the layer is {width} wide)")
+        elif isinstance(m, torch.nn.BatchNorm1d):
+            self.kind = K.NORM_BATCH
+            if m.num_features != width:
+                raise NotImplementedError(f"BatchNorm1d({m.num_features}) after a {width}-wide layer")
+            if not m.track_running_stats or m.momentum is None:
+                raise NotImplementedError("BatchNorm1d with running statistics and a fixed momentum (torch defaults)")
+        else:
+            raise NotImplementedError(f"norm module {type(m).__name__} (norm_type 'layer' or 'batch')")
+        self.m = m
+        self.eps = float(m.eps)
+        self.momentum = float(getattr(m, "momentum", 0.0) or 0.0)
+        self.params = [p for p in (m.weight, m.bias) if p is not None]
+
+    @property
+    def batch(self):
+        return self.kind == K.NORM_BATCH
+
+    def gamma(self):
+        return None if self.m.weight is None else self.m.weight.data
+
+    def beta(self):
+        return None if self.m.bias is None else self.m.bias.data
+
+
+def _norms_of(model, n_hidden, width):
+    """The model's norm modules (one per hidden layer) as _Norm, or [] for norm_type 'none'."""
+    mods = list(getattr(model, "norms", []))
+    if not mods:
+        return []
+    if len(mods) != n_hidden:
+        raise NotImplementedError(f"{len(mods)} norm modules for {n_hidden} hidden layers")
+    return [_Norm(m, width) for m in mods]
+
+
 def _acc_dtype(t):
     """f32, or the tensor's own dtype when that is wider (gloo has no bf16 sums)."""
     return t.dtype if t.dtype in (torch.float32, torch.float64) else torch.float32
@@ -552,6 +599,41 @@ class EngineBase:
         m = self._act_mask.get(id(act))
         return m if m is not None else act
 
+    def _norm_forward(self, nm, tag, y, out, p_drop, module, layer, rows=None, count=0.0, sync=False, training=True):
+        """out = dropout(relu(norm(y))) (src/models.py:49-53 / :114-118).  BatchNorm in
+        training: column sums over this call's rows, SUM-all-reduced across ranks when
+        ``sync`` (each rank holds a different share of the batch), then normalised by the
+        ``count`` rows of the whole batch.  The per-layer statistics stay in buffer
+        nstat_<tag> for the backward."""
+        M, H = y.shape
+        stats = self._buf(f"nstat_{tag}", (2, H if nm.batch else M), torch.float32)
+        sums = None
+        if nm.batch and training:
+            sums = self._buf(f"nsum_{tag}", (2, H), torch.float64)
+            K.norm_colsums(y, sums, self._ws("ws_norm", K.norm_ws_bytes(M, H)))
+            if sync and self.world > 1:
+                self._collective(lambda: dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group))
+        m = nm.m
+        K.norm_fwd(nm.kind, y, out, stats, nm.gamma(), nm.beta(), nm.eps, training, sums, count, nm.momentum,
+                   getattr(m, "running_mean", None), getattr(m, "running_var", None),
+                   getattr(m, "num_batches_tracked", None), relu=True,
+                   dropout=self._dropout(p_drop, module, layer) if training else None, rows=rows)
+
+    def _norm_backward(self, nm, tag, gout, out, alpha, y, gy, rows=None, count=0.0, sync=False):
+        """gy = d(loss)/dy of _norm_forward from gout = d(loss)/dout; gamma / beta gradients
+        (this rank's rows) into the module's .grad.  BatchNorm's sum(g), sum(g*xhat) are
+        SUM-all-reduced across ranks when ``sync`` before they enter gy."""
+        M, H = y.shape
+        stats = self._buf(f"nstat_{tag}", (2, H if nm.batch else M), torch.float32)
+        sums = self._buf(f"nsumb_{tag}", (2, H), torch.float64)
+        m = nm.m
+        K.norm_bwd_sums(nm.kind, gout, out, alpha, y, stats, sums, self._ws("ws_norm", K.norm_ws_bytes(M, H)),
+                        dgamma=None if m.weight is None else m.weight.grad,
+                        dbeta=None if m.bias is None else m.bias.grad, rows=rows)
+        if nm.batch and sync and self.world > 1:
+            self._collective(lambda: dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group))
+        K.norm_bwd(nm.kind, gout, out, alpha, y, stats, gy, nm.gamma(), sums, count, rows=rows)
+
     def _allreduce_tail_begin(self):
         """Start the SUM all-reduce of the predictor's gradients on RCCL's stream
         (async; it waits for the kernels already queued) so it overlaps the
@@ -684,7 +766,10 @@ class DistillEngine(EngineBase):
             l0.k_in = self.F_pad
         for l in self.stu:
             self._set_shadow(l.lin.weight, l.Wc, l.Wt, l.k_in if l.Wc is not None else 0)
-        stu_params = [p for l in stu for p in (l.weight, l.bias)]
+        # norm_type 'layer' / 'batch' (src/models.py:27-37): a norm after every hidden layer, its
+        # parameters after the Linear ones, as in model.parameters()
+        self.stu_norms = _norms_of(model, len(stu) - 1, self.stu[0].out_f if len(stu) > 1 else 0)
+        stu_params = [p for l in stu for p in (l.weight, l.bias)] + [p for n in self.stu_norms for p in n.params]
         prd_params = self._setup_predictor(predictor, args.predictor)
         self._init_params(stu_params + prd_params, [0] * len(stu_params) + [1] * len(prd_params), optimizer)
 
@@ -814,7 +899,8 @@ class DistillEngine(EngineBase):
         # ---- unique-node compaction: without dropout the student is a row-wise
         # function, so duplicate rows of x[this_target] give identical activations;
         # run it on the U distinct nodes and sum each node's row gradients.
-        dedup = self.dedup and p_drop == 0.0 and self._grouped_ok(H)
+        # (BatchNorm's statistics run over every row of x[this_target], duplicates included: row-wise student)
+        dedup = self.dedup and p_drop == 0.0 and self._grouped_ok(H) and not self._batch_norm
         n_u = None
         if dedup:
             fresh = "uniq" not in self._bufs or self._bufs["uniq"].numel() < R1
@@ -854,6 +940,7 @@ class DistillEngine(EngineBase):
             A = K.operand(x_rows, count=n_u)
         else:
             A = K.operand(self.x, gather_s, count=n_u)
+        R1_total = B_total * C1 + 2 * (P_total + n_neg_total)    # this_target rows of the whole batch
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (rows_s, lin.out_f), dt)
@@ -861,11 +948,19 @@ class DistillEngine(EngineBase):
             if timed:   # the dominant MFMA kernel, timed on the launch stream (bench.py roofline)
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            hm = None if last else self._mask(f"Hm{l}", rows_s, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
-            self._act_mask[id(out)] = hm
-            K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.k_in, out, dc, bias=lin.b,
-                      act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
-                      dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
+            if not last and self.stu_norms:
+                # Linear, then norm + ReLU + dropout (src/models.py:48-53)
+                y = self._buf(f"Y{l}", (rows_s, lin.out_f), dt)
+                K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.k_in, y, dc, bias=lin.b)
+                self._norm_forward(self.stu_norms[l], f"s{l}", y, out, p_drop, DROP_ENCODER, l, rows=n_u,
+                                   count=R1_total, sync=True)
+                self._act_mask[id(out)] = None
+            else:
+                hm = None if last else self._mask(f"Hm{l}", rows_s, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
+                self._act_mask[id(out)] = hm
+                K.gemm_nt(A, K.operand(lin.Wcomp), rows_s, lin.out_f, lin.k_in, out, dc, bias=lin.b,
+                          act=K.ACT_NONE if last else K.ACT_RELU, aux=hm,
+                          dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
             if timed:
                 ev[1].record()
                 kernel_events.append(ev)
@@ -917,9 +1012,14 @@ class DistillEngine(EngineBase):
                 K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh, count=n_u)
             else:
                 dh = dh_rows
-        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap, x_rows=x_rows)
+        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap, x_rows=x_rows,
+                               norm_count=R1_total, norm_sync=True)
         self._allreduce_and_update()
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
+
+    @property
+    def _batch_norm(self):
+        return any(n.batch for n in self.stu_norms)
 
     # ------------------------------------------------------------------ full-batch step
     def step_fullbatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
@@ -975,14 +1075,26 @@ class DistillEngine(EngineBase):
             hm = None if last else self._mask(f"Hm{l}", n_rows, lin.out_f, lin.k_in, self.stu[l + 1].out_f)
             self._act_mask[id(out)] = hm
             act = K.ACT_NONE if last else K.ACT_RELU
-            splits = self._splitk_plan(n_rows, lin.out_f, lin.k_in) if p_drop == 0.0 else 1
+            normed = not last and bool(self.stu_norms)
+            if normed:   # Linear, then norm + ReLU + dropout (src/models.py:48-53)
+                hm, act = None, K.ACT_NONE
+                self._act_mask[id(out)] = None
+                dst = self._buf(f"Y{l}", (n_loc, lin.out_f), dt)
+            else:
+                dst = out
+            splits = self._splitk_plan(n_rows, lin.out_f, lin.k_in) if (p_drop == 0.0 or normed) else 1
             if splits > 1:   # few output tiles over a long K (the first layer at 8,448 features)
                 ws = self._ws("ws_splitk", K.gemm_nt_splitk_ws_bytes(n_rows, lin.out_f, splits))
-                K.gemm_nt_splitk(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, out, splits, ws, bias=lin.b,
+                K.gemm_nt_splitk(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, dst, splits, ws, bias=lin.b,
                                  act=act, mask=hm)
             else:
-                K.gemm_nt(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, out, dc, bias=lin.b, act=act, aux=hm,
-                          dropout=None if last else self._dropout(p_drop, DROP_ENCODER, l))
+                K.gemm_nt(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, dst, dc, bias=lin.b, act=act, aux=hm,
+                          dropout=None if (last or normed) else self._dropout(p_drop, DROP_ENCODER, l))
+            if normed:
+                # the student is replicated (or row-sharded, LayerNorm only) over the ranks: BatchNorm's
+                # statistics are over all N nodes on every rank, no exchange
+                self._norm_forward(self.stu_norms[l], f"s{l}", dst[:n_rows], out[:n_rows], p_drop, DROP_ENCODER, l,
+                                   count=n_rows)
             acts.append(out)
             A = K.operand(out)
         if shard is None:
@@ -1069,7 +1181,8 @@ class DistillEngine(EngineBase):
             else:
                 dh = self._buf("gS0", (N, H), dt)
                 K.convert(dh32, dh)
-        self._student_backward(dh, n_rows, None, acts, p_drop, x_rows=None if shard is None else x_loc)
+        self._student_backward(dh, n_rows, None, acts, p_drop, x_rows=None if shard is None else x_loc,
+                               norm_count=n_rows)
         self._allreduce_and_update()
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
         return n_neg
@@ -1088,8 +1201,8 @@ class DistillEngine(EngineBase):
         world, rank = self.world, self.rank
         if world <= 1 and self.emulate_shard is not None:
             rank, world = self.emulate_shard
-        if world <= 1 or not self.shard_student or p_drop > 0.0 or not grouped:
-            return None
+        if world <= 1 or not self.shard_student or p_drop > 0.0 or not grouped or self._batch_norm:
+            return None   # (BatchNorm: statistics over all N nodes, so the student stays replicated)
         n_loc = -(-self.N // world)
         if self.N - (world - 1) * n_loc <= 0:   # a rank without rows: off on every rank alike
             return None
@@ -1189,11 +1302,14 @@ class DistillEngine(EngineBase):
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, overlap=False, x_rows=None):
+    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, overlap=False, x_rows=None, norm_count=0.0,
+                          norm_sync=False):
         """count: int32 device row count (unique-node student) or None.  dh lives in
         buffer 'gS0'.  overlap: weight-gradient GEMMs on the side stream, as in
         _predictor_backward (three data-gradient buffers).  x_rows: x[target]
-        materialised by the forward (else the first layer's input is gathered)."""
+        materialised by the forward (else the first layer's input is gathered).
+        norm_count / norm_sync: BatchNorm's batch row count and whether its sums are
+        all-reduced across ranks (_norm_backward)."""
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
         names = ["gS0", "gS1", "gS2"] if overlap & 4 else ["gS0", "gS1"]
@@ -1224,5 +1340,13 @@ class DistillEngine(EngineBase):
                 k += 1
                 self._before_write(names[k % len(names)])
                 gnext = self._buf(names[k % len(names)], (R1, lin.in_f), dt)
-                K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
-                          act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)
+                if self.stu_norms:
+                    # d(post-ReLU/dropout activations), then through the norm into d(pre-norm output)
+                    graw = self._buf("gN", (R1, lin.in_f), dt)
+                    K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, graw, dc)
+                    y = self._buf(f"Y{l - 1}", (R1, lin.in_f), dt)
+                    self._norm_backward(self.stu_norms[l - 1], f"s{l - 1}", graw, acts[l - 1], alpha, y, gnext,
+                                        rows=count, count=norm_count, sync=norm_sync)
+                else:
+                    K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
+                              act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)

@@ -77,19 +77,32 @@ class EdgeScorer:
 
 @torch.no_grad()
 def embed_mlp(model, x: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
-    """model(x) for the student MLP in eval mode (no dropout, src/models.py:45-54)."""
+    """model(x) for the student MLP in eval mode (no dropout, src/models.py:45-54; with
+    norm_type 'layer' / 'batch' the norm runs in eval mode, BatchNorm on its running
+    statistics)."""
     if x.device.type != "cuda":
         raise RuntimeError("embed_mlp runs only on a HIP device (no CPU fallback)")
     dc = K.dtype_code(dtype)
     A = K.operand(x.to(dtype).contiguous())
     layers = list(model.layers)
+    norms = list(getattr(model, "norms", []))
     h = None
     M = x.shape[0]
     for l, lin in enumerate(layers):
+        last = l == len(layers) - 1
         W = lin.weight.detach().to(dtype).contiguous()
         h = torch.empty(M, W.shape[0], dtype=dtype, device=x.device)
+        normed = norms and not last
         K.gemm_nt(A, K.operand(W), M, W.shape[0], W.shape[1], h, dc, bias=lin.bias.detach().float(),
-                  act=K.ACT_NONE if l == len(layers) - 1 else K.ACT_RELU)
+                  act=K.ACT_NONE if (last or normed) else K.ACT_RELU)
+        if normed:
+            nm = norms[l]
+            batch = isinstance(nm, torch.nn.BatchNorm1d)
+            stats = torch.empty(2, W.shape[0] if batch else M, dtype=torch.float32, device=x.device)
+            K.norm_fwd(K.NORM_BATCH if batch else K.NORM_LAYER, h, h, stats,
+                       None if nm.weight is None else nm.weight.detach(), None if nm.bias is None else nm.bias.detach(),
+                       float(nm.eps), not batch, running_mean=getattr(nm, "running_mean", None),
+                       running_var=getattr(nm, "running_var", None), relu=True)
         A = K.operand(h)
     return h
 

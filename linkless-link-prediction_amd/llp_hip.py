@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("LLP_LIB", os.path.join(HERE, "libllp_hip.so"))   # LL
 
 LLP_F32, LLP_BF16, LLP_MASK = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_RELU_BWD = 0, 1, 2
+NORM_LAYER, NORM_BATCH = 1, 2
 
 c_i64 = C.c_int64
 c_int = C.c_int
@@ -114,6 +115,14 @@ _SIGS = {
     "llp_mul": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_row_scale": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_sigmoid_bwd": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_norm_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_norm_colsums": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_norm_fwd": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_int, c_vp, c_f64, c_f32,
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_int, C.POINTER(Dropout), c_vp, c_i64, c_vp]),
+    "llp_norm_bwd_sums": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp,
+                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "llp_norm_bwd": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_vp, c_i64, c_vp, c_vp,
+                             c_vp, c_f64, c_vp, c_vp, c_i64, c_vp]),
 }
 
 _lib = None
@@ -576,3 +585,51 @@ def sigmoid_bwd(gprob, prob, out):
     L = lib()
     check(L.llp_sigmoid_bwd(prob.numel(), gprob.data_ptr(), prob.data_ptr(), out.data_ptr(), stream_ptr()),
           "llp_sigmoid_bwd")
+
+
+# ------------------------------------------------------------------ norm_type (src/models.py:27-37,50-51,90-101,114-115)
+def _ld(t):
+    assert t.dim() == 2 and t.stride(1) == 1
+    return t.stride(0)
+
+
+def norm_ws_bytes(M, H):
+    return int(load().llp_norm_workspace_bytes(int(M), int(H)))
+
+
+def norm_colsums(y, sums, ws, count=None):
+    """sums (f64 [2, H]) = column sums of y and y*y (BatchNorm statistics)."""
+    L = lib()
+    check(L.llp_norm_colsums(dtype_code(y.dtype), y.shape[0], y.shape[1], y.data_ptr(), _ld(y), ptr(count),
+                             sums.data_ptr(), ws.data_ptr(), stream_ptr()), "llp_norm_colsums")
+
+
+def norm_fwd(kind, y, out, stats, gamma=None, beta=None, eps=1e-5, training=True, sums=None, count=0.0,
+             momentum=0.1, running_mean=None, running_var=None, num_batches_tracked=None, relu=True,
+             dropout: Dropout | None = None, rows=None):
+    """out = dropout(relu(norm(y))); stats f32 [2, M] (layer) / [2, H] (batch)."""
+    L = lib()
+    check(L.llp_norm_fwd(int(kind), dtype_code(y.dtype), y.shape[0], y.shape[1], y.data_ptr(), _ld(y), ptr(gamma),
+                         ptr(beta), float(eps), int(bool(training)), ptr(sums), float(count), float(momentum),
+                         ptr(running_mean), ptr(running_var), ptr(num_batches_tracked), stats.data_ptr(), ptr(rows),
+                         int(bool(relu)), C.byref(dropout) if dropout is not None else None, out.data_ptr(), _ld(out),
+                         stream_ptr()), "llp_norm_fwd")
+
+
+def norm_bwd_sums(kind, gout, out, alpha, y, stats, sums, ws, dgamma=None, dbeta=None, rows=None):
+    """sums (f64 [2, H]) = column sums of g and g*xhat, g = alpha * gout * (out > 0);
+    also written to dbeta / dgamma when given."""
+    L = lib()
+    check(L.llp_norm_bwd_sums(int(kind), dtype_code(y.dtype), y.shape[0], y.shape[1], gout.data_ptr(), _ld(gout),
+                              ptr(out), _ld(out) if out is not None else 0, float(alpha), y.data_ptr(), _ld(y),
+                              stats.data_ptr(), ptr(rows), sums.data_ptr(), ptr(dgamma), ptr(dbeta), ws.data_ptr(),
+                              stream_ptr()), "llp_norm_bwd_sums")
+
+
+def norm_bwd(kind, gout, out, alpha, y, stats, gy, gamma=None, sums=None, count=0.0, rows=None):
+    """gy = d(loss)/dy through dropout(relu(norm(y)))."""
+    L = lib()
+    check(L.llp_norm_bwd(int(kind), dtype_code(y.dtype), y.shape[0], y.shape[1], gout.data_ptr(), _ld(gout), ptr(out),
+                         _ld(out) if out is not None else 0, float(alpha), y.data_ptr(), _ld(y), ptr(gamma),
+                         stats.data_ptr(), ptr(sums), float(count), ptr(rows), gy.data_ptr(), _ld(gy), stream_ptr()),
+          "llp_norm_bwd")

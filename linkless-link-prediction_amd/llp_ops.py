@@ -143,6 +143,75 @@ def relu_dropout(x, p=0.0, training=False):
     return _ReluDropout.apply(x2d, float(p), bool(training)).reshape(x.shape)
 
 
+class _NormAct(torch.autograd.Function):
+    """dropout(relu(norm(y))) with norm an nn.LayerNorm / nn.BatchNorm1d module
+    (norm_type 'layer' / 'batch', src/models.py:50-53, :114-118).  BatchNorm in train
+    mode normalises by the batch statistics and updates the module's running
+    statistics in place (torch's BatchNorm1d.train()); in eval mode it uses them."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, mod, p, training):
+        M, H = y.shape
+        batch = isinstance(mod, torch.nn.BatchNorm1d)
+        kind = K.NORM_BATCH if batch else K.NORM_LAYER
+        bn_train = batch and (training or not mod.track_running_stats)
+        stats = torch.empty(2, H if batch else M, dtype=torch.float32, device=y.device)
+        ws = torch.empty(K.norm_ws_bytes(M, H), dtype=torch.uint8, device=y.device)
+        sums = None
+        if bn_train:
+            if mod.momentum is None and mod.track_running_stats:
+                raise NotImplementedError("BatchNorm1d(momentum=None) (cumulative average)")
+            sums = torch.empty(2, H, dtype=torch.float64, device=y.device)
+            K.norm_colsums(y, sums, ws)
+        drop = None
+        if training and p > 0:
+            drop = K.Dropout(float(p), _dropout_seed(), _dropout_state(y.device).data_ptr(), 5)
+        out = torch.empty_like(y)
+        upd = batch and training and mod.track_running_stats
+        K.norm_fwd(kind, y, out, stats, None if gamma is None else gamma.detach(),
+                   None if beta is None else beta.detach(), float(mod.eps), bn_train or not batch, sums, float(M),
+                   float(getattr(mod, "momentum", 0.0) or 0.0), mod.running_mean if upd or (batch and not bn_train) else None,
+                   mod.running_var if upd or (batch and not bn_train) else None,
+                   mod.num_batches_tracked if upd else None, relu=True, dropout=drop)
+        if drop is not None:
+            K.increment(_dropout_state(y.device))
+        ctx.save_for_backward(y, out, stats, gamma)
+        ctx.kind, ctx.batch, ctx.bn_train = kind, batch, bn_train
+        ctx.alpha = 1.0 / (1.0 - p) if (training and p > 0) else 1.0
+        ctx.has = (gamma is not None, beta is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        y, out, stats, gamma = ctx.saved_tensors
+        if ctx.batch and not ctx.bn_train:
+            raise NotImplementedError("backward through BatchNorm1d in eval mode")
+        M, H = y.shape
+        gout = gout.contiguous()
+        ws = torch.empty(K.norm_ws_bytes(M, H), dtype=torch.uint8, device=y.device)
+        sums = torch.empty(2, H, dtype=torch.float64, device=y.device)
+        dgamma = torch.empty(H, dtype=torch.float32, device=y.device) if ctx.has[0] else None
+        dbeta = torch.empty(H, dtype=torch.float32, device=y.device) if ctx.has[1] else None
+        K.norm_bwd_sums(ctx.kind, gout, out, ctx.alpha, y, stats, sums, ws, dgamma=dgamma, dbeta=dbeta)
+        gy = torch.empty_like(y)
+        K.norm_bwd(ctx.kind, gout, out, ctx.alpha, y, stats, gy, None if gamma is None else gamma.detach(), sums,
+                   float(M))
+        return gy, dgamma, dbeta, None, None, None
+
+
+def norm_act(y, mod, p=0.0, training=False):
+    """dropout(relu(mod(y))) for mod an nn.LayerNorm(H) / nn.BatchNorm1d(H)."""
+    _require_cuda(y)
+    y2d = _row2d(y)
+    if isinstance(mod, torch.nn.LayerNorm) and tuple(mod.normalized_shape) != (y2d.shape[1],):
+        raise NotImplementedError(f"LayerNorm over {tuple(mod.normalized_shape)}")
+    if not isinstance(mod, (torch.nn.LayerNorm, torch.nn.BatchNorm1d)):
+        raise NotImplementedError(type(mod).__name__)
+    w = getattr(mod, "weight", None)
+    b = getattr(mod, "bias", None)
+    return _NormAct.apply(y2d, w, b, mod, float(p), bool(training)).reshape(y.shape)
+
+
 class _Head(torch.autograd.Function):
     """sigmoid(z w + b) (w = None: sigmoid(sum(z * z2))) — LinkPredictor's tail."""
 

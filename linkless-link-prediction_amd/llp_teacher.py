@@ -40,13 +40,14 @@ import numpy as np
 import torch
 
 import llp_hip as K
-from llp_engine import DROP_ENCODER, EngineBase
+from llp_engine import DROP_ENCODER, EngineBase, _norms_of
 from llp_sage import GCNConv, Graph, SAGEConv_updated
 
 
 class TeacherEngine(EngineBase):
     """``model``: models.SAGE (convs of SAGEConv or SAGEConv_updated, root_weight,
-    norm_type 'none') or models.GCN (GCNConv with bias); ``predictor``: LinkPredictor; ``x``: node features;
+    norm_type 'none' / 'layer' / 'batch') or models.GCN (GCNConv with bias); ``predictor``: LinkPredictor;
+    ``x``: node features;
     ``edge_index``: the message-passing graph (data.adj_t / data.edge_index,
     src/train_teacher_gnn.py:23-27,43-46); ``optimizer``: Adam over
     model.parameters() + predictor.parameters()."""
@@ -58,8 +59,6 @@ class TeacherEngine(EngineBase):
         N = self.N
         dt = self.dtype
         self.model, self.predictor = model, predictor
-        if getattr(model, "norm_type", "none") != "none":
-            raise NotImplementedError("SAGE norm_type other than 'none' (not used by the reference scripts)")
         self.convs = list(model.convs)
         self.gcn = isinstance(self.convs[0], GCNConv)
         self.updated = isinstance(self.convs[0], SAGEConv_updated)
@@ -68,6 +67,9 @@ class TeacherEngine(EngineBase):
                 raise NotImplementedError("all convs GCNConv with bias")
         elif any(isinstance(c, SAGEConv_updated) != self.updated or not c.root_weight for c in self.convs):
             raise NotImplementedError("all convs of one flavour, with root_weight")
+        # norm_type 'layer' / 'batch' (src/models.py:90-101,114-115): conv, norm, ReLU, dropout.  The
+        # encoder runs on the whole graph on every rank, so BatchNorm's statistics need no exchange.
+        self.norms = _norms_of(model, len(self.convs) - 1, self._conv_out(self.convs[0]))
         self.p_drop = float(model.dropout)
         ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
         self.graph = Graph(ei, N, self.dev, gcn=self.gcn)
@@ -130,7 +132,7 @@ class TeacherEngine(EngineBase):
         # ReLU(+dropout) bit masks of the SAGEConv layer inputs (bf16): layer l-1's forward GEMM
         # writes bit (output > 0) of layer l's input, layer l's data-gradient GEMM reads it in
         # place of the bf16 activations (16x less epilogue traffic); both on the 256-tile path
-        if not (self.gcn or self.updated) and dt == torch.bfloat16:
+        if not (self.gcn or self.updated or self.norms) and dt == torch.bfloat16:
             for l in range(1, len(self.layers)):
                 P_, L = self.layers[l - 1], self.layers[l]
                 if L["F"] % 32 == 0 and (2 * P_["F"]) % 64 == 0 and (2 * L["O"]) % 64 == 0:
@@ -139,6 +141,10 @@ class TeacherEngine(EngineBase):
         self.out_dim = self.layers[-1]["O"]
         self.h = torch.empty(N, self.out_dim, dtype=dt, device=self.dev)
         self._build_descs()
+
+    @staticmethod
+    def _conv_out(conv):
+        return conv.lin.weight.shape[0] if isinstance(conv, GCNConv) else conv.lin_l.weight.shape[0]
 
     # ------------------------------------------------------------------ encoder
     def _encode(self, training: bool):
@@ -166,7 +172,11 @@ class TeacherEngine(EngineBase):
                 YY = L["YY"]
                 K.gemm_nt(K.operand(L["X"]), K.operand(L["Wf"]), N, 2 * O, F, YY, dc, bias=L["bias"])
                 K.csr_aggregate(N, O, g.rowptr, g.col, YY[:, :O], None, 0, YY[:, O:], accumulate=True)
-                K.act_2d(YY[:, O:], self.h if last else nxt["X"], act=act, dropout=drop)
+                if self.norms and not last:
+                    self._norm_forward(self.norms[l], f"t{l}", YY[:, O:], nxt["X"], self.p_drop, DROP_ENCODER, l,
+                                       count=N, training=training)
+                else:
+                    K.act_2d(YY[:, O:], self.h if last else nxt["X"], act=act, dropout=drop)
             else:
                 XA = L["XA"]
                 # the first layer aggregates the raw features (no dropout before it,
@@ -175,9 +185,20 @@ class TeacherEngine(EngineBase):
                     K.csr_aggregate(N, F, g.rowptr, g.col, XA[:, F:], None, 0, XA[:, :F])
                     self._agg0_done = l == 0 or self._agg0_done
                 out = self.h if last else nxt["X"]
-                K.gemm_nt(K.operand(XA), K.operand(L["Wf"]), N, O, 2 * F, out, dc, bias=L["bias"], act=act,
-                          aux=None if last else nxt.get("M"), dropout=drop)
+                if self.norms and not last:
+                    Y = self._buf(f"tY{l}", (N, O), self.dtype)
+                    K.gemm_nt(K.operand(XA), K.operand(L["Wf"]), N, O, 2 * F, Y, dc, bias=L["bias"])
+                    self._norm_forward(self.norms[l], f"t{l}", Y, out, self.p_drop, DROP_ENCODER, l, count=N,
+                                       training=training)
+                else:
+                    K.gemm_nt(K.operand(XA), K.operand(L["Wf"]), N, O, 2 * F, out, dc, bias=L["bias"], act=act,
+                              aux=None if last else nxt.get("M"), dropout=drop)
         return self.h
+
+    def _pre_norm(self, l):
+        """Layer l's pre-norm output (its conv output) [N, O]."""
+        L = self.layers[l]
+        return L["YY"][:, L["O"]:] if self.updated else self._buf(f"tY{l}", (self.N, L["O"]), self.dtype)
 
     def _dh_slot(self):
         """The last layer's output-gradient slot [N, O] (compute dtype): d(loss)/dh lands here."""
@@ -219,6 +240,13 @@ class TeacherEngine(EngineBase):
                 # dX = [G | dOut] . [W_l^T | W_r^T]^T, ReLU/dropout mask of layer l-1 in the epilogue,
                 # written straight into layer l-1's output-gradient slot
                 prev = self.layers[l - 1]
+                if self.norms:
+                    # d(layer l's input) = d(dropout(relu(norm(y_{l-1})))), then through the norm
+                    graw = self._buf("tgN", (N, F), dt)
+                    K.gemm_nt(K.operand(G), K.operand(L["WT"]), N, F, 2 * O, graw, dc)
+                    self._norm_backward(self.norms[l - 1], f"t{l - 1}", graw, L["X"], alpha, self._pre_norm(l - 1),
+                                        prev["G"][:, prev["O"]:], count=N)
+                    continue
                 mask = L.get("M")
                 K.gemm_nt(K.operand(G), K.operand(L["WT"]), N, F, 2 * O, prev["G"][:, prev["O"]:], dc,
                           act=K.ACT_RELU_BWD, aux=L["X"] if mask is None else mask, alpha=alpha)

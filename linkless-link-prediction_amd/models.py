@@ -9,8 +9,10 @@
 State-dict keys match (``layers.{i}.weight``, ``lins.{i}.weight``,
 ``convs.{i}.lin_l.weight`` ...), so teacher/student checkpoints written by the
 reference load here and vice versa.  Forward/backward run as HIP kernels; a CPU
-tensor raises (no fallback).  norm_type 'batch'/'layer' (never set by the
-reference's scripts or CLIs) is not implemented.
+tensor raises (no fallback).  norm_type 'batch' / 'layer' (never set by the
+reference's scripts or CLIs, but part of its Python API) builds nn.BatchNorm1d /
+nn.LayerNorm after every hidden layer, as the reference does, and runs them as the
+fused norm + ReLU + dropout kernels (csrc/norm.hip).
 """
 import torch
 import torch.nn as nn
@@ -21,8 +23,6 @@ import llp_ops as ops
 class MLP(nn.Module):
     def __init__(self, num_layers, input_dim, hidden_dim, output_dim, dropout_ratio, norm_type="none"):
         super().__init__()
-        if norm_type != "none":
-            raise NotImplementedError("MLP norm_type other than 'none' (not on the LLP path, SURVEY §8f)")
         self.num_layers = num_layers
         self.norm_type = norm_type
         self.dropout = nn.Dropout(dropout_ratio)
@@ -32,8 +32,10 @@ class MLP(nn.Module):
             self.layers.append(nn.Linear(input_dim, output_dim))
         else:
             self.layers.append(nn.Linear(input_dim, hidden_dim))
+            _add_norm(self.norms, norm_type, hidden_dim)
             for _ in range(num_layers - 2):
                 self.layers.append(nn.Linear(hidden_dim, hidden_dim))
+                _add_norm(self.norms, norm_type, hidden_dim)
             self.layers.append(nn.Linear(hidden_dim, output_dim))
 
     def reset_parameters(self):
@@ -41,14 +43,26 @@ class MLP(nn.Module):
             layer.reset_parameters()
 
     def forward(self, feats):
-        # Linear, then ReLU + dropout on every layer but the last (src/models.py:45-54),
-        # ReLU and dropout fused into the GEMM epilogue.
+        # Linear, then (norm +) ReLU + dropout on every layer but the last (src/models.py:45-54),
+        # ReLU and dropout fused into the GEMM epilogue, or into the norm kernel.
         h = feats
         for l, layer in enumerate(self.layers):
             last = l == self.num_layers - 1
+            if not last and self.norm_type != "none":
+                h = ops.linear(h, layer.weight, layer.bias)
+                h = ops.norm_act(h, self.norms[l], p=self.dropout.p, training=self.training)
+                continue
             h = ops.linear(h, layer.weight, layer.bias, relu=not last,
                            dropout=0.0 if last else self.dropout.p, training=self.training)
         return h
+
+
+def _add_norm(norms, norm_type, width):
+    """src/models.py:27-30,34-37,90-93,98-101: BatchNorm1d / LayerNorm per hidden layer."""
+    if norm_type == "batch":
+        norms.append(nn.BatchNorm1d(width))
+    elif norm_type == "layer":
+        norms.append(nn.LayerNorm(width))
 
 
 class GCN(nn.Module):
@@ -84,15 +98,15 @@ class SAGE(nn.Module):
     def __init__(self, data_name, in_channels, hidden_channels, out_channels, num_layers, dropout, conv_layer,
                  norm_type="none"):
         super().__init__()
-        if norm_type != "none":
-            raise NotImplementedError("SAGE norm_type other than 'none' (not used by the reference scripts)")
         self.data_name = data_name
-        self.norm_type = norm_type
         self.convs = nn.ModuleList()
         self.norms = nn.ModuleList()
+        self.norm_type = norm_type
+        _add_norm(self.norms, norm_type, hidden_channels)
         self.convs.append(conv_layer(in_channels, hidden_channels))
         for _ in range(num_layers - 2):
             self.convs.append(conv_layer(hidden_channels, hidden_channels))
+            _add_norm(self.norms, norm_type, hidden_channels)
         self.convs.append(conv_layer(hidden_channels, out_channels))
         self.dropout = dropout
 
@@ -101,9 +115,12 @@ class SAGE(nn.Module):
             conv.reset_parameters()
 
     def forward(self, x, adj_t):
-        for conv in self.convs[:-1]:
+        for l, conv in enumerate(self.convs[:-1]):
             x = conv(x, adj_t)
-            x = ops.relu_dropout(x, self.dropout, self.training)
+            if self.norm_type != "none":
+                x = ops.norm_act(x, self.norms[l], self.dropout, self.training)
+            else:
+                x = ops.relu_dropout(x, self.dropout, self.training)
         return self.convs[-1](x, adj_t)
 
 

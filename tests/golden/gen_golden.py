@@ -208,7 +208,18 @@ def flat_log(rec: Recorder):
     return list(rec.log)
 
 
-def run_minibatch_case(name, ref_models, N, F_, H, L, E_und, lbs, args_over, seed, nepochs=1):
+def _norm_records(out, model, x_eval, norm_type):
+    """norm_type cases: parameter / buffer names of the student, its eval-mode output."""
+    out["norm_type"] = np.array(norm_type)
+    out["stu_param_keys"] = np.array([n for n, _ in model.named_parameters()])
+    out["stu_buffer_keys"] = np.array([n for n, _ in model.named_buffers()])
+    model.eval()
+    with torch.no_grad():
+        out["h_eval"] = model(x_eval).numpy()
+    model.train()
+
+
+def run_minibatch_case(name, ref_models, N, F_, H, L, E_und, lbs, args_over, seed, nepochs=1, norm_type="none"):
     rec = Recorder()
     ns = load_reference_main(rec, rw_seed=seed + 11, neg_seed=seed + 12)
     torch.manual_seed(seed)
@@ -224,7 +235,8 @@ def run_minibatch_case(name, ref_models, N, F_, H, L, E_und, lbs, args_over, see
     for k, v in args_over.items():
         setattr(args, k, v)
     args.node_batch_size = int(N / (pairs.size(0) / args.link_batch_size))          # main.py:335
-    model = ref_models.MLP(args.num_layers, F_, H, H, args.dropout)
+    model = ref_models.MLP(args.num_layers, F_, H, H, args.dropout, norm_type)
+    _perturb_norms(model)
     predictor = ref_models.LinkPredictor(args.predictor, H, H, 1, args.num_layers, args.dropout)
     tpred = ref_models.LinkPredictor(args.predictor, 256, 256, 1, 2, args.dropout)
     for p in tpred.parameters():
@@ -249,6 +261,8 @@ def run_minibatch_case(name, ref_models, N, F_, H, L, E_und, lbs, args_over, see
     for k, v in predictor.state_dict().items():
         out[f"final/pred/{k}"] = v.numpy()
     _dump_log(out, rec, kind_order="minibatch", args=args)
+    if norm_type != "none":
+        _norm_records(out, model, x, norm_type)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
     print(name, "steps:", out["nsteps"], "epoch losses:", losses)
 
@@ -295,7 +309,18 @@ def _dump_log(out, rec, kind_order, args):
             out[f"step{s}/grad{i}"] = g.numpy()
 
 
-def run_fullbatch_case(name, ref_models, N, F_, E_und, lbs, args_over, seed, transductive="transductive"):
+def _perturb_norms(model):
+    """Non-trivial affine parameters (torch initialises them to 1 / 0) so that the norms'
+    gamma and beta enter every gradient; the generator leaves torch's global RNG alone."""
+    g = torch.Generator().manual_seed(77)
+    with torch.no_grad():
+        for m in getattr(model, "norms", []):
+            m.weight.copy_(1.0 + 0.2 * torch.randn(m.weight.shape, generator=g))
+            m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=g))
+
+
+def run_fullbatch_case(name, ref_models, N, F_, E_und, lbs, args_over, seed, transductive="transductive",
+                       norm_type="none"):
     rec = Recorder()
     ns = load_reference_main(rec, rw_seed=seed + 21, neg_seed=seed + 22)
     torch.manual_seed(seed)
@@ -317,7 +342,8 @@ def run_fullbatch_case(name, ref_models, N, F_, E_und, lbs, args_over, seed, tra
         data = types.SimpleNamespace(x=x, edge_index=ei)
         split_edge = None
         args.node_batch_size = int(N / (ei.size(1) / args.link_batch_size))       # main.py:348
-    model = ref_models.MLP(args.num_layers, F_, H, H, args.dropout)
+    model = ref_models.MLP(args.num_layers, F_, H, H, args.dropout, norm_type)
+    _perturb_norms(model)
     predictor = ref_models.LinkPredictor(args.predictor, H, H, 1, args.num_layers, args.dropout)
     tpred = ref_models.LinkPredictor(args.predictor, 256, 256, 1, 2, args.dropout)
     for p in tpred.parameters():
@@ -340,6 +366,8 @@ def run_fullbatch_case(name, ref_models, N, F_, E_und, lbs, args_over, seed, tra
     for k, v in predictor.state_dict().items():
         out[f"final/pred/{k}"] = v.numpy()
     _dump_log(out, rec, kind_order="fullbatch", args=args)
+    if norm_type != "none":
+        _norm_records(out, model, x, norm_type)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
     print(name, "steps:", out["nsteps"], "epoch loss:", loss)
 
@@ -383,6 +411,34 @@ def run_model_case(name, ref_models, seed):
         out.update({f"lp_{kind}/xi": xi.detach().numpy(), f"lp_{kind}/xj": xj.detach().numpy(),
                     f"lp_{kind}/out": o.detach().numpy(), f"lp_{kind}/gout": go.numpy(),
                     f"lp_{kind}/gxi": xi.grad.numpy(), f"lp_{kind}/gxj": xj.grad.numpy()})
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def run_norm_model_case(name, ref_models, seed):
+    """Reference MLP with norm_type 'layer' / 'batch' (src/models.py:6-54): train-mode
+    forward + backward (BatchNorm on batch statistics, running statistics updated),
+    then an eval-mode forward on the running statistics."""
+    torch.manual_seed(seed)
+    out = {}
+    for norm in ("layer", "batch"):
+        mlp = ref_models.MLP(3, 24, 40, 40, 0.0, norm)
+        _perturb_norms(mlp)
+        x = torch.randn(67, 24, requires_grad=True)
+        y = mlp(x)
+        gy = torch.randn_like(y)
+        y.backward(gy)
+        mlp.eval()
+        with torch.no_grad():
+            x2 = torch.randn(31, 24)
+            y2 = mlp(x2)
+        pre = f"mlp_{norm}"
+        out.update({f"{pre}/{k}": v.detach().numpy() for k, v in mlp.state_dict().items()})
+        out.update({f"{pre}/x": x.detach().numpy(), f"{pre}/y": y.detach().numpy(), f"{pre}/gy": gy.numpy(),
+                    f"{pre}/gx": x.grad.numpy(), f"{pre}/x_eval": x2.numpy(), f"{pre}/y_eval": y2.numpy()})
+        out[f"{pre}/param_keys"] = np.array([n for n, _ in mlp.named_parameters()])
+        out[f"{pre}/state_keys"] = np.array(list(mlp.state_dict().keys()))
+        for k, p in mlp.named_parameters():
+            out[f"{pre}/grad/{k}"] = p.grad.numpy()
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
@@ -531,7 +587,7 @@ def load_reference_teacher_train(rec: Recorder, neg_seed: int):
 
 
 def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, dataset="cora", epochs=2,
-                     encoder="sage", self_loops=0):
+                     encoder="sage", self_loops=0, norm_type="none"):
     rec = Recorder()
     ref_mods, ref_updated = load_reference_sage()
     train = load_reference_teacher_train(rec, neg_seed=seed + 31)
@@ -548,7 +604,8 @@ def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, 
             nn.init.uniform_(c.bias, -0.1, 0.1)
     else:
         conv_layer = ref_updated if updated else ref_mods.SAGE.__init__.__globals__["SAGEConv"]
-        model = ref_mods.SAGE(dataset, F_, H, H, L, 0.0, conv_layer)
+        model = ref_mods.SAGE(dataset, F_, H, H, L, 0.0, conv_layer, norm_type)
+        _perturb_norms(model)
     predictor = ref_mods.LinkPredictor("mlp", H, H, 1, 2, 0.0)
     init_enc = {k: v.clone() for k, v in model.state_dict().items()}
     init_pred = {k: v.clone() for k, v in predictor.state_dict().items()}
@@ -575,6 +632,8 @@ def run_teacher_case(name, N, F_, H, L, E_und, bs, updated, transductive, seed, 
     for k, v in predictor.state_dict().items():
         out[f"final/pred/{k}"] = v.numpy()
     out["enc_keys"] = np.array(list(init_enc.keys()))
+    out["enc_param_keys"] = np.array([n for n, _ in model.named_parameters()])
+    out["norm_type"] = np.array(norm_type)
     out["pred_keys"] = np.array(list(init_pred.keys()))
     _dump_log(out, rec, kind_order="teacher", args=None)
     # eval-mode embedding after training (src/train_teacher_gnn.py:87): the saved teacher features
@@ -875,8 +934,29 @@ def run_logger_case(name):
         json.dump(cases, f, indent=1)
 
 
+def main_norm(ref_models):
+    """norm_type 'layer' / 'batch' (src/models.py:14,27-37,84-101): the student in the
+    minibatch and full-batch steps, the SAGE teacher, and the modules alone."""
+    run_norm_model_case("models_norm_fwd_bwd", ref_models, 3)
+    run_minibatch_case("minibatch_layernorm_small", ref_models, N=257, F_=16, H=32, L=3, E_und=300, lbs=128,
+                       args_over={}, seed=23, nepochs=1, norm_type="layer")
+    run_minibatch_case("minibatch_batchnorm_small", ref_models, N=211, F_=16, H=32, L=3, E_und=260, lbs=96,
+                       args_over={}, seed=24, nepochs=1, norm_type="batch")
+    run_fullbatch_case("fullbatch_batchnorm_small", ref_models, N=120, F_=40, E_und=260, lbs=96, args_over={},
+                       seed=25, norm_type="batch")
+    run_fullbatch_case("fullbatch_layernorm_small", ref_models, N=90, F_=30, E_und=180, lbs=1024,
+                       args_over=dict(KD_RM=0.0, KD_LM=0.0, LLP_D=1.0, LLP_R=0.5, hops=1, ns_rate=4),
+                       seed=26, transductive="production", norm_type="layer")
+    run_teacher_case("teacher_sage_batchnorm_small", N=130, F_=16, H=32, L=3, E_und=500, bs=200, updated=False,
+                     transductive="transductive", seed=27, norm_type="batch")
+    run_teacher_case("teacher_updated_layernorm_small", N=100, F_=48, H=64, L=3, E_und=350, bs=256,
+                     updated=True, transductive="production", seed=29, norm_type="layer")
+
+
 def main():
     ref_models = load_reference_models()
+    if os.environ.get("GOLDEN_ONLY") == "norm":
+        return main_norm(ref_models)
     run_edge_split_case("edge_split_small", N=200, E_und=700, seed=14)
     run_edge_split_case("edge_split_fast_small", N=150, E_und=500, seed=15, fast_split=True)
     if os.environ.get("GOLDEN_ONLY") == "edge_split":
@@ -918,6 +998,7 @@ def main():
     run_fullbatch_case("fullbatch_production_small", ref_models, N=90, F_=30, E_und=180, lbs=1024,
                        args_over=dict(KD_RM=0.0, KD_LM=0.0, LLP_D=1.0, LLP_R=0.5, hops=1, ns_rate=4),
                        seed=6, transductive="production")
+    main_norm(ref_models)
 
 
 if __name__ == "__main__":

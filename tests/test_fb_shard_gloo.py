@@ -77,7 +77,8 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     prob = _problem()
     N, x, t_h, samples, edge, neg, (sw, sb, pw, pb, tw, tb), args = prob
-    fake = types.SimpleNamespace(world=world, rank=rank, group=None, N=N, emulate_shard=None, shard_student=True)
+    fake = types.SimpleNamespace(world=world, rank=rank, group=None, N=N, emulate_shard=None, shard_student=True,
+                                 _batch_norm=False)
     r0, n_rows, n_loc, s_world, s_rank = llp_engine.DistillEngine._fb_shard(fake, 0.0, True)
     assert (s_world, s_rank, n_loc) == (world, rank, -(-N // world))
     lw = [w.clone().requires_grad_() for w in sw]
@@ -146,9 +147,11 @@ def test_fb_shard_gating():
     sys.path.insert(0, os.path.join(REPO, "linkless-link-prediction_amd"))
     import llp_engine
     f = llp_engine.DistillEngine._fb_shard
-    ns = lambda **kw: types.SimpleNamespace(**{"emulate_shard": None, "shard_student": True, **kw})
+    ns = lambda **kw: types.SimpleNamespace(**{"emulate_shard": None, "shard_student": True, "_batch_norm": False,
+                                               **kw})
     eng = ns(world=4, rank=3, N=10)
     assert f(eng, 0.0, True) == (9, 1, 3, 4, 3)
+    assert f(ns(world=4, rank=3, N=10, _batch_norm=True), 0.0, True) is None   # BatchNorm: replicated student
     eng.shard_student = False
     assert f(eng, 0.0, True) is None
     eng.shard_student = True

@@ -76,11 +76,12 @@ def test_engine_replays_reference_minibatch(name):
     import models
     case = G.load_case(name)
     a = case.args
-    model = models.MLP(case.L, case.F, case.H, case.H, float(a.dropout)).to(DEV)
+    model = models.MLP(case.L, case.F, case.H, case.H, float(a.dropout), case.norm_type).to(DEV)
     pred = models.LinkPredictor(a.predictor, case.H, case.H, 1, case.L, float(a.dropout)).to(DEV)
     tpred = models.LinkPredictor(a.predictor, 256, 256, 1, 2, float(a.dropout)).to(DEV)
+    G.set_state(model, case.stu0, case.stu_buf0)
     with torch.no_grad():
-        for p, v in zip(list(model.parameters()) + list(pred.parameters()), case.stu0 + case.pred0):
+        for p, v in zip(pred.parameters(), case.pred0):
             p.copy_(v)
         for p, v in zip(tpred.parameters(), case.tpred):
             p.copy_(v)
@@ -119,10 +120,32 @@ def test_engine_replays_reference_minibatch(name):
     # whatever its gradient's size, so a ~0 gradient whose sign depends on the
     # summation order can move it the other way (bounded by 2*lr per step).
     lr = float(a.lr)
-    for p, ref in zip(list(model.parameters()) + list(pred.parameters()), case.stu_final + case.pred_final):
+    check_final_student(name, case, model, pred, lr)
+
+
+def check_final_student(name, case, model, pred, lr):
+    """Final parameters, BatchNorm running statistics, and the eval-mode student
+    (llp_eval.embed_mlp) on the reference's final state."""
+    import llp_eval
+    free = G.free_params(case)
+    for i, (p, ref) in enumerate(zip(list(model.parameters()) + list(pred.parameters()),
+                                     case.stu_final + case.pred_final)):
         d = (p.detach().cpu() - ref).abs()
-        assert (d <= 1e-4).float().mean().item() > 0.99, (name, tuple(p.shape), d.max().item())
+        if i not in free:
+            assert (d <= 1e-4).float().mean().item() > 0.99, (name, tuple(p.shape), d.max().item())
         assert d.max().item() <= 2 * lr * len(case.steps), (name, tuple(p.shape), d.max().item())
+    if case.norm_type == "batch":   # running mean: follows the free biases (momentum x their bound)
+        shift = 0.1 * 2 * lr * len(case.steps)
+        for b, ref, nm in zip(model.buffers(), case.stu_buf_final, case.stu_buffer_names):
+            tol = 1e-5 + (shift if nm.endswith("running_mean") else 0.0)
+            assert (b.detach().cpu().to(ref.dtype) - ref).abs().max().item() <= tol + 1e-4 * ref.abs().max().item(), \
+                (name, nm)
+    if case.h_eval is not None:
+        G.set_state(model, case.stu_final, case.stu_buf_final)
+        model.eval()
+        he = llp_eval.embed_mlp(model, case.x.to(DEV)).cpu()
+        model.train()
+        assert torch.allclose(he, case.h_eval, rtol=1e-4, atol=1e-5), (name, (he - case.h_eval).abs().max())
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

@@ -93,11 +93,12 @@ def _engine(case, dtype="fp32"):
     import llp_engine
     import models
     a = case.args
-    model = models.MLP(case.L, case.F, case.H, case.H, float(a.dropout)).to(DEV)
+    model = models.MLP(case.L, case.F, case.H, case.H, float(a.dropout), case.norm_type).to(DEV)
     pred = models.LinkPredictor(a.predictor, case.H, case.H, 1, case.L, float(a.dropout)).to(DEV)
     tpred = models.LinkPredictor(a.predictor, 256, 256, 1, 2, float(a.dropout)).to(DEV)
+    G.set_state(model, case.stu0, case.stu_buf0)
     with torch.no_grad():
-        for p, v in zip(list(model.parameters()) + list(pred.parameters()), case.stu0 + case.pred0):
+        for p, v in zip(pred.parameters(), case.pred0):
             p.copy_(v)
         for p, v in zip(tpred.parameters(), case.tpred):
             p.copy_(v)
@@ -141,11 +142,8 @@ def test_engine_replays_reference_fullbatch(name):
             assert abs(ep - case.epoch_losses[(i + 1) // steps_per_epoch - 1]) < 1e-4, ep
             tot_ex = 0
             eng.begin_epoch()
-    lr = float(a.lr)
-    for p, ref in zip(list(model.parameters()) + list(pred.parameters()), case.stu_final + case.pred_final):
-        d = (p.detach().cpu() - ref).abs()
-        assert (d <= 1e-4).float().mean().item() > 0.99, (name, tuple(p.shape), d.max().item())
-        assert d.max().item() <= 2 * lr * len(case.steps), (name, tuple(p.shape), d.max().item())
+    from test_gpu_engine import check_final_student
+    check_final_student(name, case, model, pred, float(a.lr))
 
 
 def test_fullbatch_device_negatives_and_bf16():

@@ -40,7 +40,7 @@ def _problem(N=2000, n_pairs=12000, B=256, P=1024):
     return N, F_, H, L, pairs, ei, x, t_h, anchors, links, args
 
 
-def _run(rank, world, dtype, port, out):
+def _run(rank, world, dtype, port, out, norm_type="none"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "linkless-link-prediction_amd"))
@@ -54,7 +54,7 @@ def _run(rank, world, dtype, port, out):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     N, F_, H, L, pairs, ei, x, t_h, anchors, links, args = _problem()
     torch.manual_seed(3)
-    model = models.MLP(L, F_, H, H, 0.0).to(dev)
+    model = models.MLP(L, F_, H, H, 0.0, norm_type).to(dev)
     pred = models.LinkPredictor("mlp", H, H, 1, L, 0.0).to(dev)
     tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
     for p in tpred.parameters():
@@ -79,6 +79,7 @@ def _run(rank, world, dtype, port, out):
         out["params"] = [p.detach().cpu().numpy().copy() for p in list(model.parameters()) + list(pred.parameters())]
         out["grads"] = [p.grad.detach().cpu().numpy().copy() for p in
                         list(model.parameters()) + list(pred.parameters())]
+        out["buffers"] = [b.detach().cpu().numpy().copy() for b in model.buffers()]
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -178,7 +179,7 @@ def test_two_ranks_segmented_graph_matches_eager(size):
         assert np.array_equal(a, b)
 
 
-def _run_fullbatch(rank, world, port, out, shard=True):
+def _run_fullbatch(rank, world, port, out, shard=True, norm_type="none"):
     """Two full-batch steps (train(), src/main.py:167-235: the student over all
     nodes, PyG-dense negatives) of this rank's shard: the BASELINE configs[3] path."""
     import sys
@@ -196,7 +197,7 @@ def _run_fullbatch(rank, world, port, out, shard=True):
     args = types.SimpleNamespace(**{**vars(args), "KD_RM": 0.0, "KD_LM": 0.0, "LLP_D": 10.0, "LLP_R": 0.01,
                                     "True_label": 0.1, "margin": 0.2})
     torch.manual_seed(3)
-    model = models.MLP(2, F_, H, H, 0.0).to(dev)
+    model = models.MLP(2, F_, H, H, 0.0, norm_type).to(dev)
     pred = models.LinkPredictor("mlp", H, H, 1, 2, 0.0).to(dev)
     tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(dev)
     for p in tpred.parameters():
@@ -224,9 +225,9 @@ def _run_fullbatch(rank, world, port, out, shard=True):
         dist.destroy_process_group()
 
 
-def _fullbatch_worker(rank, world, port, q, shard):
+def _fullbatch_worker(rank, world, port, q, shard, norm_type="none"):
     out = {}
-    _run_fullbatch(rank, world, port, out, shard)
+    _run_fullbatch(rank, world, port, out, shard, norm_type)
     if rank == 0:
         q.put(out)
 
@@ -249,13 +250,22 @@ def test_two_ranks_fullbatch_replicated_student_equal_one_rank():
     _fullbatch_compare(shard=False)
 
 
-def _fullbatch_compare(shard=True):
+@pytest.mark.parametrize("norm_type", ["layer", "batch"])
+def test_two_ranks_fullbatch_norm_equal_one_rank(norm_type):
+    """norm_type 'layer' (row-wise: the node-sharded student) and 'batch' (the student
+    stays replicated: statistics over all nodes on every rank, no exchange)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _fullbatch_compare(norm_type=norm_type, free={1} if norm_type == "batch" else set())
+
+
+def _fullbatch_compare(shard=True, norm_type="none", free=()):
     single = {}
-    _run_fullbatch(0, 1, 0, single, shard)
+    _run_fullbatch(0, 1, 0, single, shard, norm_type)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fullbatch_worker, args=(r, 2, port, q, shard)) for r in range(2)]
+    procs = [ctx.Process(target=_fullbatch_worker, args=(r, 2, port, q, shard, norm_type)) for r in range(2)]
     for p in procs:
         p.start()
     multi = q.get(timeout=300)
@@ -266,15 +276,50 @@ def _fullbatch_compare(shard=True):
     for a, b in zip(multi["grads"], single["grads"]):
         err = float(abs(a - b).max())
         assert err <= 2e-3 * max(float(abs(b).max()), 1e-6) + 1e-7, err
-    for a, b in zip(multi["params"], single["params"]):
-        assert float((abs(a - b) <= 1e-4).mean()) > 0.99
+    for i, (a, b) in enumerate(zip(multi["params"], single["params"])):
+        if i not in free:   # (a Linear bias feeding a BatchNorm: zero gradient, Adam moves it on noise)
+            assert float((abs(a - b) <= 1e-4).mean()) > 0.99
 
 
-def _worker(rank, world, dtype, port, q):
+def _worker(rank, world, dtype, port, q, norm_type="none"):
     out = {}
-    _run(rank, world, dtype, port, out)
+    _run(rank, world, dtype, port, out, norm_type)
     if rank == 0:
         q.put(out)
+
+
+@pytest.mark.parametrize("norm_type", ["layer", "batch"])
+def test_two_ranks_norm_equal_one_rank(norm_type):
+    """norm_type 'layer' / 'batch' student in the minibatch step over 2 ranks == 1 rank.
+    BatchNorm: each rank sums its rows' statistics (and the backward's sums), the sums
+    are all-reduced, so the shards normalise as the whole batch does."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    single = {}
+    _run(0, 1, "fp32", 0, single, norm_type)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, "fp32", port, q, norm_type)) for r in range(2)]
+    for p in procs:
+        p.start()
+    multi = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert abs(multi["loss"] - single["loss"]) <= 1e-4 * max(1.0, abs(single["loss"])), (multi["loss"], single["loss"])
+    L = 3
+    free = {2 * l + 1 for l in range(L - 1)} if norm_type == "batch" else set()
+    for i, (a, b) in enumerate(zip(multi["grads"], single["grads"])):
+        err = float(abs(a - b).max())
+        assert err <= 2e-3 * max(float(abs(b).max()), 1e-6) + 1e-7, (i, err)
+    for i, (a, b) in enumerate(zip(multi["params"], single["params"])):
+        if i not in free:
+            assert float((abs(a - b) <= 1e-4).mean()) > 0.99, i
+    # BatchNorm running statistics and step counter (the running mean follows the free biases of the
+    # second step's forward: momentum 0.1 x 2 lr)
+    for a, b in zip(multi["buffers"], single["buffers"]):
+        assert float(abs(a.astype("float64") - b.astype("float64")).max()) <= 0.1 * 2 * 0.01 + 1e-4
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
