@@ -173,6 +173,32 @@ def evaluate(model, pred, data, dev):
 SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_sage.json")
 
 
+def practical_peak(dev, seconds=0.2):
+    """bf16 MFMA FLOP/s this device sustains on random operands (llp_mfma_probe: a bare
+    v_mfma_f32_16x16x32_bf16 loop on every CU, two waves per SIMD), event-timed on the
+    launch stream: the clock the chip holds under dense MFMA load on random data sets it
+    well under the 2.5 PF/s spec (MI355X_MICROARCH.md, DVFS give-back)."""
+    import llp_hip as K
+    g = torch.Generator(device="cpu").manual_seed(11)
+    data = torch.randn(1 << 16, generator=g).to(torch.bfloat16).to(dev)
+    out = torch.empty(K.mfma_probe_out_floats(), dtype=torch.float32, device=dev)
+    iters = 20000
+    K.mfma_probe(data, iters, out)      # warm-up, and a first estimate of the rate
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    fl = K.mfma_probe(data, iters, out)
+    e1.record()
+    torch.cuda.synchronize()
+    rate = fl / (e0.elapsed_time(e1) * 1e-3)
+    iters = max(1000, int(iters * seconds / (fl / rate)))
+    e0.record()
+    fl = K.mfma_probe(data, iters, out)
+    e1.record()
+    torch.cuda.synchronize()
+    return fl / (e0.elapsed_time(e1) * 1e-3) / 1e12
+
+
 def sage_aggregate(data, dev):
     """SAGE teacher's CSR mean aggregate (a11, src/sageconv_updated.py:65-81 / PyG SAGEConv mean)
     at the collab shape, forward, F = 128 and 256, fp32 and bf16, event-timed live.
@@ -499,6 +525,12 @@ def main():
             "loss": loss,
             "hipgraph": bool(graph is not None),
         }
+        if opt.dtype == "bf16":
+            pp = practical_peak(dev)
+            res["roofline"].update(practical_peak=pp, practical_frac=achieved / pp,
+                                   practical_note="bare v_mfma_f32_16x16x32_bf16 loop on random operands, every CU, "
+                                                  "timed here (llp_mfma_probe): the FLOP/s the chip sustains at the "
+                                                  "clock it holds under dense MFMA load")
         if not opt.no_eval:
             res.update(evaluate(model, pred, data, dev))
         if world == 1 and not opt.no_shard8 and not opt.profile_kernels:

@@ -471,6 +471,16 @@ int llp_norm_bwd(int kind, int dtype, int64_t M, int64_t H, const void* gout, in
                  int64_t ldo, float alpha, const void* y, int64_t ldy, const float* gamma, const float* stats,
                  const double* sums, double count, const int32_t* m_dev, void* gy, int64_t ldgy, void* stream);
 
+/* ---------------------------------------------------------------- diagnostics
+ * Practical bf16 MFMA ceiling (bench.py roofline.practical_peak): one 512-thread
+ * workgroup per CU issues v_mfma_f32_16x16x32_bf16 back to back on register operands
+ * taken from `data` (n_u4 16-byte chunks of random bf16), `iters` iterations of 16
+ * MFMAs over 4 x 4 operand pairs into 8 accumulators per wave; *flops = the FLOP count
+ * of the launch (host);
+ * out (llp_mfma_probe_out_floats() floats) keeps the accumulators live. */
+int llp_mfma_probe(const void* data, int64_t n_u4, int64_t iters, float* out, double* flops, void* stream);
+int64_t llp_mfma_probe_out_floats(void);
+
 #ifdef __cplusplus
 }
 #endif

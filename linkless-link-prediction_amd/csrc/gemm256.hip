@@ -1191,6 +1191,16 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     // the last K-tile: the next tile's K-tile 0 into buffer 0 (nk is even) when prefetching
     ktile(nk - 1, pf, 0, m1, n1, 0);
     if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
+#ifdef LLP_DIAG_EPI_SKIP
+    // diagnostic build (tools/gemm_epi_cost.py): no epilogue at all, the accumulators kept live
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) asm volatile("" ::"v"(acc[a][b]));
+    if (!pf) return;
+    t = t_next; m0 = m1; n0 = n1;
+    continue;
+#endif
     // ---- lean epilogue in two 128-row halves, staged in [64 KB, 130 KB): buffer 0 receives
     // the next tile's K-tile 0 meanwhile.  Its per-thread addresses derive from an opaque
     // copy of the thread id, so hipcc cannot hoist them above the main loop (where they
@@ -1265,10 +1275,16 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
           const u32x4 sv = {v.x, v.y, v.z, v.w};
           u32x4* dst = reinterpret_cast<u32x4*>(cbase + ii * cstep + toff);
           const bool live = rl0 + 16 * ii < rows;
+#ifdef LLP_DIAG_EPI_NOSTORE
+          // diagnostic build (tools/gemm_epi_cost.py): the staged values are read, not stored
+          asm volatile("" ::"v"(sv), "v"(dst));
+          (void)live;
+#else
           if (live && st) {
             if constexpr (decltype(NTS)::value) __builtin_nontemporal_store(sv, dst);
             else *dst = sv;
           }
+#endif
           if (RELU) {
             if (mo) {
               const uint32_t u = nz_pk_u16(v.x, ones) | (nz_pk_u16(v.y, ones) << 2) | (nz_pk_u16(v.z, ones) << 4) |

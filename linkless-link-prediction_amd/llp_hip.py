@@ -115,6 +115,8 @@ _SIGS = {
     "llp_mul": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_row_scale": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_sigmoid_bwd": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "llp_mfma_probe": (c_int, [c_vp, c_i64, c_i64, c_vp, C.POINTER(c_f64), c_vp]),
+    "llp_mfma_probe_out_floats": (c_i64, []),
     "llp_norm_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_norm_colsums": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_norm_fwd": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_int, c_vp, c_f64, c_f32,
@@ -633,3 +635,17 @@ def norm_bwd(kind, gout, out, alpha, y, stats, gy, gamma=None, sums=None, count=
                          _ld(out) if out is not None else 0, float(alpha), y.data_ptr(), _ld(y), ptr(gamma),
                          stats.data_ptr(), ptr(sums), float(count), ptr(rows), gy.data_ptr(), _ld(gy), stream_ptr()),
           "llp_norm_bwd")
+
+
+# ------------------------------------------------------------------ diagnostics
+def mfma_probe(data, iters, out):
+    """Launch the bare-MFMA ceiling loop (llp_mfma_probe); returns its FLOP count."""
+    L = lib()
+    fl = c_f64(0.0)
+    check(L.llp_mfma_probe(data.data_ptr(), data.numel() * data.element_size() // 16, int(iters), out.data_ptr(),
+                           C.byref(fl), stream_ptr()), "llp_mfma_probe")
+    return fl.value
+
+
+def mfma_probe_out_floats():
+    return int(lib().llp_mfma_probe_out_floats())
