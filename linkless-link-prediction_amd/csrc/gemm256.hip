@@ -1064,8 +1064,24 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     while (t < n_tiles && !tile_of(t, m0, n0)) t += gridDim.x;
     return t < n_tiles;
   };
+#ifdef LLP_GEMM_WALK_RANGE
+  // A/B build: workgroup b takes the contiguous tile range [b T / G, (b + 1) T / G) of the
+  // live tiles in (m-tile, n-tile) order, so one workgroup runs an m-tile's n-tiles back to
+  // back (its A panel re-read from the Infinity Cache) instead of four workgroups fetching
+  // it together
+  const int64_t T_live = tilesM * tilesN, G = gridDim.x;
+  const int64_t t_end = T_live * (blockIdx.x + 1) / G;
+  int64_t t = T_live * blockIdx.x / G, m0 = 0, n0 = 0;
+  auto tile_at = [&](int64_t i, int64_t& mm, int64_t& nn) -> bool {
+    mm = (i / tilesN) * TM;
+    nn = (i % tilesN) * TN;
+    return i < t_end;
+  };
+  if (!tile_at(t, m0, n0)) return;
+#else
   int64_t t = blockIdx.x, m0 = 0, n0 = 0;
   if (!next_tile(t, m0, n0)) return;
+#endif
 
   // DMA in SADDR form: a wave-uniform base (the tile's row panel at the K-tile) and a per-lane
   // 32-bit byte offset computed per piece: row q64_row(..) + lane / 8 of the tile, clamped to
@@ -1140,8 +1156,13 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   for (int j = 0; j < 4; ++j) issue_chunk(j, 0, m0, n0, 0);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // chunks 0, 1 landed
   for (;;) {
+#ifdef LLP_GEMM_WALK_RANGE
+    int64_t t_next = t + 1, m1 = 0, n1 = 0;
+    const bool pf = tile_at(t_next, m1, n1);
+#else
     int64_t t_next = t + gridDim.x, m1 = 0, n1 = 0;
     const bool pf = next_tile(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
+#endif
     const int64_t rows = min((int64_t)TM, p.M - m0);  // live rows (the last m-tile may be partial)
     // this tile's bias and (ReLU backward) mask tile into LDS by DMA; older than its K-tile 1
     if (BWD) {
@@ -1232,15 +1253,19 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     char* mbase = mo ? reinterpret_cast<char*>(p.mask_out + m0 * p.ld_mask + (n0 >> 3)) : nullptr;
     const uint32_t moff = (uint32_t)(rl0 * p.ld_mask + c);
     const int64_t mstep = 16 * p.ld_mask;
+    // round h stages the tile's rows [64h, 64h + 64) and [128 + 64h, 128 + 64h + 64): every
+    // wave converts half of its accumulators per round (staged row = group * 64 + local row),
+    // so no wave group waits out the other's conversion
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (ewm == h) {   // phase 1: this wave group's 128 rows (local row im*16 + li)
-        char* sb = stg + eli * ROWB + (ewn * 64 + eg * 4) * 2;
+      {   // phase 1: this wave's rows (4h + im') * 16 + li of its group's 128, im' < 4
+        char* sb = stg + (ewm * 64 + eli) * ROWB + (ewn * 64 + eg * 4) * 2;
 #pragma unroll
         for (int jn = 0; jn < 4; ++jn) {
           const float2_t b01 = {bl[jn][0], bl[jn][1]}, b23 = {bl[jn][2], bl[jn][3]};
 #pragma unroll
-          for (int im = 0; im < 8; ++im) {
+          for (int iq = 0; iq < 4; ++iq) {
+            const int im = 4 * h + iq;
             float2_t v01 = {acc[jn][im][0], acc[jn][im][1]}, v23 = {acc[jn][im][2], acc[jn][im][3]};
             if (BWD) {
               v01 = __builtin_elementwise_fma(v01, al, z2);
@@ -1251,19 +1276,19 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
             }
             uint32_t lo = pk_bf16(v01), hi = pk_bf16(v23);
             if (RELU || HEAD) { lo = relu_pk_bf16(lo); hi = relu_pk_bf16(hi); }
-            *reinterpret_cast<uint2*>(sb + im * 16 * ROWB + jn * 32) = make_uint2(lo, hi);
+            *reinterpret_cast<uint2*>(sb + iq * 16 * ROWB + jn * 32) = make_uint2(lo, hi);
           }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier();
-      // phase 2: all threads, rows rl0 + 16 i (i < 8) of this half
+      // phase 2: all threads, staged rows rl0 + 16 i (i < 8) of this round
       const char* rb = stg + rl0 * ROWB + c * 16;
       auto run = [&](auto NTS) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           uint4 v = *reinterpret_cast<const uint4*>(rb + i * 16 * ROWB);
-          const int ii = 8 * h + i;   // 16-row group of the tile
+          const int ii = i + 4 * h + (i >= 4 ? 4 : 0);   // 16-row group of the tile
           if (BWD) {
             const uint32_t bits = mlds[(rl0 + 16 * ii) * 32 + c];
             v.x &= half_mask<0>(bits, lo16);

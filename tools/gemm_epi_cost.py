@@ -1,7 +1,9 @@
 """Price of the persistent NT GEMM's epilogue: the M x 1024 x 1024 ReLU-forward launch
 (random bf16 operands, event-timed medians) of the default library against diagnostic
 builds without the epilogue's C stores (LLP_DIAG_EPI_NOSTORE) and without any epilogue
-(LLP_DIAG_EPI_SKIP).  Build here: python tools/gemm_epi_cost.py --build; run on the GPU."""
+(LLP_DIAG_EPI_SKIP).  (A build whose workgroups started staggered by 1/2 or 1/4 tile, so
+that their store bursts would not coincide, measured 1-2 % slower and was removed:
+profiles/r03_gemm_epilogue_cost.json.)  Build here: python tools/gemm_epi_cost.py --build; run on the GPU."""
 import json
 import os
 import subprocess

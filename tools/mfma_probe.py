@@ -16,6 +16,8 @@ import llp_hip as K  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--gemm", type=int, default=225280, help="M of the M x 1024 x 1024 NT GEMM (0: skip)")
+ap.add_argument("--a-one-row", action="store_true",
+                help="diagnostic: every A row aliases row 0 (stride 0), so A is always an L2 hit")
 opt = ap.parse_args()
 dev = torch.device("cuda", 0)
 res = {"practical_peak_tflops": [bench.practical_peak(dev) for _ in range(3)]}
@@ -23,6 +25,8 @@ if opt.gemm:
     M, N, Kd = opt.gemm, 1024, 1024
     g = torch.Generator(device="cpu").manual_seed(3)
     A = (torch.randn(M, Kd, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    if opt.a_one_row:
+        A = A[:1].expand(M, Kd)
     W = (torch.randn(N, Kd, generator=g) * 0.03).to(torch.bfloat16).to(dev)
     b = torch.zeros(N, device=dev)
     C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
@@ -37,5 +41,6 @@ if opt.gemm:
         t.record()
     torch.cuda.synchronize()
     ms = sorted(s.elapsed_time(t) for s, t in e)[len(e) // 2]
-    res["gemm_random"] = {"shape": [M, N, Kd], "median_ms": ms, "tflops": 2.0 * M * N * Kd / ms / 1e9}
+    res["gemm_random"] = {"shape": [M, N, Kd], "median_ms": ms, "tflops": 2.0 * M * N * Kd / ms / 1e9,
+                          "a_one_row": bool(opt.a_one_row)}
 print(json.dumps(res), flush=True)
