@@ -328,8 +328,9 @@ def physics_production_step(dtype):
     return {"config": "coauthor-physics production LLP (N_old=%d, F=%d, H=256, L=2, C=%d, 65,536 edges/step)"
                       % (r1["N_old"], r1["F"], r1["contexts_per_anchor"]),
             "dtype": dtype, "ms_per_step": r1["ms_per_step"], "edges_per_s": r1["edges_per_s"],
-            "rank0_ms_per_step_at_4_ranks": r4["ms_per_step"],
-            "note": "the full-batch student runs over all N_old nodes on every rank (src/main.py:173)"}
+            "rank0_ms_per_step_at_4_ranks": r4["ms_per_step"], "hipgraph": r1["hipgraph"],
+            "note": "eager steps with no host sync (the dense negatives' count stays on the device; a hipGraph "
+                    "replay measured 1 % slower); rank 0 of 4 runs its slice of the node-sharded student"}
 
 
 def main():

@@ -174,7 +174,14 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
                  double B_total, double n_lab_total, float margin, float T,
                  float w_label, float w_d, float w_r, float loss_scale,
                  float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
+                 const int32_t* neg_count, int64_t neg_offset, double pos_total,
                  void* workspace, int64_t workspace_bytes, void* stream);
+/* neg_count (may be NULL): the PyG-dense negatives' device count of the whole batch
+ * (llp_neg_sample_dense), so the full-batch step needs no host read of it.  The label
+ * rows are then n_pos positives and n_lab - n_pos negative SLOTS holding columns
+ * [neg_offset, ...) of the whole batch's negatives; a slot at or past *neg_count is inert
+ * (zero gradient, no loss), and the BCE mean runs over pos_total + *neg_count labels
+ * (n_lab_total unused). */
 
 /* out[r, :] = a[ia[r], :] * b[ib[r], :]   (ia/ib NULL = identity) — the
  * predictor input x_i * x_j (src/models.py:140) materialised once per step so
@@ -317,10 +324,12 @@ int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_
 
 /* Predictor-row indices of the full-batch step: rows [0, B*C) are (anchor,
  * context) pairs from samples[B, C1] (src/main.py:184-186), then P positives
- * pairs[perm[i]] and n_neg negatives neg[:, i] (train_edges, src/main.py:212). */
+ * pairs[perm[i]] and n_neg negatives neg[:, i] (train_edges, src/main.py:212).
+ * neg_count (may be NULL): negative slot i is live while neg_offset + i < *neg_count
+ * (llp_llp_loss); later slots become the inert pair (0, 0). */
 int llp_fullbatch_pairs(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
                         const int32_t* perm, int64_t P, const int32_t* neg, int64_t ld_neg, int64_t n_neg,
-                        int32_t* ia, int32_t* ib, void* stream);
+                        const int32_t* neg_count, int64_t neg_offset, int32_t* ia, int32_t* ib, void* stream);
 
 /* KD terms of the full-batch loss (src/main.py:218-219):
  *   KD_LM = mse(sigmoid(out_logit), t_prob_lab)  over n_lab rows (normaliser n_lab_total);

@@ -176,6 +176,7 @@ __global__ __launch_bounds__(256) void neg_tile_scatter(int64_t M, int64_t num_n
 __global__ void fullbatch_pairs_kernel(int64_t B, int64_t C1, const int32_t* __restrict__ samples,
                                        const int32_t* __restrict__ pairs, const int32_t* __restrict__ perm, int64_t P,
                                        const int32_t* __restrict__ neg, int64_t ld_neg, int64_t n_neg,
+                                       const int32_t* __restrict__ neg_count, int64_t neg_offset,
                                        int32_t* __restrict__ ia, int32_t* __restrict__ ib) {
   const int64_t C = C1 - 1;
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -192,8 +193,11 @@ __global__ void fullbatch_pairs_kernel(int64_t B, int64_t C1, const int32_t* __r
     ia[t] = pairs[2 * e];
     ib[t] = pairs[2 * e + 1];
   } else if (u < P + n_neg) {
-    ia[t] = neg[u - P];
-    ib[t] = neg[ld_neg + u - P];
+    // negative slot u - P: past the sampler's device count (neg_offset + slot >= *neg_count) it is
+    // an inert pair (node 0, node 0) whose logit the loss ignores (llp_llp_loss with a count)
+    const bool live = !neg_count || neg_offset + (u - P) < (int64_t)*neg_count;
+    ia[t] = live ? neg[u - P] : 0;
+    ib[t] = live ? neg[ld_neg + u - P] : 0;
   }
 }
 
@@ -345,7 +349,8 @@ extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys,
 
 extern "C" int llp_fullbatch_pairs(int64_t B, int64_t C1, const int32_t* samples, const int32_t* pairs,
                                    const int32_t* perm, int64_t P, const int32_t* neg, int64_t ld_neg, int64_t n_neg,
-                                   int32_t* ia, int32_t* ib, void* stream) {
+                                   const int32_t* neg_count, int64_t neg_offset, int32_t* ia, int32_t* ib,
+                                   void* stream) {
   LLP_CHECK_ARG(ia && ib, "llp_fullbatch_pairs: null output");
   LLP_CHECK_ARG(B == 0 || (samples && C1 >= 2), "llp_fullbatch_pairs: null samples");
   LLP_CHECK_ARG(P == 0 || (pairs && perm), "llp_fullbatch_pairs: null pairs");
@@ -353,7 +358,7 @@ extern "C" int llp_fullbatch_pairs(int64_t B, int64_t C1, const int32_t* samples
   const int64_t n = B * (C1 > 0 ? C1 - 1 : 0) + P + n_neg;
   if (n == 0) return LLP_OK;
   hipLaunchKernelGGL(fullbatch_pairs_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, B, C1,
-                     samples, pairs, perm, P, neg, ld_neg, n_neg, ia, ib);
+                     samples, pairs, perm, P, neg, ld_neg, n_neg, neg_count, neg_offset, ia, ib);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

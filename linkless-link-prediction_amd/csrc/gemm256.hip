@@ -1064,24 +1064,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     while (t < n_tiles && !tile_of(t, m0, n0)) t += gridDim.x;
     return t < n_tiles;
   };
-#ifdef LLP_GEMM_WALK_RANGE
-  // A/B build: workgroup b takes the contiguous tile range [b T / G, (b + 1) T / G) of the
-  // live tiles in (m-tile, n-tile) order, so one workgroup runs an m-tile's n-tiles back to
-  // back (its A panel re-read from the Infinity Cache) instead of four workgroups fetching
-  // it together
-  const int64_t T_live = tilesM * tilesN, G = gridDim.x;
-  const int64_t t_end = T_live * (blockIdx.x + 1) / G;
-  int64_t t = T_live * blockIdx.x / G, m0 = 0, n0 = 0;
-  auto tile_at = [&](int64_t i, int64_t& mm, int64_t& nn) -> bool {
-    mm = (i / tilesN) * TM;
-    nn = (i % tilesN) * TN;
-    return i < t_end;
-  };
-  if (!tile_at(t, m0, n0)) return;
-#else
   int64_t t = blockIdx.x, m0 = 0, n0 = 0;
   if (!next_tile(t, m0, n0)) return;
-#endif
 
   // DMA in SADDR form: a wave-uniform base (the tile's row panel at the K-tile) and a per-lane
   // 32-bit byte offset computed per piece: row q64_row(..) + lane / 8 of the tile, clamped to
@@ -1156,13 +1140,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   for (int j = 0; j < 4; ++j) issue_chunk(j, 0, m0, n0, 0);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // chunks 0, 1 landed
   for (;;) {
-#ifdef LLP_GEMM_WALK_RANGE
-    int64_t t_next = t + 1, m1 = 0, n1 = 0;
-    const bool pf = tile_at(t_next, m1, n1);
-#else
     int64_t t_next = t + gridDim.x, m1 = 0, n1 = 0;
     const bool pf = next_tile(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
-#endif
     const int64_t rows = min((int64_t)TM, p.M - m0);  // live rows (the last m-tile may be partial)
     // this tile's bias and (ReLU backward) mask tile into LDS by DMA; older than its K-tile 1
     if (BWD) {

@@ -104,13 +104,26 @@ __global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, c
   }
 }
 
+// neg_count (device, may be NULL): the label rows are n_pos positives then negative slots of
+// which those with neg_offset + slot < *neg_count are live; the others get a zero gradient and
+// no loss, and the mean is over pos_total + *neg_count labels (the whole batch's)
 __global__ __launch_bounds__(256) void bce_kernel(int64_t n, int64_t n_pos, const float* __restrict__ logit,
-                                                  double n_total, float w_label, float loss_scale,
-                                                  float* __restrict__ dlogit, float* __restrict__ partial) {
+                                                  double n_total, const int32_t* __restrict__ neg_count,
+                                                  int64_t neg_offset, double pos_total, float w_label,
+                                                  float loss_scale, float* __restrict__ dlogit,
+                                                  float* __restrict__ partial) {
   __shared__ float red[4];
   const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t n_live = n;
+  if (neg_count) {
+    const int64_t c = *neg_count;
+    const int64_t nl = c - neg_offset;
+    n_live = n_pos + (nl < 0 ? 0 : (nl > n - n_pos ? n - n_pos : nl));
+    n_total = pos_total + (double)c;
+  }
   float l = 0.f;
-  if (r < n) {
+  if (r < n && r >= n_live) dlogit[r] = 0.f;
+  if (r < n_live) {
     const float o = sigmoidf_(logit[r]);
     const float y = r < n_pos ? 1.f : 0.f;
     // nn.BCELoss: -(y*max(log o, -100) + (1-y)*max(log(1-o), -100)), mean
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
   float wv[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) wv[i] = (w && active) ? alpha * w[c * CH + i] : alpha;
-  // four rows in flight per lane: issue the loads, then consume them in order
+  // LLP_COLSUM_INFLIGHT rows in flight per lane: issue the loads, then consume them in order
   auto consume = [&](int64_t r, const uint4 raw) {
     float z[CH];
     if constexpr (sizeof(T) == 2) {
@@ -299,12 +312,16 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
   };
   if (active) {
     int64_t r = r0 + rl;
-    for (; r + 3 * rpp < r1; r += 4 * rpp) {
-      uint4 raw[4];
+#ifndef LLP_COLSUM_INFLIGHT
+#define LLP_COLSUM_INFLIGHT 8
+#endif
+    constexpr int NF = LLP_COLSUM_INFLIGHT;   // rows in flight per lane (16 B each)
+    for (; r + (NF - 1) * rpp < r1; r += NF * rpp) {
+      uint4 raw[NF];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) raw[j] = *reinterpret_cast<const uint4*>(Z + (r + j * rpp) * ldz + (int64_t)c * CH);
+      for (int j = 0; j < NF; ++j) raw[j] = *reinterpret_cast<const uint4*>(Z + (r + j * rpp) * ldz + (int64_t)c * CH);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) consume(r + j * rpp, raw[j]);
+      for (int j = 0; j < NF; ++j) consume(r + j * rpp, raw[j]);
     }
     for (; r < r1; r += rpp) consume(r, *reinterpret_cast<const uint4*>(Z + r * ldz + (int64_t)c * CH));
   }
@@ -411,8 +428,9 @@ extern "C" int64_t llp_llp_loss_workspace_bytes(int64_t B, int64_t n_lab) {
 extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob, int64_t n_lab,
                             int64_t n_pos, const float* out_logit, double B_total, double n_lab_total, float margin,
                             float T, float w_label, float w_d, float w_r, float loss_scale, float* dlogit_ctx,
-                            float* dlogit_lab, float* terms_out, int accumulate, void* workspace,
-                            int64_t workspace_bytes, void* stream) {
+                            float* dlogit_lab, float* terms_out, int accumulate, const int32_t* neg_count,
+                            int64_t neg_offset, double pos_total, void* workspace, int64_t workspace_bytes,
+                            void* stream) {
   LLP_CHECK_ARG(C <= MAXC, "llp_llp_loss: contexts per anchor C=%lld > %d", (long long)C, MAXC);
   LLP_CHECK_ARG(terms_out && workspace, "llp_llp_loss: null terms/workspace");
   LLP_CHECK_ARG(workspace_bytes >= llp_llp_loss_workspace_bytes(B, n_lab), "llp_llp_loss: workspace too small");
@@ -429,7 +447,7 @@ extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const fl
   if (nbl > 0) {
     LLP_CHECK_ARG(out_logit && dlogit_lab, "llp_llp_loss: null label buffers");
     hipLaunchKernelGGL(bce_kernel, dim3((unsigned)nbl), dim3(256), 0, s, n_lab, n_pos, out_logit, n_lab_total,
-                       w_label, loss_scale, dlogit_lab, partial + nba * 3);
+                       neg_count, neg_offset, pos_total, w_label, loss_scale, dlogit_lab, partial + nba * 3);
     LLP_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partial, nba + nbl, w_label, w_d, w_r,

@@ -427,17 +427,22 @@ class EngineBase:
         prob = 1.0 - self._neg_n_idx / population
         return int(1.1 * num_neg / prob)
 
-    def _negatives(self, P, P_total, p_offset, neg, dense):
+    def _negatives(self, P, P_total, p_offset, neg, dense, device_count=False):
         """This rank's negative edges: injected, PyG-dense (non-collab) or
         randint (collab) — src/main.py:205-209, src/train_teacher_gnn.py:49-54.
-        Returns (int32[2, n] view, n, n_total)."""
+        Returns (int32[2, n] view, n, n_total, count): count is None, or with
+        ``device_count`` and PyG-dense sampling the whole batch's int32 device count,
+        in which case the view holds this rank's P negative SLOTS (columns
+        [p_offset, p_offset + P) of the whole batch's list; slots past the count are
+        inert in llp_fullbatch_pairs / llp_llp_loss), n = P and n_total = None: no
+        host read."""
         N = self.N
         if neg is not None:
             n_neg = int(neg.shape[1])
             n_neg_total = n_neg if P_total == P else int(round(n_neg * P_total / max(P, 1)))
             negb = self._buf("neg", (2, max(n_neg, 1)), torch.int32)
             negb[:, :n_neg].copy_(neg.to(torch.int32))
-            return negb[:, :n_neg], n_neg, n_neg_total
+            return negb[:, :n_neg], n_neg, n_neg_total, None
         if dense:
             # every rank draws the same global list and keeps its column slice
             keys = self._neg_setup()
@@ -449,13 +454,15 @@ class EngineBase:
             ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
             K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
                                cnt, ws)
+            if device_count:
+                return negg[:, p_offset:p_offset + P], P, None, cnt
             n_neg_total = int(cnt.item())
             lo = min(p_offset, n_neg_total)         # this shard's columns (all of them unsharded)
             hi = min(p_offset + P, n_neg_total)
-            return negg[:, lo:hi], hi - lo, n_neg_total
+            return negg[:, lo:hi], hi - lo, n_neg_total, None
         negb = self._buf("neg", (2, max(P, 1)), torch.int32)
         K.randint_pairs(N, P, self.seed, self.step_ctr, RANDINT_STREAM, negb, n_total=P_total, offset=p_offset)
-        return negb, P, P_total
+        return negb, P, P_total, None
 
     def _predictor_forward(self, h, ia, ib, R2, logit, p_drop):
         """LinkPredictor(h[ia], h[ib]) logits (src/models.py:139-150).  Returns
@@ -873,7 +880,7 @@ class DistillEngine(EngineBase):
                                target, t_ia, t_ib, b_offset=b_offset)
             self._dbg_cut("sample")
         else:
-            negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+            negb, n_neg, n_neg_total, _ = self._negatives(P, P_total, p_offset, neg, dense_negatives)
             n_lab = P + n_neg                  # train_edges columns (src/main.py:86)
             R1 = B * C1 + 2 * n_lab
             R2 = B * C + n_lab
@@ -1034,8 +1041,10 @@ class DistillEngine(EngineBase):
         dense_negatives: PyG dense negative sampling (non-collab, src/main.py:205-207)
             else torch.randint pairs (collab, src/main.py:208-209).
         neg      optional injected negatives int32[2, n_neg] (parity tests).
-        Returns the number of negatives used (host int; the dense sampler's count
-        is read back, one sync, as the reference's shapes are host-known)."""
+        Returns the number of negatives: a host int for injected / randint ones (and
+        with KD_LM, whose kernel reads the dense count on the host), else the whole
+        batch's PyG-dense count as an int32 device tensor: that path has no host
+        sync, and capture_fullbatch records it as a hipGraph."""
         self._act_mask.clear()
         a = self.args
         B = int(anchors.numel())
@@ -1105,15 +1114,20 @@ class DistillEngine(EngineBase):
             self._collective(lambda: self._all_gather_rows(h_full, h_loc, s_world, s_rank))
             h = h_full[:N]
 
-        # ---- negatives (src/main.py:205-209)
-        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+        # ---- negatives (src/main.py:205-209).  PyG-dense ones keep their count on the device
+        # (label slots past it inert, no host read, so the step is graph-capturable) unless
+        # KD_LM, whose kernel takes the host count, needs it
+        w_rm, w_lm = float(a.KD_RM), float(a.KD_LM)
+        negb, n_neg, n_neg_total, cnt = self._negatives(P, P_total, p_offset, neg, dense_negatives,
+                                                        device_count=w_lm == 0.0)
         n_lab = P + n_neg
-        n_lab_total = P_total + n_neg_total
+        n_lab_total = P_total + n_neg_total if cnt is None else 0.0
         BC = Bc * C
         R2 = BC + n_lab
         ia_ib = self._buf("fb_iab", (max(2 * R2, 1),), torch.int32)[:2 * R2]   # [ia | ib]: endpoint rows
         ia, ib = ia_ib[:R2], ia_ib[R2:]
-        K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
+        K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib, neg_count=cnt,
+                          neg_offset=p_offset)
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
@@ -1130,8 +1144,8 @@ class DistillEngine(EngineBase):
         ws = self._ws("ws_loss", K.llp_loss_ws_bytes(Bc, n_lab))
         K.llp_loss(Bc, C, logit, t_r, n_lab, P, logit[BC:], B_total if use_llp else 1, n_lab_total,
                    float(a.margin), 1.0, float(a.True_label), float(a.LLP_D) if use_llp else 0.0,
-                   float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws)
-        w_rm, w_lm = float(a.KD_RM), float(a.KD_LM)
+                   float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws, neg_count=cnt,
+                   neg_offset=p_offset, pos_total=P_total)
         # d(loss)/dh: without KD_RM, the pair rows' Hadamard gradients are grouped by node and
         # summed in row order (deterministic, straight into the compute-dtype buffer); with KD_RM
         # (which adds at the anchors) they accumulate by f32 scatter-add, then convert
@@ -1185,7 +1199,7 @@ class DistillEngine(EngineBase):
                                norm_count=n_rows)
         self._allreduce_and_update()
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
-        return n_neg
+        return n_neg if cnt is None else cnt
 
     def _fb_shard(self, p_drop, grouped):
         """(first row, rows, rows per rank, world, rank) of this rank's slice of the full-batch student,
@@ -1247,6 +1261,22 @@ class DistillEngine(EngineBase):
         the returned object has the same ``replay()``.  ``segmented=True`` takes the
         segmented capture on one rank too, ``debug_cuts`` adds a synchronising cut after
         each stage, ``mode`` is the segments' capture mode (tests, tools/seg_diag.py)."""
+        return self._capture(lambda: self.step_minibatch(anchors, link_ids, pairs, **kw), segmented, debug_cuts,
+                             mode)
+
+    def capture_fullbatch(self, anchors, link_ids, pairs, segmented=None, mode="thread_local", **kw):
+        """Capture one step_fullbatch (train, src/main.py:167-235) into a hipGraph, as
+        capture_minibatch does: persistent ``anchors`` / ``link_ids`` buffers, refilled
+        before each ``replay()``; segments between the collectives at several ranks.
+        The PyG-dense negatives keep their count on the device (step_fullbatch), so
+        the step has no host read; KD_LM, whose kernel takes the host count, cannot
+        be captured and raises here."""
+        if float(self.args.KD_LM) != 0.0 and kw.get("dense_negatives", True) and kw.get("neg") is None:
+            raise NotImplementedError("capture_fullbatch: KD_LM reads the dense negatives' count on the host; "
+                                      "run the step eagerly")
+        return self._capture(lambda: self.step_fullbatch(anchors, link_ids, pairs, **kw), segmented, False, mode)
+
+    def _capture(self, step, segmented, debug_cuts, mode):
         if segmented is None:
             segmented = self.world > 1
         if segmented:
@@ -1258,7 +1288,7 @@ class DistillEngine(EngineBase):
             self._seg_debug = bool(debug_cuts)
             try:
                 seg.begin()
-                self.step_minibatch(anchors, link_ids, pairs, **kw)
+                step()
             finally:
                 self._seg = None
                 self._seg_debug = False
@@ -1269,7 +1299,7 @@ class DistillEngine(EngineBase):
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.graph(g, stream=s):
-            self.step_minibatch(anchors, link_ids, pairs, **kw)
+            step()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g
 

@@ -66,7 +66,7 @@ _SIGS = {
                              c_int, c_vp, c_i64, c_vp]),
     "llp_llp_loss_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_llp_loss": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32,
-                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_vp]),
+                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_vp, c_i64, c_vp]),
     "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_dedup_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
@@ -89,7 +89,8 @@ _SIGS = {
     "llp_neg_sample_dense_workspace_bytes": (c_i64, [c_i64]),
     "llp_neg_sample_dense": (c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp, c_i64, c_vp,
                                      c_vp, c_i64, c_vp]),
-    "llp_fullbatch_pairs": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "llp_fullbatch_pairs": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                    c_vp]),
     "llp_kd_terms_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_kd_terms": (c_int, [c_int, c_i64, c_vp, c_vp, c_f64, c_f32, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
                              c_f64, c_f32, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
@@ -285,12 +286,16 @@ def llp_loss_ws_bytes(B, n_lab):
 
 
 def llp_loss(B, Cc, s_logit, t_prob, n_lab, n_pos, out_logit, B_total, n_lab_total, margin, T, w_label, w_d, w_r,
-             dlogit_ctx, dlogit_lab, terms, ws, accumulate=False, loss_scale=1.0):
+             dlogit_ctx, dlogit_lab, terms, ws, accumulate=False, loss_scale=1.0, neg_count=None, neg_offset=0,
+             pos_total=0.0):
+    """neg_count: the dense negatives' int32 device count (label slots past it inert, the BCE
+    mean over pos_total + count labels); n_lab_total is then unused."""
     L = lib()
     check(L.llp_llp_loss(B, Cc, ptr(s_logit), ptr(t_prob), n_lab, n_pos, ptr(out_logit), float(B_total),
                          float(n_lab_total), margin, T, w_label, w_d, w_r, loss_scale, ptr(dlogit_ctx),
-                         ptr(dlogit_lab), terms.data_ptr(), int(accumulate), ws.data_ptr(),
-                         ws.numel() * ws.element_size(), stream_ptr()), "llp_llp_loss")
+                         ptr(dlogit_lab), terms.data_ptr(), int(accumulate), ptr(neg_count), int(neg_offset),
+                         float(pos_total), ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()),
+          "llp_llp_loss")
 
 
 def hadamard_bwd_blocks(B, Cc, L2, H, dZ, h, dh, drow=None, hidx=None):
@@ -416,11 +421,11 @@ def neg_sample_dense(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr,
                                  stream_ptr()), "llp_neg_sample_dense")
 
 
-def fullbatch_pairs(B, C1, samples, pairs, perm, P, neg, n_neg, ia, ib):
+def fullbatch_pairs(B, C1, samples, pairs, perm, P, neg, n_neg, ia, ib, neg_count=None, neg_offset=0):
     L = lib()
     check(L.llp_fullbatch_pairs(B, C1, ptr(samples), ptr(pairs), ptr(perm), P, ptr(neg),
-                                neg.stride(0) if neg is not None else 0, n_neg, ia.data_ptr(), ib.data_ptr(),
-                                stream_ptr()), "llp_fullbatch_pairs")
+                                neg.stride(0) if neg is not None else 0, n_neg, ptr(neg_count), int(neg_offset),
+                                ia.data_ptr(), ib.data_ptr(), stream_ptr()), "llp_fullbatch_pairs")
 
 
 def kd_terms_ws_bytes(B_rm, n_lab):

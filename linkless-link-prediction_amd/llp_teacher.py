@@ -276,23 +276,27 @@ class TeacherEngine(EngineBase):
         link_ids int32[P]   this rank's slice of the DataLoader permutation
         pairs    int32[E,2] pos_train_edge (src/train_teacher_gnn.py:25,28)
         dense_negatives: PyG dense sampler (non-collab) else randint (collab).
-        Returns the number of negatives used."""
+        Returns the number of negatives used: a host int (injected / randint), or the
+        PyG-dense count as an int32 device tensor (no host read in the step)."""
         P = int(link_ids.numel())
         P_total = P if P_total is None else int(P_total)
         N, O = self.N, self.out_dim
         h = self._encode(training=True)
-        negb, n_neg, n_neg_total = self._negatives(P, P_total, p_offset, neg, dense_negatives)
+        # PyG-dense negatives: their count stays on the device (slots past it inert), no host read
+        negb, n_neg, n_neg_total, cnt = self._negatives(P, P_total, p_offset, neg, dense_negatives,
+                                                        device_count=True)
         R = P + n_neg
         tgt = self._buf("t_tgt", (max(2 * R, 1),), torch.int32)[:2 * R]   # [ia | ib]: endpoint rows
         ia, ib = tgt[:R], tgt[R:]
-        K.fullbatch_pairs(0, 0, None, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib)
+        K.fullbatch_pairs(0, 0, None, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib, neg_count=cnt,
+                          neg_offset=p_offset)
         logit = self._buf("logit", (R,), torch.float32)
         A0, zacts = self._predictor_forward(h, ia, ib, R, logit, self.pred_drop)
         dlogit = self._buf("dlogit", (R,), torch.float32)
         ws = self._ws("ws_loss", K.llp_loss_ws_bytes(0, R))
         # BCE only (src/train_teacher_gnn.py:56-58)
-        K.llp_loss(0, 1, None, None, R, P, logit, 1, P_total + n_neg_total, 0.0, 1.0, 1.0, 0.0, 0.0, None, dlogit,
-                   self.terms, ws)
+        K.llp_loss(0, 1, None, None, R, P, logit, 1, P_total + n_neg_total if cnt is None else 0.0, 0.0, 1.0, 1.0,
+                   0.0, 0.0, None, dlogit, self.terms, ws, neg_count=cnt, neg_offset=p_offset, pos_total=P_total)
         dZ0 = self._predictor_backward(dlogit, R, A0, zacts, self.pred_drop)
         if self.predictor_kind == "mlp":
             self._hadamard_bwd_nodes(R, tgt, dZ0, None, h, self._dh_slot())
@@ -302,7 +306,7 @@ class TeacherEngine(EngineBase):
         self._allreduce_and_update()
         K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
         K.increment(self.step_ctr)
-        return n_neg
+        return n_neg if cnt is None else cnt
 
     @torch.no_grad()
     def embed(self):

@@ -157,7 +157,7 @@ def test_fullbatch_device_negatives_and_bf16():
         st = case.steps[0]
         n_neg = eng.step_fullbatch(st.node_perm.to(torch.int32).to(DEV), st.link_perm.to(torch.int32).to(DEV), pairs)
         torch.cuda.synchronize()
-        assert n_neg == st.link_perm.numel()
+        assert int(n_neg) == st.link_perm.numel()     # the device count (no host read in the step)
         res[dt] = (eng.terms.cpu().clone(), [p.grad.detach().cpu().clone() for p in
                                              list(model.parameters()) + list(pred.parameters())])
         assert torch.isfinite(res[dt][0]).all()
@@ -166,3 +166,92 @@ def test_fullbatch_device_negatives_and_bf16():
         assert abs(a - b) <= 3e-2 * max(abs(b), 1e-2), (i, a, b)
     for a, b in zip(res["bf16"][1], res["fp32"][1]):
         assert F.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.97
+
+
+def _dense_problem(N=22, n_und=180, P=256, seed=0):
+    """A graph so dense that PyG's sampler returns fewer negatives than asked for
+    (N (N - 1) = 462 candidates, 240 of them edges, 256 asked)."""
+    import types
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randint(0, N, (n_und,), generator=g)
+    v = torch.randint(0, N, (n_und,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.cat([pairs, pairs.flip(1)], 0).t().contiguous()
+    x = torch.randn(N, 40, generator=g) * 0.5
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    args = types.SimpleNamespace(rw_step=2, hops=2, ns_rate=1, ps_method="nb", dropout=0.0, margin=0.1, LLP_D=1.0,
+                                 LLP_R=0.5, True_label=1.0, predictor="mlp", KD_RM=0.0, KD_LM=0.0, lr=0.01)
+    return N, pairs, ei, x, t_h, args, P
+
+
+def _dense_engine(N, ei, x, t_h, args, dtype="fp32"):
+    import llp_engine
+    import models
+    torch.manual_seed(4)
+    model = models.MLP(2, x.shape[1], 256, 256, 0.0).to(DEV)
+    pred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(DEV)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(DEV)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
+    eng = llp_engine.DistillEngine(model, pred, tpred, x.to(DEV), t_h.to(DEV), ei[0].numpy(), ei[1].numpy(), N, args,
+                                   opt, dtype=dtype, seed=9)
+    return eng, model, pred
+
+
+def test_fullbatch_device_negative_count_matches_host_count():
+    """The PyG-dense negatives' count kept on the device (label slots past it inert)
+    gives the step of the same negatives injected with their host count, also when the
+    sampler returns fewer than asked for (a dense graph)."""
+    _K()
+    N, pairs, ei, x, t_h, args, P = _dense_problem()
+    anchors = torch.arange(0, N, 2, dtype=torch.int32).to(DEV)
+    links = torch.arange(P, dtype=torch.int32).remainder(pairs.size(0)).to(DEV)
+    pr = pairs.to(torch.int32).to(DEV).contiguous()
+    eng, model, pred = _dense_engine(N, ei, x, t_h, args)
+    cnt = eng.step_fullbatch(anchors, links, pr)
+    torch.cuda.synchronize()
+    n = int(cnt)
+    assert 0 < n < P, n                                   # the sampler ran short: inert slots exist
+    negs = eng._buf("neg_all", (2, P), torch.int32)[:, :n].clone()
+    C1 = args.rw_step * args.hops * (1 + args.ns_rate) + 1
+    samples = eng._bufs["samples"][:anchors.numel() * C1].view(anchors.numel(), C1).clone()
+    t_dev = eng.terms.cpu().clone()
+    g_dev = [p.grad.detach().cpu().clone() for p in list(model.parameters()) + list(pred.parameters())]
+    eng2, model2, pred2 = _dense_engine(N, ei, x, t_h, args)
+    assert eng2.step_fullbatch(anchors, links, pr, samples=samples, neg=negs) == n
+    torch.cuda.synchronize()
+    t_host = eng2.terms.cpu()
+    assert torch.allclose(t_dev[:4], t_host[:4], rtol=1e-6, atol=1e-7), (t_dev[:4], t_host[:4])
+    for a, b in zip(g_dev, [p.grad.detach().cpu() for p in list(model2.parameters()) + list(pred2.parameters())]):
+        assert (a - b).abs().max().item() <= 1e-5 * max(b.abs().max().item(), 1e-6) + 1e-9
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fullbatch_graph_replay_matches_eager(dtype):
+    """capture_fullbatch: the full-batch step (device samples, dense negatives with their
+    count on the device) replayed from a hipGraph is bit-identical to eager steps."""
+    _K()
+    case = G.load_case("fullbatch_production_small")
+    out = {}
+    for graph in (False, True):
+        eng, model, pred = _engine(case, dtype)
+        pairs = case.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+        st = case.steps[0]
+        a_buf = st.node_perm.to(torch.int32).to(DEV).clone()
+        l_buf = st.link_perm.to(torch.int32).to(DEV).clone()
+        eng.step_fullbatch(a_buf, l_buf, pairs)
+        if graph:
+            g = eng.capture_fullbatch(a_buf, l_buf, pairs)
+            for _ in range(2):
+                g.replay()
+        else:
+            for _ in range(2):
+                eng.step_fullbatch(a_buf, l_buf, pairs)
+        torch.cuda.synchronize()
+        out[graph] = ([p.detach().cpu().clone() for p in list(model.parameters()) + list(pred.parameters())],
+                      eng.terms.cpu().clone())
+    for a, b in zip(out[False][0], out[True][0]):
+        assert torch.equal(a, b)
+    assert torch.equal(out[False][1], out[True][1])

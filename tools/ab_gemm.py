@@ -1,6 +1,7 @@
-"""Same-box A/B of whole library builds on the dominant GEMM (tools/mfma_probe.py --gemm,
-random bf16 operands, event-timed medians): python tools/ab_gemm.py NAME=LIB.so ... [--rounds R].
-Each build runs in its own process (LLP_LIB), interleaved over the rounds."""
+"""Same-box A/B of whole library builds, by default on the dominant GEMM (tools/mfma_probe.py
+--gemm, random bf16 operands, event-timed medians): python tools/ab_gemm.py NAME=LIB.so ...
+[--rounds R] [--script tools/colsum_bench.py].  Each build runs in its own process (LLP_LIB),
+interleaved over the rounds; the script's last JSON line gives median_ms."""
 import json
 import os
 import subprocess
@@ -10,18 +11,20 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 args = [a for a in sys.argv[1:] if "=" in a]
 rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 3
 extra = ["--a-one-row"] if "--a-one-row" in sys.argv else []   # passed on to tools/mfma_probe.py
+script = sys.argv[sys.argv.index("--script") + 1] if "--script" in sys.argv else os.path.join("tools", "mfma_probe.py")
 res = {}
 for r in range(rounds):
     for a in args:
         name, lib = a.split("=", 1)
         env = dict(os.environ, LLP_LIB=os.path.join(REPO, lib))
-        out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_probe.py")] + extra, env=env,
+        out = subprocess.run([sys.executable, os.path.join(REPO, script)] + extra, env=env,
                              capture_output=True, text=True, timeout=300)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if not line:
             print(out.stdout, out.stderr, file=sys.stderr)
             sys.exit(1)
-        d = json.loads(line[-1])["gemm_random"]
+        d = json.loads(line[-1])
+        d = d.get("gemm_random", d)
         res.setdefault(name, []).append(round(d["median_ms"], 4))
         print(name, r, d, flush=True)
 print(json.dumps(res))

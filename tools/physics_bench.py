@@ -5,9 +5,10 @@ undirected edges) split by the reference's do_production_edge_split, student
 MLP 8,415 -> 256 -> 256 over the old-node training graph every link batch,
 LLP_D=10 LLP_R=0.01 True_label=0.1, rw_step=2 hops=2 ns_rate=4 (C=20), PyG
 dense negatives.  Prints one JSON line: ms per link batch and edges/s, per
-dtype; --emulate-ranks R times rank 0's shard of each batch (no collective).
+dtype; --emulate-ranks R times rank 0's shard of each batch (no collective).  The timed
+steps are eager launches (--graph: replays of capture_fullbatch's hipGraph).
 
-    python tools/physics_bench.py [--steps 10] [--dtype bf16] [--emulate-ranks 4 [--replicated]]
+    python tools/physics_bench.py [--steps 10] [--dtype bf16] [--emulate-ranks 4 [--replicated]] [--graph]
 """
 import argparse
 import json
@@ -35,7 +36,7 @@ def physics_args():
                                  hidden_channels=256, num_layers=2, link_batch_size=64 * 1024, predictor="mlp")
 
 
-def run(dtype, steps, warmup, emulate, split, shard_student=True):
+def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False):
     dev = torch.device("cuda", 0)
     a = physics_args()
     td = split[0]                                     # training_data: old nodes, old-old edges
@@ -73,18 +74,30 @@ def run(dtype, steps, warmup, emulate, split, shard_student=True):
 
     for s in range(warmup):
         step(s)
+    g_a = g_l = replay = None
+    if graph:   # the step replayed from a hipGraph (capture_fullbatch), inputs refilled per replay
+        g_a = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
+        g_l = torch.empty(p1 - p0, dtype=torch.int32, device=dev)
+        replay = eng.capture_fullbatch(g_a, g_l, pairs, b_offset=b0, p_offset=p0, B_total=B_full, P_total=P_full,
+                                       dense_negatives=True)
     torch.cuda.synchronize()
     eng.begin_epoch()
     t0 = time.perf_counter()
     for s in range(steps):
-        step(warmup + s)
+        if replay is not None:
+            j = (warmup + s) % n_full
+            g_a.copy_(node_perm[j * B_full + b0: j * B_full + b1])
+            g_l.copy_(link_perm[j * P_full + p0: j * P_full + p1])
+            replay.replay()
+        else:
+            step(warmup + s)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     loss = eng.end_epoch(steps * P_full)
     return {"dtype": dtype, "ms_per_step": dt * 1e3, "edges_per_s": P_full / dt if not emulate else None,
             "emulated_ranks": emulate or None, "fb_shard": eng.emulate_shard is not None, "N_old": N, "F": F, "E_train_directed": E, "anchors_per_step": B_full,
             "contexts_per_anchor": a.rw_step * a.hops * (1 + a.ns_rate), "edges_per_step": P_full,
-            "steps_per_epoch": -(-E // P_full), "loss": loss}
+            "steps_per_epoch": -(-E // P_full), "loss": loss, "hipgraph": replay is not None}
 
 
 def main():
@@ -94,6 +107,9 @@ def main():
     ap.add_argument("--dtype", default="bf16,fp32")
     ap.add_argument("--emulate-ranks", type=int, default=0)
     ap.add_argument("--replicated", action="store_true", help="every rank runs the student over all nodes")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay a hipGraph of the step (capture_fullbatch); eager measured faster, "
+                         "profiles/r03_physics_devcount_graph_ab.txt")
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "llp_physics"))
     opt = ap.parse_args()
     t0 = time.perf_counter()
@@ -102,7 +118,8 @@ def main():
     out = {"workload": "coauthor-physics production LLP distillation (train, full-batch student)",
            "split_s": prep, "runs": []}
     for dt in opt.dtype.split(","):
-        out["runs"].append(run(dt, opt.steps, opt.warmup, opt.emulate_ranks, split, not opt.replicated))
+        out["runs"].append(run(dt, opt.steps, opt.warmup, opt.emulate_ranks, split, not opt.replicated,
+                               opt.graph))
         print(json.dumps(out["runs"][-1]), flush=True)
     print(json.dumps(out), flush=True)
 
