@@ -353,6 +353,7 @@ def main():
     ap.add_argument("--no-physics", action="store_true")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 collab step leg")
     ap.add_argument("--no-shard8", action="store_true", help="skip the 8-rank per-rank shard leg")
+    ap.add_argument("--no-practical-peak", action="store_true", help="skip the bare-MFMA probe (profiling runs)")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single GPU: run only rank 0's shard of an R-rank job (no collective) and report "
                          "its per-step time, to see the per-rank fixed costs of strong scaling")
@@ -526,7 +527,7 @@ def main():
             "loss": loss,
             "hipgraph": bool(graph is not None),
         }
-        if opt.dtype == "bf16":
+        if opt.dtype == "bf16" and not opt.no_practical_peak:
             pp = practical_peak(dev)
             res["roofline"].update(practical_peak=pp, practical_frac=achieved / pp,
                                    practical_note="bare v_mfma_f32_16x16x32_bf16 loop on random operands, every CU, "
