@@ -1219,7 +1219,14 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     const int rl0 = etid >> 5, c = etid & 31;
     char* stg = reinterpret_cast<char*>(smem + STG);
     const bool st = !HEAD || p.C != nullptr;           // the head GEMM may store no C
+#ifdef LLP_DIAG_EPI_ALIAS
+    // diagnostic build (tools/gemm_epi_cost.py): every tile of this workgroup stores into the same
+    // 64 rows x 256 columns (rows 64 * blockIdx.x ..; M >= 64 * grid), so its stores stay in L2 and
+    // never reach HBM.  C and the mask hold garbage.
+    char* cbase = st ? reinterpret_cast<char*>(p.C + (int64_t)blockIdx.x * 64 * p.ldc) : nullptr;
+#else
     char* cbase = st ? reinterpret_cast<char*>(p.C + m0 * p.ldc + n0) : nullptr;
+#endif
     float* part = reinterpret_cast<float*>(smem + MLDS);   // head: [256 rows][8 quads] partial dots
     float4_t hw0 = {0.f, 0.f, 0.f, 0.f}, hw1 = hw0;
     if (HEAD) {   // this thread's 8 head weights (columns n0 + 8c ..) for the head dot
@@ -1229,7 +1236,11 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     const uint32_t toff = (uint32_t)((rl0 * p.ldc + c * 8) * 2);
     const int64_t cstep = 16 * p.ldc * 2;
     const bool mo = RELU && p.mask_out;
+#ifdef LLP_DIAG_EPI_ALIAS
+    char* mbase = mo ? reinterpret_cast<char*>(p.mask_out + (int64_t)blockIdx.x * 64 * p.ld_mask) : nullptr;
+#else
     char* mbase = mo ? reinterpret_cast<char*>(p.mask_out + m0 * p.ld_mask + (n0 >> 3)) : nullptr;
+#endif
     const uint32_t moff = (uint32_t)(rl0 * p.ld_mask + c);
     const int64_t mstep = 16 * p.ld_mask;
     // round h stages the tile's rows [64h, 64h + 64) and [128 + 64h, 128 + 64h + 64): every
@@ -1267,7 +1278,11 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           uint4 v = *reinterpret_cast<const uint4*>(rb + i * 16 * ROWB);
+#ifdef LLP_DIAG_EPI_ALIAS
+          const int ii = (i + 4 * h + (i >= 4 ? 4 : 0)) & 3;   // the aliased 64 rows
+#else
           const int ii = i + 4 * h + (i >= 4 ? 4 : 0);   // 16-row group of the tile
+#endif
           if (BWD) {
             const uint32_t bits = mlds[(rl0 + 16 * ii) * 32 + c];
             v.x &= half_mask<0>(bits, lo16);

@@ -1,7 +1,8 @@
 """Price of the persistent NT GEMM's epilogue: the M x 1024 x 1024 ReLU-forward launch
 (random bf16 operands, event-timed medians) of the default library against diagnostic
-builds without the epilogue's C stores (LLP_DIAG_EPI_NOSTORE) and without any epilogue
-(LLP_DIAG_EPI_SKIP).  (A build whose workgroups started staggered by 1/2 or 1/4 tile, so
+builds without the epilogue's C stores (LLP_DIAG_EPI_NOSTORE), without any epilogue
+(LLP_DIAG_EPI_SKIP) and with every store of a workgroup aliased onto the same 64 rows, so the
+stores stay in L2 (LLP_DIAG_EPI_ALIAS: the stores' instructions without their HBM writes).  (A build whose workgroups started staggered by 1/2 or 1/4 tile, so
 that their store bursts would not coincide, measured 1-2 % slower and was removed:
 profiles/r03_gemm_epilogue_cost.json.)  Build here: python tools/gemm_epi_cost.py --build; run on the GPU."""
 import json
@@ -11,7 +12,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "linkless-link-prediction_amd")
-VARIANTS = {"nostore": ["LLP_DIAG_EPI_NOSTORE"], "skip": ["LLP_DIAG_EPI_SKIP"]}
+VARIANTS = {"nostore": ["LLP_DIAG_EPI_NOSTORE"], "skip": ["LLP_DIAG_EPI_SKIP"], "alias": ["LLP_DIAG_EPI_ALIAS"]}
 
 if "--build" in sys.argv:
     sys.path.insert(0, PKG)
@@ -22,7 +23,7 @@ if "--build" in sys.argv:
     sys.exit(0)
 
 res = {}
-for rnd in range(2):
+for rnd in range(int(sys.argv[sys.argv.index('--rounds') + 1]) if '--rounds' in sys.argv else 2):
     for name in ["default"] + list(VARIANTS):
         env = dict(os.environ)
         if name != "default":
