@@ -706,10 +706,17 @@ extern "C" int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R) 
 extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
                               int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
                               int64_t workspace_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (R == 0) {   // an empty batch: no unique nodes, seg_ptr = {0} (zeroed by a kernel: no memset node)
+    LLP_CHECK_ARG(n_unique && seg_ptr, "llp_dedup_rows: null");
+    hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(256), 0, s, (int64_t)1, n_unique);
+    hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(256), 0, s, (int64_t)1, seg_ptr);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
   LLP_CHECK_ARG(target && uniq && pos && n_unique && seg_ptr && seg_rows && workspace, "llp_dedup_rows: null");
   LLP_CHECK_ARG(num_nodes > 0 && num_nodes < (1ll << 31) && R > 0 && R < (1ll << 31), "llp_dedup_rows: sizes");
   LLP_CHECK_ARG(workspace_bytes >= llp_dedup_rows_workspace_bytes(num_nodes, R), "llp_dedup_rows: workspace");
-  hipStream_t s = (hipStream_t)stream;
   char* w = reinterpret_cast<char*>(workspace);
   int32_t* cnt = reinterpret_cast<int32_t*>(w);
   w += al256((num_nodes + 1) * 4);
@@ -759,7 +766,7 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
 extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
                                     const void* src, int64_t ld_src, void* out, int64_t ld_out, int out_dtype,
                                     const int32_t* out_rows, const int32_t* u_dev, void* stream) {
-  LLP_CHECK_ARG(seg_ptr && rows && src && out, "llp_segment_sum_rows: null");
+  LLP_CHECK_ARG((U == 0) || (seg_ptr && rows && src && out), "llp_segment_sum_rows: null");
   LLP_CHECK_ARG(out_dtype == dtype || out_dtype == LLP_F32, "llp_segment_sum_rows: out_dtype must be dtype or f32");
   const int E = dtype == LLP_BF16 ? 8 : 4;
   const int es = dtype == LLP_BF16 ? 2 : 4;
@@ -785,7 +792,7 @@ extern "C" int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32
 }
 
 extern "C" int llp_gather_i32(int64_t n, const int32_t* idx, const int32_t* src, int32_t* out, void* stream) {
-  LLP_CHECK_ARG(idx && src && out, "llp_gather_i32: null");
+  LLP_CHECK_ARG((n == 0) || (idx && src && out), "llp_gather_i32: null");
   if (n == 0) return LLP_OK;
   hipLaunchKernelGGL(gather_i32_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, idx, src,
                      out);

@@ -508,7 +508,7 @@ extern "C" int llp_hadamard_bwd_blocks(int dtype, int64_t B, int64_t C, int64_t 
 
 extern "C" int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a, const int32_t* ia, const void* b,
                                  const int32_t* ib, void* out, void* stream) {
-  LLP_CHECK_ARG(a && b && out, "llp_hadamard_rows: null pointer");
+  LLP_CHECK_ARG(R == 0 || H == 0 || (a && b && out), "llp_hadamard_rows: null pointer");
   const int es = dtype == LLP_BF16 ? 2 : 4;
   LLP_CHECK_ARG((H * es) % 16 == 0 && (uintptr_t)a % 16 == 0 && (uintptr_t)b % 16 == 0 && (uintptr_t)out % 16 == 0,
                 "llp_hadamard_rows: rows must be 16-byte multiples and aligned");
@@ -545,7 +545,7 @@ extern "C" int llp_hadamard_rows(int dtype, int64_t R, int64_t H, const void* a,
 
 extern "C" int llp_hadamard_bwd_scatter(int dtype, int64_t R, int64_t H, const void* dZ, const float* drow,
                                         const int32_t* ia, const int32_t* ib, const void* h, float* dh, void* stream) {
-  LLP_CHECK_ARG((dZ || drow) && ia && ib && h && dh, "llp_hadamard_bwd_scatter: null pointer");
+  LLP_CHECK_ARG((R == 0) || ((dZ || drow) && ia && ib && h && dh), "llp_hadamard_bwd_scatter: null pointer");
   if (R == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == LLP_BF16)
@@ -608,7 +608,7 @@ extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, 
 }
 
 extern "C" int llp_convert(int src_dtype, int dst_dtype, int64_t n, const void* src, void* dst, void* stream) {
-  LLP_CHECK_ARG(src && dst, "llp_convert: null pointer");
+  LLP_CHECK_ARG((n == 0) || (src && dst), "llp_convert: null pointer");
   if (n == 0) return LLP_OK;
   unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(convert_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, src_dtype == LLP_BF16,

@@ -617,7 +617,7 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
                            const llp_operand* B, void* C, int64_t ldc, int c_dtype, const float* bias,
                            int act, const void* aux, int64_t ld_aux, int aux_dtype, float alpha,
                            const llp_dropout* dropout, void* stream) {
-  LLP_CHECK_ARG(A && B && C, "llp_gemm_nt: null operand");
+  LLP_CHECK_ARG(A && B && (C || M == 0 || N == 0), "llp_gemm_nt: null operand");   // empty C: null (torch)
   LLP_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "llp_gemm_nt: negative size");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_nt: bad dtype %d", dtype);
   LLP_CHECK_ARG(act != LLP_ACT_RELU_BWD || aux, "llp_gemm_nt: RELU_BWD needs aux");
@@ -704,7 +704,7 @@ extern "C" int64_t llp_gemm_nt_splitk_ws_bytes(int64_t M, int64_t N, int splits)
 extern "C" int llp_gemm_nt_splitk(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B, void* C,
                                   int64_t ldc, const float* bias, int act, void* mask_out, int64_t ld_mask, int splits,
                                   void* workspace, int64_t workspace_bytes, void* stream) {
-  LLP_CHECK_ARG(A && B && C && workspace, "llp_gemm_nt_splitk: null pointer");
+  LLP_CHECK_ARG(A && B && (M == 0 || (C && workspace)), "llp_gemm_nt_splitk: null pointer");
   LLP_CHECK_ARG(act == LLP_ACT_NONE || act == LLP_ACT_RELU, "llp_gemm_nt_splitk: act must be NONE or RELU");
   LLP_CHECK_ARG(!mask_out || act == LLP_ACT_RELU, "llp_gemm_nt_splitk: a ReLU mask needs act RELU");
   LLP_CHECK_ARG(splits >= 1 && splits <= 64, "llp_gemm_nt_splitk: splits %d not in 1..64", splits);
@@ -741,7 +741,7 @@ extern "C" int64_t llp_gemm_nt_head_parts(int64_t N) { return (N + 255) / 256; }
 extern "C" int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B, void* C,
                                 int64_t ldc, const float* bias, int act, float alpha, const llp_dropout* dropout,
                                 const float* head_w, float* head_part, void* stream) {
-  LLP_CHECK_ARG(A && B && head_w && head_part, "llp_gemm_nt_head: null pointer");
+  LLP_CHECK_ARG(A && B && head_w && (head_part || M == 0), "llp_gemm_nt_head: null pointer");
   LLP_CHECK_ARG(act == LLP_ACT_NONE || act == LLP_ACT_RELU, "llp_gemm_nt_head: act must be NONE or RELU");
   auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
   LLP_CHECK_ARG(K > 0 && K % 64 == 0 && N % 8 == 0 && !A->ptr2 && !B->ptr2 && a16(A->ptr, A->ld) && a16(B->ptr, B->ld) &&
@@ -770,7 +770,7 @@ extern "C" int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_opera
 
 extern "C" int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit, float* prob,
                                void* stream) {
-  LLP_CHECK_ARG(part, "llp_head_finish: null part");
+  LLP_CHECK_ARG(part || M == 0, "llp_head_finish: null part");
   if (M == 0) return LLP_OK;
   hipLaunchKernelGGL(head_finish_kernel, dim3(ceil_div_u(M, 256)), dim3(256), 0, (hipStream_t)stream, parts, M, part,
                      b, logit, prob);

@@ -459,7 +459,7 @@ extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const fl
 extern "C" int llp_head_fwd(int dtype, int64_t R, int64_t H, const void* Z, int64_t ldz, const void* Z2, int64_t ldz2,
                             const int32_t* iz, const int32_t* iz2, const float* w, const float* b, float* logit,
                             float* prob, void* stream) {
-  LLP_CHECK_ARG(Z, "llp_head_fwd: null Z");
+  LLP_CHECK_ARG(Z || R == 0, "llp_head_fwd: null Z");
   if (R == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(ceil_div_u(R, 4));
@@ -523,7 +523,7 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
 extern "C" int llp_head_bwd(int dtype, int64_t R, int64_t H, const float* dlogit, const void* Z, int64_t ldz,
                             const float* w, int relu_mask, float alpha, void* dZ, int64_t lddz, float* dw,
                             float* db, int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
-  LLP_CHECK_ARG(dlogit && Z, "llp_head_bwd: null input");
+  LLP_CHECK_ARG(R == 0 || (dlogit && Z), "llp_head_bwd: null input");   // R = 0: dw, db = the empty sum
   LLP_CHECK_ARG(!dZ || w, "llp_head_bwd: dZ needs w");
   return colsum_launch(dtype, R, H, Z, ldz, dlogit, w, relu_mask, alpha, dZ, lddz, dw, db, accumulate, workspace,
                        workspace_bytes, (hipStream_t)stream);
@@ -531,7 +531,7 @@ extern "C" int llp_head_bwd(int dtype, int64_t R, int64_t H, const float* dlogit
 
 extern "C" int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
                           void* workspace, int64_t workspace_bytes, void* stream) {
-  LLP_CHECK_ARG(Y && out, "llp_colsum: null input");
+  LLP_CHECK_ARG(out && (Y || M == 0), "llp_colsum: null input");   // M = 0: out = the empty sum
   return colsum_launch(dtype, M, N, Y, ldy, nullptr, nullptr, 0, 1.f, nullptr, 0, out, nullptr, accumulate, workspace,
                        workspace_bytes, (hipStream_t)stream);
 }
@@ -541,7 +541,7 @@ extern "C" int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_
 namespace llp {
 int colsum_rows_dev(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,
                     void* workspace, int64_t workspace_bytes, const int32_t* m_dev, void* stream) {
-  LLP_CHECK_ARG(Y && out, "llp_colsum: null input");
+  LLP_CHECK_ARG(out && (Y || M == 0), "llp_colsum: null input");   // M = 0: out = the empty sum
   return colsum_launch(dtype, M, N, Y, ldy, nullptr, nullptr, 0, 1.f, nullptr, 0, out, nullptr, accumulate, workspace,
                        workspace_bytes, (hipStream_t)stream, m_dev);
 }

@@ -97,7 +97,7 @@ __global__ void relu_bwd_2d_kernel(int64_t rows, int64_t cols, const T* __restri
 
 extern "C" int llp_act_2d(int dtype, int64_t rows, int64_t cols, const void* x, int64_t ldx, void* y, int64_t ldy,
                           int act, const llp_dropout* dropout, void* stream) {
-  LLP_CHECK_ARG(x && y, "llp_act_2d: null pointer");
+  LLP_CHECK_ARG((rows == 0 || cols == 0) || (x && y), "llp_act_2d: null pointer");
   LLP_CHECK_ARG(act == LLP_ACT_NONE || act == LLP_ACT_RELU, "llp_act_2d: act must be NONE or RELU");
   if (rows == 0 || cols == 0) return LLP_OK;
   uint32_t thr = 0;
@@ -127,7 +127,7 @@ extern "C" int llp_act_2d(int dtype, int64_t rows, int64_t cols, const void* x, 
 
 extern "C" int llp_relu_bwd_2d(int dtype, int64_t rows, int64_t cols, const void* gy, int64_t ldg, const void* y,
                                int64_t ldy, float alpha, void* out, int64_t ldo, void* stream) {
-  LLP_CHECK_ARG(gy && y && out, "llp_relu_bwd_2d: null pointer");
+  LLP_CHECK_ARG((rows == 0 || cols == 0) || (gy && y && out), "llp_relu_bwd_2d: null pointer");
   if (rows == 0 || cols == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   const int64_t n = rows * cols;
@@ -143,7 +143,7 @@ extern "C" int llp_relu_bwd_2d(int dtype, int64_t rows, int64_t cols, const void
 
 extern "C" int llp_relu_bwd(int dtype, int64_t n, const void* gy, const void* y, float alpha, void* out,
                             void* stream) {
-  LLP_CHECK_ARG(gy && out, "llp_relu_bwd: null pointer");
+  LLP_CHECK_ARG((n == 0) || (gy && out), "llp_relu_bwd: null pointer");
   if (n == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == LLP_BF16)
@@ -157,7 +157,7 @@ extern "C" int llp_relu_bwd(int dtype, int64_t n, const void* gy, const void* y,
 }
 
 extern "C" int llp_transpose(int dtype, int64_t rows, int64_t cols, const void* src, void* dst, void* stream) {
-  LLP_CHECK_ARG(src && dst, "llp_transpose: null pointer");
+  LLP_CHECK_ARG((rows == 0 || cols == 0) || (src && dst), "llp_transpose: null pointer");
   if (rows == 0 || cols == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(ceil_div_u(cols, 32), ceil_div_u(rows, 32));
@@ -186,7 +186,7 @@ extern "C" int llp_mul(int dtype, int64_t n, const void* a, const void* b, void*
 
 extern "C" int llp_row_scale(int dtype, int64_t rows, int64_t cols, const void* z, const float* sc, void* out,
                              void* stream) {
-  LLP_CHECK_ARG(z && sc && out, "llp_row_scale: null pointer");
+  LLP_CHECK_ARG((rows * cols == 0) || (z && sc && out), "llp_row_scale: null pointer");
   if (rows * cols == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == LLP_BF16)

@@ -289,7 +289,7 @@ extern "C" int64_t llp_norm_workspace_bytes(int64_t M, int64_t H) {
 
 extern "C" int llp_norm_colsums(int dtype, int64_t M, int64_t H, const void* y, int64_t ldy, const int32_t* m_dev,
                                 double* sums, void* ws, void* stream) {
-  LLP_CHECK_ARG(y && sums && ws, "llp_norm_colsums: null pointer");
+  LLP_CHECK_ARG((H == 0) || (sums && ws && (y || M == 0)), "llp_norm_colsums: null pointer");   // M = 0: zero sums
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_norm_colsums: dtype");
   if (H == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -310,7 +310,7 @@ extern "C" int llp_norm_fwd(int kind, int dtype, int64_t M, int64_t H, const voi
                             int64_t ldo, void* stream) {
   LLP_CHECK_ARG(kind == LN || kind == BN, "llp_norm_fwd: kind must be LLP_NORM_LAYER or LLP_NORM_BATCH");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_norm_fwd: dtype");
-  LLP_CHECK_ARG(y && out && stats, "llp_norm_fwd: null pointer");
+  LLP_CHECK_ARG((M == 0 || H == 0) || (y && out && stats), "llp_norm_fwd: null pointer");
   Drop d;
   if (int e = make_drop(dropout, d, "llp_norm_fwd")) return e;
   if (M == 0 || H == 0) return LLP_OK;
@@ -350,7 +350,7 @@ extern "C" int llp_norm_bwd_sums(int kind, int dtype, int64_t M, int64_t H, cons
                                  void* ws, void* stream) {
   LLP_CHECK_ARG(kind == LN || kind == BN, "llp_norm_bwd_sums: kind");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_norm_bwd_sums: dtype");
-  LLP_CHECK_ARG(gout && y && stats && sums && ws, "llp_norm_bwd_sums: null pointer");
+  LLP_CHECK_ARG((H == 0) || (sums && ws && (M == 0 || (gout && y && stats))), "llp_norm_bwd_sums: null pointer");
   LLP_CHECK_ARG(kind == LN || !m_dev, "llp_norm_bwd_sums: BatchNorm takes no device row count");
   if (H == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -379,7 +379,7 @@ extern "C" int llp_norm_bwd(int kind, int dtype, int64_t M, int64_t H, const voi
                             int64_t ldgy, void* stream) {
   LLP_CHECK_ARG(kind == LN || kind == BN, "llp_norm_bwd: kind");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_norm_bwd: dtype");
-  LLP_CHECK_ARG(gout && y && stats && gy, "llp_norm_bwd: null pointer");
+  LLP_CHECK_ARG((M == 0 || H == 0) || (gout && y && stats && gy), "llp_norm_bwd: null pointer");
   if (M == 0 || H == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (kind == LN) {

@@ -279,7 +279,7 @@ static int csr_aggregate_launch(int dtype, int64_t n_rows, int64_t F, const int3
 extern "C" int llp_csr_aggregate(int dtype, int64_t n_rows, int64_t F, const int32_t* rowptr, const int32_t* col,
                                  const void* x, int64_t ldx, const float* inv_deg, int mode, void* out, int64_t ldo,
                                  int accumulate, void* stream) {
-  LLP_CHECK_ARG(rowptr && x && out, "llp_csr_aggregate: null pointer");
+  LLP_CHECK_ARG(n_rows == 0 || F == 0 || (rowptr && x && out), "llp_csr_aggregate: null pointer");
   LLP_CHECK_ARG(mode == 0 || (mode == 1 && inv_deg), "llp_csr_aggregate: mode 1 needs inv_deg");
   return csr_aggregate_launch(dtype, n_rows, F, rowptr, col, x, ldx, inv_deg, mode, nullptr, out, ldo, accumulate,
                               (hipStream_t)stream);

@@ -176,7 +176,11 @@ extern "C" int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, i
                     (P == 0 || (pairs && perm && neg)),
                 "llp_minibatch_sample: null pointer");
   LLP_CHECK_ARG(ps_method == 0 || ps_method == 1, "llp_minibatch_sample: ps_method must be 0 (rw) or 1 (nb)");
-  LLP_CHECK_ARG(rw_step >= 1 && hops >= 1 && ns_rate >= 0 && rw_step < 15, "llp_minibatch_sample: bad step/hops");
+  // walks take streams 0 .. rw_step-1 of a step and the negatives stream rw_step, below the
+  // PyG-dense (S-2) and randint (S-1) negatives
+  LLP_CHECK_ARG(rw_step >= 1 && hops >= 1 && ns_rate >= 0 && rw_step <= LLP_STREAMS_PER_STEP - 3,
+                "llp_minibatch_sample: rw_step %d (1..%d), hops %d, ns_rate %d", rw_step, (int)(LLP_STREAMS_PER_STEP - 3),
+                hops, ns_rate);
   LLP_CHECK_ARG(p_offset + P <= P_total, "llp_minibatch_sample: shard out of range");
   MbSample a;
   a.rowptr = rowptr; a.col = col; a.num_nodes = num_nodes; a.start = start; a.B = B; a.b_offset = b_offset;
@@ -202,9 +206,13 @@ extern "C" int llp_context_sampler(const int32_t* rowptr, const int32_t* col, in
                                    const int32_t* start, int64_t B, int64_t b_offset, int ps_method, int rw_step,
                                    int hops, int ns_rate, uint64_t seed, const int64_t* step_ctr,
                                    int64_t stream_offset, int32_t* samples, void* stream) {
-  LLP_CHECK_ARG(rowptr && col && start && samples && step_ctr, "llp_context_sampler: null pointer");
+  LLP_CHECK_ARG((B == 0) || (rowptr && col && start && samples && step_ctr), "llp_context_sampler: null pointer");
   LLP_CHECK_ARG(ps_method == 0 || ps_method == 1, "llp_context_sampler: ps_method must be 0 (rw) or 1 (nb)");
-  LLP_CHECK_ARG(rw_step >= 1 && hops >= 1 && ns_rate >= 0 && rw_step < 15, "llp_context_sampler: bad step/hops");
+  // walks take streams 0 .. rw_step-1 of a step and the negatives stream rw_step, below the
+  // PyG-dense (S-2) and randint (S-1) negatives
+  LLP_CHECK_ARG(rw_step >= 1 && hops >= 1 && ns_rate >= 0 && rw_step <= LLP_STREAMS_PER_STEP - 3,
+                "llp_context_sampler: rw_step %d (1..%d), hops %d, ns_rate %d", rw_step, (int)(LLP_STREAMS_PER_STEP - 3),
+                hops, ns_rate);
   if (B == 0) return LLP_OK;
   hipStream_t s = (hipStream_t)stream;
   const int64_t C1 = 1 + (int64_t)rw_step * hops * (1 + ns_rate);
@@ -225,7 +233,7 @@ extern "C" int llp_context_sampler(const int32_t* rowptr, const int32_t* col, in
 
 extern "C" int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
                                  const int64_t* step_ctr, int64_t stream_offset, int32_t* out, void* stream) {
-  LLP_CHECK_ARG(out && step_ctr, "llp_randint_pairs: null pointer");
+  LLP_CHECK_ARG((n == 0) || (out && step_ctr), "llp_randint_pairs: null pointer");
   LLP_CHECK_ARG(offset + n <= n_total, "llp_randint_pairs: shard out of range");
   if (n == 0) return LLP_OK;
   hipLaunchKernelGGL(randint_pairs_kernel, dim3(ceil_div_u(2 * n, 256)), dim3(256), 0, (hipStream_t)stream,
@@ -249,7 +257,7 @@ extern "C" int llp_build_targets(int64_t B, int64_t C1, const int32_t* samples, 
 
 extern "C" int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* samples, int32_t* ia, int32_t* ib,
                                            void* stream) {
-  LLP_CHECK_ARG(samples && ia && ib, "llp_pair_index_from_samples: null pointer");
+  LLP_CHECK_ARG((B * C == 0) || (samples && ia && ib), "llp_pair_index_from_samples: null pointer");
   if (B * C == 0) return LLP_OK;
   hipLaunchKernelGGL(pair_index_kernel, dim3(ceil_div_u(B * C, 256)), dim3(256), 0, (hipStream_t)stream, B, C,
                      samples, ia, ib);

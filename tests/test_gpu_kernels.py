@@ -373,7 +373,8 @@ def test_llp_loss_matches_oracle(B, C, margin):
 
 
 # ------------------------------------------------------------------ samplers (bit-exact)
-@pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 1, 15, 0)])
+@pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 1, 15, 0),
+                                                    ("nb", 20, 2, 1), ("nb", 61, 1, 0)])
 @pytest.mark.parametrize("sorted_", [False, True])
 def test_context_sampler_bit_exact(ps, rw_step, hops, ns_rate, sorted_):
     import llp_engine
@@ -404,7 +405,8 @@ def test_context_sampler_bit_exact(ps, rw_step, hops, ns_rate, sorted_):
     assert np.array_equal(out2.cpu().numpy(), ref[60:])
 
 
-@pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 2, 3, 0)])
+@pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 2, 3, 0),
+                                                    ("nb", 20, 2, 1)])
 @pytest.mark.parametrize("b_off,p_off", [(0, 0), (40, 300)])
 def test_minibatch_sample_equals_separate_kernels(ps, rw_step, hops, ns_rate, b_off, p_off):
     """llp_minibatch_sample == context_sampler + randint_pairs + build_targets +
