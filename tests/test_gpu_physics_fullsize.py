@@ -104,8 +104,8 @@ def test_physics_fullbatch_bf16_tracks_fp32(physics):
     parameters' gradients at initialisation are differences of nearly balanced
     positive / negative pair contributions (BCE at sigmoid(0) ~ 1/2, a constant
     rank hinge), so bf16 rounding of the activations moves them by O(1)
-    relative (tools/debug_physics_bf16.py prints every parameter); the
-    reference has no bf16 path to hold them to."""
+    relative (a round-2 diagnostic printed every parameter's); the reference
+    has no bf16 path to hold them to."""
     f32 = _step(physics, "fp32")
     b16 = _step(physics, "bf16")
     for k in range(4):
