@@ -124,7 +124,7 @@ def _single():
     return torch.cat([t.reshape(-1) for t in g]).numpy(), float(loss.detach())
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])   # 4: the physics config's rank count (configs[3])
 def test_node_sharded_student_sums_to_the_batch_gradient(world):
     full, full_loss = _single()
     ctx = mp.get_context("spawn")

@@ -1,5 +1,5 @@
 """The data-parallel decomposition the engines implement, checked
-on CPU with the oracle over 2 gloo ranks: each rank takes a contiguous slice of
+on CPU with the oracle over 2, 3 and 8 gloo ranks: each rank takes a contiguous slice of
 the anchors (`node_perm`) and of the positive / negative label edges, weights
 its loss terms by global normalisers (KL and margin-rank by B_shard / B_total,
 BCE by 2 P_shard / 2 P_total), and a SUM all-reduce of the gradients equals the
@@ -11,6 +11,7 @@ import socket
 import types
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -81,7 +82,10 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_sum_to_the_batch_gradient():
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_rank_shards_sum_to_the_batch_gradient(world):
+    """2 ranks, 3 (uneven slices of the 40 label edges) and 8 (the driver's largest
+    data-parallel run: 3 anchors and 5 label edges per rank)."""
     old = torch.get_default_dtype()
     try:
         full, full_loss = _grads(0, 1)
@@ -91,7 +95,7 @@ def test_two_rank_shards_sum_to_the_batch_gradient():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     flat, loss = q.get(timeout=240)
