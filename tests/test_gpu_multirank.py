@@ -144,11 +144,11 @@ def _graph_worker(rank, world, port, q, use_graph, size):
         q.put(out)
 
 
-def _two_ranks(use_graph, size):
+def _n_ranks(use_graph, size, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, q, use_graph, size)) for r in range(2)]
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, q, use_graph, size)) for r in range(world)]
     for p in procs:
         p.start()
     out = q.get(timeout=300)
@@ -158,17 +158,17 @@ def _two_ranks(use_graph, size):
     return out
 
 
-@pytest.mark.parametrize("size", [{}, dict(N=235_868, n_pairs=400_000, B=4096, P=16384)],
-                         ids=["small", "collab_nodes"])
-def test_two_ranks_segmented_graph_matches_eager(size):
+@pytest.mark.parametrize("size,world", [({}, 2), (dict(N=235_868, n_pairs=400_000, B=4096, P=16384), 2), ({}, 4)],
+                         ids=["small", "collab_nodes", "small_4ranks"])
+def test_two_ranks_segmented_graph_matches_eager(size, world):
     """BASELINE configs[4]: the multi-rank step replayed from hipGraph segments (the
     all-reduces run between them) is bit-identical to eager multi-rank steps.  At the
     collab node count the unique-node compaction's scan runs over 116 blocks (the round-2
     replay fault was there); the 2,000-node case is one block."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    eager = _two_ranks(False, size)
-    graph = _two_ranks(True, size)
+    eager = _n_ranks(False, size, world)
+    graph = _n_ranks(True, size, world)
     # cuts: the predictor's all-reduce, one bucket per student layer but the first, the rest + clip/Adam
     assert graph["segments"] == 5
     assert graph["loss"] == eager["loss"], (graph["loss"], eager["loss"])
@@ -232,14 +232,16 @@ def _fullbatch_worker(rank, world, port, q, shard, norm_type="none"):
         q.put(out)
 
 
-def test_two_ranks_fullbatch_equal_one_rank():
-    """Anchor / link batches of the full-batch step sharded over 2 ranks (every rank
-    draws the same dense negatives and keeps its columns) == the whole batch on one.
-    Default engine: each rank runs the student on half of the nodes, the halves are
-    all-gathered and d(h) is reduce-scattered back in f32 (DistillEngine._fb_shard)."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_ranks_fullbatch_equal_one_rank(world):
+    """Anchor / link batches of the full-batch step sharded over 2 (and 4, the physics
+    config's count) ranks (every rank draws the same dense negatives and keeps its
+    columns) == the whole batch on one.  Default engine: each rank runs the student on
+    its slice of the nodes, the slices are all-gathered and d(h) is reduce-scattered
+    back in f32 (DistillEngine._fb_shard)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _fullbatch_compare()
+    _fullbatch_compare(world=world)
 
 
 def test_two_ranks_fullbatch_replicated_student_equal_one_rank():
@@ -259,13 +261,13 @@ def test_two_ranks_fullbatch_norm_equal_one_rank(norm_type):
     _fullbatch_compare(norm_type=norm_type, free={1} if norm_type == "batch" else set())
 
 
-def _fullbatch_compare(shard=True, norm_type="none", free=()):
+def _fullbatch_compare(shard=True, norm_type="none", free=(), world=2):
     single = {}
     _run_fullbatch(0, 1, 0, single, shard, norm_type)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fullbatch_worker, args=(r, 2, port, q, shard, norm_type)) for r in range(2)]
+    procs = [ctx.Process(target=_fullbatch_worker, args=(r, world, port, q, shard, norm_type)) for r in range(world)]
     for p in procs:
         p.start()
     multi = q.get(timeout=300)
@@ -322,8 +324,9 @@ def test_two_ranks_norm_equal_one_rank(norm_type):
         assert float(abs(a.astype("float64") - b.astype("float64")).max()) <= 0.1 * 2 * 0.01 + 1e-4
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_two_ranks_equal_one_rank(dtype):
+@pytest.mark.parametrize("dtype,world", [("fp32", 2), ("bf16", 2), ("fp32", 4)])
+def test_two_ranks_equal_one_rank(dtype, world):
+    """The minibatch step over 2 (and 4) gloo ranks on one GPU == the whole batch on one rank."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     single = {}
@@ -331,7 +334,7 @@ def test_two_ranks_equal_one_rank(dtype):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, dtype, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, dtype, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     multi = q.get(timeout=300)
