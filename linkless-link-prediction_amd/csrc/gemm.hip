@@ -604,7 +604,7 @@ bool aligned_op(const llp_operand* o, int esize, int64_t extent_mult) {
 int64_t tn_splits(int dtype, int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + BM - 1) / BM) * ((Q + BN - 1) / BN);
   const int64_t bkm = dtype == LLP_BF16 ? 64 : 32;
-  int64_t splits = (1024 + tiles - 1) / tiles;
+  int64_t splits = tiles >= 1024 ? 1 : 1024 / tiles;   // whole waves (two blocks per CU): no sliver of a round
   const int64_t maxs = (M + bkm * 8 - 1) / (bkm * 8);  // at least 8 m-steps per split
   if (splits > maxs) splits = maxs;
   if (splits < 1) splits = 1;
