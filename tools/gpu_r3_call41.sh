@@ -1,0 +1,15 @@
+# short-segment sort as a bitonic network in registers (default) vs the insertion sort in LDS (sortold):
+# dedup / unique-node tests, then the physics step (1 rank, rank 0 of 4) and the collab step
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/c41
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu -k "dedup or unique or segment or compaction or fullsize or engine" > $O/pytest.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+L="new=linkless-link-prediction_amd/libllp_hip.so old=tools/bin/libllp_hip_sortold.so"
+timeout -k 10 400 python -u tools/ab_gemm.py $L --rounds 3 --script tools/physics_bench.py --args "--steps 20 --dtype bf16" > $O/ab_p1.log 2>&1 || { tail -20 $O/ab_p1.log; exit 1; }
+tail -1 $O/ab_p1.log
+timeout -k 10 400 python -u tools/ab_gemm.py $L --rounds 3 --script tools/physics_bench.py --args "--steps 20 --dtype bf16 --emulate-ranks 4 --graph" > $O/ab_p4.log 2>&1 || { tail -20 $O/ab_p4.log; exit 1; }
+tail -1 $O/ab_p4.log
+timeout -k 10 600 python -u tools/ab_gemm.py $L --rounds 3 --script bench.py --args "--steps 30 --warmup 5 --no-cpu-baseline --no-eval --no-sage --no-physics --no-shard8 --no-fp32 --no-practical-peak" > $O/ab_collab.log 2>&1 || { tail -20 $O/ab_collab.log; exit 1; }
+tail -1 $O/ab_collab.log

@@ -91,13 +91,15 @@ def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False):
             replay.replay()
         else:
             step(warmup + s)
+    t_issue = (time.perf_counter() - t0) / steps    # host time to enqueue a step (the GPU runs behind it)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     loss = eng.end_epoch(steps * P_full)
     return {"dtype": dtype, "ms_per_step": dt * 1e3, "edges_per_s": P_full / dt if not emulate else None,
             "emulated_ranks": emulate or None, "fb_shard": eng.emulate_shard is not None, "N_old": N, "F": F, "E_train_directed": E, "anchors_per_step": B_full,
             "contexts_per_anchor": a.rw_step * a.hops * (1 + a.ns_rate), "edges_per_step": P_full,
-            "steps_per_epoch": -(-E // P_full), "loss": loss, "hipgraph": replay is not None}
+            "steps_per_epoch": -(-E // P_full), "loss": loss, "hipgraph": replay is not None,
+            "host_issue_ms_per_step": t_issue * 1e3}
 
 
 def main():
