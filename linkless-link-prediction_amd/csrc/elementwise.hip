@@ -263,7 +263,11 @@ __global__ __launch_bounds__(256) void hadamard_rows_wave_kernel(int64_t R, int6
 }
 
 // ---------------------------------------------------------------- optimiser
-constexpr int OPT_CHUNK = 4096;  // elements per block
+constexpr int OPT_CHUNK = 4096;  // elements per block of the gradient norm (fixes its summation order)
+#ifndef LLP_ADAM_CHUNK
+#define LLP_ADAM_CHUNK 1024
+#endif
+constexpr int ADAM_CHUNK = LLP_ADAM_CHUNK;   // elements per block of Adam / the shadow refresh (one 4-wide pass)
 
 // element e = (r, c) of a [rows, cols] parameter -> its slot in a shadow with
 // leading dimension shadow_ld (0 = packed)
@@ -344,9 +348,9 @@ __global__ __launch_bounds__(256) void adam_kernel(const llp_tensor_desc* __rest
                                                    float beta1, float beta2, float eps,
                                                    const int64_t* __restrict__ step) {
   const llp_tensor_desc d = descs[blockIdx.y];
-  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
+  const int64_t e0 = (int64_t)blockIdx.x * ADAM_CHUNK;
   if (e0 >= d.numel) return;
-  const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
+  const int64_t e1 = min(d.numel, e0 + ADAM_CHUNK);
   float coef = 1.f;
   if (sumsq) {
     const float total = sqrtf(sumsq[d.group]);
@@ -437,9 +441,9 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
 
 __global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __restrict__ descs) {
   const llp_tensor_desc d = descs[blockIdx.y];
-  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
+  const int64_t e0 = (int64_t)blockIdx.x * ADAM_CHUNK;
   if (e0 >= d.numel) return;
-  const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
+  const int64_t e1 = min(d.numel, e0 + ADAM_CHUNK);
   for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
     if (d.shadow) put_elem(d.shadow, shadow_index(d, e), d.param[e], d.shadow_dtype);
 }
@@ -465,6 +469,7 @@ __global__ void accumulate_kernel(int64_t n, const float* __restrict__ src, floa
 }
 
 int64_t max_chunks_of(int64_t max_numel) { return (max_numel + OPT_CHUNK - 1) / OPT_CHUNK; }
+int64_t adam_chunks_of(int64_t max_numel) { return (max_numel + ADAM_CHUNK - 1) / ADAM_CHUNK; }
 
 }  // namespace
 
@@ -588,7 +593,8 @@ extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_
   LLP_CHECK_ARG(descs && step, "llp_adam_step: null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int64_t mc = max_chunks_of(max_numel);
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, sumsq, max_norm, lr,
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0, s, descs,
+                     sumsq, max_norm, lr,
                      beta1, beta2, eps, (const int64_t*)step);
   LLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, step);
@@ -599,7 +605,8 @@ extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_
 extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream) {
   LLP_CHECK_ARG(descs, "llp_refresh_shadows: null pointer");
   const int64_t mc = max_chunks_of(max_numel);
-  hipLaunchKernelGGL(shadow_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream, descs);
+  hipLaunchKernelGGL(shadow_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0,
+                     (hipStream_t)stream, descs);
   LLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, (hipStream_t)stream,
                      descs, (int64_t*)nullptr);
