@@ -241,11 +241,15 @@ int llp_gather_rows(int64_t n, int64_t row_bytes, const int32_t* idx, const void
  * the [R1, H] row buffer.  anchor_rows: caller-owned [B, H] scratch (compute dtype)
  * for the anchors' context sums.  Row layouts as llp_hadamard_bwd_blocks; h is the
  * unique-node table [U, H], pos maps target rows to it; drow (dZ = NULL) is the
- * 'inner' predictor's per-pair scalar. */
+ * 'inner' predictor's per-pair scalar.  dh rows are of out_dtype (dtype, or LLP_F32:
+ * the sums unrounded, for a following cross-rank reduction) and node u's sum goes to
+ * row out_rows[u] (NULL: row u).  With B = C = 0 the rows are the label-row layout
+ * alone: the full-batch student's d(h[ia] * h[ib]) with pos = [ia | ib] node ids, h
+ * the [N, H] node table and out_rows = the unique node ids (src/main.py:173-235). */
 int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
                               const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos, const void* dZ,
                               const float* drow, const void* h, void* anchor_rows, void* dh, int64_t ld_dh,
-                              const int32_t* u_dev, void* stream);
+                              int out_dtype, const int32_t* out_rows, const int32_t* u_dev, void* stream);
 
 /* Generic scatter form (full-batch train(), src/main.py:173-214, where rows of
  * h repeat): dh[ia[r]] += dZ[r]*h2[ib[r]],  dh[ib[r]] += dZ[r]*h1[ia[r]]

@@ -137,6 +137,17 @@ __device__ __forceinline__ float round_to(float x) {
   else return x;
 }
 
+// one 16-B input chunk's E sums into an output row of type TO (T: rounded once; f32: as summed)
+template <typename T, typename TO>
+__device__ __forceinline__ void store_sums(TO* p, const float* acc) {
+  if constexpr (std::is_same<T, TO>::value) {
+    *reinterpret_cast<uint4*>(p) = V8<T>::pack(acc);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V8<T>::E; i += 4) *reinterpret_cast<uint4*>(p + i) = V8<float>::pack(acc + i);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void hadamard_anchor_rows_kernel(int64_t B, int64_t C, int64_t H,
                                                                    const T* __restrict__ dZ,
@@ -232,12 +243,12 @@ __global__ __launch_bounds__(256) void hadamard_anchor_rows_wave_kernel(int64_t 
     *reinterpret_cast<uint4*>(arow + b * H + (int64_t)(lane + 64 * j) * E) = V8<T>::pack(acc[j]);
 }
 
-template <typename T>
+template <typename T, typename TO>
 __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
     int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ rows, const int32_t* __restrict__ pos, const T* __restrict__ dZ,
-    const float* __restrict__ drow, const T* __restrict__ h, const T* __restrict__ arow, T* __restrict__ dh,
-    int64_t ldo, const int32_t* __restrict__ u_dev) {
+    const float* __restrict__ drow, const T* __restrict__ h, const T* __restrict__ arow, TO* __restrict__ dh,
+    int64_t ldo, const int32_t* __restrict__ out_rows, const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
   const int cpr = (int)(H / E);
   const int spb = 256 / cpr;
@@ -306,7 +317,7 @@ __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
 #pragma unroll
     for (int i = 0; i < E; ++i) acc[i] += v0[i];
   }
-  *reinterpret_cast<uint4*>(dh + u * ldo + col) = V8<T>::pack(acc);
+  store_sums<T, TO>(dh + (out_rows ? (int64_t)out_rows[u] : u) * ldo + col, acc);
 }
 
 // Same sums, NPW nodes per wave (LPN = 64 / NPW lanes per node; lane l of a node owns
@@ -319,12 +330,12 @@ __global__ __launch_bounds__(256) void hadamard_bwd_segments_kernel(
 // of G rows at a time are issued together from the broadcast descriptors; several
 // nodes per wave keep more of those chains in flight.  Same values, same f32 additions
 // in row order: bit-identical to the kernel above.
-template <typename T, int NCH, int G, int NPW>
+template <typename T, typename TO, int NCH, int G, int NPW>
 __global__ __launch_bounds__(256) void hadamard_bwd_segments_wave_kernel(
     int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ rows, const int32_t* __restrict__ pos, const T* __restrict__ dZ,
-    const float* __restrict__ drow, const T* __restrict__ h, const T* __restrict__ arow, T* __restrict__ dh,
-    int64_t ldo, const int32_t* __restrict__ u_dev) {
+    const float* __restrict__ drow, const T* __restrict__ h, const T* __restrict__ arow, TO* __restrict__ dh,
+    int64_t ldo, const int32_t* __restrict__ out_rows, const int32_t* __restrict__ u_dev) {
   constexpr int E = V8<T>::E;
   constexpr int LPN = 64 / NPW;
   const int lane = threadIdx.x & 63;
@@ -408,9 +419,9 @@ __global__ __launch_bounds__(256) void hadamard_bwd_segments_wave_kernel(
     }
   }
   if (!live) return;
+  const int64_t orow = out_rows ? (int64_t)out_rows[u] : u;
 #pragma unroll
-  for (int j = 0; j < NCH; ++j)
-    *reinterpret_cast<uint4*>(dh + u * ldo + (int64_t)(nl + LPN * j) * E) = V8<T>::pack(acc[j]);
+  for (int j = 0; j < NCH; ++j) store_sums<T, TO>(dh + orow * ldo + (int64_t)(nl + LPN * j) * E, acc[j]);
 }
 
 // out row r = src row idx[r] for r < min(n, *count): 16-byte chunks, one thread each
@@ -829,11 +840,13 @@ extern "C" int llp_gather_rows(int64_t n, int64_t row_bytes, const int32_t* idx,
 extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_t C, int64_t L2, int64_t H,
                                          const int32_t* seg_ptr, const int32_t* rows, const int32_t* pos,
                                          const void* dZ, const float* drow, const void* h, void* anchor_rows,
-                                         void* dh, int64_t ld_dh, const int32_t* u_dev, void* stream) {
+                                         void* dh, int64_t ld_dh, int out_dtype, const int32_t* out_rows,
+                                         const int32_t* u_dev, void* stream) {
   LLP_CHECK_ARG(seg_ptr && rows && pos && h && dh && (dZ || drow) && (anchor_rows || B == 0),
                 "llp_hadamard_bwd_segments: null");
+  LLP_CHECK_ARG(out_dtype == dtype || out_dtype == LLP_F32, "llp_hadamard_bwd_segments: out_dtype must be dtype or f32");
   const int E = dtype == LLP_BF16 ? 8 : 4;
-  const int es = dtype == LLP_BF16 ? 2 : 4;
+  const int es = out_dtype == LLP_BF16 ? 2 : 4;   // of the output rows
   LLP_CHECK_ARG(H % E == 0 && H / E <= 256 && (ld_dh * es) % 16 == 0 && (uintptr_t)h % 16 == 0 &&
                     (uintptr_t)dh % 16 == 0 && (!dZ || (uintptr_t)dZ % 16 == 0) &&
                     (uintptr_t)anchor_rows % 16 == 0,
@@ -875,30 +888,37 @@ extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_
   if (nch == 1 || nch == 2 || nch == 4 || nch == 8) {
     auto launch = [&](auto kern, auto* dz, auto* hh, auto* ar, auto* out) {
       hipLaunchKernelGGL(kern, dim3(ceil_div_u(U, 4)), dim3(256), 0, s, U, B, C, L2, H, seg_ptr, rows, pos, dz, drow,
-                         hh, ar, out, ld_dh, u_dev);
+                         hh, ar, out, ld_dh, out_rows, u_dev);
     };
     auto pick = [&](auto* dz, auto* hh, auto* ar, auto* out) {
       using TT = std::remove_const_t<std::remove_pointer_t<decltype(dz)>>;
-      if (nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, 1, 8, 1>, dz, hh, ar, out);
-      else if (nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, 2, 4, 1>, dz, hh, ar, out);
-      else if (nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, 4, 2, 1>, dz, hh, ar, out);
-      else launch(hadamard_bwd_segments_wave_kernel<TT, 8, 1, 1>, dz, hh, ar, out);
+      using TO = std::remove_pointer_t<decltype(out)>;
+      if (nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 1, 8, 1>, dz, hh, ar, out);
+      else if (nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 2, 4, 1>, dz, hh, ar, out);
+      else if (nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 4, 2, 1>, dz, hh, ar, out);
+      else launch(hadamard_bwd_segments_wave_kernel<TT, TO, 8, 1, 1>, dz, hh, ar, out);
     };
-    if (dtype == LLP_BF16)
+    if (dtype == LLP_BF16 && out_dtype == LLP_BF16)
       pick((const bf16_t*)dZ, (const bf16_t*)h, (const bf16_t*)anchor_rows, (bf16_t*)dh);
+    else if (dtype == LLP_BF16)
+      pick((const bf16_t*)dZ, (const bf16_t*)h, (const bf16_t*)anchor_rows, (float*)dh);
     else
       pick((const float*)dZ, (const float*)h, (const float*)anchor_rows, (float*)dh);
     LLP_LAUNCH_CHECK();
     return LLP_OK;
   }
-  if (dtype == LLP_BF16)
-    hipLaunchKernelGGL(hadamard_bwd_segments_kernel<bf16_t>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
-                       H, seg_ptr, rows, pos, (const bf16_t*)dZ, drow, (const bf16_t*)h, (const bf16_t*)anchor_rows,
-                       (bf16_t*)dh, ld_dh, u_dev);
+  auto go = [&](auto* dz, auto* hh, auto* ar, auto* out) {
+    using TT = std::remove_const_t<std::remove_pointer_t<decltype(dz)>>;
+    using TO = std::remove_pointer_t<decltype(out)>;
+    hipLaunchKernelGGL((hadamard_bwd_segments_kernel<TT, TO>), dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
+                       H, seg_ptr, rows, pos, dz, drow, hh, ar, out, ld_dh, out_rows, u_dev);
+  };
+  if (dtype == LLP_BF16 && out_dtype == LLP_BF16)
+    go((const bf16_t*)dZ, (const bf16_t*)h, (const bf16_t*)anchor_rows, (bf16_t*)dh);
+  else if (dtype == LLP_BF16)
+    go((const bf16_t*)dZ, (const bf16_t*)h, (const bf16_t*)anchor_rows, (float*)dh);
   else
-    hipLaunchKernelGGL(hadamard_bwd_segments_kernel<float>, dim3(ceil_div_u(U, spb)), dim3(256), 0, s, U, B, C, L2,
-                       H, seg_ptr, rows, pos, (const float*)dZ, drow, (const float*)h, (const float*)anchor_rows,
-                       (float*)dh, ld_dh, u_dev);
+    go((const float*)dZ, (const float*)h, (const float*)anchor_rows, (float*)dh);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

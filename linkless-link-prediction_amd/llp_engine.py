@@ -568,9 +568,11 @@ class EngineBase:
     def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
         """d(loss)/dh of the predictor input h[ia] * h[ib] into ``out`` [N, H] (compute dtype, or f32),
         deterministically: the 2R endpoint rows tgt = [ia | ib] are grouped by node
-        (llp_dedup_rows), each row's gradient dZ[r] * h[partner] is formed once
-        (llp_hadamard_bwd_blocks, label-row layout; drow: the 'inner' predictor's scalar) and
-        every node's rows are summed in row order (f32) into its row of ``out``; other rows are 0."""
+        (llp_dedup_rows), and one pass per node (llp_hadamard_bwd_segments in the label-row
+        layout, B = C = 0) forms each of its rows' gradient dZ[r] * h[partner] as the row
+        kernel would store it and sums them in row order (f32) into its row of ``out``
+        (drow: the 'inner' predictor's scalar); other rows are 0.  Bit-identical to
+        llp_hadamard_bwd_blocks + llp_segment_sum_rows without their [2R, H] row buffer."""
         N, H = self.N, h.shape[1]
         if not self._grouped_ok(H):
             # rows wider than the grouping kernels take: f32 scatter-add (atomics, so not
@@ -588,10 +590,9 @@ class EngineBase:
         seg_rows = self._buf("hb_segr", (R2,), torch.int32)
         wsd = self._buf("hb_ws", (K.dedup_ws_bytes(N, R2) // 4 + 16,), torch.float32)
         K.dedup_rows(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
-        dh_rows = self._buf("hb_rows", (R2, H), h.dtype)
-        K.hadamard_bwd_blocks(0, 1, R, H, dZ, h, dh_rows, drow=drow, hidx=tgt)
         out.zero_()
-        K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, out, count=n_u, out_rows=uniq)
+        K.hadamard_bwd_segments(min(R2, N), 0, 0, R, H, seg_ptr, seg_rows, tgt, dZ, h, out, None, drow=drow,
+                                count=n_u, out_rows=uniq)
 
     def _grouped_ok(self, H):
         """The node-grouped Hadamard-backward kernels (llp_hadamard_bwd_segments,

@@ -73,7 +73,7 @@ _SIGS = {
     "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_int, c_vp, c_vp,
                                      c_vp]),
     "llp_hadamard_bwd_segments": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                          c_vp, c_i64, c_vp, c_vp]),
+                                          c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "llp_gather_i32": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_gather_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "llp_minibatch_sample": (c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_u64, c_vp,
@@ -325,14 +325,17 @@ def segment_sum_rows(U, seg_ptr, rows, src, out, count=None, out_rows=None):
                                  ptr(out_rows), ptr(count), stream_ptr()), "llp_segment_sum_rows")
 
 
-def hadamard_bwd_segments(U, B, C, L2, H, seg_ptr, rows, pos, dZ, h, dh, anchor_rows, drow=None, count=None):
-    """dh[u] (U x H) = per-node sum of the Hadamard-backward rows (llp_hadamard_bwd_segments);
-    anchor_rows: [B, H] scratch of h's dtype."""
+def hadamard_bwd_segments(U, B, C, L2, H, seg_ptr, rows, pos, dZ, h, dh, anchor_rows, drow=None, count=None,
+                          out_rows=None):
+    """dh[u] (U x H; dh[out_rows[u]] with ``out_rows``) = per-node sum of the Hadamard-backward
+    rows (llp_hadamard_bwd_segments), in dh's dtype (h's, or f32); anchor_rows: [B, H] scratch
+    of h's dtype (None when B = 0)."""
     L = lib()
     t = dZ if dZ is not None else h
     check(L.llp_hadamard_bwd_segments(dtype_code(t.dtype), U, B, C, L2, H, seg_ptr.data_ptr(), rows.data_ptr(),
-                                      pos.data_ptr(), ptr(dZ), ptr(drow), h.data_ptr(), anchor_rows.data_ptr(),
-                                      dh.data_ptr(), dh.stride(0), ptr(count), stream_ptr()),
+                                      pos.data_ptr(), ptr(dZ), ptr(drow), h.data_ptr(), ptr(anchor_rows),
+                                      dh.data_ptr(), dh.stride(0), dtype_code(dh.dtype), ptr(out_rows), ptr(count),
+                                      stream_ptr()),
           "llp_hadamard_bwd_segments")
 
 

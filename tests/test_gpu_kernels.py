@@ -725,6 +725,52 @@ def test_hadamard_bwd_segments(dtype, inner, N, H):
     assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("dtype,out_f32", [(torch.float32, False), (torch.bfloat16, False), (torch.bfloat16, True)])
+@pytest.mark.parametrize("inner", [False, True])
+@pytest.mark.parametrize("H", [256, 1024])
+def test_hadamard_bwd_segments_label_rows_onto_nodes(dtype, out_f32, inner, H):
+    """The full-batch form (DistillEngine._hadamard_bwd_nodes): B = C = 0, pos = [ia | ib]
+    node ids, h the [N, H] node table, each node's sum written to row out_rows[u] = its
+    node id of a zeroed [N, H] output (compute dtype, or f32 unrounded): bit-identical to
+    llp_hadamard_bwd_blocks + llp_segment_sum_rows(out_rows) (the round-3 path)."""
+    k = K()
+    g = torch.Generator().manual_seed(H + 3 * inner)
+    N, R = 700, 2500                                   # R pairs, 2R endpoint rows, skewed degrees
+    ia = (torch.randint(0, N, (R,), generator=g) ** 2 // N).to(torch.int32)
+    ib = torch.randint(0, N, (R,), generator=g).to(torch.int32)
+    tgt = torch.cat([ia, ib]).to(DEV)
+    R2 = 2 * R
+    uniq, pos = (torch.empty(R2, dtype=torch.int32, device=DEV) for _ in range(2))
+    nu = torch.empty(1, dtype=torch.int32, device=DEV)
+    segp = torch.empty(R2 + 1, dtype=torch.int32, device=DEV)
+    segr = torch.empty(R2, dtype=torch.int32, device=DEV)
+    ws = torch.empty(k.dedup_ws_bytes(N, R2) // 4 + 16, device=DEV)
+    k.dedup_rows(N, R2, tgt, uniq, pos, nu, segp, segr, ws)
+    h = torch.randn(N, H, generator=g).to(DEV, dtype)
+    dZ = torch.randn(R, H, generator=g).to(DEV, dtype)
+    drow = torch.randn(R, generator=g).to(DEV)
+    odt = torch.float32 if out_f32 else dtype
+    out = torch.full((N, H), 5.0, device=DEV, dtype=odt)
+    out.zero_()
+    U = min(R2, N)
+    k.hadamard_bwd_segments(U, 0, 0, R, H, segp, segr, tgt, None if inner else dZ, h, out, None,
+                            drow=drow if inner else None, count=nu, out_rows=uniq)
+    rows = torch.empty(R2, H, device=DEV, dtype=dtype)
+    k.hadamard_bwd_blocks(0, 1, R, H, None if inner else dZ, h, rows, drow=drow if inner else None, hidx=tgt)
+    out2 = torch.zeros(N, H, device=DEV, dtype=odt)
+    k.segment_sum_rows(U, segp, segr, rows, out2, count=nu, out_rows=uniq)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2), (out.float() - out2.float()).abs().max().item()
+    # and against the definition: d(h[ia] * h[ib]) summed per node
+    d = drow.cpu().unsqueeze(1).expand(R, H) if inner else dZ.float().cpu()
+    hf = h.float().cpu()
+    ref = torch.zeros(N, H)
+    ref.index_add_(0, ia.long(), d * hf[ib.long()])
+    ref.index_add_(0, ib.long(), d * hf[ia.long()])
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert torch.allclose(out.float().cpu(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
 @pytest.mark.parametrize("M,N,Kd", [(1000, 1024, 128), (517, 96, 256), (300, 288, 64)])
 def test_gemm_relu_bit_mask(M, N, Kd):
     """act=RELU with a uint8 aux writes bit c%8 of byte c/8 = (bf16 output > 0);

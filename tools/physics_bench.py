@@ -36,6 +36,25 @@ def physics_args():
                                  hidden_channels=256, num_layers=2, link_batch_size=64 * 1024, predictor="mlp")
 
 
+def _hb_two_kernel(self, R, tgt, dZ, drow, h, out):
+    """A/B (--hb-two-kernel): the round-3 Hadamard backward of DistillEngine._hadamard_bwd_nodes,
+    the row kernel writing a [2R, H] buffer, then the per-node segment sum."""
+    K = llp_engine.K
+    N, H = self.N, h.shape[1]
+    R2 = 2 * R
+    uniq = self._buf("hb_uniq", (R2,), torch.int32)
+    pos = self._buf("hb_pos", (R2,), torch.int32)
+    n_u = self._buf("hb_nu", (1,), torch.int32)
+    seg_ptr = self._buf("hb_segp", (R2 + 1,), torch.int32)
+    seg_rows = self._buf("hb_segr", (R2,), torch.int32)
+    wsd = self._buf("hb_ws", (K.dedup_ws_bytes(N, R2) // 4 + 16,), torch.float32)
+    K.dedup_rows(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
+    dh_rows = self._buf("hb_rows", (R2, H), h.dtype)
+    K.hadamard_bwd_blocks(0, 1, R, H, dZ, h, dh_rows, drow=drow, hidx=tgt)
+    out.zero_()
+    K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, out, count=n_u, out_rows=uniq)
+
+
 def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False):
     dev = torch.device("cuda", 0)
     a = physics_args()
@@ -113,7 +132,11 @@ def main():
                     help="replay a hipGraph of the step (capture_fullbatch); eager measured faster, "
                          "profiles/r03_physics_devcount_graph_ab.txt")
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "llp_physics"))
+    ap.add_argument("--hb-two-kernel", action="store_true",
+                    help="A/B: the round-3 two-kernel Hadamard backward (profiles/r03_hb_fused_fb_ab.txt)")
     opt = ap.parse_args()
+    if opt.hb_two_kernel:
+        llp_engine.DistillEngine._hadamard_bwd_nodes = _hb_two_kernel
     t0 = time.perf_counter()
     split = llp_split.production_split("coauthor-physics", opt.data_dir, synthetic=True)
     prep = time.perf_counter() - t0
