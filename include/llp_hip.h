@@ -314,6 +314,8 @@ int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_
  * src/train_teacher_gnn.py:50).  edge_keys: sorted unique int64 keys
  * row*(N-1) + col - (row < col) of the non-self-loop edges.  sample_size =
  * int(1.1*num_neg/prob) as PyG computes it (host, with duplicate edges counted).
+ * edge_table (may be NULL): the keys' set from llp_edge_table_build, used instead of
+ * the sorted edge_keys for the membership test.
  * population = N(N-1) <= sample_size: the non-edges in ascending order (bit-exact
  * with PyG).  Otherwise `rounds` * sample_size Philox candidates (stream
  * 64*(*step_ctr)+stream_offset), duplicates and existing edges dropped, first
@@ -321,10 +323,19 @@ int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_
  * rounds.  out = int32[2, ld_out] (row 0 = source); *count = columns written
  * (may be < num_neg, as PyG's may). */
 int64_t llp_neg_sample_dense_workspace_bytes(int64_t max_candidates);
-int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys, int64_t num_neg,
+int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys,
+                         const uint64_t* edge_table, int64_t edge_table_size, int64_t num_neg,
                          int64_t sample_size, int rounds, uint64_t seed, const int64_t* step_ctr,
                          int64_t stream_offset, int32_t* out, int64_t ld_out, int32_t* count,
                          void* workspace, int64_t workspace_bytes, void* stream);
+/* The graph's edge keys (PyG's dense encoding, as edge_keys above) in an open-addressing
+ * set of llp_edge_table_size(n_keys) slots (a power of two), built once per graph; passed
+ * to llp_neg_sample_dense as edge_table (edge_keys may then be NULL), a candidate's
+ * membership test is one or two probes instead of a binary search of the sorted keys.
+ * Same results either way. */
+int64_t llp_edge_table_size(int64_t n_keys);
+int llp_edge_table_build(const int64_t* edge_keys, int64_t n_keys, uint64_t* table, int64_t table_size,
+                         void* stream);
 
 /* Predictor-row indices of the full-batch step: rows [0, B*C) are (anchor,
  * context) pairs from samples[B, C1] (src/main.py:184-186), then P positives

@@ -29,6 +29,37 @@ __device__ __forceinline__ uint32_t mix32(uint64_t k) {
   return (uint32_t)k;
 }
 
+// the graph's edge keys in an open-addressing set (linear probing, kEmpty = free), built
+// once per graph (llp_edge_table_build): a candidate's membership costs one or two probes
+// instead of a binary search of ~18 dependent loads over the sorted keys
+__device__ __forceinline__ bool in_table(const uint64_t* __restrict__ t, int64_t T, uint64_t v) {
+  uint32_t h = mix32(v) & (uint32_t)(T - 1);
+  while (true) {
+    const uint64_t k = t[h];
+    if (k == v) return true;
+    if (k == kEmpty) return false;
+    h = (h + 1) & (uint32_t)(T - 1);
+  }
+}
+
+__global__ void edge_table_fill(uint64_t* __restrict__ t, int64_t T) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < T) t[i] = kEmpty;
+}
+
+__global__ void edge_table_insert(const int64_t* __restrict__ keys, int64_t n, uint64_t* __restrict__ t, int64_t T) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t c = (uint64_t)keys[i];
+  uint32_t h = mix32(c) & (uint32_t)(T - 1);
+  while (true) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&t[h], (unsigned long long)kEmpty,
+                                              (unsigned long long)c);
+    if (prev == kEmpty || prev == c) return;
+    h = (h + 1) & (uint32_t)(T - 1);
+  }
+}
+
 __global__ void neg_table_init(uint64_t* __restrict__ tkeys, int32_t* __restrict__ tmin, int64_t T) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < T) {
@@ -44,7 +75,9 @@ __global__ void neg_table_init(uint64_t* __restrict__ tkeys, int32_t* __restrict
 // smallest draw index per value (first occurrence = sampling without replacement).
 __global__ void neg_candidates(int64_t M, int enumerate_all, uint64_t population, uint64_t seed,
                                const int64_t* __restrict__ step_ctr, int64_t stream_offset,
-                               const int64_t* __restrict__ edge_keys, int64_t n_keys, int64_t* __restrict__ cand,
+                               const int64_t* __restrict__ edge_keys, int64_t n_keys,
+                               const uint64_t* __restrict__ edge_table, int64_t edge_table_size,
+                               int64_t* __restrict__ cand,
                                int32_t* __restrict__ slot, uint64_t* __restrict__ tkeys, int32_t* __restrict__ tmin,
                                int64_t T) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -59,7 +92,7 @@ __global__ void neg_candidates(int64_t M, int enumerate_all, uint64_t population
     c = __umul64hi((hi << 32) | lo, population);
   }
   cand[i] = (int64_t)c;
-  if (in_sorted(edge_keys, n_keys, (int64_t)c)) {
+  if (edge_table ? in_table(edge_table, edge_table_size, c) : in_sorted(edge_keys, n_keys, (int64_t)c)) {
     slot[i] = -1;
     return;
   }
@@ -301,13 +334,32 @@ extern "C" int64_t llp_neg_sample_dense_workspace_bytes(int64_t max_candidates) 
   return T * 8 + T * 4 + max_candidates * 8 + max_candidates * 4 + ntiles * 4 + 64;
 }
 
+extern "C" int64_t llp_edge_table_size(int64_t n_keys) { return pow2_at_least(2 * (n_keys > 0 ? n_keys : 1)); }
+
+extern "C" int llp_edge_table_build(const int64_t* edge_keys, int64_t n_keys, uint64_t* table, int64_t table_size,
+                                    void* stream) {
+  LLP_CHECK_ARG(table && (n_keys == 0 || edge_keys), "llp_edge_table_build: null pointer");
+  LLP_CHECK_ARG(n_keys >= 0 && table_size >= llp_edge_table_size(n_keys) && (table_size & (table_size - 1)) == 0,
+                "llp_edge_table_build: table_size must be a power of two >= llp_edge_table_size(n_keys)");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(edge_table_fill, dim3(ceil_div_u(table_size, 256)), dim3(256), 0, s, table, table_size);
+  if (n_keys > 0)
+    hipLaunchKernelGGL(edge_table_insert, dim3(ceil_div_u(n_keys, 256)), dim3(256), 0, s, edge_keys, n_keys, table,
+                       table_size);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
 extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys,
+                                    const uint64_t* edge_table, int64_t edge_table_size,
                                     int64_t num_neg, int64_t sample_size, int rounds, uint64_t seed,
                                     const int64_t* step_ctr, int64_t stream_offset, int32_t* out, int64_t ld_out,
                                     int32_t* count, void* workspace, int64_t workspace_bytes, void* stream) {
   LLP_CHECK_ARG(out && count && workspace && step_ctr, "llp_neg_sample_dense: null pointer");
   LLP_CHECK_ARG(num_nodes >= 2 && num_nodes < (1ll << 31), "llp_neg_sample_dense: num_nodes out of range");
-  LLP_CHECK_ARG(n_keys == 0 || edge_keys, "llp_neg_sample_dense: null edge keys");
+  LLP_CHECK_ARG(n_keys == 0 || edge_keys || edge_table, "llp_neg_sample_dense: null edge keys");
+  LLP_CHECK_ARG(!edge_table || (edge_table_size > 0 && (edge_table_size & (edge_table_size - 1)) == 0),
+                "llp_neg_sample_dense: edge_table_size must be a power of two");
   LLP_CHECK_ARG(rounds >= 1 && sample_size >= 0 && num_neg >= 0 && ld_out >= num_neg,
                 "llp_neg_sample_dense: bad sizes");
   hipStream_t s = (hipStream_t)stream;
@@ -328,7 +380,8 @@ extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys,
     hipLaunchKernelGGL(neg_table_init, dim3(ceil_div_u(T, 256)), dim3(256), 0, s, tkeys, tmin, T);
     LLP_LAUNCH_CHECK();
     hipLaunchKernelGGL(neg_candidates, dim3(ceil_div_u(M, 256)), dim3(256), 0, s, M, enumerate_all, population, seed,
-                       step_ctr, stream_offset, edge_keys, n_keys, cand, slot, tkeys, tmin, T);
+                       step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size, cand, slot, tkeys,
+                       tmin, T);
     LLP_LAUNCH_CHECK();
   }
   const int64_t ntiles = (M + NC_TILE - 1) / NC_TILE;

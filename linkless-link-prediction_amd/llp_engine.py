@@ -416,6 +416,7 @@ class EngineBase:
             key = src * (self.N - 1) + dst - (src < dst)
             self._neg_n_idx = int(key.size)                              # duplicates counted, as PyG does
             self._neg_keys = torch.from_numpy(np.unique(key)).to(self.dev)
+            self._neg_table = K.edge_table_build(self._neg_keys)          # membership set for the sampler
         return self._neg_keys
 
     def neg_sample_size(self, num_neg):
@@ -453,7 +454,7 @@ class EngineBase:
             cnt = self._buf("neg_count", (1,), torch.int32)
             ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
             K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
-                               cnt, ws)
+                               cnt, ws, edge_table=self._neg_table)
             if device_count:
                 return negg[:, p_offset:p_offset + P], P, None, cnt
             n_neg_total = int(cnt.item())

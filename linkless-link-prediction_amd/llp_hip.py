@@ -87,8 +87,10 @@ _SIGS = {
                                   c_vp]),
     "llp_pair_index_from_samples": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_neg_sample_dense_workspace_bytes": (c_i64, [c_i64]),
-    "llp_neg_sample_dense": (c_int, [c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp, c_i64, c_vp,
-                                     c_vp, c_i64, c_vp]),
+    "llp_neg_sample_dense": (c_int, [c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp,
+                                     c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "llp_edge_table_size": (c_i64, [c_i64]),
+    "llp_edge_table_build": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp]),
     "llp_fullbatch_pairs": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
                                     c_vp]),
     "llp_kd_terms_workspace_bytes": (c_i64, [c_i64, c_i64]),
@@ -415,13 +417,24 @@ def neg_sample_ws_bytes(max_candidates):
 
 
 def neg_sample_dense(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr, stream_offset, out, count, ws,
-                     rounds=3):
-    """out: int32[2, ld] (ld >= num_neg); count: int32[1] on the device."""
+                     rounds=3, edge_table=None):
+    """out: int32[2, ld] (ld >= num_neg); count: int32[1] on the device; edge_table: the keys'
+    set from edge_table_build (then used for the membership test)."""
     L = lib()
-    check(L.llp_neg_sample_dense(num_nodes, ptr(edge_keys), 0 if edge_keys is None else edge_keys.numel(), num_neg,
+    check(L.llp_neg_sample_dense(num_nodes, ptr(edge_keys), 0 if edge_keys is None else edge_keys.numel(),
+                                 ptr(edge_table), 0 if edge_table is None else edge_table.numel(), num_neg,
                                  sample_size, rounds, seed, step_ctr.data_ptr(), stream_offset, out.data_ptr(),
                                  out.stride(0), count.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
                                  stream_ptr()), "llp_neg_sample_dense")
+
+
+def edge_table_build(edge_keys):
+    """The sorted int64 edge keys' open-addressing set (int64 [llp_edge_table_size] on their device)."""
+    L = lib()
+    n = edge_keys.numel()
+    t = torch.empty(int(L.llp_edge_table_size(n)), dtype=torch.int64, device=edge_keys.device)
+    check(L.llp_edge_table_build(ptr(edge_keys), n, t.data_ptr(), t.numel(), stream_ptr()), "llp_edge_table_build")
+    return t
 
 
 def fullbatch_pairs(B, C1, samples, pairs, perm, P, neg, n_neg, ia, ib, neg_count=None, neg_offset=0):

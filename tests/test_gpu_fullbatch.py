@@ -42,12 +42,18 @@ def test_neg_sample_dense_bit_exact(N, n_und, num_neg):
     cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
     ws = torch.empty(K.neg_sample_ws_bytes(M) // 4 + 16, dtype=torch.float32, device=DEV)
     ctr = torch.full((1,), step, dtype=torch.int64, device=DEV)
-    K.neg_sample_dense(N, torch.from_numpy(keys).to(DEV), num_neg, ss, seed, ctr, off, out, cnt, ws)
+    keys_d = torch.from_numpy(keys).to(DEV)
+    K.neg_sample_dense(N, keys_d, num_neg, ss, seed, ctr, off, out, cnt, ws)
+    # the membership test through the edge set (llp_edge_table_build), as the engines run it
+    out_t = torch.full((2, num_neg), -1, dtype=torch.int32, device=DEV)
+    cnt_t = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.neg_sample_dense(N, None, num_neg, ss, seed, ctr, off, out_t, cnt_t, ws, edge_table=K.edge_table_build(keys_d))
     torch.cuda.synchronize()
     n = int(cnt.item())
-    assert n == exp.shape[1]
+    assert n == exp.shape[1] and int(cnt_t.item()) == n
     got = out[:, :n].cpu().numpy().astype(np.int64)
     assert np.array_equal(got, exp)
+    assert torch.equal(out_t[:, :n], out[:, :n])
     # properties of PyG's output: no self loops, no existing edge, no repeats
     assert (got[0] != got[1]).all()
     es = set(map(tuple, ei.T.tolist()))

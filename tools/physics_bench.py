@@ -132,9 +132,14 @@ def main():
                     help="replay a hipGraph of the step (capture_fullbatch); eager measured faster, "
                          "profiles/r03_physics_devcount_graph_ab.txt")
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "llp_physics"))
+    ap.add_argument("--no-edge-table", action="store_true",
+                    help="A/B: the dense negative sampler's membership test by binary search of the sorted keys")
     ap.add_argument("--hb-two-kernel", action="store_true",
                     help="A/B: the round-3 two-kernel Hadamard backward (profiles/r03_hb_fused_fb_ab.txt)")
     opt = ap.parse_args()
+    if opt.no_edge_table:
+        _nsd = llp_engine.K.neg_sample_dense
+        llp_engine.K.neg_sample_dense = lambda *a, edge_table=None, **kw: _nsd(*a, **kw)
     if opt.hb_two_kernel:
         llp_engine.DistillEngine._hadamard_bwd_nodes = _hb_two_kernel
     t0 = time.perf_counter()
