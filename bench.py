@@ -107,12 +107,68 @@ def cpu_baseline(data, a, t_h, init_params, B_full, P_full, sample_P=8192, steps
                        f"(H=1024, L=3, C={C}); {dt:.1f} s on {nthreads} threads")
 
 
-def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, n):
+class Shard:
+    """This rank's part of every global batch (B_full anchors, P_full edges): the whole batch
+    under the engine's owner decomposition (DistillEngine.minibatch_owner: each rank picks its
+    pairs itself), else its contiguous slice of both with offsets and global totals."""
+
+    def __init__(self, eng, B_full, P_full, rank, world):
+        self.B, self.P, self.rank, self.world = B_full, P_full, rank, world
+        self.owner = eng.minibatch_owner
+        if self.owner or world == 1:
+            self.b0, self.b1, self.p0, self.p1 = 0, B_full, 0, P_full
+            self.kw = {}
+        else:
+            self.b0, self.b1 = rank * B_full // world, (rank + 1) * B_full // world
+            self.p0, self.p1 = rank * P_full // world, (rank + 1) * P_full // world
+            self.kw = dict(b_offset=self.b0, p_offset=self.p0, B_total=B_full, P_total=P_full)
+        self.name = "owner" if self.owner else ("whole batch" if world == 1 else "slice")
+
+    def batch(self, node_perm, link_perm, j):
+        return (node_perm[j * self.B + self.b0: j * self.B + self.b1],
+                link_perm[j * self.P + self.p0: j * self.P + self.p1])
+
+    def pairs(self, C):
+        """Predictor rows of this rank per step."""
+        if self.owner:
+            r, w = self.rank, self.world
+            return sum((r + 1) * n // w - r * n // w for n in (self.B * C, self.P, self.P))
+        return (self.b1 - self.b0) * C + 2 * (self.p1 - self.p0)
+
+
+def emulated_rank(eng, node_perm, link_perm, pairs, B_full, P_full, n_full, C, R, steps=20, rank=0):
+    """Rank ``rank``'s part of an R-rank collab step on this GPU, replayed from a hipGraph (the
+    N-rank step replays graph segments with the all-reduces between them): ms per step."""
+    eng.emulate_pairs = (rank, R)
+    try:
+        sh = Shard(eng, B_full, P_full, rank, R)
+        step = lambda j: eng.step_minibatch(*sh.batch(node_perm, link_perm, j % n_full), pairs, **sh.kw)
+        for s in range(3):
+            step(s)
+        ga, gl = (t.clone() for t in sh.batch(node_perm, link_perm, 3 % n_full))
+        g = eng.capture_minibatch(ga, gl, pairs, **sh.kw)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for s in range(steps):
+            an, li = sh.batch(node_perm, link_perm, (4 + s) % n_full)
+            ga.copy_(an)
+            gl.copy_(li)
+            g.replay()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t1) / steps * 1e3
+        rows = eng.last_student_rows
+        del g
+    finally:
+        eng.emulate_pairs = None
+    return {"ms_per_step": ms, "ranks": R, "rank": rank, "decomposition": sh.name, "hipgraph": True,
+            "student_rows": rows, "predictor_rows": sh.pairs(C)}
+
+
+def dominant_only(eng, batch, pairs, kw, n):
     """One real step (buffers filled), then the dominant kernel alone n times:
     the command rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes profile."""
     import llp_hip as K
-    eng.step_minibatch(node_perm[b0:b1], link_perm[p0:p1], pairs, b_offset=b0, p_offset=p0, B_total=B_full,
-                       P_total=P_full)
+    eng.step_minibatch(*batch, pairs, **kw)
     lin = eng.stu[1]
     A = eng._bufs["H0"]
     cnt = eng._rows_dev                       # the step's launch: host bound, device unique count
@@ -128,18 +184,20 @@ def dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, 
     print(json.dumps({"dominant_rows": R1, "H": lin.out_f, "launches": n}), flush=True)
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_dominant.json")
+PMC_FILES = {"bf16": os.path.join(REPO, "profiles", "r03_pmc_dominant.json"),
+             "fp32": os.path.join(REPO, "profiles", "r04_fp32_pmc_dominant.json")}
 
 
 def pmc_traffic(rows, H, dtype):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC passes (profiles/r03_pmc_dominant.json, tools/pmc_summary.py):
-    2 x FETCH_SIZE (gfx950 reports half of a wide streaming read) + WRITE_SIZE,
-    per dispatch.  None when the profile is absent or for another shape."""
+    PMC passes (profiles/r03_pmc_dominant.json, r04_fp32_pmc_dominant.json;
+    tools/pmc_summary.py): 2 x FETCH_SIZE (gfx950 reports half of a wide
+    streaming read) + WRITE_SIZE, per dispatch.  None when the profile is
+    absent or for another shape."""
     try:
-        with open(PMC_FILE) as f:
+        with open(PMC_FILES[dtype]) as f:
             p = json.load(f)
-    except (OSError, ValueError):
+    except (OSError, ValueError, KeyError):
         return None
     if p.get("H") != H or p.get("dtype") != dtype or not p.get("rows"):
         return None
@@ -307,9 +365,22 @@ def fp32_step(data, a, t_h, init, dev, steps=3):
         eng.step_minibatch(node_perm[s * B:(s + 1) * B], link_perm[s * P:(s + 1) * P], pairs)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    # the dominant f32-MFMA launch (student layer 2, as in the bf16 line), event-timed on its stream
+    ev = []
+    for s in range(steps + 1, steps + 3):
+        eng.step_minibatch(node_perm[s * B:(s + 1) * B], link_perm[s * P:(s + 1) * P], pairs, kernel_events=ev)
+    torch.cuda.synchronize()
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    rows = eng.last_student_rows
+    achieved = 2.0 * rows * H * H / (k_ms * 1e-3) / 1e12
+    roof = {"bound": "mfma", "kernel": f"{getattr(eng, 'timed_kernel', '?')} student layer-2 forward "
+                                       f"({rows}x{H}x{H})", "achieved": achieved, "peak": PEAK_F32_TFLOPS,
+            "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "kernel_ms": k_ms,
+            "traffic": pmc_traffic(rows, H, "fp32"),
+            "algorithmic_bytes": 2.0 * rows * H * 4 + 4.0 * H * H}
     del eng
     torch.cuda.empty_cache()
-    return {"dtype": "fp32", "ms_per_step": dt * 1e3, "edges_per_s": P / dt, "steps": steps,
+    return {"dtype": "fp32", "ms_per_step": dt * 1e3, "edges_per_s": P / dt, "steps": steps, "roofline": roof,
             "note": "the reference's arithmetic; same configuration, eager steps"}
 
 
@@ -404,23 +475,21 @@ def main():
     link_perm = torch.randperm(E_train, generator=g, device=dev).to(torch.int32)
     node_perm = torch.randperm(N, generator=g, device=dev).to(torch.int32)
     n_full = min(E_train // P_full, N // B_full)
-    # this rank's shard of every global batch
+    # this rank's part of every global batch (--emulate-ranks: one rank's part of an R-rank job on this GPU)
     shards = opt.emulate_ranks if (opt.emulate_ranks and world == 1) else world
     srank = opt.emulate_rank if (opt.emulate_ranks and world == 1) else rank
-    b0, b1 = srank * B_full // shards, (srank + 1) * B_full // shards
-    p0, p1 = srank * P_full // shards, (srank + 1) * P_full // shards
+    if opt.emulate_ranks and world == 1:
+        eng.emulate_pairs = (srank, shards)
+    sh = Shard(eng, B_full, P_full, srank, shards)
 
     kern_ev = []
 
     def one_step(s, timed):
-        j = s % n_full
-        anchors = node_perm[j * B_full + b0: j * B_full + b1]
-        links = link_perm[j * P_full + p0: j * P_full + p1]
-        eng.step_minibatch(anchors, links, pairs, b_offset=b0, p_offset=p0, B_total=B_full, P_total=P_full,
-                           kernel_events=kern_ev if timed else None)
+        eng.step_minibatch(*sh.batch(node_perm, link_perm, s % n_full), pairs,
+                           kernel_events=kern_ev if timed else None, **sh.kw)
 
     if opt.dominant_only:
-        dominant_only(eng, node_perm, link_perm, pairs, B_full, P_full, b0, b1, p0, p1, opt.dominant_only)
+        dominant_only(eng, sh.batch(node_perm, link_perm, 0), pairs, sh.kw, opt.dominant_only)
         return
     graph_on = use_graph(opt.graph, world)
     debug = os.environ.get("LLP_BENCH_DEBUG") == "1"   # stage markers, each after a device sync
@@ -437,13 +506,9 @@ def main():
     graph = None
     if graph_on:
         # persistent input slots, refilled before each replay (device-to-device copies)
-        g_anchors = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
-        g_links = torch.empty(p1 - p0, dtype=torch.int32, device=dev)
-        g_anchors.copy_(node_perm[b0:b1])
-        g_links.copy_(link_perm[p0:p1])
+        g_anchors, g_links = (t.clone() for t in sh.batch(node_perm, link_perm, 0))
         try:
-            graph = eng.capture_minibatch(g_anchors, g_links, pairs, b_offset=b0, p_offset=p0, B_total=B_full,
-                                          P_total=P_full)
+            graph = eng.capture_minibatch(g_anchors, g_links, pairs, **sh.kw)
             mark("captured")
         except RuntimeError as e:   # keep the run alive: eager launches instead (reported as hipgraph: false)
             print(f"bench.py: hipGraph capture failed ({e}); timing eager steps", file=sys.stderr, flush=True)
@@ -457,9 +522,9 @@ def main():
     t0 = time.perf_counter()
     for s in range(opt.steps):
         if graph is not None:
-            j = (opt.warmup + s) % n_full
-            g_anchors.copy_(node_perm[j * B_full + b0: j * B_full + b1])
-            g_links.copy_(link_perm[j * P_full + p0: j * P_full + p1])
+            an, li = sh.batch(node_perm, link_perm, (opt.warmup + s) % n_full)
+            g_anchors.copy_(an)
+            g_links.copy_(li)
             graph.replay()
             mark(f"replay {s}")
         else:
@@ -479,15 +544,14 @@ def main():
         return
     if opt.emulate_ranks and world == 1:
         print(json.dumps({"emulated_ranks": shards, "rank": srank, "rank0_ms_per_step": dt / opt.steps * 1e3,
-                          "anchors": b1 - b0, "edges": p1 - p0,
-                          "student_rows": eng.last_student_rows}), flush=True)
+                          "decomposition": sh.name, "hipgraph": graph is not None,
+                          "student_rows": eng.last_student_rows, "predictor_rows": sh.pairs(C)}), flush=True)
         return
     loss = eng.end_epoch(opt.steps * P_full)
 
     # dominant kernel: student layer-2 forward GEMM (rows_exec x 1024 x 1024, bf16 MFMA);
-    # rows_exec = unique nodes of this rank's x[this_target] rows (rows_ref)
-    rows_ref = (b1 - b0) * (C + 1) + 4 * (p1 - p0)
-    rows_exec = eng.last_student_rows or rows_ref
+    # rows_exec = unique nodes of this rank's student rows
+    rows_exec = eng.last_student_rows
     rows_all = torch.tensor([float(rows_exec)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(rows_all)
@@ -519,7 +583,7 @@ def main():
                        "student_rows_per_step": {"reference": B_full * (C + 1) + 4 * P_full,
                                                  "unique_nodes": int(rows_all.item())},
                        "mfma_util_step": flop_exec / (dt / opt.steps) / 1e12 / peak / world},
-            "roofline": {"bound": "mfma", "kernel": f"gemm_nt_bf16_pp8p<EPI_FWD_RELU> (persistent) student layer-2 forward "
+            "roofline": {"bound": "mfma", "kernel": f"{getattr(eng, 'timed_kernel', '?')} student layer-2 forward "
                          f"({rows_exec}x{H}x{H})", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": pmc_traffic(rows_exec, H, opt.dtype),
                          "algorithmic_bytes": 2.0 * rows_exec * H * 2 + 2.0 * H * H + rows_exec * H / 8.0,
@@ -536,21 +600,12 @@ def main():
         if not opt.no_eval:
             res.update(evaluate(model, pred, data, dev))
         if world == 1 and not opt.no_shard8 and not opt.profile_kernels:
-            # per-rank cost of strong scaling: rank 0's shard of the same global batches at
-            # 8 ranks on this GPU (eager, no collective): the 8-GPU step is this + the all-reduce
-            R8 = 8
-            s0, s1, q0, q1 = 0, B_full // R8, 0, P_full // R8
-            shard = lambda s: eng.step_minibatch(node_perm[(s % n_full) * B_full + s0:(s % n_full) * B_full + s1],
-                                                 link_perm[(s % n_full) * P_full + q0:(s % n_full) * P_full + q1],
-                                                 pairs, b_offset=s0, p_offset=q0, B_total=B_full, P_total=P_full)
-            for s in range(3):
-                shard(s)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for s in range(20):
-                shard(3 + s)
-            torch.cuda.synchronize()
-            res["rank0_ms_per_step_at_8_ranks"] = (time.perf_counter() - t1) / 20 * 1e3
+            # per-rank cost of strong scaling: rank 0's part of the same global batches at 8
+            # ranks on this GPU, replayed from its hipGraph as the 8-GPU step's segments are
+            # (no collective): the 8-GPU step is this + the all-reduces
+            r8 = emulated_rank(eng, node_perm, link_perm, pairs, B_full, P_full, n_full, C, 8)
+            res["rank0_ms_per_step_at_8_ranks"] = r8["ms_per_step"]
+            res["rank0_at_8_ranks"] = r8
         if world == 1 and opt.dtype == "bf16" and not opt.no_fp32:
             res["fp32_step"] = fp32_step(data, a, t_h, init, dev)
         if not opt.no_sage:

@@ -61,6 +61,9 @@ typedef struct llp_operand {
 
 int llp_version(void);
 const char* llp_last_error(void);
+/* Name of the NT GEMM kernel the last llp_gemm_nt / llp_gemm_nt_head call on this thread
+ * launched (thread-local, "" before the first): the bench labels its roofline kernel with it. */
+const char* llp_last_gemm_kernel(void);
 /* 1 if the HIP runtime sees a device (never required to load the library). */
 int llp_device_count(void);
 
@@ -175,13 +178,47 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
                  float w_label, float w_d, float w_r, float loss_scale,
                  float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
                  const int32_t* neg_count, int64_t neg_offset, double pos_total,
+                 int64_t term_b0, int64_t term_b1,
                  void* workspace, int64_t workspace_bytes, void* stream);
-/* neg_count (may be NULL): the PyG-dense negatives' device count of the whole batch
+/* [term_b0, term_b1): the anchors whose KL / rank terms enter terms_out (every anchor's
+ * gradient is written): with the owner decomposition every rank evaluates the loss of
+ * all B anchors on the all-reduced logits and reports the terms of its own slice
+ * (llp_pair_owner_assign); [0, B) otherwise.
+ * neg_count (may be NULL): the PyG-dense negatives' device count of the whole batch
  * (llp_neg_sample_dense), so the full-batch step needs no host read of it.  The label
  * rows are then n_pos positives and n_lab - n_pos negative SLOTS holding columns
  * [neg_offset, ...) of the whole batch's negatives; a slot at or past *neg_count is inert
  * (zero gradient, no loss), and the BCE mean runs over pos_total + *neg_count labels
  * (n_lab_total unused). */
+
+/* ---------------------------------------------------------------- multi-rank owner decomposition
+ * The N-rank form of train_minibatch's pairs (src/main.py:86-130; the reference is single-GPU):
+ * each predictor pair goes to exactly one rank, the owner of its key node (owner = node /
+ * ceil(N / world)), balanced so that rank r gets cap_r = (r+1)n/world - rn/world pairs of each
+ * category (an owner keeps its first cap_r pairs in item order; the owners' overflow, in
+ * (owner, position) order, fills the ranks' free positions in rank order).  Category c's
+ * ends: item i's node e[(i / kc) * kld + koff + (i % kc) * kstep] (a context pair (b, k): a = the
+ * anchor samples[b, 0] (kc = C, kld = C + 1, koff = kstep = 0), b = samples[b, 1 + k] (koff =
+ * kstep = 1), key_b = 1; a label pair: a = src, b = dst (kc = kld = 1, koff = kstep = 0), key_b = 0).
+ * sel [sum n]: rank r's items of category c at sel[sum_{c'<c} n_c' + r n_c / world + j];
+ * gpos [sum n] (may be NULL): item -> its slot (minus the category base); target [2 R2]
+ * (may be NULL): this rank's pairs, categories in order, as [a ends (R2) | b ends (R2)] (the
+ * student's rows).  Deterministic integer work, 3 launches; oracle: pair_owner_assign. */
+typedef struct llp_owner_cat {
+  const int32_t* a; int64_t a_kc, a_kld, a_koff, a_kstep;
+  const int32_t* b; int64_t b_kc, b_kld, b_koff, b_kstep;
+  int32_t key_b; int32_t pad;
+  int64_t n;
+} llp_owner_cat;
+int64_t llp_pair_owner_workspace_bytes(int64_t n0, int64_t n1, int64_t n2, int world);
+int llp_pair_owner_assign(int ncat, const llp_owner_cat* cats, int64_t num_nodes, int world, int rank,
+                          int32_t* sel, int32_t* gpos, int32_t* target, int64_t R2, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+/* s_full[i] = s_loc[gpos[i] - lo] if lo <= gpos[i] < hi else 0 (i < n), t likewise (either
+ * output may be NULL): this rank's context logits placed into the [B*C] grid that one SUM
+ * all-reduce completes (the other ranks' slots are zero here). */
+int llp_pair_owner_scatter(int64_t n, const int32_t* gpos, int64_t lo, int64_t hi, const float* s_loc,
+                           const float* t_loc, float* s_full, float* t_full, void* stream);
 
 /* out[r, :] = a[ia[r], :] * b[ib[r], :]   (ia/ib NULL = identity) — the
  * predictor input x_i * x_j (src/models.py:140) materialised once per step so
@@ -300,7 +337,8 @@ int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* samples,
  * llp_context_sampler(.., stream_offset, samples) + llp_randint_pairs(num_nodes, P,
  * P_total, p_offset, seed, step_ctr, neg_stream_offset, neg) + llp_build_targets(B,
  * C1, samples, pairs, perm, NULL, 0, P, neg, P, P, target) +
- * llp_pair_index_from_samples(B, C, samples, t_ia, t_ib), same draws, bit for bit. */
+ * llp_pair_index_from_samples(B, C, samples, t_ia, t_ib), same draws, bit for bit (t_ia = t_ib =
+ * NULL skips the pair index: the owner decomposition builds its own). */
 int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_nodes, const int32_t* start,
                          int64_t B, int64_t b_offset, int ps_method, int rw_step, int hops, int ns_rate,
                          uint64_t seed, const int64_t* step_ctr, int64_t stream_offset, const int32_t* pairs,

@@ -14,11 +14,15 @@ int set_error(int code, const char* fmt, ...) {
   va_end(ap);
   return code;
 }
+thread_local const char* g_kernel = "";
+void note_kernel(const char* name) { g_kernel = name; }
 }  // namespace llp
 
 extern "C" int llp_version(void) { return 1; }
 
 extern "C" const char* llp_last_error(void) { return llp::g_err; }
+
+extern "C" const char* llp_last_gemm_kernel(void) { return llp::g_kernel; }
 
 extern "C" int llp_device_count(void) {
   int n = 0;

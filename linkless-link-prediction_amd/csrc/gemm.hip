@@ -307,7 +307,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
         if (row >= p.M) continue;
         float v = p.alpha * acc[i][j][r] + bias;
         if (p.act == LLP_ACT_RELU) {
-          v = fmaxf(v, 0.f);
+          // f32: torch.relu's NaN propagation (fmaxf would give 0); bf16 output: the 256-tile
+          // epilogues' sign-bit rule, so every bf16 kernel agrees
+          v = p.c_bf16 ? (__float_as_int(v) < 0 ? 0.f : v) : (v < 0.f ? 0.f : v);
         } else if (p.act == LLP_ACT_RELU_BWD) {
           const float a = p.aux_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p.aux)[row * p.ld_aux + col])
                                      : reinterpret_cast<const float*>(p.aux)[row * p.ld_aux + col];
@@ -604,7 +606,8 @@ bool aligned_op(const llp_operand* o, int esize, int64_t extent_mult) {
 int64_t tn_splits(int dtype, int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + BM - 1) / BM) * ((Q + BN - 1) / BN);
   const int64_t bkm = dtype == LLP_BF16 ? 64 : 32;
-  int64_t splits = tiles >= 1024 ? 1 : 1024 / tiles;   // whole waves (two blocks per CU): no sliver of a round
+  const int64_t wave = 4 * (int64_t)llp_cu_count();   // whole waves (4 blocks per CU): no sliver of a round
+  int64_t splits = tiles >= wave ? 1 : wave / tiles;
   const int64_t maxs = (M + bkm * 8 - 1) / (bkm * 8);  // at least 8 m-steps per split
   if (splits > maxs) splits = maxs;
   if (splits < 1) splits = 1;
@@ -671,9 +674,12 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   const bool vec = aligned_op(A, es, K) && aligned_op(B, es, K);
   dim3 grid((unsigned)tiles);
   if (dtype == LLP_BF16) {
+    llp::note_kernel(vec ? "gemm_nt_kernel<bf16, vec> (128x128)" : "gemm_nt_kernel<bf16> (128x128)");
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, false>), grid, dim3(NTHREADS), 0, s, p);
   } else {
+    llp::note_kernel(vec ? "gemm_nt_kernel<f32, vec> (128x128, v_mfma_f32_16x16x4_f32)"
+                         : "gemm_nt_kernel<f32> (128x128, v_mfma_f32_16x16x4_f32)");
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<float, false>), grid, dim3(NTHREADS), 0, s, p);
   }

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         v[r] = p.alpha * acc[jn][im][r] + bv[r];
-        if (p.act == LLP_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+        if (p.act == LLP_ACT_RELU) v[r] = __float_as_int(v[r]) < 0 ? 0.f : v[r];   // the lean epilogues' sign rule
       }
       if (p.drop_p > 0.f) {
         // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
@@ -1474,6 +1474,7 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   const int64_t tiles = (A->rows_dev ? ((M + 8 * TM - 1) / (8 * TM)) * 8 : (M + TM - 1) / TM) * ((N + TN - 1) / TN);
   const dim3 grid((unsigned)tiles), block(NT2);
   if (A->ptr2) {   // A = A1[ia] * A2[ia2] formed on load (rows whose width is not a multiple of 8)
+    llp::note_kernel("gemm_nt_bf16_256<hadamard A>");
     hipLaunchKernelGGL(gemm_nt_bf16_256<true>, grid, block, 0, s, p);
     return (int)hipGetLastError();
   }
@@ -1488,12 +1489,20 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   if ((mode == EPI_FWD_RELU || mode == EPI_FWD_NONE || mode == EPI_BWD_MASK) && lean_shapes && !A->idx && !B->idx &&
       (K / TK) % 2 == 0 && tiles > 256) {
     const dim3 pgrid = persistent_grid(tiles);
+    llp::note_kernel(mode == EPI_FWD_RELU   ? "gemm_nt_bf16_pp8p<EPI_FWD_RELU> (persistent)"
+                     : mode == EPI_FWD_NONE ? "gemm_nt_bf16_pp8p<EPI_FWD_NONE> (persistent)"
+                                            : "gemm_nt_bf16_pp8p<EPI_BWD_MASK> (persistent)");
     if (mode == EPI_FWD_RELU) hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_RELU>), pgrid, block, 0, s, p);
     else if (mode == EPI_FWD_NONE) hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_NONE>), pgrid, block, 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_BWD_MASK>), pgrid, block, 0, s, p);
     return (int)hipGetLastError();
   }
 #endif
+  llp::note_kernel(mode == EPI_FWD_RELU   ? "gemm_nt_bf16_pp8<EPI_FWD_RELU>"
+                   : mode == EPI_FWD_NONE ? "gemm_nt_bf16_pp8<EPI_FWD_NONE>"
+                   : mode == EPI_BWD_MASK ? "gemm_nt_bf16_pp8<EPI_BWD_MASK>"
+                   : mode == EPI_HEAD_RELU ? "gemm_nt_bf16_pp8<EPI_HEAD_*>"
+                                           : "gemm_nt_bf16_pp8<EPI_ANY>");
   switch (mode) {
     case EPI_FWD_RELU: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_RELU>), grid, block, 0, s, p); break;
     case EPI_FWD_NONE: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_FWD_NONE>), grid, block, 0, s, p); break;

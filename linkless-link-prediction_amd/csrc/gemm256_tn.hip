@@ -528,11 +528,13 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
 
 }  // namespace
 
+int llp_cu_count();
+
 int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
-  const int64_t target = 256;   // one wave of workgroups over the 256 CUs
-  // whole waves only: tiles * splits <= 256 (33 tiles x 8 splits = 264 blocks ran as two
-  // rounds, the second one 8 blocks long -- the physics first layer's weight gradient)
+  const int64_t target = llp_cu_count();   // one wave of workgroups, one per CU
+  // whole waves only: tiles * splits <= CUs (33 tiles x 8 splits = 264 blocks ran as two
+  // rounds on 256 CUs, the second one 8 blocks long -- the physics first layer's weight gradient)
   int64_t splits = tiles >= target ? 1 : target / tiles;
   const int64_t maxs = (M + TKM * 16 - 1) / (TKM * 16);   // >= 16 m-steps per split
   if (splits > maxs) splits = maxs;

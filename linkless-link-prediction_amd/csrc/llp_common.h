@@ -12,6 +12,8 @@
 namespace llp {
 extern thread_local char g_err[512];
 int set_error(int code, const char* fmt, ...);
+// records (thread-local) the name of the NT GEMM kernel a launch chose: llp_last_gemm_kernel()
+void note_kernel(const char* name);
 }  // namespace llp
 
 #define LLP_CHECK_ARG(cond, ...)                                        \
@@ -106,3 +108,13 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 static inline unsigned ceil_div_u(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+// Workgroups are dealt to the 8 XCDs round-robin (workgroup b runs on XCD b % 8): this bijection
+// gives each XCD a contiguous range of logical blocks instead, so neighbouring work (rows of a
+// locality-ordered graph) shares one XCD's L2 (cdna_hip_programming.md, XCD-aware mapping).
+__device__ __forceinline__ int64_t llp_xcd_block(int64_t bid, int64_t nblocks) {
+  if (nblocks < 8) return bid;
+  const int64_t q = nblocks / 8, r = nblocks % 8;
+  const int64_t xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}

@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, c
                                                          const float* __restrict__ t_prob, double B_total,
                                                          float margin, float T, float w_d, float w_r,
                                                          float loss_scale, float* __restrict__ dlogit,
-                                                         float* __restrict__ partial) {
+                                                         float* __restrict__ partial, int64_t tb0, int64_t tb1) {
   __shared__ float ss[WAVES][MAXC];
   __shared__ float tt[WAVES][MAXC];
   __shared__ float red[WAVES][2];
@@ -86,6 +86,7 @@ __global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, c
     }
     kl_acc = wave_sum(kl_acc) * (T * T) * inv_b;
     rk_acc = wave_sum(rk_acc) * inv_bp;
+    if (b < tb0 || b >= tb1) kl_acc = rk_acc = 0.f;   // another rank reports this anchor's terms
   }
   if (lane == 0) {
     red[w][0] = kl_acc;
@@ -429,8 +430,8 @@ extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const fl
                             int64_t n_pos, const float* out_logit, double B_total, double n_lab_total, float margin,
                             float T, float w_label, float w_d, float w_r, float loss_scale, float* dlogit_ctx,
                             float* dlogit_lab, float* terms_out, int accumulate, const int32_t* neg_count,
-                            int64_t neg_offset, double pos_total, void* workspace, int64_t workspace_bytes,
-                            void* stream) {
+                            int64_t neg_offset, double pos_total, int64_t term_b0, int64_t term_b1,
+                            void* workspace, int64_t workspace_bytes, void* stream) {
   LLP_CHECK_ARG(C <= MAXC, "llp_llp_loss: contexts per anchor C=%lld > %d", (long long)C, MAXC);
   LLP_CHECK_ARG(terms_out && workspace, "llp_llp_loss: null terms/workspace");
   LLP_CHECK_ARG(workspace_bytes >= llp_llp_loss_workspace_bytes(B, n_lab), "llp_llp_loss: workspace too small");
@@ -441,7 +442,7 @@ extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const fl
   if (nba > 0) {
     LLP_CHECK_ARG(s_logit && t_prob && dlogit_ctx, "llp_llp_loss: null context buffers");
     hipLaunchKernelGGL(llp_anchor_kernel, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob, B_total,
-                       margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial);
+                       margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial, term_b0, term_b1);
     LLP_LAUNCH_CHECK();
   }
   if (nbl > 0) {

@@ -74,7 +74,9 @@ __global__ void act_2d_kernel(int64_t rows, int64_t cols, const T* __restrict__ 
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cols, c = i % cols;
     float v = ldv<T>(x, r * ldx + c);
-    if (relu) v = fmaxf(v, 0.f);
+    // torch.relu propagates NaN (fmaxf would turn it into 0); bf16 follows the 256-tile GEMM
+    // epilogues' sign-bit rule (a -NaN becomes 0 there)
+    if (relu) v = sizeof(T) == 2 ? (__float_as_int(v) < 0 ? 0.f : v) : (v < 0.f ? 0.f : v);
     if (thr) v = ((philox_u32(seed, stream, (uint64_t)i) >> 8) >= thr) ? v * scale : 0.f;
     stv<T>(y, r * ldy + c, v);
   }

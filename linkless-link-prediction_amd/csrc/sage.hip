@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void csr_agg_vec_kernel(int64_t n_rows, int64_
   __shared__ float red[4][64 * E];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nch = F / E;                 // chunks per row (F % E == 0 here)
-  const int64_t row = (int64_t)blockIdx.x * 4 + w;
+  const int64_t row = llp_xcd_block(blockIdx.x, gridDim.x) * 4 + w;
   if (row >= n_rows) return;
   const int64_t beg = rowptr[row], end = rowptr[row + 1];
   // chunk sweep: columns in blocks of 64 chunks
@@ -148,7 +148,9 @@ __global__ __launch_bounds__(256) void csr_agg_rows_kernel(int64_t n_rows, const
   constexpr int RPW = 64 / NCH;
   const int lane = threadIdx.x & 63;
   const int rl = lane / NCH, ch = lane % NCH;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + rl;
+  // each XCD a contiguous range of rows: with a locality-ordered graph (llp_sage.locality_order)
+  // the neighbour rows of those rows are L2 hits
+  const int64_t row = (llp_xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6)) * RPW + rl;
   if (row >= n_rows) return;
   const int64_t beg = rowptr[row], end = rowptr[row + 1];
   float acc[E];
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int
                                                              const float* __restrict__ bias, T* __restrict__ out,
                                                              int64_t ldo, int accumulate) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = llp_xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
   if (row >= n_rows) return;
   const int64_t beg = rowptr[row], end = rowptr[row + 1];
   const float sc = mode == 0 ? 1.f / (float)max(end - beg, (int64_t)1) : (mode == 2 ? inv_deg[row] : 1.f);

@@ -129,8 +129,10 @@ __global__ void minibatch_sample_kernel(MbSample a) {
       const int64_t c = colbase + l;          // context column c + 1 of row b
       a.samples[b * a.C1 + c + 1] = cur;
       a.target[b * a.C1 + c + 1] = cur;
-      a.t_ia[b * a.C + c] = anchor;
-      a.t_ib[b * a.C + c] = cur;
+      if (a.t_ia) {
+        a.t_ia[b * a.C + c] = anchor;
+        a.t_ib[b * a.C + c] = cur;
+      }
     }
     return;
   }
@@ -143,8 +145,10 @@ __global__ void minibatch_sample_kernel(MbSample a) {
     const int64_t c = a.C - a.nneg + q;       // negatives follow the walk columns
     a.samples[b * a.C1 + c + 1] = v;
     a.target[b * a.C1 + c + 1] = v;
-    a.t_ia[b * a.C + c] = a.start[b];
-    a.t_ib[b * a.C + c] = v;
+    if (a.t_ia) {
+      a.t_ia[b * a.C + c] = a.start[b];
+      a.t_ib[b * a.C + c] = v;
+    }
     return;
   }
   u -= nn;
@@ -172,7 +176,7 @@ extern "C" int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, i
                                     int64_t stream_offset, const int32_t* pairs, const int32_t* perm, int64_t P,
                                     int64_t P_total, int64_t p_offset, int64_t neg_stream_offset, int32_t* samples,
                                     int32_t* neg, int32_t* target, int32_t* t_ia, int32_t* t_ib, void* stream) {
-  LLP_CHECK_ARG(rowptr && col && start && samples && step_ctr && target && t_ia && t_ib &&
+  LLP_CHECK_ARG(rowptr && col && start && samples && step_ctr && target && (!t_ia == !t_ib) &&
                     (P == 0 || (pairs && perm && neg)),
                 "llp_minibatch_sample: null pointer");
   LLP_CHECK_ARG(ps_method == 0 || ps_method == 1, "llp_minibatch_sample: ps_method must be 0 (rw) or 1 (nb)");

@@ -27,30 +27,6 @@ import torch
 import torch.distributed as dist
 
 import llp_hip as K
-from contextlib import nullcontext as _nullctx
-
-# unique-node path: the Hadamard backward is reduced straight onto the unique nodes
-# (llp_hadamard_bwd_segments: the anchors' context sums, then one pass per node over its rows),
-# bit-identical to the row gradients + segment sum (False: the A/B path) without their [R1, H]
-# buffer: collab step 12.87 -> 12.66 ms (same-box A/B)
-_SEGMENT_FUSED = True
-# unique-node path: the unique count stays on the device (GEMM grids sized by the bound min(R1, N));
-# False reads it on the host instead (a sync per step, not capturable; A/B switch)
-_DEVICE_COUNT = True
-# minibatch step: weight-gradient (TN) GEMMs and the frozen teacher predictor run on a second HIP
-# stream beside the data-gradient GEMMs / Hadamard backward / student forward of the main stream
-# (fork/join by events, hipGraph-capturable), measured slower, so 0: one stream;
-# bit mask: 1 teacher predictor beside the student forward; 2 the predictor's first-layer weight
-# gradient beside the Hadamard backward; 4 every other weight gradient beside its data gradient
-_OVERLAP = 0
-# minibatch step, bf16: x[this_target] (src/main.py:95) is gathered once into a plain buffer
-# (llp_gather_rows) that the first student layer's forward and weight-gradient GEMMs read, so the
-# weight gradient runs the lean TN loop (gathered operands fall back to the staggered one)
-_GATHER_X = True
-# minibatch step with device sampling and randint negatives (collab): one launch builds the
-# samples, negatives, target rows and teacher pair index (llp_minibatch_sample, bit-identical
-# to the five separate kernels; False runs them separately)
-_FUSED_SAMPLE = True
 
 # Philox streams per step (csrc/llp_common.h LLP_STREAMS_PER_STEP): a draw of step s at
 # offset o uses stream STREAMS_PER_STEP * s + o.  Offsets under self.seed: the context
@@ -233,42 +209,10 @@ class EngineBase:
         self._bufs = {}
         self._shadows = {}
         self._act_mask = {}     # id(activation buffer) -> its ReLU bit mask (or None)
-        self._side = None       # second stream (created on first use) for the overlapped kernels
-        self._forked = False
-        self._side_reads = {}   # buffer name -> event after the side-stream launches that read it
         self._seg = None        # _SegmentedGraph while a multi-rank step is being captured
         self._seg_debug = False  # extra segment cuts that sync and name the stage (capture_minibatch)
         self.emulate_shard = None   # (rank, world): time one rank's full-batch student slice (_fb_shard)
-
-    def _fork(self):
-        """Context that runs the enclosed launches on the side stream, after
-        everything already queued on the current (main) stream."""
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.dev)
-        self._side.wait_stream(torch.cuda.current_stream(self.dev))
-        self._forked = True
-        return torch.cuda.stream(self._side)
-
-    def _join(self):
-        """The main stream waits for the side stream's launches."""
-        if self._forked:
-            torch.cuda.current_stream(self.dev).wait_stream(self._side)
-            self._forked = False
-        self._side_reads.clear()
-
-    def _side_read(self, name):
-        """Record that the side-stream launches queued so far read buffer ``name``:
-        the main stream waits for them (``_before_write``) before it overwrites it."""
-        ev = torch.cuda.Event()
-        ev.record(self._side)
-        self._side_reads[name] = ev
-
-    def _before_write(self, name):
-        """The main stream is about to write buffer ``name``: wait for the side-stream
-        launches that still read it (rotated data-gradient buffers, overlap bit 4)."""
-        ev = self._side_reads.pop(name, None)
-        if ev is not None:
-            torch.cuda.current_stream(self.dev).wait_event(ev)
+        self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
 
     def _init_params(self, all_params, groups, optimizer):
         """``groups[i]``: clip group of all_params[i] (clip_grad_norm_ per module, Q9)."""
@@ -356,10 +300,6 @@ class EngineBase:
         numel = int(np.prod(shape))
         b = self._bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype:
-            if b is not None and self._side is not None:
-                # a side-stream launch may still use the old storage: the allocator
-                # must not hand it out again before that stream's work is done
-                b.record_stream(self._side)
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.dev)
             self._bufs[name] = b
         return b[:numel].view(*shape)
@@ -508,11 +448,12 @@ class EngineBase:
                        logit=logit)
         return A0, zacts
 
-    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop, overlap=False):
-        """overlap: each weight-gradient GEMM runs on the side stream (its inputs are
-        final, its output is only flat_grad) beside the next data-gradient GEMM; the
-        data gradients then take three buffers so none is overwritten while a side
-        GEMM still reads it.  The caller joins (``_join``) before clip + Adam."""
+    def _predictor_backward(self, dlogit, R2, A0, zacts, p_drop):
+        """Backward of _predictor_forward from d(loss)/d(logit): the head (dZ of the last
+        hidden layer, the head's weight / bias gradients), then per layer the weight-gradient
+        (TN) and data-gradient (NT, ReLU-mask epilogue) GEMMs.  The predictor's gradients are
+        final after its first layer's weight gradient: their all-reduce starts there.
+        (A second HIP stream for the weight gradients measured slower)"""
         dt, dc = self.dtype, self.dc
         if self.predictor_kind != "mlp":
             self._allreduce_tail_begin()
@@ -525,45 +466,25 @@ class EngineBase:
         K.head_bwd(dlogit, Zl, R2, Hh, self.head.weight.data.view(-1), True, g, self.head.weight.grad.view(-1),
                    self.head.bias.grad, ws, alpha=alpha)
         self._dbg_cut("head backward")
-        names = ["gP0", "gP1", "gP2"] if overlap & 4 else ["gP0", "gP1"]
+        names = ["gP0", "gP1"]
         k = 0
         for l in range(len(self.prd) - 1, -1, -1):
             lin = self.prd[l]
-            gcur = self._buf(names[k % len(names)], (R2, lin.out_f), dt)
+            gcur = self._buf(names[k % 2], (R2, lin.out_f), dt)
             A_in = K.operand(zacts[l - 1]) if l > 0 else A0
             wsb = K.gemm_tn_ws_bytes(dc, R2, lin.out_f, lin.in_f)
-            late = bool(overlap & 2) and l == 0   # forked after the data-gradient GEMM below
-            if (overlap & 4) and l > 0 or (overlap & 4) and l == 0 and not late:
-                with self._fork():
-                    # side-stream TN GEMMs have a split-K workspace of their own: the main
-                    # stream's TN GEMMs (student backward) must not share it
-                    K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
-                              self._ws("ws_tn_side", wsb), colsum_a=lin.lin.bias.grad)
-                    self._side_read(names[k % len(names)])
-                    if l == 0:
-                        self._allreduce_tail_begin()      # issued after the side stream's last predictor GEMM
-            elif late:
-                pass
-            else:
-                K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
-                          self._ws("ws_tn", wsb), colsum_a=lin.lin.bias.grad)
-                self._dbg_cut(f"predictor weight gradient {l}")
-                if l == 0:
-                    self._allreduce_tail_begin()      # every predictor gradient is final here
+            K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc, self._ws("ws_tn", wsb),
+                      colsum_a=lin.lin.bias.grad)
+            self._dbg_cut(f"predictor weight gradient {l}")
+            if l == 0:
+                self._allreduce_tail_begin()      # every predictor gradient is final here
             k += 1
-            self._before_write(names[k % len(names)])
-            gnext = self._buf(names[k % len(names)], (R2, lin.in_f), dt)
+            gnext = self._buf(names[k % 2], (R2, lin.in_f), dt)
             if l > 0:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc,
                           act=K.ACT_RELU_BWD, aux=self._relu_aux(zacts[l - 1]), alpha=alpha)
             else:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
-            if late:
-                with self._fork():
-                    K.gemm_tn(K.operand(gcur), A_in, R2, lin.out_f, lin.in_f, lin.lin.weight.grad, dc,
-                              self._ws("ws_tn_side", wsb), colsum_a=lin.lin.bias.grad)
-                    self._side_read(names[(k - 1) % len(names)])
-                    self._allreduce_tail_begin()
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
     def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
@@ -695,7 +616,6 @@ class EngineBase:
             self._seg.cut(fn)
 
     def _allreduce_and_update(self):
-        self._join()
         if self.world > 1:
             rest, pos = [], 0
             for lo, hi in sorted(self._issued):
@@ -740,16 +660,18 @@ class DistillEngine(EngineBase):
     """
 
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
-                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, overlap=True,
-                 shard_student=True):
+                 dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, shard_student=True,
+                 owner_pairs=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
         # run the dropout-free student on unique nodes (step_minibatch); the unique
         # count stays on the device, so this path is hipGraph-capturable too
         self.dedup = bool(dedup)
         # multi-rank full-batch step: each rank runs the student on its slice of the nodes
-        # (_fb_shard); rank 0 of 4 on coauthor-physics 0.94 -> 0.80 ms (profiles/r03_fb_shard_ab.txt)
+        # (_fb_shard); rank 0 of 4 on coauthor-physics 0.94 -> 0.81 ms (first
+        # table: tools/physics_bench.py --emulate-ranks 4 with and without --replicated)
         self.shard_student = bool(shard_student)
-        self.overlap = bool(overlap)   # second stream for the TN GEMMs / teacher predictor (step_minibatch)
+        # multi-rank minibatch step: the owner decomposition (minibatch_owner)
+        self.owner_pairs = bool(owner_pairs)
         self._rows_dev = None      # int32 device count of the unique-node student (last step), or None
         self._rows_host = 0
         self.args = args
@@ -839,6 +761,28 @@ class DistillEngine(EngineBase):
         return self._bufs[("rows", B, C, P2)][2].view(-1)
 
     # ------------------------------------------------------------------ the step
+    @property
+    def minibatch_owner(self):
+        """Whether step_minibatch runs the owner decomposition: several ranks
+        (or ``emulate_pairs``), ``owner_pairs`` on, and the unique-node student (no dropout,
+        no BatchNorm, rows the grouping kernels take).  Callers then pass the WHOLE batch on
+        every rank; otherwise each rank passes its slice with offsets."""
+        if not self.owner_pairs or (self.world <= 1 and self.emulate_pairs is None):
+            return False
+        return self._dedup_ok()
+
+    def _dedup_ok(self):
+        """The unique-node student applies: without dropout the student is row-wise, so
+        duplicate rows of x[this_target] give identical activations (BatchNorm's statistics
+        run over every row, duplicates included, so it keeps the row-wise student)."""
+        return (self.dedup and float(self.args.dropout) == 0.0 and self._grouped_ok(self.stu[-1].out_f)
+                and not self._batch_norm)
+
+    def _owner_rank(self):
+        if self.world > 1:
+            return self.rank, self.world
+        return self.emulate_pairs
+
     def step_minibatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
                        samples=None, neg=None, kernel_events=None, dense_negatives=False):
         """One link batch of train_minibatch (src/main.py:73-143).
@@ -850,12 +794,19 @@ class DistillEngine(EngineBase):
         (parity tests); otherwise drawn on the device: randint (collab,
         src/main.py:83-84) or, with dense_negatives, PyG dense sampling
         (non-collab, src/main.py:80-82; one host read of its count).
+        With ``minibatch_owner`` (several ranks) anchors / link_ids / samples / neg are the
+        WHOLE batch on every rank (no offsets): every rank draws the same samples, and
+        llp_pair_owner_assign gives each predictor pair to one rank.
         Returns nothing; the loss terms stay on the device (self.terms).
         """
         self._act_mask.clear()
         a = self.args
         B = int(anchors.numel())
         P = int(link_ids.numel())
+        owner = self.minibatch_owner
+        if owner and (b_offset or p_offset or B_total not in (None, B) or P_total not in (None, P)):
+            raise ValueError("step_minibatch: the owner decomposition takes the whole batch on every rank "
+                             "(no offsets / totals); see DistillEngine.minibatch_owner")
         B_total = B if B_total is None else int(B_total)
         P_total = P if P_total is None else int(P_total)
         rw_step, hops, ns_rate = int(a.rw_step), int(a.hops), int(a.ns_rate)
@@ -864,52 +815,54 @@ class DistillEngine(EngineBase):
         H = self.stu[-1].out_f
         dt, dc = self.dtype, self.dc
 
-        # ---- a1-a3: negatives and samples (src/main.py:80-84,93)
+        # ---- a1-a3: negatives and samples (src/main.py:80-84,93); ``target`` = this_target
+        # (src/main.py:95): samples.flat | src | dst
         samp = self._buf("samples", (B, C1), torch.int32)
-        t_ia = self._buf("t_ia", (B * C,), torch.int32)
-        t_ib = self._buf("t_ib", (B * C,), torch.int32)
-        if _FUSED_SAMPLE and samples is None and neg is None and not dense_negatives:
+        t_ia = t_ib = None
+        if not owner:
+            t_ia = self._buf("t_ia", (B * C,), torch.int32)
+            t_ib = self._buf("t_ib", (B * C,), torch.int32)
+        if samples is None and neg is None and not dense_negatives:
             # collab path: walks, context negatives, randint label negatives, the student's
             # target rows and the teacher's pair index in one launch (llp_minibatch_sample)
             negb, n_neg, n_neg_total = self._buf("neg", (2, max(P, 1)), torch.int32), P, P_total
-            n_lab = P + n_neg
-            R1 = B * C1 + 2 * n_lab
-            R2 = B * C + n_lab
-            target = self._buf("target", (R1,), torch.int32)
+            target = self._buf("target", (B * C1 + 4 * P,), torch.int32)
             K.minibatch_sample(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                self.seed, self.step_ctr, 0, pairs, link_ids, P, P_total, p_offset, RANDINT_STREAM,
-                               samp, negb,
-                               target, t_ia, t_ib, b_offset=b_offset)
+                               samp, negb, target, t_ia, t_ib, b_offset=b_offset)
             self._dbg_cut("sample")
         else:
             negb, n_neg, n_neg_total, _ = self._negatives(P, P_total, p_offset, neg, dense_negatives)
-            n_lab = P + n_neg                  # train_edges columns (src/main.py:86)
-            R1 = B * C1 + 2 * n_lab
-            R2 = B * C + n_lab
             if samples is not None:
                 samp.copy_(samples.to(torch.int32))
             else:
                 K.context_sampler(self.rowptr, self.col, self.N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                   self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
-            target = self._buf("target", (R1,), torch.int32)
+            target = self._buf("target", (B * C1 + 2 * (P + n_neg),), torch.int32)
             K.build_targets(B, C1, samp, pairs, link_ids, None, 0, P, negb, target, n_neg=n_neg)
-            K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
-        ia, ib = self._rows_index(B, C, n_lab)
+            if not owner:
+                K.pair_index_from_samples(B, C, samp, t_ia, t_ib)
+        n_lab = P + n_neg                      # train_edges columns (src/main.py:86)
         p_drop = float(a.dropout)
-        overlap = _OVERLAP if (self.overlap and self._seg is None) else 0
-        side_teacher = bool(overlap & 1) and kernel_events is None   # bench's timed launch runs alone
-        if side_teacher:
-            # a6 (frozen teacher predictor, src/main.py:104,106) depends only on the
-            # samples: it runs on the side stream beside the student forward
-            t_r = self._buf("t_r", (B * C,), torch.float32)
-            with self._fork():
-                self._teacher_forward(B * C, t_ia, t_ib, t_r)
 
-        # ---- unique-node compaction: without dropout the student is a row-wise
-        # function, so duplicate rows of x[this_target] give identical activations;
-        # run it on the U distinct nodes and sum each node's row gradients.
-        # (BatchNorm's statistics run over every row of x[this_target], duplicates included: row-wise student)
-        dedup = self.dedup and p_drop == 0.0 and self._grouped_ok(H) and not self._batch_norm
+        if owner:
+            # ---- the owner decomposition: this rank's context pairs (by the context node's owner)
+            # and label pairs (by the source's owner); the student rows are their ends [ia | ib]
+            rank, world = self._owner_rank()
+            own = self._owner_assign(B, C, C1, P, n_neg, target, rank, world)
+            R2, n_ctx, n_pos = own["R2"], own["ctx"], own["pos"]
+            n_lab_loc = R2 - n_ctx
+            target = own["rows"]
+            R1 = 2 * R2
+        else:
+            R1 = B * C1 + 2 * n_lab
+            R2 = B * C + n_lab
+            n_ctx, n_pos, n_lab_loc = B * C, P, n_lab
+            ia, ib = self._rows_index(B, C, n_lab)
+
+        # ---- unique-node compaction: run the student on the U distinct nodes of the rows
+        # and sum each node's row gradients (_dedup_ok)
+        dedup = self._dedup_ok()
         n_u = None
         if dedup:
             fresh = "uniq" not in self._bufs or self._bufs["uniq"].numel() < R1
@@ -923,33 +876,121 @@ class DistillEngine(EngineBase):
             wsd = self._buf("ws_dedup", (K.dedup_ws_bytes(self.N, R1) // 4 + 16,), torch.float32)
             K.dedup_rows(self.N, R1, target, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
             self._dbg_cut("sample + dedup")
-            iab_h = self._buf("iab_u", (2, R2), torch.int32)   # both pair sides in one gather
-            K.gather_i32(self._rows_index_flat(B, C, n_lab), pos, iab_h.view(-1))
-            ia_h, ib_h = iab_h[0], iab_h[1]
+            if owner:   # the rows ARE the pairs' ends: row k and row R2 + k
+                ia_h, ib_h = pos[:R2], pos[R2:R1]
+            else:
+                iab_h = self._buf("iab_u", (2, R2), torch.int32)   # both pair sides in one gather
+                K.gather_i32(self._rows_index_flat(B, C, n_lab), pos, iab_h.view(-1))
+                ia_h, ib_h = iab_h[0], iab_h[1]
             # No host read of U: the student kernels are launched for the bound
             # min(R1, N) and run on the *n_unique live rows (llp_operand.rows_dev),
             # so the step stays asynchronous and hipGraph-capturable.
-            # (LLP_DEVICE_COUNT=0: read U on the host and size the launches by it.)
-            if _DEVICE_COUNT:
-                rows_s, gather_s = min(R1, self.N), uniq
-            else:
-                rows_s = int(n_u.item())
-                gather_s, n_u = uniq[:rows_s], None
+            rows_s, gather_s = min(R1, self.N), uniq
         else:
             rows_s, gather_s, ia_h, ib_h = R1, target, ia, ib
         self._rows_dev = n_u
         self._rows_host = rows_s
 
         # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
+        R1_total = B_total * C1 + 2 * (P_total + n_neg_total)    # this_target rows of the whole batch
+        acts, x_rows = self._student_forward(rows_s, gather_s, n_u, p_drop, R1_total, kernel_events)
+        h = acts[-1]
+
+        # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
+        logit = self._buf("logit", (R2,), torch.float32)
+        self._dbg_cut("student forward")
+        A0, zacts = self._predictor_forward(h, ia_h, ib_h, R2, logit, p_drop)
+        self._dbg_cut("predictor forward")
+
+        # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
+        t_r = self._buf("t_r", (max(n_ctx, 1),), torch.float32)[:n_ctx]
+        if owner:
+            self._teacher_forward(n_ctx, target[:n_ctx], target[R2:R2 + n_ctx], t_r)
+        else:
+            self._teacher_forward(B * C, t_ia, t_ib, t_r)
+
+        # ---- a7-a9: fused LLP_D + LLP_R + BCE and d(loss)/d(logit) (src/main.py:107-130)
+        if not (a.LLP_D or a.LLP_R):
+            raise UnboundLocalError("train_minibatch: loss is only defined when LLP_D or LLP_R is set "
+                                    "(src/main.py:129-130)")
+        dlogit = self._buf("dlogit", (R2,), torch.float32)
+        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(B, n_lab_loc))
+        if owner:
+            # every anchor's KL / rank needs all C of its logits: this rank's context logits and
+            # teacher probabilities go into the [B, C] grid (zeros elsewhere), one SUM all-reduce
+            # completes it, every rank evaluates the anchors' loss and keeps its pairs' gradients
+            # (the anchors' terms are reported by the rank of their slice, the BCE by each rank)
+            lo = own["ctx_lo"]
+            full = self._buf("owner_full", (2, B * C), torch.float32)
+            K.pair_owner_scatter(B * C, own["gpos"], lo, lo + n_ctx, logit, t_r, full[0], full[1])
+            if self.world > 1:
+                self._collective(lambda: dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group))
+            dfull = self._buf("owner_dfull", (B * C,), torch.float32)
+            K.llp_loss(B, C, full[0], full[1], n_lab_loc, n_pos, logit[n_ctx:], B, P + n_neg, float(a.margin), 1.0,
+                       float(a.True_label), float(a.LLP_D), float(a.LLP_R), dfull, dlogit[n_ctx:], self.terms, ws,
+                       term_range=(rank * B // world, (rank + 1) * B // world))
+            K.gather_i32(own["sel"][lo:lo + n_ctx], dfull.view(torch.int32), dlogit[:n_ctx].view(torch.int32))
+        else:
+            K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin),
+                       1.0, float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms,
+                       ws)
+
+        # ---- a10: backward
+        self._dbg_cut("teacher + loss")
+        dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
+        mlp = self.predictor_kind == "mlp"
+        if dedup:
+            # Hadamard backward reduced straight onto the unique nodes (no [R1, H] row gradients);
+            # the owner layout is label rows only (B = C = 0: rows k and R2 + k are pair k's ends)
+            dh = self._buf("gS0", (rows_s, H), dt)
+            Bl, Cl = (0, 0) if owner else (B, C)
+            arow = None if owner else self._buf("anchor_rows", (max(B, 1), H), dt)
+            K.hadamard_bwd_segments(rows_s, Bl, Cl, R2 if owner else n_lab, H, seg_ptr, seg_rows, pos,
+                                    dZ0 if mlp else None, h, dh, arow, drow=None if mlp else dlogit, count=n_u)
+        else:
+            dh = self._buf("gS0", (R1, H), dt)
+            K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0 if mlp else None, h, dh, drow=None if mlp else dlogit)
+        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, x_rows=x_rows, norm_count=R1_total,
+                               norm_sync=True)
+        self._allreduce_and_update()
+        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
+
+    def _owner_assign(self, B, C, C1, P, n_neg, target, rank, world):
+        """This rank's pairs under the owner decomposition (llp_pair_owner_assign): categories
+        context pairs (b, c) keyed by the context node, positive and negative label pairs
+        keyed by their source; ``target`` is the whole batch's this_target (samples.flat |
+        src | dst).  Returns the rank's [ia | ib] rows, its counts, sel / gpos."""
+        n_lab = P + n_neg
+        BC1 = B * C1
+        ns = (B * C, P, n_neg)
+        caps = [(rank + 1) * n // world - rank * n // world for n in ns]
+        R2 = sum(caps)
+        cats = [K.owner_cat(B * C, target, target, (C, C1, 0, 0), (C, C1, 1, 1), key_b=True),
+                K.owner_cat(P, target[BC1:], target[BC1 + n_lab:]),
+                K.owner_cat(n_neg, target[BC1 + P:], target[BC1 + n_lab + P:])]
+        n_all = sum(ns)
+        sel = self._buf("owner_sel", (max(n_all, 1),), torch.int32)
+        gpos = self._buf("owner_gpos", (max(n_all, 1),), torch.int32)
+        rows = self._buf("owner_rows", (max(2 * R2, 1),), torch.int32)[:2 * R2]
+        ws = self._buf("owner_ws", (K.pair_owner_ws_bytes(ns, world) // 4 + 16,), torch.int32)
+        K.pair_owner_assign(cats, self.N, world, rank, sel, ws, gpos=gpos, target=rows, R2=R2)
+        return {"R2": R2, "ctx": caps[0], "pos": caps[1], "neg": caps[2], "rows": rows, "sel": sel,
+                "gpos": gpos, "ctx_lo": rank * ns[0] // world}
+
+    def _student_forward(self, rows_s, gather_s, n_u, p_drop, R1_total, kernel_events=None):
+        """Student MLP over x[gather_s] (src/models.py:45-54), rows_s rows (n_u: device row
+        count of the unique-node student).  bf16: x[gather_s] is gathered once into a plain
+        buffer that the first layer's forward and weight-gradient GEMMs read.  Returns
+        (activations per layer, the gathered x rows or None)."""
+        dt, dc = self.dtype, self.dc
         acts = []
         x_rows = None
-        if _GATHER_X and self.dtype == torch.bfloat16:
+        if self.dtype == torch.bfloat16:
             x_rows = self._buf("Xg", (rows_s, self.x.shape[1]), dt)
             K.gather_rows(self.x, gather_s, x_rows, count=n_u)
             A = K.operand(x_rows, count=n_u)
         else:
             A = K.operand(self.x, gather_s, count=n_u)
-        R1_total = B_total * C1 + 2 * (P_total + n_neg_total)    # this_target rows of the whole batch
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (rows_s, lin.out_f), dt)
@@ -973,58 +1014,10 @@ class DistillEngine(EngineBase):
             if timed:
                 ev[1].record()
                 kernel_events.append(ev)
+                self.timed_kernel = K.last_gemm_kernel()
             acts.append(out)
             A = K.operand(out, count=n_u)
-        h = acts[-1]
-
-        # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
-        logit = self._buf("logit", (R2,), torch.float32)
-        self._dbg_cut("student forward")
-        A0, zacts = self._predictor_forward(h, ia_h, ib_h, R2, logit, p_drop)
-        self._dbg_cut("predictor forward")
-
-        # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
-        t_r = self._buf("t_r", (B * C,), torch.float32)
-        if side_teacher:
-            self._join()
-        else:
-            self._teacher_forward(B * C, t_ia, t_ib, t_r)
-
-        # ---- a7-a9: fused LLP_D + LLP_R + BCE and d(loss)/d(logit) (src/main.py:107-130)
-        if not (a.LLP_D or a.LLP_R):
-            raise UnboundLocalError("train_minibatch: loss is only defined when LLP_D or LLP_R is set "
-                                    "(src/main.py:129-130)")
-        dlogit = self._buf("dlogit", (R2,), torch.float32)
-        ws = self._ws("ws_loss", K.llp_loss_ws_bytes(B, n_lab))
-        K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin), 1.0,
-                   float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms, ws)
-
-        # ---- a10: backward
-        self._dbg_cut("teacher + loss")
-        dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop, overlap=overlap)
-        mlp = self.predictor_kind == "mlp"
-        if dedup and _SEGMENT_FUSED:
-            # Hadamard backward reduced straight onto the unique nodes (no [R1, H] row gradients)
-            dh = self._buf("gS0", (rows_s, H), dt)
-            arow = self._buf("anchor_rows", (max(B, 1), H), dt)
-            K.hadamard_bwd_segments(rows_s, B, C, n_lab, H, seg_ptr, seg_rows, pos, dZ0 if mlp else None, h, dh,
-                                    arow, drow=None if mlp else dlogit, count=n_u)
-        else:
-            dh_rows = self._buf("dh_rows" if dedup else "gS0", (R1, H), dt)
-            hidx = pos if dedup else None
-            if mlp:
-                K.hadamard_bwd_blocks(B, C, n_lab, H, dZ0, h, dh_rows, hidx=hidx)
-            else:
-                K.hadamard_bwd_blocks(B, C, n_lab, H, None, h, dh_rows, drow=dlogit, hidx=hidx)
-            if dedup:
-                dh = self._buf("gS0", (rows_s, H), dt)
-                K.segment_sum_rows(rows_s, seg_ptr, seg_rows, dh_rows, dh, count=n_u)
-            else:
-                dh = dh_rows
-        self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, overlap=overlap, x_rows=x_rows,
-                               norm_count=R1_total, norm_sync=True)
-        self._allreduce_and_update()
-        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
+        return acts, x_rows
 
     @property
     def _batch_norm(self):
@@ -1334,21 +1327,19 @@ class DistillEngine(EngineBase):
         w, b = self.t_head
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
-    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, overlap=False, x_rows=None, norm_count=0.0,
+    def _student_backward(self, dh, R1, target, acts, p_drop, count=None, x_rows=None, norm_count=0.0,
                           norm_sync=False):
         """count: int32 device row count (unique-node student) or None.  dh lives in
-        buffer 'gS0'.  overlap: weight-gradient GEMMs on the side stream, as in
-        _predictor_backward (three data-gradient buffers).  x_rows: x[target]
-        materialised by the forward (else the first layer's input is gathered).
-        norm_count / norm_sync: BatchNorm's batch row count and whether its sums are
-        all-reduced across ranks (_norm_backward)."""
+        buffer 'gS0'.  x_rows: x[target] materialised by the forward (else the first
+        layer's input is gathered).  norm_count / norm_sync: BatchNorm's batch row count
+        and whether its sums are all-reduced across ranks (_norm_backward)."""
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
-        names = ["gS0", "gS1", "gS2"] if overlap & 4 else ["gS0", "gS1"]
+        names = ["gS0", "gS1"]
         k = 0
         for l in range(len(self.stu) - 1, -1, -1):
             lin = self.stu[l]
-            gcur = self._buf(names[k % len(names)], (R1, lin.out_f), dt)
+            gcur = self._buf(names[k % 2], (R1, lin.out_f), dt)
             if l > 0:
                 A_in = K.operand(acts[l - 1], count=count)
             elif x_rows is not None:
@@ -1358,20 +1349,14 @@ class DistillEngine(EngineBase):
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
             dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad
-            side = bool(overlap & 4)
-            with self._fork() if side else _nullctx():
-                K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc,
-                          self._ws("ws_tn_side" if side else "ws_tn", wsb), colsum_a=lin.lin.bias.grad)
-                if side:
-                    self._side_read(names[k % len(names)])
-                if padded:   # the zero-padded input columns' gradient is dropped
-                    lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
-                if l > 0:    # this layer's gradients are final: all-reduce them under the next layers' GEMMs
-                    self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))
-            if l > 0:
+            K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc, self._ws("ws_tn", wsb),
+                      colsum_a=lin.lin.bias.grad)
+            if padded:   # the zero-padded input columns' gradient is dropped
+                lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
+            if l > 0:    # this layer's gradients are final: all-reduce them under the next layers' GEMMs
+                self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))
                 k += 1
-                self._before_write(names[k % len(names)])
-                gnext = self._buf(names[k % len(names)], (R1, lin.in_f), dt)
+                gnext = self._buf(names[k % 2], (R1, lin.in_f), dt)
                 if self.stu_norms:
                     # d(post-ReLU/dropout activations), then through the norm into d(pre-norm output)
                     graw = self._buf("gN", (R1, lin.in_f), dt)

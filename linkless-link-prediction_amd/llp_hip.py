@@ -44,6 +44,7 @@ class TensorDesc(C.Structure):
 _SIGS = {
     "llp_version": (c_int, []),
     "llp_last_error": (C.c_char_p, []),
+    "llp_last_gemm_kernel": (C.c_char_p, []),
     "llp_device_count": (c_int, []),
     "llp_gemm_nt": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_int, c_vp, c_i64, c_int, c_f32, C.POINTER(Dropout), c_vp]),
@@ -66,7 +67,11 @@ _SIGS = {
                              c_int, c_vp, c_i64, c_vp]),
     "llp_llp_loss_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_llp_loss": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32,
-                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_vp, c_i64, c_vp]),
+                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64, c_vp, c_i64,
+                             c_vp]),
+    "llp_pair_owner_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_int]),
+    "llp_pair_owner_assign": (c_int, [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "llp_pair_owner_scatter": (c_int, [c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_dedup_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
@@ -161,6 +166,11 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = _lib.llp_last_error().decode() if _lib else ""
         raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def last_gemm_kernel() -> str:
+    """The NT GEMM kernel the last gemm_nt call on this thread launched (llp_last_gemm_kernel)."""
+    return lib().llp_last_gemm_kernel().decode()
 
 
 def stream_ptr() -> int:
@@ -289,15 +299,58 @@ def llp_loss_ws_bytes(B, n_lab):
 
 def llp_loss(B, Cc, s_logit, t_prob, n_lab, n_pos, out_logit, B_total, n_lab_total, margin, T, w_label, w_d, w_r,
              dlogit_ctx, dlogit_lab, terms, ws, accumulate=False, loss_scale=1.0, neg_count=None, neg_offset=0,
-             pos_total=0.0):
+             pos_total=0.0, term_range=None):
     """neg_count: the dense negatives' int32 device count (label slots past it inert, the BCE
-    mean over pos_total + count labels); n_lab_total is then unused."""
+    mean over pos_total + count labels); n_lab_total is then unused.  term_range (b0, b1): the
+    anchors whose KL / rank terms are reported (default all B; every gradient is written)."""
     L = lib()
+    tb0, tb1 = (0, B) if term_range is None else term_range
     check(L.llp_llp_loss(B, Cc, ptr(s_logit), ptr(t_prob), n_lab, n_pos, ptr(out_logit), float(B_total),
                          float(n_lab_total), margin, T, w_label, w_d, w_r, loss_scale, ptr(dlogit_ctx),
                          ptr(dlogit_lab), terms.data_ptr(), int(accumulate), ptr(neg_count), int(neg_offset),
-                         float(pos_total), ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()),
+                         float(pos_total), int(tb0), int(tb1), ws.data_ptr(), ws.numel() * ws.element_size(),
+                         stream_ptr()),
           "llp_llp_loss")
+
+
+class OwnerCat(C.Structure):
+    """llp_owner_cat: one category of pairs for llp_pair_owner_assign; end e of item i is
+    e[(i // kc) * kld + koff + (i % kc) * kstep]."""
+    _fields_ = [("a", c_vp), ("a_kc", c_i64), ("a_kld", c_i64), ("a_koff", c_i64), ("a_kstep", c_i64), ("b", c_vp),
+                ("b_kc", c_i64), ("b_kld", c_i64), ("b_koff", c_i64), ("b_kstep", c_i64), ("key_b", C.c_int32),
+                ("pad", C.c_int32), ("n", c_i64)]
+
+
+def owner_cat(n, a, b, a_view=None, b_view=None, key_b=False):
+    """a / b: int32 tensors of node ids; *_view = (kc, kld, koff, kstep) strided view (default
+    contiguous: (1, 1, 0, 0))."""
+    av = a_view or (1, 1, 0, 0)
+    bv = b_view or (1, 1, 0, 0)
+    c = OwnerCat(ptr(a), *av, ptr(b), *bv, int(bool(key_b)), 0, int(n))
+    c._keep = (a, b)
+    return c
+
+
+def pair_owner_ws_bytes(ns, world):
+    ns = list(ns) + [0] * (3 - len(ns))
+    return load().llp_pair_owner_workspace_bytes(ns[0], ns[1], ns[2], int(world))
+
+
+def pair_owner_assign(cats, num_nodes, world, rank, sel, ws, gpos=None, target=None, R2=0):
+    """llp_pair_owner_assign over 1-3 OwnerCat categories: sel (int32[sum n]) holds rank r's items
+    of each category at [cat base + r n / world, ...); gpos (int32[sum n], optional) item -> slot;
+    target (int32[2 R2], optional) = this rank's pairs' [a ends | b ends] in its order."""
+    arr = (OwnerCat * len(cats))(*cats)
+    check(lib().llp_pair_owner_assign(len(cats), C.cast(arr, c_vp), int(num_nodes), int(world), int(rank),
+                                      sel.data_ptr(), ptr(gpos), ptr(target), int(R2), ws.data_ptr(),
+                                      ws.numel() * ws.element_size(), stream_ptr()),
+          "llp_pair_owner_assign")
+
+
+def pair_owner_scatter(n, gpos, lo, hi, s_loc, t_loc, s_full, t_full):
+    """s_full[i] = s_loc[gpos[i] - lo] when lo <= gpos[i] < hi else 0 (t likewise; either may be None)."""
+    check(lib().llp_pair_owner_scatter(int(n), gpos.data_ptr(), int(lo), int(hi), ptr(s_loc), ptr(t_loc),
+                                       ptr(s_full), ptr(t_full), stream_ptr()), "llp_pair_owner_scatter")
 
 
 def hadamard_bwd_blocks(B, Cc, L2, H, dZ, h, dh, drow=None, hidx=None):
@@ -387,7 +440,7 @@ def minibatch_sample(rowptr, col, num_nodes, start, B, ps_method, rw_step, hops,
                                  1 if ps_method == "nb" else 0, rw_step, hops, ns_rate, seed, step_ctr.data_ptr(),
                                  stream_offset, pairs.data_ptr(), perm.data_ptr(), P, P_total, p_offset,
                                  neg_stream_offset, samples.data_ptr(), neg.data_ptr(), target.data_ptr(),
-                                 t_ia.data_ptr(), t_ib.data_ptr(), stream_ptr()), "llp_minibatch_sample")
+                                 ptr(t_ia), ptr(t_ib), stream_ptr()), "llp_minibatch_sample")
 
 
 def randint_pairs(num_nodes, n, seed, step_ctr, stream_offset, out, n_total=None, offset=0):

@@ -66,6 +66,41 @@ class Graph:
             self.dinv = torch.from_numpy((1.0 / np.sqrt(deg.astype(np.float64))).astype(np.float32)).to(dev)
 
 
+def locality_order(edge_index, num_nodes: int, iters: int = 10):
+    """A node order that puts each node's neighbours near it, for the CSR aggregate's L2 reuse
+    (SAGE / GCN teacher, src/models.py:110-119): synchronous label propagation over the
+    (symmetric) graph -- every node takes the most frequent label of its in-neighbours,
+    ties to the smallest label, starting from its own id -- for up to ``iters`` rounds, then
+    nodes sorted by (label, id).  Deterministic host numpy, O(E log E) per round.
+
+    Returns (order, pi): new id i holds node order[i]; pi[v] = new id of node v."""
+    ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
+    N = int(num_nodes)
+    src, dst = ei[0].astype(np.int64), ei[1].astype(np.int64)
+    lab = np.arange(N, dtype=np.int64)
+    for _ in range(iters):
+        key = dst * N + lab[src]
+        key.sort()
+        b = np.flatnonzero(np.diff(key)) + 1
+        starts = np.concatenate([[0], b]) if key.size else np.zeros(0, np.int64)
+        ends = np.concatenate([b, [key.size]]) if key.size else np.zeros(0, np.int64)
+        rk, cnt = key[starts], ends - starts
+        v, lb = rk // N, rk % N
+        o = np.lexsort((lb, -cnt, v))            # per node: the largest count, then the smallest label
+        vo = v[o]
+        first = np.ones(vo.size, bool)
+        first[1:] = vo[1:] != vo[:-1]
+        new = lab.copy()
+        new[vo[first]] = lb[o][first]
+        if np.array_equal(new, lab):
+            break
+        lab = new
+    order = np.lexsort((np.arange(N), lab))
+    pi = np.empty(N, np.int64)
+    pi[order] = np.arange(N)
+    return order, pi
+
+
 _GRAPH_CACHE = {}
 
 

@@ -41,7 +41,7 @@ import torch
 
 import llp_hip as K
 from llp_engine import DROP_ENCODER, EngineBase, _norms_of
-from llp_sage import GCNConv, Graph, SAGEConv_updated
+from llp_sage import GCNConv, Graph, SAGEConv_updated, locality_order
 
 
 class TeacherEngine(EngineBase):
@@ -53,7 +53,7 @@ class TeacherEngine(EngineBase):
     model.parameters() + predictor.parameters()."""
 
     def __init__(self, model, predictor, x, edge_index, num_nodes, optimizer, dtype="fp32", seed=0, group=None,
-                 device=None):
+                 device=None, reorder=True):
         self._init_device(x.device, device, dtype, seed, group, "TeacherEngine")
         self.N = int(num_nodes)
         N = self.N
@@ -72,8 +72,21 @@ class TeacherEngine(EngineBase):
         self.norms = _norms_of(model, len(self.convs) - 1, self._conv_out(self.convs[0]))
         self.p_drop = float(model.dropout)
         ei = edge_index.cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
-        self.graph = Graph(ei, N, self.dev, gcn=self.gcn)
-        self._neg_rc = (ei[0], ei[1])        # row, col = data.adj_t (src/train_teacher_gnn.py:23)
+        # Node order inside the engine (``reorder``): a locality order (llp_sage.locality_order,
+        # label propagation) under which most of a node's neighbours sit next to it, so the CSR
+        # aggregate's neighbour rows are L2 hits; node v lives in row pi[v] of every node table
+        # (x, activations, h), the edges are relabelled with their order kept (so every row's
+        # neighbour sum runs in the same order: the same values), link and negative pairs are
+        # drawn on the original ids and mapped, and embed() returns rows in the original order
+        self._pi = self._order = None
+        ei_int = ei
+        if reorder and N > 1:
+            order, pi = locality_order(ei, N)
+            self._order = torch.from_numpy(order.astype(np.int32)).to(self.dev)   # engine row -> node
+            self._pi = torch.from_numpy(pi.astype(np.int32)).to(self.dev)         # node -> engine row
+            ei_int = pi[ei]
+        self.graph = Graph(ei_int, N, self.dev, gcn=self.gcn)
+        self._neg_rc = (ei[0], ei[1])        # row, col = data.adj_t (src/train_teacher_gnn.py:23), original ids
         self.num_edges = int(ei.shape[1])
 
         # ---------------- per-layer weights and shadows
@@ -113,6 +126,8 @@ class TeacherEngine(EngineBase):
 
         # ---------------- activations (HBM-resident for the whole run)
         x = x.to(self.dev)
+        if self._order is not None:
+            x = x.index_select(0, self._order.long())
         for l, L in enumerate(self.layers):
             F, O = L["F"], L["O"]
             if self.gcn:
@@ -290,6 +305,8 @@ class TeacherEngine(EngineBase):
         ia, ib = tgt[:R], tgt[R:]
         K.fullbatch_pairs(0, 0, None, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib, neg_count=cnt,
                           neg_offset=p_offset)
+        if self._pi is not None:   # node ids -> the engine's rows (in place)
+            K.gather_i32(tgt, self._pi, tgt)
         logit = self._buf("logit", (R,), torch.float32)
         A0, zacts = self._predictor_forward(h, ia, ib, R, logit, self.pred_drop)
         dlogit = self._buf("dlogit", (R,), torch.float32)
@@ -310,5 +327,11 @@ class TeacherEngine(EngineBase):
 
     @torch.no_grad()
     def embed(self):
-        """model(x, adj_t) in eval mode (src/train_teacher_gnn.py:87) -> f32 [N, O]."""
-        return self._encode(training=False).float()
+        """model(x, adj_t) in eval mode (src/train_teacher_gnn.py:87) -> f32 [N, O], rows in the
+        original node order."""
+        h = self._encode(training=False)
+        if self._pi is not None:
+            out = torch.empty_like(h)
+            K.gather_rows(h, self._pi, out)     # node v <- engine row pi[v]
+            h = out
+        return h.float()

@@ -26,8 +26,11 @@ reproducible under seed_everything but not bit-identical to the reference's
 streams (RNG streams are not portable anyway).
 
 Multi-GPU: when torch.distributed is initialised, every rank draws the same
-permutations and takes its contiguous slice of each global anchor / link
-batch; gradients are all-reduced inside the engine (strong scaling).
+permutations.  The minibatch step gives each rank the whole batch and the
+engine assigns every predictor pair to one rank (the owner decomposition,
+DistillEngine.minibatch_owner; with dropout or BatchNorm each rank takes its
+contiguous slice of the anchor / link batch instead); the full-batch step
+slices.  Gradients are all-reduced inside the engine (strong scaling).
 """
 from __future__ import annotations
 
@@ -110,10 +113,13 @@ def train_minibatch(model, predictor, t_h, teacher_predictor, data, split_edge, 
         if n0 >= N:
             raise StopIteration("node loader exhausted (the reference's next(node_loader) raises here)")
         B_tot = min(nbs, N - n0)
-        b0, b1 = _slices(B_tot, world, rank)
-        p0, p1 = _slices(P_tot, world, rank)
-        eng.step_minibatch(node_perm[n0 + b0:n0 + b1], link_perm[s + p0:s + p1], pairs, b_offset=b0, p_offset=p0,
-                           B_total=B_tot, P_total=P_tot, dense_negatives=dense)
+        if eng.minibatch_owner:   # every rank takes the whole batch and evaluates the pairs it owns
+            eng.step_minibatch(node_perm[n0:n0 + B_tot], link_perm[s:s + P_tot], pairs, dense_negatives=dense)
+        else:
+            b0, b1 = _slices(B_tot, world, rank)
+            p0, p1 = _slices(P_tot, world, rank)
+            eng.step_minibatch(node_perm[n0 + b0:n0 + b1], link_perm[s + p0:s + p1], pairs, b_offset=b0,
+                               p_offset=p0, B_total=B_tot, P_total=P_tot, dense_negatives=dense)
         total += P_tot
     return eng.end_epoch(total)
 

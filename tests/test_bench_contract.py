@@ -28,13 +28,13 @@ def test_step_flops_matches_survey():
 
 
 def test_pmc_traffic_reads_committed_profile():
-    prof = bench.PMC_FILE
+    prof = bench.PMC_FILES["bf16"]
     p = json.load(open(prof))
     t = bench.pmc_traffic(p["rows"], p["H"], p["dtype"])
     assert t == pytest.approx(p["traffic_bytes_per_launch"], rel=1e-9)
     assert t / p["algorithmic_bytes"] == pytest.approx(p["traffic_over_algorithmic"], rel=1e-9)
     assert bench.pmc_traffic(p["rows"], 2 * p["H"], p["dtype"]) is None        # another shape
-    assert bench.pmc_traffic(p["rows"], p["H"], "fp32") is None
+    assert bench.pmc_traffic(p["rows"], p["H"], "fp16") is None                 # no such profile
 
 
 def test_graph_default_at_every_world_size():

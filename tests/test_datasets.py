@@ -123,3 +123,18 @@ def test_synthetic_collab_matches_the_benchmark_spec():
         assert tuple(d.split_edge[s]["edge"].shape) == (n, 2)
         assert tuple(d.split_edge[s]["edge_neg"].shape) == (C["n_neg"], 2)
     assert d.x.dtype == torch.float32 and tuple(d.x.shape) == (d.N, 128)
+
+
+def test_locality_order_is_a_permutation_that_groups_communities():
+    """locality_order on a planted-partition graph: a permutation, and most edges end up
+    between nearby rows (the L2 reuse the aggregate relies on)."""
+    import numpy as np
+    import llp_data
+    import llp_sage
+    d = llp_data.synthetic_collab(seed=3, scale=0.05, with_eval=False)
+    ei = d.edge_index.numpy()
+    order, pi = llp_sage.locality_order(ei, d.N)
+    assert np.array_equal(np.sort(order), np.arange(d.N)) and np.array_equal(pi[order], np.arange(d.N))
+    near = float((np.abs(pi[ei[0]] - pi[ei[1]]) < 1024).mean())
+    near_id = float((np.abs(ei[0] - ei[1]) < 1024).mean())
+    assert near > 0.6 and near > 4 * near_id, (near, near_id)

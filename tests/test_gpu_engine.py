@@ -237,89 +237,6 @@ def test_engine_unique_node_step_graph_replay_matches_eager():
     assert 0 < res["graph"][2] == res["eager"][2] < 300 * 37 + 4 * 2048
 
 
-@pytest.mark.parametrize("mode,L", [(2, 3), (7, 3), (7, 5)])
-def test_engine_overlap_modes_bit_identical(mode, L):
-    """LLP_OVERLAP (second stream for the weight-gradient GEMMs and the frozen
-    teacher predictor) against one stream: the same kernels with the same inputs,
-    so two steps give bit-identical loss terms, gradients and parameters.  L=5
-    rotates the three data-gradient buffers past their first reuse, where the
-    main stream must wait for the side GEMM still reading the buffer."""
-    import types
-
-    import llp_engine
-    N, F_, H = 2000, 128, 256
-    args = types.SimpleNamespace(rw_step=3, hops=2, ns_rate=2, ps_method="nb", dropout=0.0, margin=0.01,
-                                 LLP_D=1.0, LLP_R=1.0, True_label=1.0, predictor="mlp", lr=0.001)
-    g = torch.Generator().manual_seed(4)
-    u = torch.randint(0, N, (15000,), generator=g)
-    v = torch.randint(0, N, (15000,), generator=g)
-    keep = u != v
-    pairs = torch.stack([u[keep], v[keep]], 1)
-    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
-    x = torch.randn(N, F_, generator=g) * 0.3
-    t_h = torch.randn(N, 256, generator=g) * 0.3
-    pd = pairs.to(torch.int32).to(DEV)
-    res = {}
-    saved = llp_engine._OVERLAP
-    try:
-        for m in (0, mode):
-            llp_engine._OVERLAP = m
-            eng, model, pred = _make_engine("bf16", N, F_, H, L, 3, args, x, t_h, ei)
-            params = list(model.parameters()) + list(pred.parameters())
-            for it in range(2):
-                anchors = torch.randperm(N, generator=torch.Generator().manual_seed(10 + it))[:256]
-                link = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(20 + it))[:4096]
-                eng.step_minibatch(anchors.to(torch.int32).to(DEV), link.to(torch.int32).to(DEV), pd)
-            torch.cuda.synchronize()
-            res[m] = (eng.terms.cpu().clone(), [p.grad.detach().cpu().clone() for p in params],
-                      [p.detach().cpu().clone() for p in params])
-    finally:
-        llp_engine._OVERLAP = saved
-    (t0, g0, p0), (t1, g1, p1) = res[0], res[mode]
-    assert torch.equal(t0, t1), (t0, t1)
-    for a, b in zip(g0 + p0, g1 + p1):
-        assert torch.equal(a, b), (tuple(a.shape), (a - b).abs().max().item())
-
-
-def test_engine_fused_segment_backward_bit_identical():
-    """LLP_SEGMENT_FUSED (Hadamard backward reduced straight onto the unique nodes)
-    against the row-gradient + segment-sum path: bit-identical steps (bf16 and fp32)."""
-    import types
-
-    import llp_engine
-    N, F_, H, L = 1500, 128, 256, 3
-    args = types.SimpleNamespace(rw_step=3, hops=2, ns_rate=2, ps_method="nb", dropout=0.0, margin=0.01,
-                                 LLP_D=1.0, LLP_R=1.0, True_label=1.0, predictor="mlp", lr=0.001)
-    g = torch.Generator().manual_seed(8)
-    u = torch.randint(0, N, (12000,), generator=g)
-    v = torch.randint(0, N, (12000,), generator=g)
-    keep = u != v
-    pairs = torch.stack([u[keep], v[keep]], 1)
-    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
-    x = torch.randn(N, F_, generator=g) * 0.3
-    t_h = torch.randn(N, 256, generator=g) * 0.3
-    pd = pairs.to(torch.int32).to(DEV)
-    saved = llp_engine._SEGMENT_FUSED
-    try:
-        for dt in ("bf16", "fp32"):
-            res = {}
-            for fused in (False, True):
-                llp_engine._SEGMENT_FUSED = fused
-                eng, model, pred = _make_engine(dt, N, F_, H, L, 3, args, x, t_h, ei)
-                params = list(model.parameters()) + list(pred.parameters())
-                for it in range(2):
-                    anchors = torch.randperm(N, generator=torch.Generator().manual_seed(30 + it))[:200]
-                    link = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(40 + it))[:3000]
-                    eng.step_minibatch(anchors.to(torch.int32).to(DEV), link.to(torch.int32).to(DEV), pd)
-                torch.cuda.synchronize()
-                res[fused] = [p.grad.detach().cpu().clone() for p in params] + [p.detach().cpu().clone()
-                                                                               for p in params]
-            for a, b in zip(res[False], res[True]):
-                assert torch.equal(a, b), (dt, tuple(a.shape), (a - b).abs().max().item())
-    finally:
-        llp_engine._SEGMENT_FUSED = saved
-
-
 def test_engine_fp32_hidden_2048_matches_oracle():
     """The collab sweep's hidden_channels=2048 in fp32 (configurations/collab_transductive.yaml;
     collab runs train_minibatch): 8 KiB rows exceed the node-grouped Hadamard-backward

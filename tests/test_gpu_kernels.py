@@ -1022,3 +1022,107 @@ def test_gemm_nt_splitk(M, N, Kd, relu):
     assert bool(((C1.float() - C0.float()).abs()[diff] <= 2.0 ** -7 * C0.float().abs()[diff] + 1e-6).all())
     if relu:
         assert torch.equal(_mask_bits(m1, N), (C1 != 0).to(torch.int32))
+
+
+# ------------------------------------------------------------------ owner decomposition (bit-exact)
+def _owner_case(seed, N, B, C, P, n_neg, skew):
+    g = np.random.default_rng(seed)
+    C1 = C + 1
+    if skew:   # most keys in the first node range: heavy overflow into the other ranks
+        samples = np.minimum(g.integers(0, max(1, N // 5), (B, C1)), N - 1)
+    else:
+        samples = g.integers(0, N, (B, C1))
+    pos = g.integers(0, N, (2, P))
+    neg = g.integers(0, N, (2, n_neg))
+    return samples, pos, neg
+
+
+@pytest.mark.parametrize("N,B,C,P,n_neg", [(235_868, 13_110, 36, 65_536, 65_536), (1000, 37, 5, 111, 90),
+                                           (50, 3, 2, 0, 7), (10, 1, 1, 1, 0)])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("skew", [False, True])
+def test_pair_owner_assign_matches_oracle(N, B, C, P, n_neg, world, skew):
+    """llp_pair_owner_assign == oracle pair_owner_assign for the three categories of one
+    minibatch (context pairs keyed by the context node, label pairs by their source): sel,
+    gpos and every rank's [ia | ib] rows, at the collab shape and small / skewed cases."""
+    k = K()
+    samples, pos, neg = _owner_case(B * 7 + world, N, B, C, P, n_neg, skew)
+    C1 = C + 1
+    n_lab = P + n_neg
+    # the whole batch's this_target layout: samples.flat | src | dst (src/main.py:95)
+    tgt = np.concatenate([samples.reshape(-1), pos[0], neg[0], pos[1], neg[1]]).astype(np.int32)
+    td = torch.from_numpy(tgt).to(DEV)
+    BC1 = B * C1
+    ns = (B * C, P, n_neg)
+    n_all = sum(ns)
+    for rank in range(world):
+        caps = [(rank + 1) * n // world - rank * n // world for n in ns]
+        R2 = sum(caps)
+        cats = [k.owner_cat(B * C, td, td, (C, C1, 0, 0), (C, C1, 1, 1), key_b=True),
+                k.owner_cat(P, td[BC1:], td[BC1 + n_lab:]),
+                k.owner_cat(n_neg, td[BC1 + P:], td[BC1 + n_lab + P:])]
+        sel = torch.full((max(n_all, 1),), -7, dtype=torch.int32, device=DEV)
+        gpos = torch.full((max(n_all, 1),), -7, dtype=torch.int32, device=DEV)
+        rows = torch.full((max(2 * R2, 1),), -7, dtype=torch.int32, device=DEV)
+        ws = torch.empty(k.pair_owner_ws_bytes(ns, world) // 4 + 16, dtype=torch.int32, device=DEV)
+        k.pair_owner_assign(cats, N, world, rank, sel, ws, gpos=gpos, target=rows, R2=R2)
+        sel_h, gpos_h, rows_h = sel.cpu().numpy(), gpos.cpu().numpy(), rows.cpu().numpy()
+        base = 0
+        ia, ib = [], []
+        keys = (samples[:, 1:].reshape(-1), pos[0], neg[0])
+        ends = ((np.repeat(samples[:, 0], C), samples[:, 1:].reshape(-1)), (pos[0], pos[1]), (neg[0], neg[1]))
+        for key, n, (ea, eb) in zip(keys, ns, ends):
+            ref, off = O.pair_owner_assign(key, N, world)
+            assert np.array_equal(sel_h[base:base + n], ref)
+            inv = np.empty(n, np.int64)
+            inv[ref] = np.arange(n)
+            assert np.array_equal(gpos_h[base:base + n], inv)
+            mine = ref[off[rank]:off[rank + 1]]
+            ia.append(ea[mine])
+            ib.append(eb[mine])
+            base += n
+        assert np.array_equal(rows_h[:2 * R2], np.concatenate(ia + ib))
+    # the oracle's rank split of the whole batch equals pair_owner_rank_items
+    cs, ps, ns_ = O.pair_owner_rank_items(samples, pos, neg, N, world, world - 1)
+    assert len(cs) + len(ps) + len(ns_) == sum((world * n) // world - ((world - 1) * n) // world for n in ns)
+
+
+def test_pair_owner_scatter_and_loss_term_range():
+    """llp_pair_owner_scatter places a rank's context logits into the [B, C] grid (zeros
+    elsewhere); the sum over ranks is the whole grid, and llp_llp_loss with term ranges
+    [rB/W, (r+1)B/W) gives the whole-batch terms summed over ranks, every gradient written."""
+    k = K()
+    N, B, C, W = 500, 24, 6, 3
+    samples, pos, neg = _owner_case(5, N, B, C, 0, 0, False)
+    key = samples[:, 1:].reshape(-1)
+    sel, off = O.pair_owner_assign(key, N, W)
+    gpos = np.empty(B * C, np.int64)
+    gpos[sel] = np.arange(B * C)
+    g = torch.Generator().manual_seed(3)
+    s_all = torch.randn(B * C, generator=g)
+    t_all = torch.rand(B * C, generator=g)
+    gp = torch.from_numpy(gpos.astype(np.int32)).to(DEV)
+    tot_s = torch.zeros(B * C, device=DEV)
+    tot_t = torch.zeros(B * C, device=DEV)
+    terms_sum = torch.zeros(4)
+    for r in range(W):
+        mine = torch.from_numpy(sel[off[r]:off[r + 1]])
+        s_loc, t_loc = s_all[mine].to(DEV), t_all[mine].to(DEV)
+        fs = torch.full((B * C,), 9.0, device=DEV)
+        ft = torch.full((B * C,), 9.0, device=DEV)
+        k.pair_owner_scatter(B * C, gp, int(off[r]), int(off[r + 1]), s_loc, t_loc, fs, ft)
+        tot_s += fs
+        tot_t += ft
+        d = torch.empty(B * C, device=DEV)
+        terms = torch.zeros(4, device=DEV)
+        ws = torch.empty(k.llp_loss_ws_bytes(B, 0) // 4 + 16, device=DEV)
+        k.llp_loss(B, C, s_all.to(DEV), t_all.to(DEV), 0, 0, None, B, 1, 0.05, 1.0, 1.0, 1.0, 1.0, d, None, terms, ws,
+                   term_range=(r * B // W, (r + 1) * B // W))
+        terms_sum += terms.cpu()
+    assert torch.equal(tot_s.cpu(), s_all) and torch.equal(tot_t.cpu(), t_all)
+    d1 = torch.empty(B * C, device=DEV)
+    t1 = torch.zeros(4, device=DEV)
+    ws = torch.empty(k.llp_loss_ws_bytes(B, 0) // 4 + 16, device=DEV)
+    k.llp_loss(B, C, s_all.to(DEV), t_all.to(DEV), 0, 0, None, B, 1, 0.05, 1.0, 1.0, 1.0, 1.0, d1, None, t1, ws)
+    assert torch.allclose(terms_sum, t1.cpu(), rtol=1e-5, atol=1e-7)
+    assert torch.equal(d.cpu(), d1.cpu())    # every anchor's gradient, whatever the term range

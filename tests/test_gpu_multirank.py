@@ -40,7 +40,17 @@ def _problem(N=2000, n_pairs=12000, B=256, P=1024):
     return N, F_, H, L, pairs, ei, x, t_h, anchors, links, args
 
 
-def _run(rank, world, dtype, port, out, norm_type="none"):
+def _part(eng, rank, world, B, P):
+    """This rank's part of the batch: all of it under the owner decomposition (the engine picks
+    its pairs), else its contiguous slice with offsets and totals."""
+    if eng.minibatch_owner or world == 1:
+        return 0, B, 0, P, {}
+    b0, b1 = rank * B // world, (rank + 1) * B // world
+    p0, p1 = rank * P // world, (rank + 1) * P // world
+    return b0, b1, p0, p1, dict(b_offset=b0, p_offset=p0, B_total=B, P_total=P)
+
+
+def _run(rank, world, dtype, port, out, norm_type="none", owner_pairs=True):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "linkless-link-prediction_amd"))
@@ -61,17 +71,16 @@ def _run(rank, world, dtype, port, out, norm_type="none"):
         p.requires_grad = False
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
     eng = llp_engine.DistillEngine(model, pred, tpred, x.to(dev), t_h.to(dev), ei[0].numpy(), ei[1].numpy(), N, args,
-                                   opt, dtype=dtype, seed=11)
+                                   opt, dtype=dtype, seed=11, owner_pairs=owner_pairs)
     B, P = anchors.numel(), links.numel()
-    b0, b1 = rank * B // world, (rank + 1) * B // world
-    p0, p1 = rank * P // world, (rank + 1) * P // world
+    b0, b1, p0, p1, kw = _part(eng, rank, world, B, P)
     pr = pairs.to(torch.int32).to(dev).contiguous()
     if rank == 0:
         out["params0"] = [p.detach().cpu().numpy().copy() for p in list(model.parameters()) + list(pred.parameters())]
+        out["owner"] = eng.minibatch_owner
     eng.begin_epoch()
     for _ in range(2):
-        eng.step_minibatch(anchors[b0:b1].to(dev), links[p0:p1].to(dev), pr, b_offset=b0, p_offset=p0, B_total=B,
-                           P_total=P)
+        eng.step_minibatch(anchors[b0:b1].to(dev), links[p0:p1].to(dev), pr, **kw)
     loss = eng.end_epoch(2 * P)
     torch.cuda.synchronize()
     if rank == 0:   # numpy copies: torch tensors through an mp.Queue share fds with an exiting child
@@ -109,12 +118,11 @@ def _run_graph(rank, world, port, out, use_graph, size):
     eng = llp_engine.DistillEngine(model, pred, tpred, x.to(dev), t_h.to(dev), ei[0].numpy(), ei[1].numpy(), N, args,
                                    opt, dtype="bf16", seed=11)
     B, P = anchors.numel(), links.numel()
-    b0, b1 = rank * B // world, (rank + 1) * B // world
-    p0, p1 = rank * P // world, (rank + 1) * P // world
+    b0, b1, p0, p1, kw = _part(eng, rank, world, B, P)
     pr = pairs.to(torch.int32).to(dev).contiguous()
     a_dev = anchors[b0:b1].to(dev)
     l_dev = links[p0:p1].to(dev)
-    kw = dict(b_offset=b0, p_offset=p0, B_total=B, P_total=P)
+    out["owner"] = eng.minibatch_owner
     eng.begin_epoch()
     eng.step_minibatch(a_dev, l_dev, pr, **kw)
     if use_graph:
@@ -169,8 +177,10 @@ def test_two_ranks_segmented_graph_matches_eager(size, world):
         pytest.skip("no GPU")
     eager = _n_ranks(False, size, world)
     graph = _n_ranks(True, size, world)
-    # cuts: the predictor's all-reduce, one bucket per student layer but the first, the rest + clip/Adam
-    assert graph["segments"] == 5
+    # cuts: the context logits' all-reduce (owner decomposition), the predictor's all-reduce, one
+    # bucket per student layer but the first, the rest + clip/Adam
+    assert graph["owner"]
+    assert graph["segments"] == 6
     assert graph["loss"] == eager["loss"], (graph["loss"], eager["loss"])
     import numpy as np
     for a, b in zip(graph["grads"], eager["grads"]):
@@ -283,9 +293,9 @@ def _fullbatch_compare(shard=True, norm_type="none", free=(), world=2):
             assert float((abs(a - b) <= 1e-4).mean()) > 0.99
 
 
-def _worker(rank, world, dtype, port, q, norm_type="none"):
+def _worker(rank, world, dtype, port, q, norm_type="none", owner_pairs=True):
     out = {}
-    _run(rank, world, dtype, port, out, norm_type)
+    _run(rank, world, dtype, port, out, norm_type, owner_pairs)
     if rank == 0:
         q.put(out)
 
@@ -324,9 +334,13 @@ def test_two_ranks_norm_equal_one_rank(norm_type):
         assert float(abs(a.astype("float64") - b.astype("float64")).max()) <= 0.1 * 2 * 0.01 + 1e-4
 
 
-@pytest.mark.parametrize("dtype,world", [("fp32", 2), ("bf16", 2), ("fp32", 4)])
-def test_two_ranks_equal_one_rank(dtype, world):
-    """The minibatch step over 2 (and 4) gloo ranks on one GPU == the whole batch on one rank."""
+@pytest.mark.parametrize("dtype,world,owner", [("fp32", 2, True), ("bf16", 2, True), ("fp32", 4, True),
+                                               ("fp32", 8, True), ("bf16", 8, True), ("fp32", 2, False)])
+def test_two_ranks_equal_one_rank(dtype, world, owner):
+    """The minibatch step over 2, 4 and 8 gloo ranks on one GPU == the whole batch on one rank:
+    the owner decomposition (every pair on one rank, the context logits all-reduced; the
+    default) and the slice decomposition (owner_pairs=False: each rank its slice of anchors and
+    links, the path of steps with dropout or BatchNorm)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     single = {}
@@ -334,13 +348,14 @@ def test_two_ranks_equal_one_rank(dtype, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, dtype, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, dtype, port, q, "none", owner)) for r in range(world)]
     for p in procs:
         p.start()
     multi = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    assert multi["owner"] == owner
     tol = 1e-4 if dtype == "fp32" else 2e-2
     assert abs(multi["loss"] - single["loss"]) <= tol * max(1.0, abs(single["loss"])), (multi["loss"], single["loss"])
     import numpy as np

@@ -209,3 +209,38 @@ def test_teacher_bf16_relu_bit_masks_match_activation_masks():
         runs.append([p.detach().cpu().clone() for p in ps])
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["teacher_sage_small", "teacher_gcn_small", "teacher_updated_production_small"])
+def test_teacher_locality_order_same_results(name):
+    """TeacherEngine(reorder=True), the default: nodes renumbered by llp_sage.locality_order inside
+    the engine (edges relabelled in their order, pairs and negatives mapped).  Against
+    reorder=False on the same steps: the eval embedding (returned in the original node order) and
+    the BCE are identical -- every row's neighbour sum runs in the same order -- and the
+    gradients agree up to the order of the weight-gradient sums over the (renumbered) nodes."""
+    _need_gpu()
+    import llp_sage
+    import llp_teacher
+    import models
+    c = G.load_teacher_case(name)
+    pairs = c.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+    res = {}
+    for reorder in (False, True):
+        eng, model, pred = _build(c)
+        if not reorder:   # rebuild without the order (same modules and weights)
+            opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=0.005)
+            eng = llp_teacher.TeacherEngine(model, pred, c.x.to(DEV), c.edge_index, c.N, opt, dtype="fp32", seed=3,
+                                            reorder=False)
+        else:
+            assert eng._pi is not None
+        h0 = eng.embed().cpu()
+        st = c.steps[0]
+        eng.step(st.link_perm.to(torch.int32).to(DEV), pairs, neg=st.neg_edge.to(DEV))
+        torch.cuda.synchronize()
+        res[reorder] = (h0, eng.terms[1].item(), [p.grad.detach().cpu().clone() for p in
+                                                   list(model.parameters()) + list(pred.parameters())])
+    assert torch.equal(res[True][0], res[False][0])
+    assert abs(res[True][1] - res[False][1]) <= 1e-6 * max(1.0, abs(res[False][1]))
+    for a, b in zip(res[True][2], res[False][2]):
+        assert (a - b).abs().max().item() <= 1e-4 * max(b.abs().max().item(), 1e-6) + 1e-7
+

@@ -53,8 +53,11 @@ def main():
     # FETCH_SIZE / WRITE_SIZE are in KiB
     f_b = 1024.0 * sum(fetch) / len(fetch)
     w_b = 1024.0 * sum(write) / len(write)
-    # A read + C write (bf16) + W read + the ReLU bit mask the step's launch writes
-    alg = 2.0 * a.rows * a.H * 2 + 2.0 * a.H * a.H + a.rows * a.H / 8.0
+    # bf16: A read + C write + W read + the ReLU bit mask the step's launch writes; fp32: A, C, W
+    if a.dtype == "bf16":
+        alg = 2.0 * a.rows * a.H * 2 + 2.0 * a.H * a.H + a.rows * a.H / 8.0
+    else:
+        alg = 2.0 * a.rows * a.H * 4 + 4.0 * a.H * a.H
     out = {"kernel": names[-1] if names else a.kernel, "rows": a.rows, "H": a.H, "dtype": a.dtype,
            "dispatches": len(fetch), "fetch_size_bytes": f_b, "write_size_bytes": w_b,
            "traffic_bytes_per_launch": 2.0 * f_b + w_b, "algorithmic_bytes": alg,

@@ -54,3 +54,20 @@ for R in (1, 2, 4, 8):
     print(f"R={R}: unique per rank {np.mean(per):9.0f} (max {max(per)}), sum over ranks {sum(per):8d} "
           f"= {sum(per) / glob.size:.2f}x global; owner-computes: {glob.size / R:8.0f} rows per rank, "
           f"remote h rows fetched per rank {np.mean(fetch):8.0f} ({np.mean(fetch) * 2048 / 1e6:.0f} MB bf16 H=1024)")
+
+# the owner decomposition (DistillEngine owner mode): context pairs to the owner of the context
+# node, label pairs to the owner of their source (balanced, O.pair_owner_assign), anchors where
+# their pairs are; the student runs on the unique endpoints of the rank's pairs
+C = samples.shape[1] - 1
+pos_all = pairs[links].T
+print("owner decomposition (student rows = unique endpoints of the rank's pairs):")
+for R in (2, 4, 8):
+    per = []
+    for r in range(R):
+        cs, ps, ns = O.pair_owner_rank_items(samples, pos_all, neg, N, R, r)
+        b, c = cs // C, cs % C
+        ends = np.concatenate([samples[b, 0], samples[b, 1 + c], pos_all[0, ps], pos_all[1, ps], neg[0, ns],
+                               neg[1, ns]])
+        per.append(np.unique(ends).size)
+    print(f"R={R}: unique per rank {np.mean(per):9.0f} (max {max(per)}, min {min(per)}); "
+          f"pairs per rank {(B * C + 2 * P) / R:9.0f}")

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--agg-only", action="store_true",
                     help="every aggregate configuration (fp32 / bf16, F 128 / 256, fwd / bwd), 3 warm-up + --iters "
                          "launches each, in the printed order (rocprofv3 --pmc passes), then exit")
+    ap.add_argument("--no-agg", action="store_true", help="only the teacher step (kernel traces of it)")
     opt = ap.parse_args()
     if opt.agg_only:
         return agg_only(opt.iters)
@@ -74,7 +75,7 @@ def main():
     E = g.num_edges
     es = 4 if dt == torch.float32 else 2
     res = {"N": N, "E": E, "dtype": opt.dtype, "aggregate": []}
-    for F_ in (128, 256):
+    for F_ in (() if opt.no_agg else (128, 256)):
         x = torch.randn(N, F_, device=dev).to(dt)
         out = torch.empty(N, F_, device=dev, dtype=dt)
         for mode, (rp, cl, w) in (("fwd", (g.rowptr, g.col, None)), ("bwd", (g.rowptr_t, g.col_t, g.inv_deg))):
