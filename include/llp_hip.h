@@ -193,8 +193,8 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
 
 /* ---------------------------------------------------------------- multi-rank owner decomposition
  * The N-rank form of train_minibatch's pairs (src/main.py:86-130; the reference is single-GPU):
- * each predictor pair goes to exactly one rank, the owner of its key node (owner = node /
- * ceil(N / world)), balanced so that rank r gets cap_r = (r+1)n/world - rn/world pairs of each
+ * each predictor pair goes to exactly one rank, the owner of its key node (owner = owner_tab[node]
+ * in [0, world), or node / ceil(N / world) when owner_tab is NULL), balanced so that rank r gets cap_r = (r+1)n/world - rn/world pairs of each
  * category (an owner keeps its first cap_r pairs in item order; the owners' overflow, in
  * (owner, position) order, fills the ranks' free positions in rank order).  Category c's
  * ends: item i's node e[(i / kc) * kld + koff + (i % kc) * kstep] (a context pair (b, k): a = the
@@ -212,8 +212,8 @@ typedef struct llp_owner_cat {
 } llp_owner_cat;
 int64_t llp_pair_owner_workspace_bytes(int64_t n0, int64_t n1, int64_t n2, int world);
 int llp_pair_owner_assign(int ncat, const llp_owner_cat* cats, int64_t num_nodes, int world, int rank,
-                          int32_t* sel, int32_t* gpos, int32_t* target, int64_t R2, void* workspace,
-                          int64_t workspace_bytes, void* stream);
+                          const int32_t* owner_tab, int32_t* sel, int32_t* gpos, int32_t* target, int64_t R2,
+                          void* workspace, int64_t workspace_bytes, void* stream);
 /* s_full[i] = s_loc[gpos[i] - lo] if lo <= gpos[i] < hi else 0 (i < n), t likewise (either
  * output may be NULL): this rank's context logits placed into the [B*C] grid that one SUM
  * all-reduce completes (the other ranks' slots are zero here). */

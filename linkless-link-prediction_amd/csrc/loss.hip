@@ -17,14 +17,16 @@ constexpr int WAVES = 4;
 
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + expf(-z)); }
 
-// partial sums per block: [bce, kl, rank]
+// partial sums per block: [bce, kl, rank].  CMAX: the LDS row per wave (64 for C <= 64, the
+// collab / physics shapes: 2 KiB of LDS per block instead of 32 KiB, so a CU holds 8x the waves)
+template <int CMAX>
 __global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, const float* __restrict__ s_logit,
                                                          const float* __restrict__ t_prob, double B_total,
                                                          float margin, float T, float w_d, float w_r,
                                                          float loss_scale, float* __restrict__ dlogit,
                                                          float* __restrict__ partial, int64_t tb0, int64_t tb1) {
-  __shared__ float ss[WAVES][MAXC];
-  __shared__ float tt[WAVES][MAXC];
+  __shared__ float ss[WAVES][CMAX];
+  __shared__ float tt[WAVES][CMAX];
   __shared__ float red[WAVES][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * WAVES + w;
@@ -441,8 +443,12 @@ extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const fl
   const int64_t nbl = (n_lab + 255) / 256;
   if (nba > 0) {
     LLP_CHECK_ARG(s_logit && t_prob && dlogit_ctx, "llp_llp_loss: null context buffers");
-    hipLaunchKernelGGL(llp_anchor_kernel, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob, B_total,
-                       margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial, term_b0, term_b1);
+    if (C <= 64)
+      hipLaunchKernelGGL(llp_anchor_kernel<64>, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob, B_total,
+                         margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial, term_b0, term_b1);
+    else
+      hipLaunchKernelGGL(llp_anchor_kernel<MAXC>, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob,
+                         B_total, margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial, term_b0, term_b1);
     LLP_LAUNCH_CHECK();
   }
   if (nbl > 0) {

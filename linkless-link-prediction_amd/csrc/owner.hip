@@ -3,7 +3,8 @@
 //
 // The reference step is single-GPU.  Its N-rank form here gives every predictor pair to
 // one rank: a context pair (anchor b, context c) to the owner of the context node, a label
-// pair to the owner of its source node (owner = node / ceil(N / world)), balanced so that
+// pair to the owner of its source node (owner = owner_tab[node], a locality order's contiguous
+// ranges, or node / ceil(N / world)), balanced so that
 // rank r receives exactly cap_r = (r+1)n/W - rn/W pairs of each category: an owner keeps
 // its first cap pairs in item order, and the owners' overflow, ordered by (owner, rank in
 // the owner's list), fills the ranks' free positions in rank order.  A rank then runs the
@@ -12,16 +13,20 @@
 // pair_owner_assign is the same rule; the assignment is integer work and bit-exact.
 //
 // Three launches for up to three categories (context, positive, negative pairs):
-//   owner_hist_kernel    per 4,096-item block: items per owner
-//   owner_scan_kernel    one block: per-block offsets per owner, caps, overflow / free bases
+//   owner_hist_kernel    per 1,024-item block: items per owner (hist[owner][block])
+//   owner_scan_kernel    one block, a wave per (category, owner): per-block offsets, then the
+//                        caps, overflow and free-position bases
 //   owner_place_kernel   per item: (rank, position) -> sel / gpos, and this rank's pairs'
 //                        node ids into target = [ia | ib] (the student's rows)
+// Every thread loads its items' ends up front (four loads in flight), so a block is one
+// memory latency plus its ranking passes (collab, 603k items on 8 ranks: the round-4 first
+// version with 4,096-item blocks and one pass after another took 75 us for the three).
 #include "llp_common.h"
 
 namespace {
 
 constexpr int OW_T = 256;
-constexpr int OW_PASS = 16;                       // passes of 256 items per block
+constexpr int OW_PASS = 4;                        // passes of 256 items per block
 constexpr int OW_ITEMS = OW_T * OW_PASS;          // items per block
 constexpr int OW_MAXW = 64;
 
@@ -42,9 +47,10 @@ struct OwnerArgs {
   int64_t nblk;
   int64_t num_nodes, n_loc;
   int world, rank;
+  const int32_t* owner_tab;   // node -> owner rank, or NULL: node / ceil(N / world)
   int64_t R2;                 // this rank's pairs (all categories): target = [ia (R2) | ib (R2)]
-  int32_t* hist;              // [nblk][world] items per owner, then per-block offsets (in place)
-  int64_t* meta;              // [3][world][4]: cap, kept, overflow base, free base
+  int32_t* hist;              // [world][nblk] items per owner and block, then exclusive offsets (in place)
+  int64_t* meta;              // [3][OW_MAXW][4]: cap, kept, overflow base, free base
   int32_t* sel;               // [sum n]: rank r's items of category c at sel[sel0 + off_r ...]
   int32_t* gpos;              // [sum n] or NULL: item -> its slot in sel (minus sel0)
   int32_t* target;            // [2 R2] or NULL
@@ -56,9 +62,9 @@ __device__ __forceinline__ int32_t node_at(const int32_t* base, int64_t kc, int6
   return base[q * kld + koff + (i - q * kc) * kstep];
 }
 
-__device__ __forceinline__ int owner_of(int32_t v, int64_t n_loc, int world) {
-  const int64_t o = v < 0 ? 0 : (int64_t)v / n_loc;
-  return (int)(o < world ? o : world - 1);
+__device__ __forceinline__ int owner_of(const OwnerArgs& a, int32_t v) {
+  const int64_t o = v < 0 ? 0 : (a.owner_tab ? (int64_t)a.owner_tab[v] : (int64_t)v / a.n_loc);
+  return (int)(o < a.world ? o : a.world - 1);
 }
 
 __device__ __forceinline__ int cat_of_block(const OwnerArgs& a, int64_t blk) {
@@ -72,58 +78,64 @@ __global__ __launch_bounds__(OW_T) void owner_hist_kernel(OwnerArgs a) {
   const int64_t blk = blockIdx.x;
   const Cat& c = a.c[cat_of_block(a, blk)];
   if (threadIdx.x < a.world) cnt[threadIdx.x] = 0;
-  __syncthreads();
   const int64_t i0 = (blk - c.blk0) * OW_ITEMS;
-  for (int p = 0; p < OW_PASS; ++p) {
+  int32_t v[OW_PASS];
+#pragma unroll
+  for (int p = 0; p < OW_PASS; ++p) {   // all loads first
     const int64_t i = i0 + p * OW_T + threadIdx.x;
-    if (i < c.n) {
-      const int32_t v = c.key_b ? node_at(c.b, c.b_kc, c.b_kld, c.b_koff, c.b_kstep, i)
-                                : node_at(c.a, c.a_kc, c.a_kld, c.a_koff, c.a_kstep, i);
-      atomicAdd(&cnt[owner_of(v, a.n_loc, a.world)], 1);
-    }
+    v[p] = i < c.n ? (c.key_b ? node_at(c.b, c.b_kc, c.b_kld, c.b_koff, c.b_kstep, i)
+                              : node_at(c.a, c.a_kc, c.a_kld, c.a_koff, c.a_kstep, i))
+                   : -1;
   }
   __syncthreads();
-  if (threadIdx.x < a.world) a.hist[blk * a.world + threadIdx.x] = cnt[threadIdx.x];
+#pragma unroll
+  for (int p = 0; p < OW_PASS; ++p)
+    if (i0 + p * OW_T + threadIdx.x < c.n) atomicAdd(&cnt[owner_of(a, v[p])], 1);
+  __syncthreads();
+  if (threadIdx.x < a.world) a.hist[threadIdx.x * a.nblk + blk] = cnt[threadIdx.x];
 }
 
-// one block of 1024: for every (category, owner) an exclusive scan of the per-block counts
-// over the category's blocks (in place), then the balancing bases on thread 0
+// one block of 1024 threads, one wave per (category, owner) sequence of per-block counts: an
+// exclusive scan in place (256 counts per round, four per lane), then thread 0 derives the
+// balancing bases from the totals
 __global__ __launch_bounds__(1024) void owner_scan_kernel(OwnerArgs a) {
-  __shared__ int32_t wsum[16];
   __shared__ int64_t tot[3][OW_MAXW];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  for (int ci = 0; ci < a.ncat; ++ci) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int npair = a.ncat * a.world;
+  for (int q = wv; q < npair; q += 16) {
+    const int ci = q / a.world, o = q % a.world;
     const Cat& c = a.c[ci];
     const int64_t nb = (c.n + OW_ITEMS - 1) / OW_ITEMS;
-    for (int o = 0; o < a.world; ++o) {
-      int64_t carry = 0;
-      for (int64_t j0 = 0; j0 < nb; j0 += 1024) {
-        const int64_t j = j0 + t;
-        int32_t* p = a.hist + (c.blk0 + j) * a.world + o;
-        const int32_t v = j < nb ? *p : 0;
-        // inclusive wave scan
-        int32_t x = v;
+    int32_t* h = a.hist + (int64_t)o * a.nblk + c.blk0;
+    int64_t carry = 0;
+    for (int64_t j0 = 0; j0 < nb; j0 += 256) {
+      int32_t x[4];
+      int32_t s = 0;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const int32_t y = __shfl_up(x, d, 64);
-          if (lane >= d) x += y;
-        }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        int32_t before = 0, all = 0;
-        for (int k = 0; k < 16; ++k) {
-          before += k < w ? wsum[k] : 0;
-          all += wsum[k];
-        }
-        if (j < nb) *p = (int32_t)(carry + before + x - v);   // exclusive offset of block j
-        carry += all;
-        __syncthreads();
+      for (int k = 0; k < 4; ++k) {
+        const int64_t j = j0 + 4 * lane + k;
+        x[k] = j < nb ? h[j] : 0;
+        s += x[k];
       }
-      if (t == 0) tot[ci][o] = carry;
+      int32_t inc = s;   // inclusive scan of the lanes' sums
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+      }
+      int64_t run = carry + inc - s;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t j = j0 + 4 * lane + k;
+        if (j < nb) h[j] = (int32_t)run;
+        run += x[k];
+      }
+      carry += __shfl(inc, 63, 64);
     }
+    if (lane == 0) tot[ci][o] = carry;
   }
   __syncthreads();
-  if (t == 0) {
+  if (threadIdx.x == 0) {
     for (int ci = 0; ci < a.ncat; ++ci) {
       const int64_t n = a.c[ci].n, W = a.world;
       int64_t ov = 0, fr = 0;
@@ -148,24 +160,27 @@ __global__ __launch_bounds__(OW_T) void owner_place_kernel(OwnerArgs a) {
   const Cat& c = a.c[ci];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int W = a.world;
+  const int64_t i0 = (blk - c.blk0) * OW_ITEMS;
+  int32_t va[OW_PASS], vb[OW_PASS];
+#pragma unroll
+  for (int p = 0; p < OW_PASS; ++p) {   // all loads first
+    const int64_t i = i0 + p * OW_T + t;
+    const bool live = i < c.n;
+    va[p] = live ? node_at(c.a, c.a_kc, c.a_kld, c.a_koff, c.a_kstep, i) : 0;
+    vb[p] = live ? node_at(c.b, c.b_kc, c.b_kld, c.b_koff, c.b_kstep, i) : 0;
+  }
   if (t < W) {
-    base[t] = a.hist[blk * W + t];
+    base[t] = a.hist[(int64_t)t * a.nblk + blk];
 #pragma unroll
     for (int k = 0; k < 4; ++k) meta[t][k] = a.meta[((int64_t)ci * OW_MAXW + t) * 4 + k];
   }
   __syncthreads();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t i0 = (blk - c.blk0) * OW_ITEMS;
+#pragma unroll
   for (int p = 0; p < OW_PASS; ++p) {
     const int64_t i = i0 + p * OW_T + t;
     const bool live = i < c.n;
-    int32_t va = 0, vb = 0;
-    int o = -1;
-    if (live) {
-      va = node_at(c.a, c.a_kc, c.a_kld, c.a_koff, c.a_kstep, i);
-      vb = node_at(c.b, c.b_kc, c.b_kld, c.b_koff, c.b_kstep, i);
-      o = owner_of(c.key_b ? vb : va, a.n_loc, W);
-    }
+    const int o = live ? owner_of(a, c.key_b ? vb[p] : va[p]) : -1;
     // rank among this pass's items of the same owner: lanes below in the wave, then earlier waves
     int in_wave = 0;
     for (int q = 0; q < W; ++q) {
@@ -194,8 +209,8 @@ __global__ __launch_bounds__(OW_T) void owner_place_kernel(OwnerArgs a) {
       if (a.gpos) a.gpos[c.sel0 + i] = (int32_t)(off + pos);
       if (a.target && r == a.rank) {
         const int64_t k = c.row0 + pos;
-        a.target[k] = va;
-        a.target[a.R2 + k] = vb;
+        a.target[k] = va[p];
+        a.target[a.R2 + k] = vb[p];
       }
     }
     __syncthreads();
@@ -229,8 +244,8 @@ extern "C" int64_t llp_pair_owner_workspace_bytes(int64_t n0, int64_t n1, int64_
 }
 
 extern "C" int llp_pair_owner_assign(int ncat, const llp_owner_cat* cats, int64_t num_nodes, int world, int rank,
-                                     int32_t* sel, int32_t* gpos, int32_t* target, int64_t R2, void* workspace,
-                                     int64_t workspace_bytes, void* stream) {
+                                     const int32_t* owner_tab, int32_t* sel, int32_t* gpos, int32_t* target,
+                                     int64_t R2, void* workspace, int64_t workspace_bytes, void* stream) {
   LLP_CHECK_ARG(ncat >= 1 && ncat <= 3 && cats, "llp_pair_owner_assign: 1..3 categories");
   LLP_CHECK_ARG(world >= 1 && world <= OW_MAXW && rank >= 0 && rank < world,
                 "llp_pair_owner_assign: world %d (1..%d), rank %d", world, OW_MAXW, rank);
@@ -241,6 +256,7 @@ extern "C" int llp_pair_owner_assign(int ncat, const llp_owner_cat* cats, int64_
   a.n_loc = (num_nodes + world - 1) / world;
   a.world = world;
   a.rank = rank;
+  a.owner_tab = owner_tab;
   a.R2 = R2;
   int64_t blk = 0, sel0 = 0, row0 = 0, n[3] = {0, 0, 0};
   for (int i = 0; i < ncat; ++i) {

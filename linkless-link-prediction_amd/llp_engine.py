@@ -661,7 +661,7 @@ class DistillEngine(EngineBase):
 
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
                  dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, shard_student=True,
-                 owner_pairs=True):
+                 owner_pairs=True, owner_locality=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
         # run the dropout-free student on unique nodes (step_minibatch); the unique
         # count stays on the device, so this path is hipGraph-capturable too
@@ -670,8 +670,10 @@ class DistillEngine(EngineBase):
         # (_fb_shard); rank 0 of 4 on coauthor-physics 0.94 -> 0.81 ms (first
         # table: tools/physics_bench.py --emulate-ranks 4 with and without --replicated)
         self.shard_student = bool(shard_student)
-        # multi-rank minibatch step: the owner decomposition (minibatch_owner)
+        # multi-rank minibatch step: the owner decomposition (minibatch_owner), node
+        # ownership by a locality order of the graph (_owner_table) or by id ranges
         self.owner_pairs = bool(owner_pairs)
+        self.owner_locality = bool(owner_locality)
         self._rows_dev = None      # int32 device count of the unique-node student (last step), or None
         self._rows_host = 0
         self.args = args
@@ -973,9 +975,28 @@ class DistillEngine(EngineBase):
         gpos = self._buf("owner_gpos", (max(n_all, 1),), torch.int32)
         rows = self._buf("owner_rows", (max(2 * R2, 1),), torch.int32)[:2 * R2]
         ws = self._buf("owner_ws", (K.pair_owner_ws_bytes(ns, world) // 4 + 16,), torch.int32)
-        K.pair_owner_assign(cats, self.N, world, rank, sel, ws, gpos=gpos, target=rows, R2=R2)
+        K.pair_owner_assign(cats, self.N, world, rank, sel, ws, gpos=gpos, target=rows, R2=R2,
+                            owner_tab=self._owner_table(world))
         return {"R2": R2, "ctx": caps[0], "pos": caps[1], "neg": caps[2], "rows": rows, "sel": sel,
                 "gpos": gpos, "ctx_lo": rank * ns[0] // world}
+
+    def _owner_table(self, world):
+        """Node -> owner rank for the owner decomposition (``owner_locality``): contiguous ranges
+        of a locality order of the sampler graph (llp_sage.locality_order, label propagation),
+        so a positive label pair's two ends and a walk's contexts mostly have one owner and a
+        rank's pairs reach fewer foreign nodes; None: contiguous ranges of node ids.  Host
+        work once per engine (the same on every rank: deterministic)."""
+        if not self.owner_locality:
+            return None
+        key = ("owner_tab", int(world))
+        if key not in self._bufs:
+            if getattr(self, "_locality_pi", None) is None:
+                import llp_sage
+                r, c = self._neg_rc
+                self._locality_pi = llp_sage.locality_order(np.stack([np.asarray(r), np.asarray(c)]), self.N)[1]
+            tab = (self._locality_pi * int(world)) // self.N
+            self._bufs[key] = torch.from_numpy(tab.astype(np.int32)).to(self.dev)
+        return self._bufs[key]
 
     def _student_forward(self, rows_s, gather_s, n_u, p_drop, R1_total, kernel_events=None):
         """Student MLP over x[gather_s] (src/models.py:45-54), rows_s rows (n_u: device row

@@ -70,7 +70,8 @@ _SIGS = {
                              c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64, c_vp, c_i64,
                              c_vp]),
     "llp_pair_owner_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_int]),
-    "llp_pair_owner_assign": (c_int, [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "llp_pair_owner_assign": (c_int, [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                      c_vp]),
     "llp_pair_owner_scatter": (c_int, [c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
@@ -336,13 +337,14 @@ def pair_owner_ws_bytes(ns, world):
     return load().llp_pair_owner_workspace_bytes(ns[0], ns[1], ns[2], int(world))
 
 
-def pair_owner_assign(cats, num_nodes, world, rank, sel, ws, gpos=None, target=None, R2=0):
+def pair_owner_assign(cats, num_nodes, world, rank, sel, ws, gpos=None, target=None, R2=0, owner_tab=None):
     """llp_pair_owner_assign over 1-3 OwnerCat categories: sel (int32[sum n]) holds rank r's items
     of each category at [cat base + r n / world, ...); gpos (int32[sum n], optional) item -> slot;
-    target (int32[2 R2], optional) = this rank's pairs' [a ends | b ends] in its order."""
+    target (int32[2 R2], optional) = this rank's pairs' [a ends | b ends] in its order;
+    owner_tab (int32[N], optional): node -> owner rank (default node // ceil(N / world))."""
     arr = (OwnerCat * len(cats))(*cats)
     check(lib().llp_pair_owner_assign(len(cats), C.cast(arr, c_vp), int(num_nodes), int(world), int(rank),
-                                      sel.data_ptr(), ptr(gpos), ptr(target), int(R2), ws.data_ptr(),
+                                      ptr(owner_tab), sel.data_ptr(), ptr(gpos), ptr(target), int(R2), ws.data_ptr(),
                                       ws.numel() * ws.element_size(), stream_ptr()),
           "llp_pair_owner_assign")
 

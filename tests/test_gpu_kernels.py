@@ -1041,12 +1041,16 @@ def _owner_case(seed, N, B, C, P, n_neg, skew):
                                            (50, 3, 2, 0, 7), (10, 1, 1, 1, 0)])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("skew", [False, True])
-def test_pair_owner_assign_matches_oracle(N, B, C, P, n_neg, world, skew):
+@pytest.mark.parametrize("table", [False, True])
+def test_pair_owner_assign_matches_oracle(N, B, C, P, n_neg, world, skew, table):
     """llp_pair_owner_assign == oracle pair_owner_assign for the three categories of one
     minibatch (context pairs keyed by the context node, label pairs by their source): sel,
-    gpos and every rank's [ia | ib] rows, at the collab shape and small / skewed cases."""
+    gpos and every rank's [ia | ib] rows, at the collab shape and small / skewed cases, with
+    owners by id ranges or by a node -> owner table (DistillEngine's locality ownership)."""
     k = K()
     samples, pos, neg = _owner_case(B * 7 + world, N, B, C, P, n_neg, skew)
+    tab = np.random.default_rng(N + world).integers(0, world, N).astype(np.int32) if table else None
+    tab_d = torch.from_numpy(tab).to(DEV) if table else None
     C1 = C + 1
     n_lab = P + n_neg
     # the whole batch's this_target layout: samples.flat | src | dst (src/main.py:95)
@@ -1065,14 +1069,14 @@ def test_pair_owner_assign_matches_oracle(N, B, C, P, n_neg, world, skew):
         gpos = torch.full((max(n_all, 1),), -7, dtype=torch.int32, device=DEV)
         rows = torch.full((max(2 * R2, 1),), -7, dtype=torch.int32, device=DEV)
         ws = torch.empty(k.pair_owner_ws_bytes(ns, world) // 4 + 16, dtype=torch.int32, device=DEV)
-        k.pair_owner_assign(cats, N, world, rank, sel, ws, gpos=gpos, target=rows, R2=R2)
+        k.pair_owner_assign(cats, N, world, rank, sel, ws, gpos=gpos, target=rows, R2=R2, owner_tab=tab_d)
         sel_h, gpos_h, rows_h = sel.cpu().numpy(), gpos.cpu().numpy(), rows.cpu().numpy()
         base = 0
         ia, ib = [], []
         keys = (samples[:, 1:].reshape(-1), pos[0], neg[0])
         ends = ((np.repeat(samples[:, 0], C), samples[:, 1:].reshape(-1)), (pos[0], pos[1]), (neg[0], neg[1]))
         for key, n, (ea, eb) in zip(keys, ns, ends):
-            ref, off = O.pair_owner_assign(key, N, world)
+            ref, off = O.pair_owner_assign(key, N, world, tab)
             assert np.array_equal(sel_h[base:base + n], ref)
             inv = np.empty(n, np.int64)
             inv[ref] = np.arange(n)

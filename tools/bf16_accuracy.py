@@ -24,6 +24,7 @@ for _p in (REPO, PKG):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 KS = (10, 20, 50, 100)
@@ -102,6 +103,26 @@ def compare(scale=0.1, link_batch=8192, epochs=8, seed=0, hidden=1024, eval_ever
             "epochs": epochs, "runs": runs, "final": last, "bf16_minus_fp32": diff}
 
 
+def paired(runs, k="Hits@20", last=3):
+    """Paired bf16 - fp32 difference of Hits@K (percentage points) per seed: each run's value is
+    the mean of its last ``last`` checkpoints; returns per split the per-seed differences, their
+    mean, the standard error of the mean, and the fp32 runs' own seed-to-seed SD."""
+    out = {}
+    for split in ("valid", "test"):
+        d, f = [], []
+        for r in runs:
+            v = {dt: 100 * float(np.mean([h["hits"][k][split] for h in r["runs"][dt]["history"][-last:]]))
+                 for dt in ("fp32", "bf16")}
+            d.append(v["bf16"] - v["fp32"])
+            f.append(v["fp32"])
+        d = np.asarray(d)
+        se = float(d.std(ddof=1) / np.sqrt(d.size)) if d.size > 1 else float("nan")
+        out[split] = {"diff_pp": d.tolist(), "mean_pp": float(d.mean()), "se_pp": se,
+                      "bound_pp": abs(float(d.mean())) + 2 * se, "fp32_mean_pp": float(np.mean(f)),
+                      "fp32_seed_sd_pp": float(np.std(f, ddof=1)) if len(f) > 1 else float("nan"), "seeds": len(runs)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=0.1)
@@ -111,11 +132,17 @@ def main():
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--eval-every", type=int, default=1)
     ap.add_argument("--communities", type=int, default=None)
+    ap.add_argument("--last", type=int, default=3, help="checkpoints averaged per run in the paired summary")
     opt = ap.parse_args()
+    runs = []
     for s in range(opt.seeds):
         r = compare(opt.scale, opt.link_batch, opt.epochs, seed=s, hidden=opt.hidden, eval_every=opt.eval_every,
                     communities=opt.communities)
+        runs.append(r)
         print(json.dumps(r), flush=True)
+    summary = {k: paired(runs, k, opt.last) for k in ("Hits@20", "Hits@50")}
+    print(json.dumps({"paired_bf16_minus_fp32": summary, "scale": opt.scale, "epochs": opt.epochs,
+                      "eval_every": opt.eval_every, "last_checkpoints": opt.last}), flush=True)
 
 
 if __name__ == "__main__":

@@ -19,14 +19,16 @@ PROF="rocprofv3 --kernel-trace --stats --output-format csv"
 
 fail() { echo "step failed: $1"; tail -30 "$2"; exit 1; }
 
-for R in "$@"; do
-  echo "== $R"
+for RA in "$@"; do
+  R=${RA%%:*}                                 # RECIPE or RECIPE:ARGS (ARGS comma-separated)
+  ARGS=$([ "$R" != "$RA" ] && echo "${RA#*:}" | tr ',' ' ')
+  echo "== $RA"
   case $R in
     tests)          # the whole GPU suite
       timeout -k 10 900 $PYT tests -m gpu -q > $O/pytest_gpu.log 2>&1 || fail tests $O/pytest_gpu.log
       tail -1 $O/pytest_gpu.log ;;
-    tests-sel)      # a selection: TESTS="tests/x.py -k y"
-      timeout -k 10 900 $PYT $TESTS -m gpu > $O/pytest_sel.log 2>&1 || fail tests-sel $O/pytest_sel.log
+    tests-sel)      # a selection: tests-sel:tests/x.py::test_a,tests/y.py
+      timeout -k 10 900 $PYT $ARGS -m gpu > $O/pytest_sel.log 2>&1 || fail tests-sel $O/pytest_sel.log
       tail -1 $O/pytest_sel.log ;;
     tests-multirank)
       timeout -k 10 900 $PYT tests/test_gpu_multirank.py -q > $O/pytest_multirank.log 2>&1 || fail multirank $O/pytest_multirank.log
@@ -57,6 +59,9 @@ for R in "$@"; do
       D="python bench.py --dominant-only 6 $F32"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/fp32_pmc_fetch -o p --output-format csv -- $D > $O/fp32_pmc_fetch.log 2>&1 || fail fp32-fetch $O/fp32_pmc_fetch.log
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/fp32_pmc_write -o p --output-format csv -- $D > $O/fp32_pmc_write.log 2>&1 || fail fp32-write $O/fp32_pmc_write.log ;;
+    fp32-sq)        # SQ / GRBM counters of the dominant fp32 GEMM (MFMA busy, waits, LDS)
+      D="python bench.py --dominant-only 6 --dtype fp32 $LEAN --no-practical-peak"
+      timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d $O/fp32_pmc_sq -o p --output-format csv -- $D > $O/fp32_pmc_sq.log 2>&1 || fail fp32-sq $O/fp32_pmc_sq.log ;;
     teacher)        # kernel trace of the SAGE teacher step (a11-a13) at the collab shape, bf16 and fp32
       for dt in bf16 fp32; do
         timeout -k 10 300 python tools/sage_bench.py --no-agg --dtype $dt --steps 10 > $O/teacher_$dt.json 2> $O/teacher_$dt.err || fail teacher-$dt $O/teacher_$dt.err
@@ -88,8 +93,11 @@ for R in "$@"; do
       timeout -k 10 300 python tools/physics_bench.py --steps 20 --dtype bf16 > $O/phys1.json 2> $O/phys1.err || fail phys1 $O/phys1.err
       timeout -k 10 300 python tools/physics_bench.py --steps 20 --dtype bf16 --emulate-ranks 4 > $O/phys4.json 2> $O/phys4.err || fail phys4 $O/phys4.err
       cat $O/phys1.json $O/phys4.json
-      timeout -k 10 300 $PROF -d $O/phys_t1 -o t -- python tools/physics_bench.py --steps 10 --dtype bf16 > $O/phys_t1.log 2>&1 || fail phys-t1 $O/phys_t1.log
-      timeout -k 10 300 $PROF -d $O/phys_t4 -o t -- python tools/physics_bench.py --steps 10 --dtype bf16 --emulate-ranks 4 > $O/phys_t4.log 2>&1 || fail phys-t4 $O/phys_t4.log ;;
+      timeout -k 10 300 python tools/physics_bench.py --steps 20 --dtype bf16 --graph > $O/phys1g.json 2> $O/phys1g.err || fail phys1g $O/phys1g.err
+      timeout -k 10 300 python tools/physics_bench.py --steps 20 --dtype bf16 --emulate-ranks 4 --graph > $O/phys4g.json 2> $O/phys4g.err || fail phys4g $O/phys4g.err
+      cat $O/phys1g.json $O/phys4g.json
+      timeout -k 10 300 $PROF -d $O/phys_t1 -o t -- python tools/physics_bench.py --steps 10 --dtype bf16 --graph > $O/phys_t1.log 2>&1 || fail phys-t1 $O/phys_t1.log
+      timeout -k 10 300 $PROF -d $O/phys_t4 -o t -- python tools/physics_bench.py --steps 10 --dtype bf16 --emulate-ranks 4 --graph > $O/phys_t4.log 2>&1 || fail phys-t4 $O/phys_t4.log ;;
     bf16-accuracy)  # paired bf16 - fp32 Hits@K over seeds (tools/bf16_accuracy.py)
       timeout -k 10 1000 python tools/bf16_accuracy.py ${ACC_ARGS:-} > $O/bf16_accuracy.jsonl 2> $O/bf16_accuracy.err || fail bf16-accuracy $O/bf16_accuracy.err
       tail -5 $O/bf16_accuracy.jsonl ;;

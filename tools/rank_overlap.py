@@ -71,3 +71,18 @@ for R in (2, 4, 8):
         per.append(np.unique(ends).size)
     print(f"R={R}: unique per rank {np.mean(per):9.0f} (max {max(per)}, min {min(per)}); "
           f"pairs per rank {(B * C + 2 * P) / R:9.0f}")
+
+# the same with node ownership by a locality order (DistillEngine owner_locality: label propagation)
+import llp_sage  # noqa: E402
+_, pi = llp_sage.locality_order(ei, N)
+print("owner decomposition, ownership by the locality order:")
+for R in (2, 4, 8):
+    tab = (pi * R) // N
+    per = []
+    for r in range(R):
+        cs, ps, ns = O.pair_owner_rank_items(samples, pos_all, neg, N, R, r, owner_tab=tab)
+        b, c = cs // C, cs % C
+        ends = np.concatenate([samples[b, 0], samples[b, 1 + c], pos_all[0, ps], pos_all[1, ps], neg[0, ns],
+                               neg[1, ns]])
+        per.append(np.unique(ends).size)
+    print(f"R={R}: unique per rank {np.mean(per):9.0f} (max {max(per)}, min {min(per)})")
