@@ -191,6 +191,30 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
  * (zero gradient, no loss), and the BCE mean runs over pos_total + *neg_count labels
  * (n_lab_total unused). */
 
+/* llp_llp_loss in ONE launch, with the Linear(H, 1) heads finished inside it
+ * (llp_head_finish's fixed-order sum: bit-identical logits).  s_head (may be NULL): the
+ * student predictor's gemm_nt_head partials over its B*C + n_lab rows (contexts, then labels):
+ * logit of row m = *bias + sum_t part[t * ld + m], written to s_logit[m] (m < B*C) and
+ * out_logit[m - B*C]; NULL: the logits are read from those buffers.  t_head (may be NULL):
+ * the teacher predictor's partials over the B*C context rows; t_prob[m] = sigmoid(logit),
+ * written.  ticket (may be NULL: a separate finalize launch follows): one uint32, zero
+ * before the first call; the workgroup that arrives last on it sums the partials of
+ * terms_out and returns it to zero.  Replaces src/main.py:103-130 (head, sigmoid, losses). */
+typedef struct llp_head_parts {
+  const float* part;   /* [parts][ld] f32 */
+  const float* bias;   /* [1] or NULL */
+  int64_t parts, ld;
+} llp_head_parts;
+int llp_llp_loss_heads(int64_t B, int64_t C, float* s_logit, float* t_prob,
+                       int64_t n_lab, int64_t n_pos, float* out_logit,
+                       double B_total, double n_lab_total, float margin, float T,
+                       float w_label, float w_d, float w_r, float loss_scale,
+                       float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
+                       const int32_t* neg_count, int64_t neg_offset, double pos_total,
+                       int64_t term_b0, int64_t term_b1,
+                       const llp_head_parts* s_head, const llp_head_parts* t_head, uint32_t* ticket,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- multi-rank owner decomposition
  * The N-rank form of train_minibatch's pairs (src/main.py:86-130; the reference is single-GPU):
  * each predictor pair goes to exactly one rank, the owner of its key node (owner = owner_tab[node]
@@ -461,6 +485,16 @@ int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64_t max_nume
 int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
                   float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
                   void* stream);
+/* The same two calls in ONE launch each (ticket: one uint32, zero before the first call,
+ * returned to zero by each call; NULL = the two-launch forms above): the gradient norm's
+ * finalize runs in the last workgroup to arrive, and Adam writes both shadows in its own
+ * pass (transposed ones through 32 x 32 LDS tiles) with the step counter advanced by its
+ * last workgroup.  Results bit-identical to the two-launch forms. */
+int llp_grad_sumsq_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
+                     float* sumsq, uint32_t* ticket, void* workspace, int64_t workspace_bytes, void* stream);
+int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
+                    float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
+                    uint32_t* ticket, void* stream);
 /* Refresh bf16 shadows from masters (after loading weights). */
 int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream);
 

@@ -302,9 +302,38 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* 
   if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors,
-                                                           int64_t max_chunks, const float* __restrict__ partial,
-                                                           int n_groups, float* __restrict__ sumsq) {
+// One workgroup's agent-scope arrival on a launch's ticket (cdna_hip_programming.md §5 "In-launch
+// split-K reduction"): every store of this workgroup that the last arriver reads was made by
+// thread 0 (drained and released here); true in the LAST workgroup to arrive, which has acquired
+// and returned the ticket to zero.  Called by every thread.
+__device__ __forceinline__ bool arrive_last(uint32_t* ticket, uint32_t n_blocks) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == n_blocks - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// a value another workgroup of this launch stored: a vector load behind the acquire
+__device__ __forceinline__ float load_handed(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <bool HANDOFF>
+__device__ __forceinline__ void grad_sumsq_finalize_block(const llp_tensor_desc* __restrict__ descs, int n_tensors,
+                                                          int64_t max_chunks, const float* partial, int n_groups,
+                                                          float* __restrict__ sumsq) {
   // one block, one pass: thread i sums (in double) the chunk partials i, i+256, ... of
   // every tensor into its group's register, then a fixed LDS tree per group
   // (deterministic; was one block-wide reduction per tensor)
@@ -314,7 +343,8 @@ __global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc
     const int gidx = descs[t].group;
     const int64_t nch = (descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK;
     double ts = 0.0;
-    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) ts += (double)partial[t * max_chunks + c];
+    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x)
+      ts += (double)(HANDOFF ? load_handed(partial + t * max_chunks + c) : partial[t * max_chunks + c]);
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (k == gidx) gs[k] += ts;
@@ -329,6 +359,36 @@ __global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc
     __syncthreads();
   }
   if ((int)threadIdx.x < n_groups) sumsq[threadIdx.x] = (float)red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors,
+                                                           int64_t max_chunks, const float* __restrict__ partial,
+                                                           int n_groups, float* __restrict__ sumsq) {
+  grad_sumsq_finalize_block<false>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
+}
+
+// grad_sumsq_kernel with the finalize in the launch's last workgroup (ticket: zero, left zero)
+__global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_desc* __restrict__ descs,
+                                                               int n_tensors, int64_t max_chunks, float* partial,
+                                                               int n_groups, float* __restrict__ sumsq,
+                                                               uint32_t* ticket) {
+  __shared__ float red[4];
+  const llp_tensor_desc d = descs[blockIdx.y];
+  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
+  float acc = 0.f;
+  if (e0 < d.numel) {
+    const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      const float g = d.grad[e];
+      acc += g * g;
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (arrive_last(ticket, gridDim.x * gridDim.y))
+    grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
 __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float beta1, float beta2, float eps,
@@ -437,6 +497,142 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
     }
     __syncthreads();
   }
+}
+
+// adam_kernel and shadow_t_kernel in one launch.  A tensor with a transposed shadow is walked
+// in 32 x 32 tiles (thread t: row t / 8, columns 4 (t % 8) ..): Adam per element exactly as
+// adam_kernel, the row-major shadow written from registers and the transposed one through an
+// LDS tile; other tensors take adam_kernel's 1,024-element chunks.  Grid-strided over each
+// tensor's tiles / chunks.  The Adam step counter is advanced by the launch's last workgroup
+// (every workgroup has read it before its ticket add; ticket zero on entry, left zero).
+__global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* __restrict__ descs,
+                                                         const float* __restrict__ sumsq, float max_norm, float lr,
+                                                         float beta1, float beta2, float eps, int64_t* step,
+                                                         uint32_t* ticket) {
+  __shared__ float tile[32][33];
+  const llp_tensor_desc d = descs[blockIdx.y];
+  float coef = 1.f;
+  if (sumsq) {
+    const float total = sqrtf(sumsq[d.group]);
+    const float q = max_norm / (total + 1e-6f);
+    coef = (q != q) ? q : fminf(q, 1.f);
+  }
+  const double tt = (double)(*step + 1);
+  const float bc1 = (float)(1.0 - pow((double)beta1, tt));
+  const float bc2s = (float)sqrt(1.0 - pow((double)beta2, tt));
+  const float step_size = lr / bc1;
+  if (d.shadow_t) {
+    const int64_t rows = d.rows, cols = d.cols;
+    const int64_t ldt = d.shadow_t_ld ? d.shadow_t_ld : rows;
+    const int64_t tr = (rows + 31) / 32, tc = (cols + 31) / 32;
+    const int r = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;
+    const bool vec = (cols & 3) == 0 &&
+                     ((((uintptr_t)d.grad) | ((uintptr_t)d.exp_avg) | ((uintptr_t)d.exp_avg_sq) | ((uintptr_t)d.param)) &
+                      15) == 0;
+    for (int64_t ti = blockIdx.x; ti < tr * tc; ti += gridDim.x) {
+      const int64_t r0 = (ti / tc) * 32, c0 = (ti % tc) * 32;
+      const int64_t gr = r0 + r, gc = c0 + c4;
+      float pv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (gr < rows) {
+        const int64_t e = gr * cols + gc;
+        if (vec && gc + 3 < cols) {
+          float4 g = *reinterpret_cast<const float4*>(d.grad + e);
+          if (coef != 1.f) {
+            g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
+            *reinterpret_cast<float4*>(d.grad + e) = g;
+          }
+          float4 m = *reinterpret_cast<const float4*>(d.exp_avg + e);
+          float4 v = *reinterpret_cast<const float4*>(d.exp_avg_sq + e);
+          float4 p = *reinterpret_cast<const float4*>(d.param + e);
+          p.x = adam_elem(g.x, m.x, v.x, p.x, beta1, beta2, eps, bc2s, step_size);
+          p.y = adam_elem(g.y, m.y, v.y, p.y, beta1, beta2, eps, bc2s, step_size);
+          p.z = adam_elem(g.z, m.z, v.z, p.z, beta1, beta2, eps, bc2s, step_size);
+          p.w = adam_elem(g.w, m.w, v.w, p.w, beta1, beta2, eps, bc2s, step_size);
+          *reinterpret_cast<float4*>(d.exp_avg + e) = m;
+          *reinterpret_cast<float4*>(d.exp_avg_sq + e) = v;
+          *reinterpret_cast<float4*>(d.param + e) = p;
+          pv[0] = p.x; pv[1] = p.y; pv[2] = p.z; pv[3] = p.w;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (gc + i >= cols) break;
+            const float g = d.grad[e + i] * coef;
+            if (coef != 1.f) d.grad[e + i] = g;
+            float m = d.exp_avg[e + i], v = d.exp_avg_sq[e + i];
+            pv[i] = adam_elem(g, m, v, d.param[e + i], beta1, beta2, eps, bc2s, step_size);
+            d.exp_avg[e + i] = m;
+            d.exp_avg_sq[e + i] = v;
+            d.param[e + i] = pv[i];
+          }
+        }
+        if (d.shadow) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (gc + i < cols) put_elem(d.shadow, shadow_index(d, e + i), pv[i], d.shadow_dtype);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tile[r][c4 + i] = pv[i];
+      __syncthreads();
+      // transposed: thread t writes shadow_t row c0 + t / 8, columns r0 + 4 (t % 8) ..
+      const int64_t oc = c0 + r;
+      if (oc < cols) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (r0 + c4 + i < rows) put_elem(d.shadow_t, oc * ldt + r0 + c4 + i, tile[c4 + i][r], d.shadow_dtype);
+      }
+      __syncthreads();
+    }
+  } else {
+    const bool vec = ((d.numel & 3) == 0) &&
+                     ((((uintptr_t)d.grad) | ((uintptr_t)d.exp_avg) | ((uintptr_t)d.exp_avg_sq) | ((uintptr_t)d.param) |
+                       (d.shadow ? (uintptr_t)d.shadow : 0)) & 15) == 0 &&
+                     (d.shadow_ld == 0 || d.shadow_ld == d.cols);
+    for (int64_t e0 = (int64_t)blockIdx.x * ADAM_CHUNK; e0 < d.numel; e0 += (int64_t)gridDim.x * ADAM_CHUNK) {
+      const int64_t e1 = min(d.numel, e0 + ADAM_CHUNK);
+      if (vec) {
+        for (int64_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
+          float4 g = *reinterpret_cast<const float4*>(d.grad + e);
+          if (coef != 1.f) {
+            g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
+            *reinterpret_cast<float4*>(d.grad + e) = g;
+          }
+          float4 m = *reinterpret_cast<const float4*>(d.exp_avg + e);
+          float4 v = *reinterpret_cast<const float4*>(d.exp_avg_sq + e);
+          float4 p = *reinterpret_cast<const float4*>(d.param + e);
+          p.x = adam_elem(g.x, m.x, v.x, p.x, beta1, beta2, eps, bc2s, step_size);
+          p.y = adam_elem(g.y, m.y, v.y, p.y, beta1, beta2, eps, bc2s, step_size);
+          p.z = adam_elem(g.z, m.z, v.z, p.z, beta1, beta2, eps, bc2s, step_size);
+          p.w = adam_elem(g.w, m.w, v.w, p.w, beta1, beta2, eps, bc2s, step_size);
+          *reinterpret_cast<float4*>(d.exp_avg + e) = m;
+          *reinterpret_cast<float4*>(d.exp_avg_sq + e) = v;
+          *reinterpret_cast<float4*>(d.param + e) = p;
+          if (d.shadow) {
+            if (d.shadow_dtype == LLP_BF16) {
+              uint2 o;
+              o.x = (uint32_t)f2bf(p.x) | ((uint32_t)f2bf(p.y) << 16);
+              o.y = (uint32_t)f2bf(p.z) | ((uint32_t)f2bf(p.w) << 16);
+              *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(d.shadow) + e) = o;
+            } else {
+              *reinterpret_cast<float4*>(reinterpret_cast<float*>(d.shadow) + e) = p;
+            }
+          }
+        }
+      } else {
+        for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+          const float g = d.grad[e] * coef;
+          if (coef != 1.f) d.grad[e] = g;
+          float m = d.exp_avg[e], v = d.exp_avg_sq[e];
+          const float pnew = adam_elem(g, m, v, d.param[e], beta1, beta2, eps, bc2s, step_size);
+          d.exp_avg[e] = m;
+          d.exp_avg_sq[e] = v;
+          d.param[e] = pnew;
+          if (d.shadow) put_elem(d.shadow, shadow_index(d, e), pnew, d.shadow_dtype);
+        }
+      }
+    }
+  }
+  if (arrive_last(ticket, gridDim.x * gridDim.y) && threadIdx.x == 0) *step += 1;
 }
 
 __global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __restrict__ descs) {
@@ -569,8 +765,9 @@ extern "C" int64_t llp_grad_sumsq_workspace_bytes(int n_tensors, int64_t max_num
   return (int64_t)n_tensors * max_chunks_of(max_numel) * (int64_t)sizeof(float);
 }
 
-extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
-                              float* sumsq, void* workspace, int64_t workspace_bytes, void* stream) {
+extern "C" int llp_grad_sumsq_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
+                                float* sumsq, uint32_t* ticket, void* workspace, int64_t workspace_bytes,
+                                void* stream) {
   LLP_CHECK_ARG(descs && sumsq && workspace, "llp_grad_sumsq: null pointer");
   LLP_CHECK_ARG(n_groups >= 1 && n_groups <= 8, "llp_grad_sumsq: n_groups in [1,8]");
   LLP_CHECK_ARG(workspace_bytes >= llp_grad_sumsq_workspace_bytes(n_tensors, max_numel),
@@ -578,6 +775,12 @@ extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64
   hipStream_t s = (hipStream_t)stream;
   const int64_t mc = max_chunks_of(max_numel);
   // blocks past a tensor's numel exit immediately; x extent bounded by kMaxNumel
+  if (ticket) {   // one launch: the last workgroup finalizes
+    hipLaunchKernelGGL(grad_sumsq_fused_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs,
+                       n_tensors, mc, (float*)workspace, n_groups, sumsq, ticket);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
   hipLaunchKernelGGL(grad_sumsq_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, mc,
                      (float*)workspace);
   LLP_LAUNCH_CHECK();
@@ -587,12 +790,23 @@ extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64
   return LLP_OK;
 }
 
-extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
-                             float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
-                             void* stream) {
+extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
+                              float* sumsq, void* workspace, int64_t workspace_bytes, void* stream) {
+  return llp_grad_sumsq_t(descs, n_tensors, max_numel, n_groups, sumsq, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
+                               float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
+                               uint32_t* ticket, void* stream) {
   LLP_CHECK_ARG(descs && step, "llp_adam_step: null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int64_t mc = max_chunks_of(max_numel);
+  if (ticket) {   // one launch: Adam, both shadows, the step counter by the last workgroup
+    hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0,
+                       s, descs, sumsq, max_norm, lr, beta1, beta2, eps, step, ticket);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0, s, descs,
                      sumsq, max_norm, lr,
                      beta1, beta2, eps, (const int64_t*)step);
@@ -600,6 +814,12 @@ extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_
   hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, step);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
+}
+
+extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
+                             float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
+                             void* stream) {
+  return llp_adam_step_t(descs, n_tensors, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, nullptr, stream);
 }
 
 extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream) {

@@ -17,30 +17,58 @@ constexpr int WAVES = 4;
 
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + expf(-z)); }
 
+// The Linear(H, 1) head's finish (head_finish_kernel, gemm.hip) inside the loss: logit of
+// predictor row m = bias + the per-256-column GEMM partials part[t * ld + m] in column order --
+// the same fp32 sum, so the logits are bit-identical to a separate head_finish launch.
+struct HeadIn {
+  const float* part;   // [parts][ld] partials of gemm_nt_head, or NULL: logits read as given
+  const float* bias;   // [1] or NULL
+  int64_t parts, ld;
+};
+__device__ __forceinline__ float head_sum(const HeadIn& h, int64_t m) {
+  float s = h.bias ? h.bias[0] : 0.f;
+  for (int64_t t = 0; t < h.parts; ++t) s += h.part[t * h.ld + m];
+  return s;
+}
+
 // partial sums per block: [bce, kl, rank].  CMAX: the LDS row per wave (64 for C <= 64, the
 // collab / physics shapes: 2 KiB of LDS per block instead of 32 KiB, so a CU holds 8x the waves)
+// With hs.part / ht.part the student logits (rows b*C + c of the predictor) and the teacher's
+// probabilities are finished here from the head partials and written to s_logit / t_prob.
 template <int CMAX>
-__global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, const float* __restrict__ s_logit,
-                                                         const float* __restrict__ t_prob, double B_total,
-                                                         float margin, float T, float w_d, float w_r,
-                                                         float loss_scale, float* __restrict__ dlogit,
-                                                         float* __restrict__ partial, int64_t tb0, int64_t tb1) {
+__device__ __forceinline__ void llp_anchor_block(int64_t blk, int64_t B, int64_t C, float* __restrict__ s_logit,
+                                                 float* __restrict__ t_prob, const HeadIn& hs, const HeadIn& ht,
+                                                 double B_total, float margin, float T, float w_d, float w_r,
+                                                 float loss_scale, float* __restrict__ dlogit,
+                                                 float* __restrict__ partial, int64_t tb0, int64_t tb1) {
   __shared__ float ss[WAVES][CMAX];
   __shared__ float tt[WAVES][CMAX];
   __shared__ float red[WAVES][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t b = (int64_t)blockIdx.x * WAVES + w;
+  const int64_t b = blk * WAVES + w;
   float kl_acc = 0.f, rk_acc = 0.f;
   if (b < B) {
-    const float* sl = s_logit + b * C;
-    const float* tp = t_prob + b * C;
+    float* sl = s_logit + b * C;
+    float* tp = t_prob + b * C;
     float* sw = ss[w];
     float* tw = tt[w];
     // sigmoid probabilities (Q4) and the softmax statistics of s/T and t/T
     float ms = -INFINITY, mt = -INFINITY;
     for (int c = lane; c < C; c += 64) {
-      const float s = sigmoidf_(sl[c]);
-      const float t = tp[c];
+      float z = 0.f, t = 0.f;
+      if (hs.part) {
+        z = head_sum(hs, b * C + c);
+        sl[c] = z;
+      } else {
+        z = sl[c];
+      }
+      if (ht.part) {
+        t = 1.f / (1.f + expf(-head_sum(ht, b * C + c)));
+        tp[c] = t;
+      } else {
+        t = tp[c];
+      }
+      const float s = sigmoidf_(z);
       sw[c] = s;
       tw[c] = t;
       ms = fmaxf(ms, s / T);
@@ -101,22 +129,24 @@ __global__ __launch_bounds__(256) void llp_anchor_kernel(int64_t B, int64_t C, c
       k += red[i][0];
       r += red[i][1];
     }
-    partial[blockIdx.x * 3 + 0] = 0.f;
-    partial[blockIdx.x * 3 + 1] = k;
-    partial[blockIdx.x * 3 + 2] = r;
+    partial[blk * 3 + 0] = 0.f;
+    partial[blk * 3 + 1] = k;
+    partial[blk * 3 + 2] = r;
   }
 }
 
 // neg_count (device, may be NULL): the label rows are n_pos positives then negative slots of
 // which those with neg_offset + slot < *neg_count are live; the others get a zero gradient and
-// no loss, and the mean is over pos_total + *neg_count labels (the whole batch's)
-__global__ __launch_bounds__(256) void bce_kernel(int64_t n, int64_t n_pos, const float* __restrict__ logit,
-                                                  double n_total, const int32_t* __restrict__ neg_count,
-                                                  int64_t neg_offset, double pos_total, float w_label,
-                                                  float loss_scale, float* __restrict__ dlogit,
-                                                  float* __restrict__ partial) {
+// no loss, and the mean is over pos_total + *neg_count labels (the whole batch's).
+// With hl.part the label logits (predictor rows lab_row0 + r) are finished from the head partials
+// and written to logit[r].
+__device__ __forceinline__ void bce_block(int64_t blk, int64_t n, int64_t n_pos, float* __restrict__ logit,
+                                          const HeadIn& hl, int64_t lab_row0, double n_total,
+                                          const int32_t* __restrict__ neg_count, int64_t neg_offset,
+                                          double pos_total, float w_label, float loss_scale,
+                                          float* __restrict__ dlogit, float* __restrict__ partial) {
   __shared__ float red[4];
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t r = blk * (int64_t)blockDim.x + threadIdx.x;
   int64_t n_live = n;
   if (neg_count) {
     const int64_t c = *neg_count;
@@ -125,6 +155,7 @@ __global__ __launch_bounds__(256) void bce_kernel(int64_t n, int64_t n_pos, cons
     n_total = pos_total + (double)c;
   }
   float l = 0.f;
+  if (r < n && hl.part) logit[r] = head_sum(hl, lab_row0 + r);   // every slot, inert ones too
   if (r < n && r >= n_live) dlogit[r] = 0.f;
   if (r < n_live) {
     const float o = sigmoidf_(logit[r]);
@@ -139,18 +170,27 @@ __global__ __launch_bounds__(256) void bce_kernel(int64_t n, int64_t n_pos, cons
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
   __syncthreads();
   if (threadIdx.x == 0) {
-    partial[blockIdx.x * 3 + 0] = (red[0] + red[1] + red[2] + red[3]) / (float)n_total;
-    partial[blockIdx.x * 3 + 1] = 0.f;
-    partial[blockIdx.x * 3 + 2] = 0.f;
+    partial[blk * 3 + 0] = (red[0] + red[1] + red[2] + red[3]) / (float)n_total;
+    partial[blk * 3 + 1] = 0.f;
+    partial[blk * 3 + 2] = 0.f;
   }
 }
 
-__global__ void loss_finalize_kernel(const float* __restrict__ partial, int64_t nblocks, float w_label, float w_d,
-                                     float w_r, float* __restrict__ terms, int accumulate) {
+// the three terms from the per-block partials: a fixed tree in double (deterministic)
+template <bool HANDOFF>
+__device__ __forceinline__ void loss_finalize_block(const float* partial, int64_t nblocks, float w_label, float w_d,
+                                                    float w_r, float* __restrict__ terms, int accumulate) {
   __shared__ double red[3][256];
   double a[3] = {0, 0, 0};
   for (int64_t i = threadIdx.x; i < nblocks; i += blockDim.x)
-    for (int k = 0; k < 3; ++k) a[k] += (double)partial[i * 3 + k];
+    for (int k = 0; k < 3; ++k) {
+      // partials of other workgroups of this launch: vector loads behind the acquire (never the
+      // scalar path, cdna_hip_programming.md Guideline 16 Pitfall 6)
+      const float v = HANDOFF ? __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(partial) + i * 3 + k,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : partial[i * 3 + k];
+      a[k] += (double)v;
+    }
   for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = a[k];
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
@@ -167,6 +207,59 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partial, int64_t 
       terms[0] = loss; terms[1] = bce; terms[2] = kl; terms[3] = rk;
     }
   }
+}
+
+struct LossArgs {
+  int64_t B, C, n_lab, n_pos, nba, nbl;
+  float* s_logit; float* t_prob; HeadIn hs, ht;
+  float* out_logit; int64_t lab_row0;
+  double B_total, n_lab_total, pos_total;
+  float margin, T, w_label, w_d, w_r, loss_scale;
+  float* dlogit_ctx; float* dlogit_lab;
+  const int32_t* neg_count; int64_t neg_offset;
+  int64_t tb0, tb1;
+  float* partial; float* terms; int accumulate;
+  uint32_t* ticket;   // NULL: loss_finalize_kernel follows; else zero on entry, left zero
+};
+
+// The whole loss in one launch: blocks [0, nba) are the anchors' (llp_anchor_block), the
+// rest the label rows' (bce_block); the workgroup that arrives last on the ticket sums every
+// block's partials (the same tree as loss_finalize_kernel) and returns the ticket to zero.
+// Hand-off: each block's partials are stored by one lane, drained (vmcnt(0)), published by an
+// agent-scope release before the relaxed ticket add; the last arriver acquires (agent) before
+// it reads them (cdna_hip_programming.md §5 "In-launch split-K reduction", Guideline 16).
+template <int CMAX>
+__global__ __launch_bounds__(256) void llp_loss_kernel(LossArgs a) {
+  const int64_t blk = blockIdx.x;
+  if (blk < a.nba)
+    llp_anchor_block<CMAX>(blk, a.B, a.C, a.s_logit, a.t_prob, a.hs, a.ht, a.B_total, a.margin, a.T, a.w_d, a.w_r,
+                           a.loss_scale, a.dlogit_ctx, a.partial, a.tb0, a.tb1);
+  else
+    bce_block(blk - a.nba, a.n_lab, a.n_pos, a.out_logit, a.hs, a.lab_row0, a.n_lab_total, a.neg_count,
+              a.neg_offset, a.pos_total, a.w_label, a.loss_scale, a.dlogit_lab, a.partial + a.nba * 3);
+  if (!a.ticket) return;
+  __shared__ int last;
+  if (threadIdx.x == 0) {   // the lane that stored this block's partials
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t nb = (uint32_t)(a.nba + a.nbl);
+    const uint32_t old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == nb - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  loss_finalize_block<true>(a.partial, a.nba + a.nbl, a.w_label, a.w_d, a.w_r, a.terms, a.accumulate);
+}
+
+__global__ void loss_finalize_kernel(const float* __restrict__ partial, int64_t nblocks, float w_label, float w_d,
+                                     float w_r, float* __restrict__ terms, int accumulate) {
+  loss_finalize_block<false>(partial, nblocks, w_label, w_d, w_r, terms, accumulate);
 }
 
 // ------------------------------------------------------------------ head
@@ -428,39 +521,64 @@ extern "C" int64_t llp_llp_loss_workspace_bytes(int64_t B, int64_t n_lab) {
   return nb * 3 * (int64_t)sizeof(float);
 }
 
+extern "C" int llp_llp_loss_heads(int64_t B, int64_t C, float* s_logit, float* t_prob, int64_t n_lab,
+                                  int64_t n_pos, float* out_logit, double B_total, double n_lab_total, float margin,
+                                  float T, float w_label, float w_d, float w_r, float loss_scale, float* dlogit_ctx,
+                                  float* dlogit_lab, float* terms_out, int accumulate, const int32_t* neg_count,
+                                  int64_t neg_offset, double pos_total, int64_t term_b0, int64_t term_b1,
+                                  const llp_head_parts* s_head, const llp_head_parts* t_head, uint32_t* ticket,
+                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(C <= MAXC, "llp_llp_loss: contexts per anchor C=%lld > %d", (long long)C, MAXC);
+  LLP_CHECK_ARG(terms_out && workspace, "llp_llp_loss: null terms/workspace");
+  LLP_CHECK_ARG(workspace_bytes >= llp_llp_loss_workspace_bytes(B, n_lab), "llp_llp_loss: workspace too small");
+  LLP_CHECK_ARG(!s_head || (s_head->part && s_head->ld >= B * C + n_lab && s_head->parts >= 1),
+                "llp_llp_loss: student head partials must cover the B*C + n_lab predictor rows");
+  LLP_CHECK_ARG(!t_head || (t_head->part && t_head->ld >= B * C && t_head->parts >= 1),
+                "llp_llp_loss: teacher head partials must cover the B*C context rows");
+  hipStream_t s = (hipStream_t)stream;
+  LossArgs a = {};
+  a.B = B; a.C = C; a.n_lab = n_lab; a.n_pos = n_pos;
+  a.nba = B > 0 ? (B + WAVES - 1) / WAVES : 0;
+  a.nbl = (n_lab + 255) / 256;
+  if (a.nba > 0) LLP_CHECK_ARG(s_logit && t_prob && dlogit_ctx, "llp_llp_loss: null context buffers");
+  if (a.nbl > 0) LLP_CHECK_ARG(out_logit && dlogit_lab, "llp_llp_loss: null label buffers");
+  a.s_logit = s_logit; a.t_prob = t_prob; a.out_logit = out_logit;
+  if (s_head) a.hs = {s_head->part, s_head->bias, s_head->parts, s_head->ld};
+  if (t_head) a.ht = {t_head->part, t_head->bias, t_head->parts, t_head->ld};
+  a.lab_row0 = B * C;
+  a.B_total = B_total; a.n_lab_total = n_lab_total; a.pos_total = pos_total;
+  a.margin = margin; a.T = T; a.w_label = w_label; a.w_d = w_d; a.w_r = w_r; a.loss_scale = loss_scale;
+  a.dlogit_ctx = dlogit_ctx; a.dlogit_lab = dlogit_lab;
+  a.neg_count = neg_count; a.neg_offset = neg_offset;
+  a.tb0 = term_b0; a.tb1 = term_b1;
+  a.partial = reinterpret_cast<float*>(workspace);
+  a.terms = terms_out; a.accumulate = accumulate;
+  a.ticket = ticket;
+  const int64_t nb = a.nba + a.nbl;
+  if (nb > 0) {
+    if (C <= 64) hipLaunchKernelGGL(llp_loss_kernel<64>, dim3((unsigned)nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(llp_loss_kernel<MAXC>, dim3((unsigned)nb), dim3(256), 0, s, a);
+    LLP_LAUNCH_CHECK();
+  }
+  if (!ticket || nb == 0) {
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, a.partial, nb, w_label, w_d, w_r, terms_out,
+                       accumulate);
+    LLP_LAUNCH_CHECK();
+  }
+  return LLP_OK;
+}
+
 extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob, int64_t n_lab,
                             int64_t n_pos, const float* out_logit, double B_total, double n_lab_total, float margin,
                             float T, float w_label, float w_d, float w_r, float loss_scale, float* dlogit_ctx,
                             float* dlogit_lab, float* terms_out, int accumulate, const int32_t* neg_count,
                             int64_t neg_offset, double pos_total, int64_t term_b0, int64_t term_b1,
                             void* workspace, int64_t workspace_bytes, void* stream) {
-  LLP_CHECK_ARG(C <= MAXC, "llp_llp_loss: contexts per anchor C=%lld > %d", (long long)C, MAXC);
-  LLP_CHECK_ARG(terms_out && workspace, "llp_llp_loss: null terms/workspace");
-  LLP_CHECK_ARG(workspace_bytes >= llp_llp_loss_workspace_bytes(B, n_lab), "llp_llp_loss: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  float* partial = reinterpret_cast<float*>(workspace);
-  const int64_t nba = B > 0 ? (B + WAVES - 1) / WAVES : 0;
-  const int64_t nbl = (n_lab + 255) / 256;
-  if (nba > 0) {
-    LLP_CHECK_ARG(s_logit && t_prob && dlogit_ctx, "llp_llp_loss: null context buffers");
-    if (C <= 64)
-      hipLaunchKernelGGL(llp_anchor_kernel<64>, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob, B_total,
-                         margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial, term_b0, term_b1);
-    else
-      hipLaunchKernelGGL(llp_anchor_kernel<MAXC>, dim3((unsigned)nba), dim3(256), 0, s, B, C, s_logit, t_prob,
-                         B_total, margin, T, w_d, w_r, loss_scale, dlogit_ctx, partial, term_b0, term_b1);
-    LLP_LAUNCH_CHECK();
-  }
-  if (nbl > 0) {
-    LLP_CHECK_ARG(out_logit && dlogit_lab, "llp_llp_loss: null label buffers");
-    hipLaunchKernelGGL(bce_kernel, dim3((unsigned)nbl), dim3(256), 0, s, n_lab, n_pos, out_logit, n_lab_total,
-                       neg_count, neg_offset, pos_total, w_label, loss_scale, dlogit_lab, partial + nba * 3);
-    LLP_LAUNCH_CHECK();
-  }
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partial, nba + nbl, w_label, w_d, w_r,
-                     terms_out, accumulate);
-  LLP_LAUNCH_CHECK();
-  return LLP_OK;
+  return llp_llp_loss_heads(B, C, const_cast<float*>(s_logit), const_cast<float*>(t_prob), n_lab, n_pos,
+                            const_cast<float*>(out_logit), B_total, n_lab_total, margin, T, w_label, w_d, w_r,
+                            loss_scale, dlogit_ctx, dlogit_lab, terms_out, accumulate, neg_count, neg_offset,
+                            pos_total, term_b0, term_b1, nullptr, nullptr, nullptr, workspace, workspace_bytes,
+                            stream);
 }
 
 extern "C" int llp_head_fwd(int dtype, int64_t R, int64_t H, const void* Z, int64_t ldz, const void* Z2, int64_t ldz2,

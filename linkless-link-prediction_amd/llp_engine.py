@@ -205,6 +205,10 @@ class EngineBase:
         self.rank = dist.get_rank(group) if self.world > 1 else 0
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)   # RNG stream counter
         self.terms = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        # last-arriver tickets of the one-launch loss, gradient norm and Adam (llp_llp_loss_heads,
+        # llp_grad_sumsq_t, llp_adam_step_t): zero, and left zero by every call
+        self.tickets = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        self.loss_ticket = self.tickets[0:1]
         self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self._bufs = {}
         self._shadows = {}
@@ -380,7 +384,14 @@ class EngineBase:
         N = self.N
         if neg is not None:
             n_neg = int(neg.shape[1])
-            n_neg_total = n_neg if P_total == P else int(round(n_neg * P_total / max(P, 1)))
+            if self.world > 1:
+                # the true total over the ranks' shards (BCE normaliser, BatchNorm row count),
+                # not a proportional estimate; injected negatives are host-known (no capture)
+                t = torch.tensor([n_neg], dtype=torch.int64, device=self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                n_neg_total = int(t.item())
+            else:   # one rank, or an emulated shard (timing): proportional to the link slice
+                n_neg_total = n_neg if P_total == P else int(round(n_neg * P_total / max(P, 1)))
             negb = self._buf("neg", (2, max(n_neg, 1)), torch.int32)
             negb[:, :n_neg].copy_(neg.to(torch.int32))
             return negb[:, :n_neg], n_neg, n_neg_total, None
@@ -405,12 +416,16 @@ class EngineBase:
         K.randint_pairs(N, P, self.seed, self.step_ctr, RANDINT_STREAM, negb, n_total=P_total, offset=p_offset)
         return negb, P, P_total, None
 
-    def _predictor_forward(self, h, ia, ib, R2, logit, p_drop):
+    def _predictor_forward(self, h, ia, ib, R2, logit, p_drop, defer_head=False):
         """LinkPredictor(h[ia], h[ib]) logits (src/models.py:139-150).  Returns
-        (A0, zacts): the first layer's input operand and hidden activations."""
+        (A0, zacts): the first layer's input operand and hidden activations.  With
+        ``defer_head`` and the head fused into the last GEMM, the logits are left as head
+        partials in ``self._s_head`` (K.head_in) for the loss launch to finish and write;
+        otherwise ``self._s_head`` is None and ``logit`` is written here."""
         H = h.shape[1]
         dt, dc = self.dtype, self.dc
         zacts = []
+        self._s_head = None
         if self.predictor_kind != "mlp":
             K.head_fwd(h, R2, H, None, None, logit=logit, Z2=h, iz=ia, iz2=ib)
             return None, zacts
@@ -434,7 +449,10 @@ class EngineBase:
                 hpart = self._buf("hpart", (parts, R2), torch.float32)
                 K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, self.head.weight.data.view(-1),
                                hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, DROP_PREDICTOR, l))
-                K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
+                if defer_head:
+                    self._s_head = K.head_in(hpart, parts, R2, self.head.bias.data)
+                else:
+                    K.head_finish(parts, R2, hpart, self.head.bias.data, logit=logit)
                 fused = True
             else:
                 zm = self._mask(f"Zm{l}", R2, lin.out_f, lin.in_f, self.prd[l + 1].out_f) if not last else None
@@ -627,10 +645,11 @@ class EngineBase:
             self._issued = []
             self._collective(lambda: self._finish_allreduce(rest))
         g = self.optimizer.param_groups[0]
-        K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq)
+        K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq,
+                     ticket=self.tickets[1:2])
         b1, b2 = g["betas"]
         K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
-                    float(b2), float(g["eps"]), self.adam_step)
+                    float(b2), float(g["eps"]), self.adam_step, ticket=self.tickets[2:3])
 
     # ------------------------------------------------------------------ epoch bookkeeping
     def begin_epoch(self):
@@ -901,7 +920,9 @@ class DistillEngine(EngineBase):
         # ---- a5: predictor on context pairs + label pairs (src/main.py:103-105,126)
         logit = self._buf("logit", (R2,), torch.float32)
         self._dbg_cut("student forward")
-        A0, zacts = self._predictor_forward(h, ia_h, ib_h, R2, logit, p_drop)
+        # (one rank: the heads' finish is left to the loss launch; the owner decomposition
+        # all-reduces the logits first)
+        A0, zacts = self._predictor_forward(h, ia_h, ib_h, R2, logit, p_drop, defer_head=not owner)
         self._dbg_cut("predictor forward")
 
         # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
@@ -909,7 +930,7 @@ class DistillEngine(EngineBase):
         if owner:
             self._teacher_forward(n_ctx, target[:n_ctx], target[R2:R2 + n_ctx], t_r)
         else:
-            self._teacher_forward(B * C, t_ia, t_ib, t_r)
+            self._teacher_forward(B * C, t_ia, t_ib, t_r, defer_head=True)
 
         # ---- a7-a9: fused LLP_D + LLP_R + BCE and d(loss)/d(logit) (src/main.py:107-130)
         if not (a.LLP_D or a.LLP_R):
@@ -935,7 +956,7 @@ class DistillEngine(EngineBase):
         else:
             K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin),
                        1.0, float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms,
-                       ws)
+                       ws, s_head=self._s_head, t_head=self._t_head, ticket=self.loss_ticket)
 
         # ---- a10: backward
         self._dbg_cut("teacher + loss")
@@ -1147,13 +1168,14 @@ class DistillEngine(EngineBase):
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
-        A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop)
+        A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop, defer_head=True)
 
         # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215)
         R_t = R2 if float(a.KD_LM) != 0.0 else BC
         t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
-        if R_t > 0:
-            self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r)
+        self._t_head = None
+        if R_t > 0:   # (KD_LM reads the label pairs' probabilities: finished here, not in the loss)
+            self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r, defer_head=R_t == BC)
 
         # ---- a7-a9: LLP_D + LLP_R + BCE, then KD_RM / KD_LM (src/main.py:217-222)
         dlogit = self._buf("dlogit", (R2,), torch.float32)
@@ -1161,7 +1183,8 @@ class DistillEngine(EngineBase):
         K.llp_loss(Bc, C, logit, t_r, n_lab, P, logit[BC:], B_total if use_llp else 1, n_lab_total,
                    float(a.margin), 1.0, float(a.True_label), float(a.LLP_D) if use_llp else 0.0,
                    float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws, neg_count=cnt,
-                   neg_offset=p_offset, pos_total=P_total)
+                   neg_offset=p_offset, pos_total=P_total, s_head=self._s_head, t_head=self._t_head,
+                   ticket=self.loss_ticket)
         # d(loss)/dh: without KD_RM, the pair rows' Hadamard gradients are grouped by node and
         # summed in row order (deterministic, straight into the compute-dtype buffer); with KD_RM
         # (which adds at the anchors) they accumulate by f32 scatter-add, then convert
@@ -1319,8 +1342,12 @@ class DistillEngine(EngineBase):
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g
 
-    def _teacher_forward(self, R, t_ia, t_ib, t_r):
+    def _teacher_forward(self, R, t_ia, t_ib, t_r, defer_head=False):
+        """The frozen teacher predictor's probabilities t_r over R pairs; with ``defer_head``
+        and the fused head GEMM, left as head partials in ``self._t_head`` (the loss launch
+        finishes them, see _predictor_forward)."""
         dt, dc = self.dtype, self.dc
+        self._t_head = None
         if self.t_kind == "inner":
             K.head_fwd(self.t_h, R, self.t_h.shape[1], None, None, prob=t_r, Z2=self.t_h, iz=t_ia, iz2=t_ib)
             return
@@ -1336,7 +1363,10 @@ class DistillEngine(EngineBase):
             tpart = self._buf("tpart", (parts, R), torch.float32)
             K.gemm_nt_head(K.operand(tin), K.operand(W), R, W.shape[0], W.shape[1], None, w2, tpart, bias=b,
                            act=K.ACT_RELU, dropout=self._dropout(self.t_dropout, DROP_TEACHER_PRED, 0))
-            K.head_finish(parts, R, tpart, b2, prob=t_r)
+            if defer_head:
+                self._t_head = K.head_in(tpart, parts, R, b2)
+            else:
+                K.head_finish(parts, R, tpart, b2, prob=t_r)
             return
         A = K.operand(self.t_h, t_ia, self.t_h, t_ib)
         out = None

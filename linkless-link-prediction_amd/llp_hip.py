@@ -35,6 +35,11 @@ class Dropout(C.Structure):
     _fields_ = [("p", c_f32), ("seed", c_u64), ("step_ctr", c_vp), ("stream_offset", c_i64)]
 
 
+class HeadParts(C.Structure):
+    """llp_head_parts: a gemm_nt_head's per-256-column partials [parts][ld] and the head bias."""
+    _fields_ = [("part", c_vp), ("bias", c_vp), ("parts", c_i64), ("ld", c_i64)]
+
+
 class TensorDesc(C.Structure):
     _fields_ = [("param", c_vp), ("grad", c_vp), ("exp_avg", c_vp), ("exp_avg_sq", c_vp), ("shadow", c_vp),
                 ("shadow_t", c_vp), ("numel", c_i64), ("rows", c_i64), ("cols", c_i64), ("group", C.c_int32),
@@ -69,6 +74,9 @@ _SIGS = {
     "llp_llp_loss": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32,
                              c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64, c_vp, c_i64,
                              c_vp]),
+    "llp_llp_loss_heads": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32,
+                                   c_f32, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64,
+                                   c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "llp_pair_owner_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64, c_int]),
     "llp_pair_owner_assign": (c_int, [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
                                       c_vp]),
@@ -110,6 +118,8 @@ _SIGS = {
     "llp_grad_sumsq_workspace_bytes": (c_i64, [c_int, c_i64]),
     "llp_grad_sumsq": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
     "llp_adam_step": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
+    "llp_grad_sumsq_t": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "llp_adam_step_t": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "llp_refresh_shadows": (c_int, [c_vp, c_int, c_i64, c_vp]),
     "llp_convert": (c_int, [c_int, c_int, c_i64, c_vp, c_vp, c_vp]),
     "llp_accumulate": (c_int, [c_i64, c_vp, c_f32, c_vp, c_vp]),
@@ -298,19 +308,29 @@ def llp_loss_ws_bytes(B, n_lab):
     return load().llp_llp_loss_workspace_bytes(B, n_lab)
 
 
+def head_in(part, parts, ld, bias):
+    """HeadParts of a gemm_nt_head partial buffer (finished inside llp_loss)."""
+    return HeadParts(part.data_ptr(), ptr(bias), int(parts), int(ld))
+
+
 def llp_loss(B, Cc, s_logit, t_prob, n_lab, n_pos, out_logit, B_total, n_lab_total, margin, T, w_label, w_d, w_r,
              dlogit_ctx, dlogit_lab, terms, ws, accumulate=False, loss_scale=1.0, neg_count=None, neg_offset=0,
-             pos_total=0.0, term_range=None):
+             pos_total=0.0, term_range=None, s_head=None, t_head=None, ticket=None):
     """neg_count: the dense negatives' int32 device count (label slots past it inert, the BCE
     mean over pos_total + count labels); n_lab_total is then unused.  term_range (b0, b1): the
-    anchors whose KL / rank terms are reported (default all B; every gradient is written)."""
+    anchors whose KL / rank terms are reported (default all B; every gradient is written).
+    s_head / t_head (HeadParts): the student / teacher logits finished inside the loss launch and
+    written to s_logit + out_logit / t_prob; ticket (int32 device word, zero, left zero): the
+    terms are finalised by the launch's last workgroup (one launch in all)."""
     L = lib()
     tb0, tb1 = (0, B) if term_range is None else term_range
-    check(L.llp_llp_loss(B, Cc, ptr(s_logit), ptr(t_prob), n_lab, n_pos, ptr(out_logit), float(B_total),
-                         float(n_lab_total), margin, T, w_label, w_d, w_r, loss_scale, ptr(dlogit_ctx),
-                         ptr(dlogit_lab), terms.data_ptr(), int(accumulate), ptr(neg_count), int(neg_offset),
-                         float(pos_total), int(tb0), int(tb1), ws.data_ptr(), ws.numel() * ws.element_size(),
-                         stream_ptr()),
+    check(L.llp_llp_loss_heads(B, Cc, ptr(s_logit), ptr(t_prob), n_lab, n_pos, ptr(out_logit), float(B_total),
+                               float(n_lab_total), margin, T, w_label, w_d, w_r, loss_scale, ptr(dlogit_ctx),
+                               ptr(dlogit_lab), terms.data_ptr(), int(accumulate), ptr(neg_count), int(neg_offset),
+                               float(pos_total), int(tb0), int(tb1),
+                               C.byref(s_head) if s_head is not None else None,
+                               C.byref(t_head) if t_head is not None else None, ptr(ticket),
+                               ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()),
           "llp_llp_loss")
 
 
@@ -574,16 +594,18 @@ def grad_sumsq_ws_bytes(n, max_numel):
     return load().llp_grad_sumsq_workspace_bytes(n, max_numel)
 
 
-def grad_sumsq(descs_dev, n, max_numel, n_groups, sumsq, ws):
+def grad_sumsq(descs_dev, n, max_numel, n_groups, sumsq, ws, ticket=None):
+    """ticket (int32 device word, zero, left zero): one launch (the finalize in its last workgroup)."""
     L = lib()
-    check(L.llp_grad_sumsq(descs_dev.data_ptr(), n, max_numel, n_groups, sumsq.data_ptr(), ws.data_ptr(),
-                           ws.numel() * ws.element_size(), stream_ptr()), "llp_grad_sumsq")
+    check(L.llp_grad_sumsq_t(descs_dev.data_ptr(), n, max_numel, n_groups, sumsq.data_ptr(), ptr(ticket),
+                             ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_grad_sumsq")
 
 
-def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step):
+def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, ticket=None):
+    """ticket: one launch (both shadows in the Adam pass, the step advanced by its last workgroup)."""
     L = lib()
-    check(L.llp_adam_step(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
-                          step.data_ptr(), stream_ptr()), "llp_adam_step")
+    check(L.llp_adam_step_t(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
+                            step.data_ptr(), ptr(ticket), stream_ptr()), "llp_adam_step")
 
 
 def refresh_shadows(descs_dev, n, max_numel):

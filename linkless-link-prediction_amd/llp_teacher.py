@@ -308,12 +308,13 @@ class TeacherEngine(EngineBase):
         if self._pi is not None:   # node ids -> the engine's rows (in place)
             K.gather_i32(tgt, self._pi, tgt)
         logit = self._buf("logit", (R,), torch.float32)
-        A0, zacts = self._predictor_forward(h, ia, ib, R, logit, self.pred_drop)
+        A0, zacts = self._predictor_forward(h, ia, ib, R, logit, self.pred_drop, defer_head=True)
         dlogit = self._buf("dlogit", (R,), torch.float32)
         ws = self._ws("ws_loss", K.llp_loss_ws_bytes(0, R))
-        # BCE only (src/train_teacher_gnn.py:56-58)
+        # BCE only (src/train_teacher_gnn.py:56-58), the head's finish in the same launch
         K.llp_loss(0, 1, None, None, R, P, logit, 1, P_total + n_neg_total if cnt is None else 0.0, 0.0, 1.0, 1.0,
-                   0.0, 0.0, None, dlogit, self.terms, ws, neg_count=cnt, neg_offset=p_offset, pos_total=P_total)
+                   0.0, 0.0, None, dlogit, self.terms, ws, neg_count=cnt, neg_offset=p_offset, pos_total=P_total,
+                   s_head=self._s_head, ticket=self.loss_ticket)
         dZ0 = self._predictor_backward(dlogit, R, A0, zacts, self.pred_drop)
         if self.predictor_kind == "mlp":
             self._hadamard_bwd_nodes(R, tgt, dZ0, None, h, self._dh_slot())

@@ -372,6 +372,51 @@ def test_llp_loss_matches_oracle(B, C, margin):
     assert torch.allclose(d[B * C:], o.grad, rtol=1e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("B,C,n_lab,parts,dense", [(3277, 36, 16384, 4, False), (1, 20, 300, 1, True),
+                                                    (0, 1, 5000, 4, False), (70, 100, 0, 2, False)])
+def test_llp_loss_heads_one_launch(B, C, n_lab, parts, dense):
+    """llp_llp_loss_heads (the student / teacher heads finished in the loss launch, the terms
+    summed by its last workgroup on a self-resetting ticket) == llp_head_finish x 2 + the
+    separate llp_llp_loss: logits, teacher probabilities, gradients and terms bit for bit, over
+    repeated calls (the ticket must come back to zero each time)."""
+    k = K()
+    g = torch.Generator().manual_seed(B + n_lab)
+    R = B * C + n_lab
+    n_pos = n_lab // 2
+    sp = (torch.randn(parts, max(R, 1), generator=g) * 0.7).to(DEV)
+    tp = (torch.randn(parts, max(B * C, 1), generator=g) * 0.7).to(DEV)
+    sb = torch.randn(1, generator=g).to(DEV)
+    tb = torch.randn(1, generator=g).to(DEV)
+    cnt = torch.tensor([n_lab - n_pos - 3], dtype=torch.int32, device=DEV) if dense else None
+    ws = torch.empty(k.llp_loss_ws_bytes(B, n_lab) // 4 + 16, device=DEV)
+    ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for it in range(3):
+        # reference: the heads finished by their own launches, the loss in three
+        logit1 = torch.empty(max(R, 1), device=DEV)
+        tprob1 = torch.empty(max(B * C, 1), device=DEV)
+        k.head_finish(parts, R, sp, sb, logit=logit1)
+        if B > 0:
+            k.head_finish(parts, B * C, tp, tb, prob=tprob1)
+        d1 = torch.empty(max(R, 1), device=DEV)
+        t1 = torch.zeros(4, device=DEV)
+        k.llp_loss(B, C, logit1, tprob1, n_lab, n_pos, logit1[B * C:], max(B, 1), n_lab, 0.1, 1.0, 0.3, 1.1, 0.9, d1,
+                   d1[B * C:], t1, ws, neg_count=cnt, pos_total=n_pos)
+        logit2 = torch.full((max(R, 1),), 7.0, device=DEV)
+        tprob2 = torch.full((max(B * C, 1),), 7.0, device=DEV)
+        d2 = torch.empty(max(R, 1), device=DEV)
+        t2 = torch.zeros(4, device=DEV)
+        k.llp_loss(B, C, logit2, tprob2, n_lab, n_pos, logit2[B * C:], max(B, 1), n_lab, 0.1, 1.0, 0.3, 1.1, 0.9, d2,
+                   d2[B * C:], t2, ws, neg_count=cnt, pos_total=n_pos, s_head=k.head_in(sp, parts, R, sb),
+                   t_head=k.head_in(tp, parts, B * C, tb) if B > 0 else None, ticket=ticket)
+        torch.cuda.synchronize()
+        assert torch.equal(logit1[:R], logit2[:R]), it
+        assert torch.equal(tprob1[:B * C], tprob2[:B * C]), it
+        assert torch.equal(d1[:R], d2[:R]), it
+        assert torch.equal(t1, t2), it
+        assert int(ticket.item()) == 0
+        sp.mul_(1.1)
+
+
 # ------------------------------------------------------------------ samplers (bit-exact)
 @pytest.mark.parametrize("ps,rw_step,hops,ns_rate", [("nb", 3, 3, 3), ("rw", 2, 2, 1), ("nb", 1, 15, 0),
                                                     ("nb", 20, 2, 1), ("nb", 61, 1, 0)])
@@ -504,11 +549,14 @@ _ADAM_CASES = {
 
 @pytest.mark.parametrize("case", sorted(_ADAM_CASES))
 @pytest.mark.parametrize("nan_group", [None, 1])
-def test_clip_and_adam_match_oracle(case, nan_group):
+@pytest.mark.parametrize("fused", [False, True])
+def test_clip_and_adam_match_oracle(case, nan_group, fused):
     """grad_sumsq (chunk partials + one-pass finalize) + clip per group + Adam
     against the oracle's clip_grad_norm_ / Adam (src/main.py:132-138); a NaN
-    gradient turns its group's clip coefficient into NaN, as torch.clamp does."""
+    gradient turns its group's clip coefficient into NaN, as torch.clamp does.
+    fused: the one-launch forms (llp_grad_sumsq_t / llp_adam_step_t with tickets)."""
     k = K()
+    tickets = torch.zeros(2, dtype=torch.int32, device=DEV) if fused else None
     spec = _ADAM_CASES[case]
     g = torch.Generator().manual_seed(9 + len(spec))
     shapes = [sh for sh, _, _ in spec]
@@ -548,9 +596,11 @@ def test_clip_and_adam_match_oracle(case, nan_group):
         gs = [x * (it + 1) for x in grads]
         for i in range(len(dp)):
             dg[i].copy_(gs[i].to(DEV))
-        k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws)
-        k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step)
+        k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets[0:1] if fused else None)
+        k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step,
+                    ticket=tickets[1:2] if fused else None)
         assert step.item() == it + 1       # one increment per adam_step
+        assert not fused or int(tickets.abs().sum()) == 0
         clipped = []
         for gr in range(n_groups):
             idx = [i for i in range(len(dp)) if groups[i] == gr]
@@ -572,6 +622,54 @@ def test_clip_and_adam_match_oracle(case, nan_group):
             rows, cols = sh[i].shape
             assert torch.equal(sh[i], a.view(rows, cols).to(torch.bfloat16))
             assert torch.equal(sht[i], a.view(rows, cols).t().to(torch.bfloat16))
+
+
+def test_clip_and_adam_one_launch_bit_identical():
+    """The one-launch norm and Adam (tickets) give the two-launch forms' parameters, moments,
+    gradients, bf16 shadows and transposed shadows bit for bit (big case, 3 steps)."""
+    k = K()
+    spec = _ADAM_CASES["big"]
+    g = torch.Generator().manual_seed(77)
+    shapes = [sh for sh, _, _ in spec]
+    groups = [gr for _, gr, _ in spec]
+    n_groups = max(groups) + 1
+    params = [torch.randn(*s, generator=g) for s in shapes]
+    grads = [torch.randn(*s, generator=g) * 3 for s in shapes]
+    max_numel = max(p.numel() for p in params)
+    runs = []
+    for fused in (False, True):
+        dp = [p.to(DEV).clone() for p in params]
+        dg = [x.to(DEV).clone() for x in grads]
+        m = [torch.zeros_like(p) for p in dp]
+        v = [torch.zeros_like(p) for p in dp]
+        sh, descs = [], []
+        for i, p in enumerate(dp):
+            rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+            s_ = st_ = None
+            if spec[i][2]:
+                s_ = torch.zeros(rows, cols, dtype=torch.bfloat16, device=DEV)
+                st_ = torch.zeros(cols, rows, dtype=torch.bfloat16, device=DEV)
+            sh += [s_, st_]
+            descs.append(k.TensorDesc(p.data_ptr(), dg[i].data_ptr(), m[i].data_ptr(), v[i].data_ptr(),
+                                      k.ptr(s_), k.ptr(st_), p.numel(), rows, cols, groups[i],
+                                      k.LLP_BF16 if s_ is not None else 0))
+        dd = k.descs_to_device(descs, DEV)
+        sumsq = torch.zeros(n_groups, device=DEV)
+        ws = torch.empty(k.grad_sumsq_ws_bytes(len(dp), max_numel) // 4 + 16, device=DEV)
+        step = torch.zeros(1, dtype=torch.int64, device=DEV)
+        tickets = torch.zeros(2, dtype=torch.int32, device=DEV)
+        for it in range(3):
+            for i in range(len(dp)):
+                dg[i].copy_((grads[i] * (it + 1)).to(DEV))
+            k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets[0:1] if fused else None)
+            k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step,
+                        ticket=tickets[1:2] if fused else None)
+        torch.cuda.synchronize()
+        runs.append((dp, dg, m, v, [x for x in sh if x is not None], sumsq, int(step.item())))
+    for a, b in zip(runs[0][:5], runs[1][:5]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    assert torch.equal(runs[0][5], runs[1][5]) and runs[0][6] == runs[1][6] == 3
 
 
 # ------------------------------------------------------------------ unique-node compaction
@@ -925,6 +1023,36 @@ def test_gemm_nt_persistent_bit_identical(mode, M, N, Kd):
         assert torch.equal(C1, C2)
         ref = 2.0 * (G.float() @ Wt.float().t()) * (Y.float() > 0)
         assert torch.allclose(C1.float(), ref, rtol=2e-2, atol=2e-2 * (1 + ref.abs().max().item()))
+
+
+@pytest.mark.parametrize("mode", ["relu_mask", "bwd_mask"])
+def test_gemm_nt_persistent_race_screen(mode):
+    """Race screen of the persistent kernel's DMA schedule (three half K-tiles in flight, the
+    next tile's K-tile 0 issued across the tile boundary) at the collab student shape: six
+    launches on fresh random operands, each bit-identical to pp8 on row slices."""
+    k = K()
+    M, N, Kd = 225_280, 1024, 1024
+    g = torch.Generator().manual_seed(5)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV) * 0.1
+    mask = None
+    if mode == "bwd_mask":
+        mask = torch.randint(0, 256, (M, N // 8), generator=g, dtype=torch.uint8).to(DEV)
+    for it in range(6):
+        A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+        C1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        if mode == "relu_mask":
+            m1 = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8)
+            k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C1, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=m1)
+            m2 = torch.empty_like(m1)
+            C2 = _nt_sliced(k, A, W, M, N, Kd, k.LLP_BF16, 64 * 256, bias=b, act=k.ACT_RELU, mask=m2)
+            torch.cuda.synchronize()
+            assert torch.equal(m1, m2), it
+        else:
+            k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C1, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=mask, alpha=0.5)
+            C2 = _nt_sliced(k, A, W, M, N, Kd, k.LLP_BF16, 64 * 256, act=k.ACT_RELU_BWD, aux=mask, alpha=0.5)
+            torch.cuda.synchronize()
+        assert torch.equal(C1, C2), it
 
 
 def test_gemm_nt_persistent_device_row_count():
