@@ -231,27 +231,29 @@ def evaluate(model, pred, data, dev):
 SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_sage.json")
 
 
-def practical_peak(dev, seconds=0.2):
-    """bf16 MFMA FLOP/s this device sustains on random operands (llp_mfma_probe: a bare
-    v_mfma_f32_16x16x32_bf16 loop on every CU, two waves per SIMD), event-timed on the
+def practical_peak(dev, seconds=0.2, dtype="bf16"):
+    """MFMA FLOP/s this device sustains on random operands (llp_mfma_probe: a bare
+    v_mfma_f32_16x16x32_bf16 loop on every CU, two waves per SIMD; dtype "fp32":
+    llp_mfma_probe_f32, the same loop on v_mfma_f32_16x16x4_f32), event-timed on the
     launch stream: the clock the chip holds under dense MFMA load on random data sets it
-    well under the 2.5 PF/s spec (MI355X_MICROARCH.md, DVFS give-back)."""
+    well under the spec peak (MI355X_MICROARCH.md, DVFS give-back)."""
     import llp_hip as K
     g = torch.Generator(device="cpu").manual_seed(11)
-    data = torch.randn(1 << 16, generator=g).to(torch.bfloat16).to(dev)
+    data = torch.randn(1 << 16, generator=g).to(torch.bfloat16 if dtype == "bf16" else torch.float32).to(dev)
     out = torch.empty(K.mfma_probe_out_floats(), dtype=torch.float32, device=dev)
-    iters = 20000
-    K.mfma_probe(data, iters, out)      # warm-up, and a first estimate of the rate
+    probe = K.mfma_probe if dtype == "bf16" else K.mfma_probe_f32
+    iters = 20000 if dtype == "bf16" else 5000
+    probe(data, iters, out)      # warm-up, and a first estimate of the rate
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    fl = K.mfma_probe(data, iters, out)
+    fl = probe(data, iters, out)
     e1.record()
     torch.cuda.synchronize()
     rate = fl / (e0.elapsed_time(e1) * 1e-3)
     iters = max(1000, int(iters * seconds / (fl / rate)))
     e0.record()
-    fl = K.mfma_probe(data, iters, out)
+    fl = probe(data, iters, out)
     e1.record()
     torch.cuda.synchronize()
     return fl / (e0.elapsed_time(e1) * 1e-3) / 1e12
@@ -378,6 +380,9 @@ def fp32_step(data, a, t_h, init, dev, steps=3):
             "unit": "TFLOP/s", "frac": achieved / PEAK_F32_TFLOPS, "kernel_ms": k_ms,
             "traffic": pmc_traffic(rows, H, "fp32"),
             "algorithmic_bytes": 2.0 * rows * H * 4 + 4.0 * H * H}
+    pp = practical_peak(dev, dtype="fp32")
+    roof.update(practical_peak=pp, practical_frac=achieved / pp,
+                practical_note="bare v_mfma_f32_16x16x4_f32 loop on random f32 operands, every CU (llp_mfma_probe_f32)")
     del eng
     torch.cuda.empty_cache()
     return {"dtype": "fp32", "ms_per_step": dt * 1e3, "edges_per_s": P / dt, "steps": steps, "roofline": roof,

@@ -283,6 +283,24 @@ int64_t llp_dedup_rows_workspace_bytes(int64_t num_nodes, int64_t R);
 int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
                    int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* workspace,
                    int64_t workspace_bytes, void* stream);
+/* llp_dedup_rows in four launches instead of ten (the same outputs): per-node counts, ONE
+ * pass over the nodes (the exclusive scan by decoupled look-back between workgroups + the
+ * compaction), the scatter, and every segment's sort in one launch.  The workspace
+ * (llp_dedup_rows2_workspace_bytes) starts with llp_dedup_rows2_state_bytes(num_nodes) bytes
+ * of state that persists between calls (counts, look-back flags tagged with a per-call
+ * epoch, a ticket); state_clean = 1 vouches that they are as a previous llp_dedup_rows2 call
+ * on this workspace (with this num_nodes) left them, or zero; 0 zeroes them first (one more
+ * launch).  Word [2] of the 256-byte control block at the end of the state is set nonzero if
+ * a look-back ever timed out (bounded spin; the results are then invalid).
+ * zero_rows (may be NULL): rows [node * zero_ld_bytes, + zero_row_bytes) of the nodes absent
+ * from target are zeroed in the same pass (16-B aligned multiples of 16 bytes) -- the
+ * 'other rows are 0' of a per-node gradient scatter, without a fill of the whole matrix. */
+int64_t llp_dedup_rows2_state_bytes(int64_t num_nodes);
+int64_t llp_dedup_rows2_workspace_bytes(int64_t num_nodes, int64_t R);
+int llp_dedup_rows2(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
+                    int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* zero_rows,
+                    int64_t zero_ld_bytes, int64_t zero_row_bytes, int state_clean, void* workspace,
+                    int64_t workspace_bytes, void* stream);
 int llp_segment_sum_rows(int dtype, int64_t U, int64_t H, const int32_t* seg_ptr, const int32_t* rows,
                          const void* src, int64_t ld_src, void* out, int64_t ld_out, int out_dtype,
                          const int32_t* out_rows, const int32_t* u_dev, void* stream);
@@ -575,6 +593,8 @@ int llp_norm_bwd(int kind, int dtype, int64_t M, int64_t H, const void* gout, in
  * of the launch (host);
  * out (llp_mfma_probe_out_floats() floats) keeps the accumulators live. */
 int llp_mfma_probe(const void* data, int64_t n_u4, int64_t iters, float* out, double* flops, void* stream);
+/* The same loop on v_mfma_f32_16x16x4_f32 (the fp32 GEMMs' instruction) over n random f32. */
+int llp_mfma_probe_f32(const float* data, int64_t n, int64_t iters, float* out, double* flops, void* stream);
 int64_t llp_mfma_probe_out_floats(void);
 
 #ifdef __cplusplus

@@ -708,6 +708,229 @@ __global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __rest
   }
 }
 
+// ---------------------------------------------------------------- the compaction in four launches
+// (llp_dedup_rows2).  Same outputs as llp_dedup_rows; launches:
+//   count_rank_kernel                      per-node counts and each row's arrival rank
+//   dedup_scan_kernel                      ONE pass over the nodes: the exclusive scan of
+//                                          pack_count by decoupled look-back between blocks, the
+//                                          compaction (compact_count_kernel's writes), the counts
+//                                          returned to zero, optionally zero rows for absent nodes
+//   scatter_rank_kernel                    rows to their segment slots
+//   segsort_all_kernel                     every segment sorted, short / mid / huge in one launch
+// The count array, the look-back flags and the control words persist in the workspace between
+// calls: zero at the first call (a zeroing launch when the caller does not vouch for it), left so
+// by every call (counts reset by the scan, the ticket by its last workgroup, the flags tagged with a
+// per-call epoch that the last workgroup advances).
+constexpr int LB_T = 256, LB_I = 8, LB_B = LB_T * LB_I;   // nodes per scan block: 2,048
+constexpr uint32_t LB_AGG = 1u, LB_INC = 2u;               // flag status: aggregate / inclusive prefix
+constexpr uint32_t LB_SPIN_LIMIT = 1u << 22;               // bounded spin: a missing publisher sets an error
+
+__device__ __forceinline__ uint32_t lb_flag_wait(const uint32_t* flag, uint32_t epoch, uint32_t* err) {
+  uint32_t f = 0;
+  for (uint32_t it = 0;; ++it) {
+    f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((f >> 2) == (epoch & 0x3FFFFFFFu) && (f & 3u)) break;
+    if (it > LB_SPIN_LIMIT) {   // never seen: a publisher that did not run (report, do not hang)
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return LB_INC;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return f & 3u;
+}
+
+struct ScanArgs {
+  int64_t N, R;
+  int32_t* cnt;                 // [N] per-node counts (zeroed here after use)
+  uint32_t* flags;              // [nb] (epoch << 2) | status
+  unsigned long long* agg;      // [nb] block aggregates
+  unsigned long long* incl;     // [nb] block inclusive prefixes
+  uint32_t* ctl;                // [0] epoch of the last completed call, [1] ticket, [2] error
+  int32_t* uniq; int32_t* seg_ptr; int32_t* uidx; int32_t* start;
+  int32_t* n_unique; int32_t* n_long;
+  char* zero_rows; int64_t zero_ld; int64_t zero_u4;   // optional: rows of absent nodes zeroed (16-B words)
+};
+
+__global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
+  __shared__ unsigned long long ts[LB_T];
+  __shared__ unsigned long long excl_s;
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const uint32_t epoch = a.ctl[0] + 1u;   // read by every workgroup before its ticket add
+  const int64_t base = b * (int64_t)LB_B + t * LB_I;
+  int32_t c[LB_I];
+  unsigned long long v[LB_I];
+  unsigned long long s = 0;
+#pragma unroll
+  for (int i = 0; i < LB_I; ++i) {
+    c[i] = base + i < a.N ? a.cnt[base + i] : 0;
+    v[i] = pack_count(c[i]);
+    s += v[i];
+  }
+  ts[t] = s;
+  __syncthreads();
+  for (int o = 1; o < LB_T; o <<= 1) {   // inclusive scan of the thread sums
+    const unsigned long long y = t >= o ? ts[t - o] : 0ull;
+    __syncthreads();
+    ts[t] += y;
+    __syncthreads();
+  }
+  const unsigned long long blk_sum = ts[LB_T - 1];
+  // publish this block's aggregate (block 0: its inclusive prefix), then look back
+  if (t == 0) {
+    if (b == 0) {
+      __hip_atomic_store(&a.incl[0], blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&a.flags[0], (epoch << 2) | LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl_s = 0ull;
+    } else {
+      __hip_atomic_store(&a.agg[b], blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&a.flags[b], (epoch << 2) | LB_AGG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (b > 0 && t < 64) {   // wave 0: 64 predecessors per window, nearest first
+    unsigned long long acc = 0;
+    for (int64_t j0 = b - 1;; j0 -= 64) {
+      const int64_t j = j0 - t;
+      uint32_t st = 0;
+      unsigned long long val = 0;
+      if (j >= 0) {
+        st = lb_flag_wait(&a.flags[j], epoch, &a.ctl[2]);
+        val = __hip_atomic_load(st == LB_INC ? &a.incl[j] : &a.agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // the nearest lane holding an inclusive prefix (block 0 always does) ends the look-back
+      const unsigned long long inc_mask = __ballot(j >= 0 && st == LB_INC);
+      const int stop = inc_mask ? __builtin_ctzll(inc_mask) : 64;
+      unsigned long long part = t <= stop && j >= 0 ? val : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      acc += part;
+      if (inc_mask || j0 - 64 < 0) break;
+    }
+    if (t == 0) {
+      excl_s = acc;
+      __hip_atomic_store(&a.incl[b], acc + blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&a.flags[b], (epoch << 2) | LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  // compaction (compact_count_kernel's writes), counts back to zero, absent nodes' rows zeroed
+  unsigned long long run = excl_s + ts[t] - s;
+#pragma unroll
+  for (int i = 0; i < LB_I; ++i) {
+    const int64_t node = base + i;
+    if (node < a.N) {
+      const int32_t slot = (int32_t)(run >> 32), st = (int32_t)(run & 0xFFFFFFFFull);
+      if (c[i] > 0) {
+        a.uniq[slot] = (int32_t)node;
+        a.seg_ptr[slot] = st;
+        a.uidx[node] = slot;
+        a.start[node] = st;
+        a.cnt[node] = 0;
+      } else if (a.zero_rows) {
+        uint4* zr = reinterpret_cast<uint4*>(a.zero_rows + node * a.zero_ld);
+        for (int64_t w = 0; w < a.zero_u4; ++w) zr[w] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      if (node == a.N - 1) {
+        const int32_t U = slot + (c[i] > 0 ? 1 : 0);
+        *a.n_unique = U;
+        a.seg_ptr[U] = (int32_t)a.R;
+        a.n_long[0] = 0;
+        a.n_long[1] = 0;
+      }
+    }
+    run += v[i];
+  }
+  // the last workgroup advances the epoch (every workgroup read it above)
+  if (llp_arrive_last(&a.ctl[1], gridDim.x) && t == 0)
+    __hip_atomic_store(&a.ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every segment sorted by row id in one launch (segsort_short / mid_wave / long fused): thread t of
+// block b takes slot t * gridDim + b (strided, so hot nodes with neighbouring ids land in different
+// blocks); a segment of up to SHORT_SEG rows is sorted in the thread's registers, longer ones go
+// on the block's LDS lists and are ranked by one wave each (up to WAVE_SEG rows) or by the whole
+// block, as the three-launch form does.
+constexpr int SS_T = 256;
+__global__ __launch_bounds__(SS_T) void segsort_all_kernel(const int32_t* __restrict__ n_unique,
+                                                           const int32_t* __restrict__ seg_ptr,
+                                                           int32_t* __restrict__ seg_rows,
+                                                           int32_t* __restrict__ scratch) {
+  __shared__ int32_t wbuf[4][WAVE_SEG];
+  __shared__ int32_t mid_list[SS_T], huge_list[SS_T];
+  __shared__ int n_mid, n_huge;
+  const int32_t U = *n_unique;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t per_round = (int64_t)gridDim.x * SS_T;
+  for (int64_t r0 = 0; r0 < U; r0 += per_round) {
+    if (threadIdx.x == 0) n_mid = n_huge = 0;
+    __syncthreads();
+    const int64_t s = r0 + (int64_t)threadIdx.x * gridDim.x + blockIdx.x;
+    if (s < U) {
+      const int32_t b = seg_ptr[s], len = seg_ptr[s + 1] - b;
+      if (len > WAVE_SEG) {
+        huge_list[atomicAdd(&n_huge, 1)] = (int32_t)s;
+      } else if (len > SHORT_SEG) {
+        mid_list[atomicAdd(&n_mid, 1)] = (int32_t)s;
+      } else if (len > 1) {
+        int32_t v[SHORT_SEG];
+#pragma unroll
+        for (int i = 0; i < SHORT_SEG; ++i) v[i] = i < len ? seg_rows[b + i] : INT32_MAX;
+#pragma unroll
+        for (int k = 2; k <= SHORT_SEG; k <<= 1)
+#pragma unroll
+          for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < SHORT_SEG; ++i) {
+              const int l = i ^ j;
+              if (l > i) {
+                const int32_t lo = min(v[i], v[l]), hi = max(v[i], v[l]);
+                if ((i & k) == 0) { v[i] = lo; v[l] = hi; } else { v[i] = hi; v[l] = lo; }
+              }
+            }
+#pragma unroll
+        for (int i = 0; i < SHORT_SEG; ++i)
+          if (i < len) seg_rows[b + i] = v[i];
+      }
+    }
+    __syncthreads();
+    const int nm = n_mid, nh = n_huge;
+    for (int i = w; i < nm; i += 4) {   // a wave per mid segment, from its own LDS row
+      const int32_t sg = mid_list[i];
+      const int32_t beg = seg_ptr[sg], len = seg_ptr[sg + 1] - beg;
+      int32_t* bw = wbuf[w];
+      for (int k = lane; k < len; k += 64) bw[k] = seg_rows[beg + k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int k = lane; k < len; k += 64) {
+        const int32_t x = bw[k];
+        int32_t rank = 0;
+        for (int j = 0; j < len; ++j) rank += bw[j] < x ? 1 : 0;
+        seg_rows[beg + rank] = x;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    for (int i = 0; i < nh; ++i) {   // the whole block per huge segment (LDS up to 4 x WAVE_SEG ids)
+      const int32_t sg = huge_list[i];
+      const int32_t beg = seg_ptr[sg], len = seg_ptr[sg + 1] - beg;
+      rank_segment_block(seg_rows, beg, len, &wbuf[0][0], 4 * WAVE_SEG, scratch);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void zero_u32_kernel(int64_t n, uint32_t* __restrict__ p) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
 }  // namespace
 
 static int64_t counting_ws_bytes(int64_t num_nodes, int64_t R) {
@@ -775,6 +998,78 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
                      huge_list, n_long + 1);
   hipLaunchKernelGGL(segsort_long_kernel, dim3(256), dim3(256), 0, s, n_long + 1, huge_list, seg_ptr, seg_rows,
                      scratch);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+// workspace of llp_dedup_rows2: [state: counts | look-back flags | control words] then scratch
+static int64_t dedup2_state_bytes(int64_t num_nodes) {
+  const int64_t nb = (num_nodes + LB_B - 1) / LB_B;
+  return al256((num_nodes + 1) * 4) + al256(nb * 4) + 256;
+}
+
+extern "C" int64_t llp_dedup_rows2_state_bytes(int64_t num_nodes) { return dedup2_state_bytes(num_nodes); }
+
+extern "C" int64_t llp_dedup_rows2_workspace_bytes(int64_t num_nodes, int64_t R) {
+  const int64_t nb = (num_nodes + LB_B - 1) / LB_B;
+  return dedup2_state_bytes(num_nodes) + 2 * al256(nb * 8) + 2 * al256((num_nodes + 1) * 4) + 2 * al256(R * 4) + 512;
+}
+
+extern "C" int llp_dedup_rows2(int64_t num_nodes, int64_t R, const int32_t* target, int32_t* uniq, int32_t* pos,
+                               int32_t* n_unique, int32_t* seg_ptr, int32_t* seg_rows, void* zero_rows,
+                               int64_t zero_ld_bytes, int64_t zero_row_bytes, int state_clean, void* workspace,
+                               int64_t workspace_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  LLP_CHECK_ARG(num_nodes > 0 && num_nodes < (1ll << 31) && R >= 0 && R < (1ll << 31), "llp_dedup_rows2: sizes");
+  LLP_CHECK_ARG(workspace && workspace_bytes >= llp_dedup_rows2_workspace_bytes(num_nodes, R),
+                "llp_dedup_rows2: workspace");
+  LLP_CHECK_ARG(!zero_rows || (zero_row_bytes % 16 == 0 && zero_ld_bytes % 16 == 0 && ((uintptr_t)zero_rows & 15) == 0),
+                "llp_dedup_rows2: zero_rows must be 16-B aligned rows of a multiple of 16 bytes");
+  char* w = reinterpret_cast<char*>(workspace);
+  const int64_t nb = (num_nodes + LB_B - 1) / LB_B;
+  if (!state_clean) {   // first call on this workspace: the persistent state from zero
+    const int64_t n32 = dedup2_state_bytes(num_nodes) / 4;
+    hipLaunchKernelGGL(zero_u32_kernel, dim3(ceil_div_u(n32, 256)), dim3(256), 0, s, n32, (uint32_t*)w);
+    LLP_LAUNCH_CHECK();
+  }
+  ScanArgs a = {};
+  a.N = num_nodes; a.R = R;
+  a.cnt = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  a.flags = reinterpret_cast<uint32_t*>(w);
+  w += al256(nb * 4);
+  a.ctl = reinterpret_cast<uint32_t*>(w);
+  w += 256;
+  a.agg = reinterpret_cast<unsigned long long*>(w);
+  w += al256(nb * 8);
+  a.incl = reinterpret_cast<unsigned long long*>(w);
+  w += al256(nb * 8);
+  a.uidx = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  a.start = reinterpret_cast<int32_t*>(w);
+  w += al256((num_nodes + 1) * 4);
+  int32_t* rank = reinterpret_cast<int32_t*>(w);   // row ranks, then the huge segments' scratch
+  w += al256(R * 4);
+  w += al256(R * 4);                                // (the long lists of the three-launch form: unused)
+  a.n_long = reinterpret_cast<int32_t*>(w);
+  a.uniq = uniq; a.seg_ptr = seg_ptr; a.n_unique = n_unique;
+  a.zero_rows = reinterpret_cast<char*>(zero_rows);
+  a.zero_ld = zero_ld_bytes;
+  a.zero_u4 = zero_row_bytes / 16;
+  if (R > 0) {
+    LLP_CHECK_ARG(target && uniq && pos && n_unique && seg_ptr && seg_rows, "llp_dedup_rows2: null");
+    hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, a.cnt, rank);
+    LLP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(dedup_scan_kernel, dim3((unsigned)nb), dim3(LB_T), 0, s, a);
+  LLP_LAUNCH_CHECK();
+  if (R == 0) return LLP_OK;
+  hipLaunchKernelGGL(scatter_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, a.uidx, a.start,
+                     rank, pos, seg_rows);
+  LLP_LAUNCH_CHECK();
+  const int64_t ubound = R < num_nodes ? R : num_nodes;
+  const int64_t g = std::min<int64_t>((ubound + SS_T - 1) / SS_T, 4096);
+  hipLaunchKernelGGL(segsort_all_kernel, dim3((unsigned)g), dim3(SS_T), 0, s, n_unique, seg_ptr, seg_rows, rank);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

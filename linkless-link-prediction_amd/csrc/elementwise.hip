@@ -302,34 +302,6 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* 
   if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// One workgroup's agent-scope arrival on a launch's ticket (cdna_hip_programming.md §5 "In-launch
-// split-K reduction"): every store of this workgroup that the last arriver reads was made by
-// thread 0 (drained and released here); true in the LAST workgroup to arrive, which has acquired
-// and returned the ticket to zero.  Called by every thread.
-__device__ __forceinline__ bool arrive_last(uint32_t* ticket, uint32_t n_blocks) {
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == n_blocks - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  return last != 0;
-}
-
-// a value another workgroup of this launch stored: a vector load behind the acquire
-__device__ __forceinline__ float load_handed(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT));
-}
-
 template <bool HANDOFF>
 __device__ __forceinline__ void grad_sumsq_finalize_block(const llp_tensor_desc* __restrict__ descs, int n_tensors,
                                                           int64_t max_chunks, const float* partial, int n_groups,
@@ -344,7 +316,7 @@ __device__ __forceinline__ void grad_sumsq_finalize_block(const llp_tensor_desc*
     const int64_t nch = (descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK;
     double ts = 0.0;
     for (int64_t c = threadIdx.x; c < nch; c += blockDim.x)
-      ts += (double)(HANDOFF ? load_handed(partial + t * max_chunks + c) : partial[t * max_chunks + c]);
+      ts += (double)(HANDOFF ? llp_load_handed(partial + t * max_chunks + c) : partial[t * max_chunks + c]);
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (k == gidx) gs[k] += ts;
@@ -387,7 +359,7 @@ __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-  if (arrive_last(ticket, gridDim.x * gridDim.y))
+  if (llp_arrive_last(ticket, gridDim.x * gridDim.y))
     grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
@@ -632,7 +604,7 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
       }
     }
   }
-  if (arrive_last(ticket, gridDim.x * gridDim.y) && threadIdx.x == 0) *step += 1;
+  if (llp_arrive_last(ticket, gridDim.x * gridDim.y) && threadIdx.x == 0) *step += 1;
 }
 
 __global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __restrict__ descs) {

@@ -118,3 +118,33 @@ __device__ __forceinline__ int64_t llp_xcd_block(int64_t bid, int64_t nblocks) {
   const int64_t xcd = bid % 8, loc = bid / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
+
+// One workgroup's agent-scope arrival on a launch-wide ticket (cdna_hip_programming.md §5 "In-launch
+// split-K reduction", Guideline 16): every store of this workgroup that the last arriver reads must
+// have been made by its thread 0 (drained and released here).  Returns true in the LAST workgroup
+// to arrive, which has acquired and returned the ticket to zero (so a ticket zeroed once at
+// allocation stays valid call after call, graph replays included).  Called by every thread.
+__device__ __forceinline__ bool llp_arrive_last(uint32_t* ticket, uint32_t n_blocks) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == n_blocks - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// a 32-bit word another workgroup of this launch stored: a vector load behind the acquire
+// (never the scalar path, Guideline 16 Pitfall 6)
+__device__ __forceinline__ float llp_load_handed(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}

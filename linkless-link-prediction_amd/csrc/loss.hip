@@ -186,9 +186,7 @@ __device__ __forceinline__ void loss_finalize_block(const float* partial, int64_
     for (int k = 0; k < 3; ++k) {
       // partials of other workgroups of this launch: vector loads behind the acquire (never the
       // scalar path, cdna_hip_programming.md Guideline 16 Pitfall 6)
-      const float v = HANDOFF ? __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(partial) + i * 3 + k,
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                              : partial[i * 3 + k];
+      const float v = HANDOFF ? llp_load_handed(partial + i * 3 + k) : partial[i * 3 + k];
       a[k] += (double)v;
     }
   for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = a[k];
@@ -238,22 +236,7 @@ __global__ __launch_bounds__(256) void llp_loss_kernel(LossArgs a) {
     bce_block(blk - a.nba, a.n_lab, a.n_pos, a.out_logit, a.hs, a.lab_row0, a.n_lab_total, a.neg_count,
               a.neg_offset, a.pos_total, a.w_label, a.loss_scale, a.dlogit_lab, a.partial + a.nba * 3);
   if (!a.ticket) return;
-  __shared__ int last;
-  if (threadIdx.x == 0) {   // the lane that stored this block's partials
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t nb = (uint32_t)(a.nba + a.nbl);
-    const uint32_t old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == nb - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  if (!last) return;
+  if (!llp_arrive_last(a.ticket, (uint32_t)(a.nba + a.nbl))) return;
   loss_finalize_block<true>(a.partial, a.nba + a.nbl, a.w_label, a.w_d, a.w_r, a.terms, a.accumulate);
 }
 

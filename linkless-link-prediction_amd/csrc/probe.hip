@@ -42,7 +42,43 @@ __global__ __launch_bounds__(PROBE_THREADS) void mfma_probe_kernel(const uint4* 
   out[t] = s;
 }
 
+// The f32 counterpart (v_mfma_f32_16x16x4_f32, the fp32 GEMMs' instruction, gemm.hip): four
+// random f32 A and B operands per lane, 16 MFMAs per iteration into 8 accumulators.
+__global__ __launch_bounds__(PROBE_THREADS) void mfma_probe_f32_kernel(const float* __restrict__ data, int64_t n,
+                                                                       int64_t iters, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * PROBE_THREADS + threadIdx.x;
+  float a[4], b[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = data[(8 * t + i) % n];
+    b[i] = data[(8 * t + 4 + i) % n];
+  }
+  float4_t acc[PROBE_ACC];
+#pragma unroll
+  for (int j = 0; j < PROBE_ACC; ++j) acc[j] = float4_t{0.f, 0.f, 0.f, 0.f};
+  for (int64_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      acc[j & 7] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j & 3], b[(j >> 2) ^ (j & 1)], acc[j & 7], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < PROBE_ACC; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  out[t] = s;
+}
+
 }  // namespace
+
+extern "C" int llp_mfma_probe_f32(const float* data, int64_t n, int64_t iters, float* out, double* flops,
+                                  void* stream) {
+  LLP_CHECK_ARG(data && out && flops && n >= 8 && iters >= 0, "llp_mfma_probe_f32: arguments");
+  const int cus = llp_cu_count();
+  *flops = (double)cus * (PROBE_THREADS / 64) * (double)iters * 16 * (16.0 * 16.0 * 4.0 * 2.0);
+  hipLaunchKernelGGL(mfma_probe_f32_kernel, dim3((unsigned)cus), dim3(PROBE_THREADS), 0, (hipStream_t)stream, data,
+                     n, iters, out);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
 
 extern "C" int llp_mfma_probe(const void* data, int64_t n_u4, int64_t iters, float* out, double* flops,
                               void* stream) {

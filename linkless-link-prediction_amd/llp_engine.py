@@ -320,6 +320,14 @@ class EngineBase:
     def _ws(self, name, nbytes):
         return self._buf(name, (nbytes // 4 + 16,), torch.float32)
 
+    def _dedup_ws(self, name, num_nodes, R):
+        """The llp_dedup_rows2 workspace of one call site (its state persists between steps)."""
+        d = self.__dict__.setdefault("_dedup_wss", {})
+        w = d.get(name)
+        if w is None or not w.fits(num_nodes, R):
+            w = d[name] = K.DedupWorkspace(num_nodes, R, self.dev)
+        return w
+
     def _splitk_plan(self, M, N, Kd):
         """Split count of the bf16 split-K GEMM for this shape (1: the plain GEMM), cached."""
         if self.dtype != torch.bfloat16:
@@ -508,7 +516,7 @@ class EngineBase:
     def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
         """d(loss)/dh of the predictor input h[ia] * h[ib] into ``out`` [N, H] (compute dtype, or f32),
         deterministically: the 2R endpoint rows tgt = [ia | ib] are grouped by node
-        (llp_dedup_rows), and one pass per node (llp_hadamard_bwd_segments in the label-row
+        (llp_dedup_rows2), and one pass per node (llp_hadamard_bwd_segments in the label-row
         layout, B = C = 0) forms each of its rows' gradient dZ[r] * h[partner] as the row
         kernel would store it and sums them in row order (f32) into its row of ``out``
         (drow: the 'inner' predictor's scalar); other rows are 0.  Bit-identical to
@@ -528,9 +536,15 @@ class EngineBase:
         n_u = self._buf("hb_nu", (1,), torch.int32)
         seg_ptr = self._buf("hb_segp", (R2 + 1,), torch.int32)
         seg_rows = self._buf("hb_segr", (R2,), torch.int32)
-        wsd = self._buf("hb_ws", (K.dedup_ws_bytes(N, R2) // 4 + 16,), torch.float32)
-        K.dedup_rows(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
-        out.zero_()
+        # the rows of nodes no pair touches are zeroed by the compaction's pass over the nodes
+        # (no fill of the whole [N, H] before the per-node sums overwrite nearly all of it)
+        rb = out.element_size()
+        zfill = (out.dim() == 2 and out.stride(1) == 1 and (out.stride(0) * rb) % 16 == 0
+                 and (out.shape[1] * rb) % 16 == 0 and out.data_ptr() % 16 == 0)
+        K.dedup_rows2(N, R2, tgt, uniq, pos, n_u, seg_ptr, seg_rows, self._dedup_ws("hb", N, R2),
+                      zero_rows=out if zfill else None)
+        if not zfill:
+            out.zero_()
         K.hadamard_bwd_segments(min(R2, N), 0, 0, R, H, seg_ptr, seg_rows, tgt, dZ, h, out, None, drow=drow,
                                 count=n_u, out_rows=uniq)
 
@@ -894,8 +908,7 @@ class DistillEngine(EngineBase):
             n_u = self._buf("n_unique", (1,), torch.int32)
             seg_ptr = self._buf("seg_ptr", (R1 + 1,), torch.int32)
             seg_rows = self._buf("seg_rows", (R1,), torch.int32)
-            wsd = self._buf("ws_dedup", (K.dedup_ws_bytes(self.N, R1) // 4 + 16,), torch.float32)
-            K.dedup_rows(self.N, R1, target, uniq, pos, n_u, seg_ptr, seg_rows, wsd)
+            K.dedup_rows2(self.N, R1, target, uniq, pos, n_u, seg_ptr, seg_rows, self._dedup_ws("mb", self.N, R1))
             self._dbg_cut("sample + dedup")
             if owner:   # the rows ARE the pairs' ends: row k and row R2 + k
                 ia_h, ib_h = pos[:R2], pos[R2:R1]

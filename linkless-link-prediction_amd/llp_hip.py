@@ -84,6 +84,10 @@ _SIGS = {
     "llp_hadamard_bwd_blocks": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_dedup_rows_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_dedup_rows": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "llp_dedup_rows2_state_bytes": (c_i64, [c_i64]),
+    "llp_dedup_rows2_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "llp_dedup_rows2": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp,
+                                c_i64, c_vp]),
     "llp_segment_sum_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_int, c_vp, c_vp,
                                      c_vp]),
     "llp_hadamard_bwd_segments": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -136,6 +140,7 @@ _SIGS = {
     "llp_sigmoid_bwd": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_mfma_probe": (c_int, [c_vp, c_i64, c_i64, c_vp, C.POINTER(c_f64), c_vp]),
     "llp_mfma_probe_out_floats": (c_i64, []),
+    "llp_mfma_probe_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, C.POINTER(c_f64), c_vp]),
     "llp_norm_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_norm_colsums": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_norm_fwd": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_int, c_vp, c_f64, c_f32,
@@ -390,6 +395,39 @@ def dedup_rows(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, ws)
     check(L.llp_dedup_rows(num_nodes, R, target.data_ptr(), uniq.data_ptr(), pos.data_ptr(), n_unique.data_ptr(),
                            seg_ptr.data_ptr(), seg_rows.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
                            stream_ptr()), "llp_dedup_rows")
+
+
+class DedupWorkspace:
+    """The workspace of llp_dedup_rows2 for one num_nodes, with the clean-state bookkeeping:
+    the first call zeroes the persistent state, later calls vouch for it."""
+
+    def __init__(self, num_nodes, R, device):
+        import torch
+        self.num_nodes = int(num_nodes)
+        self.R = int(R)
+        nbytes = load().llp_dedup_rows2_workspace_bytes(self.num_nodes, self.R)
+        self.buf = torch.empty(nbytes // 4 + 16, dtype=torch.float32, device=device)
+        self.clean = False
+
+    def fits(self, num_nodes, R):
+        return int(num_nodes) == self.num_nodes and int(R) <= self.R
+
+    def error_word(self):
+        """Word [2] of the control block (nonzero: a look-back timed out)."""
+        off = load().llp_dedup_rows2_state_bytes(self.num_nodes) - 256
+        return self.buf.view(-1)[off // 4 + 2].view(__import__("torch").int32)
+
+
+def dedup_rows2(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, dws, zero_rows=None):
+    """llp_dedup_rows2 (four launches, same outputs as dedup_rows) on a DedupWorkspace;
+    zero_rows (2-D, may be None): rows of nodes absent from target are zeroed."""
+    L = lib()
+    zr = 0 if zero_rows is None else zero_rows.stride(0) * zero_rows.element_size()
+    zb = 0 if zero_rows is None else zero_rows.shape[1] * zero_rows.element_size()
+    check(L.llp_dedup_rows2(num_nodes, R, ptr(target), ptr(uniq), ptr(pos), ptr(n_unique), ptr(seg_ptr),
+                            ptr(seg_rows), ptr(zero_rows), zr, zb, int(dws.clean), dws.buf.data_ptr(),
+                            dws.buf.numel() * dws.buf.element_size(), stream_ptr()), "llp_dedup_rows2")
+    dws.clean = True
 
 
 def segment_sum_rows(U, seg_ptr, rows, src, out, count=None, out_rows=None):
@@ -742,6 +780,15 @@ def mfma_probe(data, iters, out):
     fl = c_f64(0.0)
     check(L.llp_mfma_probe(data.data_ptr(), data.numel() * data.element_size() // 16, int(iters), out.data_ptr(),
                            C.byref(fl), stream_ptr()), "llp_mfma_probe")
+    return fl.value
+
+
+def mfma_probe_f32(data, iters, out):
+    """The f32-MFMA ceiling loop (llp_mfma_probe_f32) over the f32 tensor ``data``; returns its FLOP count."""
+    L = lib()
+    fl = c_f64(0.0)
+    check(L.llp_mfma_probe_f32(data.data_ptr(), data.numel(), int(iters), out.data_ptr(), C.byref(fl), stream_ptr()),
+          "llp_mfma_probe_f32")
     return fl.value
 
 

@@ -747,6 +747,55 @@ def test_dedup_rows_and_segment_sum(N, R, hub):
     assert np.array_equal(o.cpu().numpy(), inv[idx.numpy()])
 
 
+@pytest.mark.parametrize("N,R,hot,hub", [(235868, 747214, 2000, 0.0), (3000, 40000, 0, 0.3), (50, 1000, 0, 0.0),
+                                         (7, 7, 0, 0.0), (31044, 263_000, 0, 0.0), (200_000, 5, 0, 0.0)])
+def test_dedup_rows2_four_launches(N, R, hot, hub):
+    """llp_dedup_rows2 (counts, one look-back scan + compaction pass, scatter, one fused segment
+    sort) == the stable sort's outputs, on one workspace over five calls with fresh targets
+    (the persistent counts / epoch-tagged flags / ticket must come back clean each time, and the
+    first call zeroes them), the rows of absent nodes zeroed, the others untouched, and the
+    look-back's error word clear.  Hot / hub cases put 33..1024-row and 12k-row segments on
+    neighbouring ids (the wave and block sorts inside the one launch)."""
+    k = K()
+    g = torch.Generator().manual_seed(N + R)
+    dws = k.DedupWorkspace(N, R, DEV)
+    H = 24
+    for call in range(5):
+        target = torch.randint(0, N, (R,), generator=g, dtype=torch.int32)
+        if hot:
+            target[: R // 4] = torch.randint(0, hot, (R // 4,), generator=g, dtype=torch.int32)
+        if hub:
+            u = torch.rand(R, generator=g)
+            target[u < hub] = 7
+            for j, v in enumerate(range(11, 16)):
+                lo = hub + 0.02 * j
+                target[(u >= lo) & (u < lo + 0.02)] = v
+        tg = target.to(DEV)
+        uniq = torch.empty(R, dtype=torch.int32, device=DEV)
+        pos = torch.empty(R, dtype=torch.int32, device=DEV)
+        nu = torch.empty(1, dtype=torch.int32, device=DEV)
+        segp = torch.empty(R + 1, dtype=torch.int32, device=DEV)
+        segr = torch.empty(R, dtype=torch.int32, device=DEV)
+        rows = torch.full((N, H), 5.0, device=DEV, dtype=torch.bfloat16)
+        k.dedup_rows2(N, R, tg, uniq, pos, nu, segp, segr, dws, zero_rows=rows if call % 2 == 0 else None)
+        torch.cuda.synchronize()
+        assert int(dws.error_word().item()) == 0
+        u_ref, inv = np.unique(target.numpy(), return_inverse=True)
+        U = int(nu.item())
+        assert U == u_ref.size, call
+        assert np.array_equal(uniq[:U].cpu().numpy(), u_ref), call
+        assert np.array_equal(pos.cpu().numpy(), inv), call
+        assert np.array_equal(segr.cpu().numpy(), np.argsort(inv, kind="stable")), call
+        assert np.array_equal(segp[:U + 1].cpu().numpy(), np.concatenate([[0], np.cumsum(np.bincount(inv))])), call
+        present = np.zeros(N, dtype=bool)
+        present[u_ref] = True
+        r = rows.float().cpu().numpy()
+        if call % 2 == 0:
+            assert (r[~present] == 0).all() and (r[present] == 5).all(), call
+        else:
+            assert (r == 5).all(), call
+
+
 @pytest.mark.parametrize("dtype,F", [(torch.bfloat16, 128), (torch.bfloat16, 13), (torch.float32, 37)])
 def test_gather_rows(dtype, F):
     """llp_gather_rows: out[r] = x[idx[r]] bit-exact, rows past the device count untouched
