@@ -408,6 +408,20 @@ int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys, int64_t n_
                          int64_t sample_size, int rounds, uint64_t seed, const int64_t* step_ctr,
                          int64_t stream_offset, int32_t* out, int64_t ld_out, int32_t* count,
                          void* workspace, int64_t workspace_bytes, void* stream);
+/* llp_neg_sample_dense in two launches (the same outputs): the candidates, then ONE pass
+ * that counts, scans (decoupled look-back over tiles) and scatters.  The candidates' set and
+ * the look-back flags persist in the workspace (llp_neg_sample_dense2_workspace_bytes,
+ * its first llp_neg_sample_dense2_state_bytes bytes) tagged with a per-call epoch instead of
+ * being cleared each call; state_clean = 1 vouches that a previous call with the same
+ * max_candidates left them (or that they are zero), 0 clears them first (one more launch).
+ * Needs N(N-1) < 2^40. */
+int64_t llp_neg_sample_dense2_state_bytes(int64_t max_candidates);
+int64_t llp_neg_sample_dense2_workspace_bytes(int64_t max_candidates);
+int llp_neg_sample_dense2(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys,
+                          const uint64_t* edge_table, int64_t edge_table_size, int64_t num_neg,
+                          int64_t sample_size, int rounds, uint64_t seed, const int64_t* step_ctr,
+                          int64_t stream_offset, int32_t* out, int64_t ld_out, int32_t* count,
+                          int state_clean, void* workspace, int64_t workspace_bytes, void* stream);
 /* The graph's edge keys (PyG's dense encoding, as edge_keys above) in an open-addressing
  * set of llp_edge_table_size(n_keys) slots (a power of two), built once per graph; passed
  * to llp_neg_sample_dense as edge_table (edge_keys may then be NULL), a candidate's

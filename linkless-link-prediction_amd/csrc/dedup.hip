@@ -722,24 +722,6 @@ __global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __rest
 // by every call (counts reset by the scan, the ticket by its last workgroup, the flags tagged with a
 // per-call epoch that the last workgroup advances).
 constexpr int LB_T = 256, LB_I = 8, LB_B = LB_T * LB_I;   // nodes per scan block: 2,048
-constexpr uint32_t LB_AGG = 1u, LB_INC = 2u;               // flag status: aggregate / inclusive prefix
-constexpr uint32_t LB_SPIN_LIMIT = 1u << 22;               // bounded spin: a missing publisher sets an error
-
-__device__ __forceinline__ uint32_t lb_flag_wait(const uint32_t* flag, uint32_t epoch, uint32_t* err) {
-  uint32_t f = 0;
-  for (uint32_t it = 0;; ++it) {
-    f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((f >> 2) == (epoch & 0x3FFFFFFFu) && (f & 3u)) break;
-    if (it > LB_SPIN_LIMIT) {   // never seen: a publisher that did not run (report, do not hang)
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return LB_INC;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return f & 3u;
-}
-
 struct ScanArgs {
   int64_t N, R;
   int32_t* cnt;                 // [N] per-node counts (zeroed here after use)
@@ -754,7 +736,6 @@ struct ScanArgs {
 
 __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
   __shared__ unsigned long long ts[LB_T];
-  __shared__ unsigned long long excl_s;
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const uint32_t epoch = a.ctl[0] + 1u;   // read by every workgroup before its ticket add
@@ -777,48 +758,9 @@ __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
     __syncthreads();
   }
   const unsigned long long blk_sum = ts[LB_T - 1];
-  // publish this block's aggregate (block 0: its inclusive prefix), then look back
-  if (t == 0) {
-    if (b == 0) {
-      __hip_atomic_store(&a.incl[0], blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(&a.flags[0], (epoch << 2) | LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      excl_s = 0ull;
-    } else {
-      __hip_atomic_store(&a.agg[b], blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(&a.flags[b], (epoch << 2) | LB_AGG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (b > 0 && t < 64) {   // wave 0: 64 predecessors per window, nearest first
-    unsigned long long acc = 0;
-    for (int64_t j0 = b - 1;; j0 -= 64) {
-      const int64_t j = j0 - t;
-      uint32_t st = 0;
-      unsigned long long val = 0;
-      if (j >= 0) {
-        st = lb_flag_wait(&a.flags[j], epoch, &a.ctl[2]);
-        val = __hip_atomic_load(st == LB_INC ? &a.incl[j] : &a.agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      // the nearest lane holding an inclusive prefix (block 0 always does) ends the look-back
-      const unsigned long long inc_mask = __ballot(j >= 0 && st == LB_INC);
-      const int stop = inc_mask ? __builtin_ctzll(inc_mask) : 64;
-      unsigned long long part = t <= stop && j >= 0 ? val : 0ull;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      acc += part;
-      if (inc_mask || j0 - 64 < 0) break;
-    }
-    if (t == 0) {
-      excl_s = acc;
-      __hip_atomic_store(&a.incl[b], acc + blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(&a.flags[b], (epoch << 2) | LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
+  const unsigned long long excl = llp_lookback_u64(a.flags, a.agg, a.incl, b, blk_sum, epoch, &a.ctl[2]);
   // compaction (compact_count_kernel's writes), counts back to zero, absent nodes' rows zeroed
-  unsigned long long run = excl_s + ts[t] - s;
+  unsigned long long run = excl + ts[t] - s;
 #pragma unroll
   for (int i = 0; i < LB_I; ++i) {
     const int64_t node = base + i;

@@ -204,6 +204,112 @@ __global__ __launch_bounds__(256) void neg_tile_scatter(int64_t M, int64_t num_n
   }
 }
 
+// ---------------------------------------------------------------- dense negatives in two launches
+// (llp_neg_sample_dense2; the same outputs as llp_neg_sample_dense): the candidates' table and the
+// tile scan's look-back flags persist in the workspace with a per-call epoch instead of being
+// reset every call (neg_table_init), and the tile count / scan / scatter run as ONE pass with a
+// decoupled look-back.  Table entry = (epoch & 0xFFFFFF) << 40 | candidate value (values < 2^40):
+// an entry of another epoch is free; a stale entry that happens to carry the current tag is
+// only ever taken as occupied (a wasted slot) or as the same value, which the first-index word
+// (epoch << 32 | ~index, atomicMax) then claims correctly.
+constexpr int64_t NEG2_VALUE_BITS = 40;
+constexpr uint64_t NEG2_VALUE_MASK = (1ull << NEG2_VALUE_BITS) - 1;
+
+__global__ void neg_candidates2(int64_t M, int enumerate_all, uint64_t population, uint64_t seed,
+                                const int64_t* __restrict__ step_ctr, int64_t stream_offset,
+                                const int64_t* __restrict__ edge_keys, int64_t n_keys,
+                                const uint64_t* __restrict__ edge_table, int64_t edge_table_size,
+                                int64_t* __restrict__ cand, int32_t* __restrict__ slot, uint64_t* __restrict__ tkeys,
+                                unsigned long long* __restrict__ tfirst, int64_t T, const uint32_t* __restrict__ ctl) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const uint32_t epoch = ctl[0] + 1u;
+  const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << NEG2_VALUE_BITS;
+  uint64_t c;
+  if (enumerate_all) {
+    c = (uint64_t)(i % (int64_t)population);
+  } else {
+    const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * (*step_ctr) + stream_offset);
+    const uint64_t lo = philox_u32(seed, stream, 2 * (uint64_t)i);
+    const uint64_t hi = philox_u32(seed, stream, 2 * (uint64_t)i + 1);
+    c = __umul64hi((hi << 32) | lo, population);
+  }
+  cand[i] = (int64_t)c;
+  if (edge_table ? in_table(edge_table, edge_table_size, c) : in_sorted(edge_keys, n_keys, (int64_t)c)) {
+    slot[i] = -1;
+    return;
+  }
+  const unsigned long long mine = ((unsigned long long)epoch << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)i);
+  uint32_t h = mix32(c) & (uint32_t)(T - 1);
+  while (true) {
+    unsigned long long e = __hip_atomic_load((unsigned long long*)&tkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((e & ~NEG2_VALUE_MASK) != tag) {   // free in this epoch: claim it
+      const unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[h], e, (unsigned long long)(tag | c));
+      if (prev != e) continue;   // taken meanwhile: look at the same slot again
+      e = tag | c;
+    }
+    if ((e & NEG2_VALUE_MASK) == c) {
+      atomicMax(&tfirst[h], mine);
+      slot[i] = (int32_t)h;
+      return;
+    }
+    h = (h + 1) & (uint32_t)(T - 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void neg_compact2(int64_t M, int64_t num_nodes, int64_t num_neg,
+                                                    const int64_t* __restrict__ cand, const int32_t* __restrict__ slot,
+                                                    const unsigned long long* __restrict__ tfirst,
+                                                    uint32_t* flags, unsigned long long* agg, unsigned long long* incl,
+                                                    uint32_t* ctl, int32_t* __restrict__ out, int64_t ld_out,
+                                                    int32_t* __restrict__ count) {
+  __shared__ int wsum[4];
+  const uint32_t epoch = ctl[0] + 1u;
+  const int64_t b = blockIdx.x;
+  const int64_t i0 = b * NC_TILE + 4 * threadIdx.x;
+  int v[4], mine = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = i0 + k;
+    v[k] = 0;
+    if (i < M) {
+      const int32_t s = slot[i];
+      v[k] = (s >= 0 && tfirst[s] == (((unsigned long long)epoch << 32) |
+                                      (unsigned long long)(0xFFFFFFFFu - (uint32_t)i))) ? 1 : 0;
+    }
+    mine += v[k];
+  }
+  int total;
+  const int ex = block_excl_scan256(mine, wsum, &total);
+  const int64_t base = (int64_t)llp_lookback_u64(flags, agg, incl, b, (unsigned long long)total, epoch, &ctl[2]);
+  int64_t pos = base + ex;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (v[k]) {
+      if (pos < num_neg) {
+        const int64_t c = cand[i0 + k];
+        const int64_t r = c / (num_nodes - 1);
+        int64_t cc = c % (num_nodes - 1);
+        if (r <= cc) cc += 1;
+        out[pos] = (int32_t)r;
+        out[ld_out + pos] = (int32_t)cc;
+      }
+      ++pos;
+    }
+  }
+  // the last workgroup: the count (the last tile's inclusive prefix) and the next call's epoch
+  if (llp_arrive_last(&ctl[1], gridDim.x) && threadIdx.x == 0) {
+    const unsigned long long all = __hip_atomic_load(&incl[gridDim.x - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *count = (int32_t)(all < (unsigned long long)num_neg ? all : (unsigned long long)num_neg);
+    __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void zero_u32_kernel(int64_t n, uint32_t* __restrict__ p) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
 // ia/ib for the full-batch predictor rows: B*C context pairs (anchor, context)
 // then P positive and n_neg negative label pairs (train_edges, src/main.py:212).
 __global__ void fullbatch_pairs_kernel(int64_t B, int64_t C1, const int32_t* __restrict__ samples,
@@ -397,6 +503,79 @@ extern "C" int llp_neg_sample_dense(int64_t num_nodes, const int64_t* edge_keys,
                        tmin, tbase, out, ld_out);
     LLP_LAUNCH_CHECK();
   }
+  return LLP_OK;
+}
+
+static int64_t al256b(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+static int64_t neg2_state_bytes(int64_t M) {
+  const int64_t T = pow2_at_least(2 * (M > 0 ? M : 1));
+  const int64_t ntiles = (M + NC_TILE - 1) / NC_TILE;
+  return al256b(T * 8) + al256b(T * 8) + al256b(ntiles * 4) + 256;
+}
+
+extern "C" int64_t llp_neg_sample_dense2_state_bytes(int64_t max_candidates) { return neg2_state_bytes(max_candidates); }
+
+extern "C" int64_t llp_neg_sample_dense2_workspace_bytes(int64_t max_candidates) {
+  const int64_t ntiles = (max_candidates + NC_TILE - 1) / NC_TILE;
+  return neg2_state_bytes(max_candidates) + 2 * al256b(ntiles * 8) + al256b(max_candidates * 8) +
+         al256b(max_candidates * 4);
+}
+
+extern "C" int llp_neg_sample_dense2(int64_t num_nodes, const int64_t* edge_keys, int64_t n_keys,
+                                     const uint64_t* edge_table, int64_t edge_table_size, int64_t num_neg,
+                                     int64_t sample_size, int rounds, uint64_t seed, const int64_t* step_ctr,
+                                     int64_t stream_offset, int32_t* out, int64_t ld_out, int32_t* count,
+                                     int state_clean, void* workspace, int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(out && count && workspace && step_ctr, "llp_neg_sample_dense2: null pointer");
+  LLP_CHECK_ARG(num_nodes >= 2 && num_nodes < (1ll << 31), "llp_neg_sample_dense2: num_nodes out of range");
+  LLP_CHECK_ARG(n_keys == 0 || edge_keys || edge_table, "llp_neg_sample_dense2: null edge keys");
+  LLP_CHECK_ARG(!edge_table || (edge_table_size > 0 && (edge_table_size & (edge_table_size - 1)) == 0),
+                "llp_neg_sample_dense2: edge_table_size must be a power of two");
+  LLP_CHECK_ARG(rounds >= 1 && sample_size >= 0 && num_neg >= 0 && ld_out >= num_neg,
+                "llp_neg_sample_dense2: bad sizes");
+  const uint64_t population = (uint64_t)num_nodes * (uint64_t)(num_nodes - 1);
+  LLP_CHECK_ARG(population <= NEG2_VALUE_MASK, "llp_neg_sample_dense2: N(N-1) >= 2^40 (use llp_neg_sample_dense)");
+  hipStream_t s = (hipStream_t)stream;
+  const int enumerate_all = population <= (uint64_t)sample_size;
+  const int64_t M = enumerate_all ? (int64_t)population : (int64_t)rounds * sample_size;
+  LLP_CHECK_ARG(M < (1ll << 31), "llp_neg_sample_dense2: too many candidates");
+  LLP_CHECK_ARG(workspace_bytes >= llp_neg_sample_dense2_workspace_bytes(M), "llp_neg_sample_dense2: workspace");
+  const int64_t T = pow2_at_least(2 * (M > 0 ? M : 1));
+  const int64_t ntiles = (M + NC_TILE - 1) / NC_TILE;
+  char* w = reinterpret_cast<char*>(workspace);
+  if (!state_clean) {
+    const int64_t n32 = neg2_state_bytes(M) / 4;
+    hipLaunchKernelGGL(zero_u32_kernel, dim3(ceil_div_u(n32, 256)), dim3(256), 0, s, n32, (uint32_t*)w);
+    LLP_LAUNCH_CHECK();
+  }
+  uint64_t* tkeys = reinterpret_cast<uint64_t*>(w);
+  w += al256b(T * 8);
+  unsigned long long* tfirst = reinterpret_cast<unsigned long long*>(w);
+  w += al256b(T * 8);
+  uint32_t* flags = reinterpret_cast<uint32_t*>(w);
+  w += al256b(ntiles * 4);
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(w);
+  w += 256;
+  unsigned long long* agg = reinterpret_cast<unsigned long long*>(w);
+  w += al256b(ntiles * 8);
+  unsigned long long* incl = reinterpret_cast<unsigned long long*>(w);
+  w += al256b(ntiles * 8);
+  int64_t* cand = reinterpret_cast<int64_t*>(w);
+  w += al256b(M * 8);
+  int32_t* slot = reinterpret_cast<int32_t*>(w);
+  if (M == 0) {   // nothing to draw: no negatives
+    hipLaunchKernelGGL(zero_u32_kernel, dim3(1), dim3(256), 0, s, (int64_t)1, (uint32_t*)count);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
+  hipLaunchKernelGGL(neg_candidates2, dim3(ceil_div_u(M, 256)), dim3(256), 0, s, M, enumerate_all, population, seed,
+                     step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size, cand, slot, tkeys, tfirst,
+                     T, (const uint32_t*)ctl);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(neg_compact2, dim3((unsigned)ntiles), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot, tfirst,
+                     flags, agg, incl, ctl, out, ld_out, count);
+  LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
 

@@ -148,3 +148,71 @@ __device__ __forceinline__ float llp_load_handed(const float* p) {
   return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
+
+// ---------------------------------------------------------------- single-pass scan (decoupled look-back)
+// Workgroup b of a launch publishes its aggregate, looks back over its predecessors' published
+// aggregates / inclusive prefixes (64 per window, one wave) and publishes its inclusive prefix;
+// returns its exclusive prefix to every thread.  flags[b] = (epoch << 2) | status (1 aggregate,
+// 2 inclusive): the epoch tags one call, so the flags never need resetting (the caller advances
+// the epoch once per call).  Waits only on lower-numbered workgroups, which the dispatcher starts
+// first on each XCD; spins are bounded (a publisher never seen sets *err and the result is
+// invalid, the launch does not hang).  u64 sums: any association gives the same result.
+constexpr uint32_t LLP_LB_AGG = 1u, LLP_LB_INC = 2u;
+
+__device__ __forceinline__ uint32_t llp_lb_wait(const uint32_t* flag, uint32_t epoch, uint32_t* err) {
+  uint32_t f = 0;
+  for (uint32_t it = 0;; ++it) {
+    f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((f >> 2) == (epoch & 0x3FFFFFFFu) && (f & 3u)) break;
+    if (it > (1u << 22)) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return LLP_LB_INC;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return f & 3u;
+}
+
+__device__ __forceinline__ unsigned long long llp_lookback_u64(uint32_t* flags, unsigned long long* agg,
+                                                               unsigned long long* incl, int64_t b,
+                                                               unsigned long long blk_sum, uint32_t epoch,
+                                                               uint32_t* err) {
+  __shared__ unsigned long long lb_excl;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    __hip_atomic_store(b == 0 ? &incl[0] : &agg[b], blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&flags[b], (epoch << 2) | (b == 0 ? LLP_LB_INC : LLP_LB_AGG), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (b == 0) lb_excl = 0ull;
+  }
+  if (b > 0 && t < 64) {   // wave 0: 64 predecessors per window, nearest first
+    unsigned long long acc = 0;
+    for (int64_t j0 = b - 1;; j0 -= 64) {
+      const int64_t j = j0 - t;
+      uint32_t st = 0;
+      unsigned long long val = 0;
+      if (j >= 0) {
+        st = llp_lb_wait(&flags[j], epoch, err);
+        val = __hip_atomic_load(st == LLP_LB_INC ? &incl[j] : &agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // the nearest predecessor holding an inclusive prefix (workgroup 0 always does) ends it
+      const unsigned long long inc_mask = __ballot(j >= 0 && st == LLP_LB_INC);
+      const int stop = inc_mask ? __builtin_ctzll(inc_mask) : 64;
+      unsigned long long part = (t <= stop && j >= 0) ? val : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      acc += part;
+      if (inc_mask || j0 - 64 < 0) break;
+    }
+    if (t == 0) {
+      lb_excl = acc;
+      __hip_atomic_store(&incl[b], acc + blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&flags[b], (epoch << 2) | LLP_LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return lb_excl;
+}

@@ -411,9 +411,16 @@ class EngineBase:
             M = population if population <= ss else 3 * ss
             negg = self._buf("neg_all", (2, max(P_total, 1)), torch.int32)
             cnt = self._buf("neg_count", (1,), torch.int32)
-            ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
-            K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
-                               cnt, ws, edge_table=self._neg_table)
+            if population < (1 << 40):   # two launches, the sampler's state persisting between steps
+                d = self.__dict__.setdefault("_neg_wss", {})
+                if d.get("neg") is None or d["neg"].key != M:
+                    d["neg"] = K.StatefulWorkspace(K.neg_sample2_ws_bytes(M), M, self.dev)
+                K.neg_sample_dense2(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
+                                    cnt, d["neg"], edge_table=self._neg_table)
+            else:
+                ws = self._buf("ws_neg", (K.neg_sample_ws_bytes(M) // 4 + 16,), torch.float32)
+                K.neg_sample_dense(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
+                                   cnt, ws, edge_table=self._neg_table)
             if device_count:
                 return negg[:, p_offset:p_offset + P], P, None, cnt
             n_neg_total = int(cnt.item())

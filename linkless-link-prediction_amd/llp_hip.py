@@ -105,6 +105,10 @@ _SIGS = {
                                   c_vp]),
     "llp_pair_index_from_samples": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_neg_sample_dense_workspace_bytes": (c_i64, [c_i64]),
+    "llp_neg_sample_dense2_state_bytes": (c_i64, [c_i64]),
+    "llp_neg_sample_dense2_workspace_bytes": (c_i64, [c_i64]),
+    "llp_neg_sample_dense2": (c_int, [c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp,
+                                      c_i64, c_vp, c_int, c_vp, c_i64, c_vp]),
     "llp_neg_sample_dense": (c_int, [c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_int, c_u64, c_vp, c_i64, c_vp,
                                      c_i64, c_vp, c_vp, c_i64, c_vp]),
     "llp_edge_table_size": (c_i64, [c_i64]),
@@ -539,6 +543,35 @@ def neg_sample_dense(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr,
                                  sample_size, rounds, seed, step_ctr.data_ptr(), stream_offset, out.data_ptr(),
                                  out.stride(0), count.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
                                  stream_ptr()), "llp_neg_sample_dense")
+
+
+class StatefulWorkspace:
+    """A workspace whose leading state persists between calls of one llp_* entry point (the
+    two-launch dense sampler, ...): the first call clears it (state_clean = 0), later calls
+    vouch for it."""
+
+    def __init__(self, nbytes, key, device):
+        import torch
+        self.key = key
+        self.buf = torch.empty(int(nbytes) // 4 + 16, dtype=torch.float32, device=device)
+        self.clean = False
+
+
+def neg_sample_dense2(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr, stream_offset, out, count, sws,
+                      rounds=3, edge_table=None):
+    """llp_neg_sample_dense2 (two launches, the same outputs as neg_sample_dense) on a
+    StatefulWorkspace sized by neg_sample2_ws_bytes(max_candidates)."""
+    L = lib()
+    check(L.llp_neg_sample_dense2(num_nodes, ptr(edge_keys), 0 if edge_keys is None else edge_keys.numel(),
+                                  ptr(edge_table), 0 if edge_table is None else edge_table.numel(), num_neg,
+                                  sample_size, rounds, seed, step_ctr.data_ptr(), stream_offset, out.data_ptr(),
+                                  out.stride(0), count.data_ptr(), int(sws.clean), sws.buf.data_ptr(),
+                                  sws.buf.numel() * sws.buf.element_size(), stream_ptr()), "llp_neg_sample_dense2")
+    sws.clean = True
+
+
+def neg_sample2_ws_bytes(max_candidates):
+    return load().llp_neg_sample_dense2_workspace_bytes(max_candidates)
 
 
 def edge_table_build(edge_keys):

@@ -62,6 +62,20 @@ def test_neg_sample_dense_bit_exact(N, n_und, num_neg):
     if pop <= ss:   # enumerate branch: exactly PyG's (deterministic) result
         ref = O.negative_sampling_dense(torch.from_numpy(ei), N, num_neg).numpy()
         assert np.array_equal(got, ref)
+    # the two-launch form on one persistent workspace over several steps (epoch-tagged state:
+    # the first call clears it, later ones reuse it): the oracle's draws bit for bit each step
+    sws = K.StatefulWorkspace(K.neg_sample2_ws_bytes(M), M, DEV)
+    table = K.edge_table_build(keys_d)
+    for st in range(step, step + 4):
+        ctr.fill_(st)
+        exp = O.negative_sampling_dense_philox(ei, N, num_neg, seed, O.STREAMS_PER_STEP * st + off)
+        out2 = torch.full((2, num_neg), -1, dtype=torch.int32, device=DEV)
+        cnt2 = torch.full((1,), -5, dtype=torch.int32, device=DEV)
+        K.neg_sample_dense2(N, None, num_neg, ss, seed, ctr, off, out2, cnt2, sws, edge_table=table)
+        torch.cuda.synchronize()
+        n2 = int(cnt2.item())
+        assert n2 == exp.shape[1], st
+        assert np.array_equal(out2[:, :n2].cpu().numpy().astype(np.int64), exp), st
 
 
 def test_kd_terms_match_autograd():
