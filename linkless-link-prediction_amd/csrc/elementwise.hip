@@ -363,12 +363,14 @@ __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_
     grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
+// Every contraction written out (fmaf), so the arithmetic does not depend on which kernel the
+// compiler inlines it into (the one-launch and two-launch Adam agree bit for bit).
 __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float beta1, float beta2, float eps,
                                            float bc2s, float step_size) {
-  m = beta1 * m + (1.f - beta1) * g;
-  v = beta2 * v + (1.f - beta2) * g * g;
+  m = fmaf(beta1, m, (1.f - beta1) * g);
+  v = fmaf(beta2, v, ((1.f - beta2) * g) * g);
   const float denom = sqrtf(v) / bc2s + eps;
-  return p - step_size * (m / denom);
+  return fmaf(-step_size, m / denom, p);
 }
 
 // torch.optim.Adam (foreach=False semantics, see reference main.py:train_minibatch

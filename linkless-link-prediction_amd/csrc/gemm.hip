@@ -64,6 +64,7 @@ struct NTParams {
   const int64_t* drop_ctr;
   int64_t drop_stream;
   const int32_t* m_dev;  // device row count (llp_operand.rows_dev) or NULL
+  int64_t ngroups;       // column groups walked one after another (nt_groups): B panel per XCD's L2
 };
 
 struct TNParams {
@@ -185,7 +186,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
   const int64_t tilesM = (p.M + BM - 1) / BM;
   if ((int64_t)blockIdx.x >= tilesM * tilesN) return;
   const int64_t lt = xcd_remap(blockIdx.x, tilesM * tilesN);
-  const int64_t tm = lt / tilesN, tn = lt % tilesN;
+  // column group outermost (ngroups divides tilesN): the XCDs that take a group hold only its
+  // slice of B in L2 while the row panels stream past (f32 B of 4 MB thrashed a 4 MB L2 with
+  // the A panels: 3.4x A re-reads, profiles/r04_fp32_pmc_dominant.json)
+  const int64_t tnG = tilesN / p.ngroups, per = tilesM * tnG;
+  const int64_t grp = lt / per, rem = lt % per;
+  const int64_t tm = rem / tnG, tn = grp * tnG + rem % tnG;
   const int64_t m0 = tm * BM, n0 = tn * BN;
 
   // staging assignment: chunk c = tid + 256*i -> row (tid>>3) + 32*i, kc = tid&7
@@ -353,8 +359,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
   const int64_t ntile = tilesP * tilesQ;
   const int64_t splits = p.splits;
   const int64_t lt = xcd_remap(blockIdx.x, ntile * splits);
-  // the splits of one tile are adjacent in logical order -> tile = lt / splits
-  const int64_t tile = lt / splits, z = lt % splits;
+  // bf16: the splits of one tile are adjacent in logical order (tile = lt / splits); f32: the
+  // tiles of one split are (z = lt / ntile), so the workgroups an XCD runs together read the
+  // same m rows of A and B (one HBM read, served from L2 to every tile of the split)
+  const int64_t tile = BF ? lt / splits : lt % ntile, z = BF ? lt % splits : lt / ntile;
   const int64_t tp = tile / tilesQ, tq = tile % tilesQ;
   const int64_t p0 = tp * BM, q0 = tq * BN;
   if (p.m_dev) {   // live rows from the device count; the grid (splits) is the host M's
@@ -616,6 +624,15 @@ int64_t tn_splits(int dtype, int64_t M, int64_t P, int64_t Q) {
 
 }  // namespace
 
+// Column groups of the 128x128 NT kernel's tile walk: B (N x K) split into groups of at most
+// 2 MB, half an XCD's 4 MB L2, when the row panels are many (each group then re-reads A once).
+static int64_t nt_groups(int64_t N, int64_t K, int es, int64_t tilesM) {
+  const int64_t tilesN = (N + BN - 1) / BN;
+  int64_t g = 1;
+  while (g * 2 <= tilesN && tilesN % (g * 2) == 0 && N * K * es / g > (2ll << 20) && tilesM >= 64) g *= 2;
+  return g;
+}
+
 extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp_operand* A,
                            const llp_operand* B, void* C, int64_t ldc, int c_dtype, const float* bias,
                            int act, const void* aux, int64_t ld_aux, int aux_dtype, float alpha,
@@ -672,6 +689,7 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
                        "N %% 32 == 0, 16-byte aligned operands)");
   const int es = dtype == LLP_BF16 ? 2 : 4;
   const bool vec = aligned_op(A, es, K) && aligned_op(B, es, K);
+  p.ngroups = nt_groups(N, K, es, (M + BM - 1) / BM);
   dim3 grid((unsigned)tiles);
   if (dtype == LLP_BF16) {
     llp::note_kernel(vec ? "gemm_nt_kernel<bf16, vec> (128x128)" : "gemm_nt_kernel<bf16> (128x128)");

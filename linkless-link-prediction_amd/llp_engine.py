@@ -1220,8 +1220,10 @@ class DistillEngine(EngineBase):
                        t_prob_lab=t_r[BC:R2] if w_lm != 0.0 else None, n_lab_total=n_lab_total, w_lm=w_lm,
                        dlogit_lab=dlogit[BC:], B_rm=B if w_rm != 0.0 else 0, h=h, t_h=self.t_h, idx_rm=anchors,
                        B_rm_total=B_total, w_rm=w_rm, dh=None if grouped else dh32)
-        else:
+            self._kd_clear = False
+        elif not getattr(self, "_kd_clear", False):   # no KD terms: cleared once, not every step
             self.terms[4:6].zero_()
+            self._kd_clear = True
 
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)

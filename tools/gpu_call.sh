@@ -74,7 +74,7 @@ for RA in "$@"; do
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/tpmc_write -o run --output-format csv -- $S > $O/tpmc_write.log 2>&1 || fail tpmc-write $O/tpmc_write.log
       timeout -k 10 180 rocprofv3 --kernel-trace -d $O/tpmc_trace -o run --output-format csv -- $S > $O/tpmc_trace.log 2>&1 || fail tpmc-trace $O/tpmc_trace.log ;;
     sage-agg)       # every aggregate configuration, event-timed, with PMC passes
-      A="python tools/sage_bench.py --agg-only --iters 10"
+      A="python tools/sage_bench.py --agg-only --iters 10 --orders id,locality"
       timeout -k 10 180 $A > $O/sage_plan.json 2> $O/sage_plan.err || fail sage-plan $O/sage_plan.err
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/sage_fetch -o run --output-format csv -- $A > $O/sage_fetch.log 2>&1 || fail sage-fetch $O/sage_fetch.log
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/sage_write -o run --output-format csv -- $A > $O/sage_write.log 2>&1 || fail sage-write $O/sage_write.log ;;

@@ -22,15 +22,26 @@ import llp_teacher  # noqa: E402
 import models  # noqa: E402
 
 
-def agg_only(iters):
+def agg_only(iters, orders=("id",)):
     """Each configuration's launches in a fixed order: tools/pmc_kernels.py matches the
-    csr_agg dispatches of a PMC pass to it by position."""
+    csr_agg dispatches of a PMC pass to it by position.  order "locality": the graph's nodes
+    renumbered by llp_sage.locality_order first, as TeacherEngine runs them."""
     dev = torch.device("cuda", 0)
     data = llp_data.synthetic_collab(seed=0, with_eval=False)
     N = data.N
-    g = llp_sage.Graph(data.edge_index, N, dev)
-    E = g.num_edges
     plan = []
+    for order in orders:
+        ei = data.edge_index
+        if order == "locality":
+            _, pi = llp_sage.locality_order(ei, N)
+            ei = torch.from_numpy(pi[ei.numpy()])
+        g = llp_sage.Graph(ei, N, dev)
+        E = g.num_edges
+        _agg_configs(g, N, E, iters, dev, plan, order)
+    print(json.dumps({"N": N, "E": E, "plan": plan}))
+
+
+def _agg_configs(g, N, E, iters, dev, plan, order):
     for dts in ("fp32", "bf16"):
         dt = torch.float32 if dts == "fp32" else torch.bfloat16
         es = 4 if dts == "fp32" else 2
@@ -49,10 +60,9 @@ def agg_only(iters):
                 ms = s.elapsed_time(e) / iters
                 nbytes = E * F_ * es + 4 * E + 4 * (N + 1) + N * F_ * es + (4 * E if mode == "bwd" else 0)
                 compulsory = N * F_ * es + 4 * E + 4 * (N + 1) + N * F_ * es + (4 * N if mode == "bwd" else 0)
-                plan.append({"dtype": dts, "F": F_, "mode": mode, "launches": 3 + iters, "ms": ms,
+                plan.append({"order": order, "dtype": dts, "F": F_, "mode": mode, "launches": 3 + iters, "ms": ms,
                              "algorithmic_bytes": nbytes, "compulsory_bytes": compulsory,
                              "algorithmic_GBs": nbytes / (ms * 1e-3) / 1e9})
-    print(json.dumps({"N": N, "E": E, "plan": plan}))
 
 
 def main():
@@ -64,9 +74,10 @@ def main():
                     help="every aggregate configuration (fp32 / bf16, F 128 / 256, fwd / bwd), 3 warm-up + --iters "
                          "launches each, in the printed order (rocprofv3 --pmc passes), then exit")
     ap.add_argument("--no-agg", action="store_true", help="only the teacher step (kernel traces of it)")
+    ap.add_argument("--orders", default="id", help="--agg-only node orders, comma-separated: id, locality")
     opt = ap.parse_args()
     if opt.agg_only:
-        return agg_only(opt.iters)
+        return agg_only(opt.iters, tuple(opt.orders.split(",")))
     dev = torch.device("cuda", 0)
     dt = torch.float32 if opt.dtype == "fp32" else torch.bfloat16
     data = llp_data.synthetic_collab(seed=0, with_eval=False)
