@@ -1121,16 +1121,21 @@ extern "C" int llp_hadamard_bwd_segments(int dtype, int64_t U, int64_t B, int64_
   // one wave per node when a row is 64 * NCH 16-B chunks (1, 2, 4 or 8 per lane): 487 us at the
   // collab shape against 598 for the thread-group kernel below; two or four nodes per wave
   // measured 530 / 633 us (profiles/r02_seg_npw.txt)
+  // rows of 32 or 16 chunks (H = 256 / 128 bf16, the physics student): two / four nodes per wave,
+  // a 32- / 16-lane group each (the thread-group kernel below ran 117 us on the physics step)
   const int nch = (cpr % 64 == 0) ? (int)(cpr / 64) : 0;   // chunks per lane
-  if (nch == 1 || nch == 2 || nch == 4 || nch == 8) {
+  const int npw = cpr == 32 ? 2 : (cpr == 16 ? 4 : 1);     // nodes per wave for rows under 64 chunks
+  if (nch == 1 || nch == 2 || nch == 4 || nch == 8 || npw > 1) {
     auto launch = [&](auto kern, auto* dz, auto* hh, auto* ar, auto* out) {
-      hipLaunchKernelGGL(kern, dim3(ceil_div_u(U, 4)), dim3(256), 0, s, U, B, C, L2, H, seg_ptr, rows, pos, dz, drow,
-                         hh, ar, out, ld_dh, out_rows, u_dev);
+      hipLaunchKernelGGL(kern, dim3(ceil_div_u(U, 4 * npw)), dim3(256), 0, s, U, B, C, L2, H, seg_ptr, rows, pos, dz,
+                         drow, hh, ar, out, ld_dh, out_rows, u_dev);
     };
     auto pick = [&](auto* dz, auto* hh, auto* ar, auto* out) {
       using TT = std::remove_const_t<std::remove_pointer_t<decltype(dz)>>;
       using TO = std::remove_pointer_t<decltype(out)>;
-      if (nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 1, 8, 1>, dz, hh, ar, out);
+      if (npw == 2) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 1, 8, 2>, dz, hh, ar, out);
+      else if (npw == 4) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 1, 8, 4>, dz, hh, ar, out);
+      else if (nch == 1) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 1, 8, 1>, dz, hh, ar, out);
       else if (nch == 2) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 2, 4, 1>, dz, hh, ar, out);
       else if (nch == 4) launch(hadamard_bwd_segments_wave_kernel<TT, TO, 4, 2, 1>, dz, hh, ar, out);
       else launch(hadamard_bwd_segments_wave_kernel<TT, TO, 8, 1, 1>, dz, hh, ar, out);

@@ -874,7 +874,7 @@ def test_hadamard_bwd_segments(dtype, inner, N, H):
 
 @pytest.mark.parametrize("dtype,out_f32", [(torch.float32, False), (torch.bfloat16, False), (torch.bfloat16, True)])
 @pytest.mark.parametrize("inner", [False, True])
-@pytest.mark.parametrize("H", [256, 1024])
+@pytest.mark.parametrize("H", [128, 256, 1024])
 def test_hadamard_bwd_segments_label_rows_onto_nodes(dtype, out_f32, inner, H):
     """The full-batch form (DistillEngine._hadamard_bwd_nodes): B = C = 0, pos = [ia | ib]
     node ids, h the [N, H] node table, each node's sum written to row out_rows[u] = its
