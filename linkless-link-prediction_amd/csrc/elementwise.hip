@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) llp_store_handed(partial + blockIdx.y * max_chunks + blockIdx.x, red[0] + red[1] + red[2] + red[3]);
   if (llp_arrive_last(ticket, gridDim.x * gridDim.y))
     grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
@@ -606,6 +606,7 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
       }
     }
   }
+  __syncthreads();   // every wave of this workgroup past its use of *step
   if (llp_arrive_last(ticket, gridDim.x * gridDim.y) && threadIdx.x == 0) *step += 1;
 }
 

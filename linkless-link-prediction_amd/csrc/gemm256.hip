@@ -1138,10 +1138,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   // first tile: its K-tile 0 (all four chunks) into buffer 0
 #pragma unroll
   for (int j = 0; j < 4; ++j) issue_chunk(j, 0, m0, n0, 0);
-#ifdef LLP_PP8P_SHALLOW
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // chunks 0, 1 landed
-#endif
-  bool first = true;
   for (;;) {
     int64_t t_next = t + gridDim.x, m1 = 0, n1 = 0;
     const bool pf = next_tile(t_next, m1, n1);         // the next tile's K-tile 0 issued by this tile's last K-tile
@@ -1154,89 +1151,12 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
       if (p.bias && wu == 0) glds16(p.bias + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + BLDS)));
       if (HEAD && wu == 1) glds16(p.head_w + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + HWLDS)));
     }
-#ifndef LLP_PP8P_SHALLOW
-    // this tile's K-tile 1, chunks 0 and 1, into buffer 1 (its chunks 2 and 3 follow in
-    // K-tile 0's phases 0 and 1); buffer 1 was the previous epilogue's staging area, whose
-    // last reads the epilogue's final barrier ordered before this point
-    issue_chunk(0, 1, m0, n0, TK);
-    issue_chunk(1, 1, m0, n0, TK);
-    // first tile: K-tile 0 (and the bias / mask DMA) landed, K-tile 1's 4 pieces in flight;
-    // later tiles: K-tile 0 was waited for inside the previous epilogue
-    if (first) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-#endif
-    first = false;
     barrier();
     if (grp1) barrier();          // waves 4-7: one barrier behind from here on
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 8; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
-#ifndef LLP_PP8P_SHALLOW
-    // Deep schedule: chunks 2, 3 of K-tile kt+1 are issued in phases 0, 1 of K-tile kt
-    // (`i01`), chunks 0, 1 of K-tile kt+2 in phases 2, 3 (`i23`) -- two phases earlier than
-    // the shallow schedule, so an A chunk (streamed from HBM) has 4-5 phases to land
-    // instead of 2-3 and three half K-tiles are in flight at each wait (vmcnt(6) in the
-    // steady state, cdna_hip_programming.md "The 256² 8-phase template").
-    //   WAR: chunk j of K-tile kt+2 goes into the buffer K-tile kt is read from; its last
-    //   read there is phase 0 (chunks 0, 1), so the refill in phase 2 / 3 comes two and
-    //   three phases later: every read of phase p has retired (lgkmcnt(0) before the MFMA
-    //   segment of p, group 1 one barrier behind) before barrier 2p + 2, and a DMA of phase
-    //   q is issued after barrier 2q - 1 -- safe for q >= p + 2.  Chunks 2, 3 of K-tile kt+1
-    //   refill buffer (kt+1) & 1 in phases 0, 1 of kt, 3 phases after their last reads
-    //   (phases 1, 2 of kt-1).
-    //   RAW: a chunk read in phase p is waited for (each wave its own pieces, in issue
-    //   order) in phase p - 1, before the barrier that ends that LOAD segment for both
-    //   groups.  vmcnt(n) leaves the n youngest pieces in flight: the pieces issued after
-    //   the one waited for (2 per chunk).
-    //   Tile ends: the last K-tile issues the next tile's K-tile 0 chunks 2, 3 (its chunks
-    //   0, 1 came in phases 2, 3 of K-tile nk-2) and nothing in phases 2, 3 (buffer 1 is the
-    //   epilogue's staging area); the epilogue waits for all four (vmcnt(0) before its first
-    //   barrier), the next tile issues its K-tile 1 chunks 0, 1 above and skips the waits
-    //   of K-tile 0's phases 0, 1.
-    auto wait_vm = [&](int n) {   // n in {0, 2, 4, 6}: the pieces left in flight
-      if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    auto ktile = [&](int64_t kt, int pi23, int i01, int i23, int b01, int64_t t01m, int64_t t01n, int64_t k01,
-                     int b23, int64_t t23m, int64_t t23n, int64_t k23) {
-      const uint4* sA = smem + (int)(kt & 1) * TILE_U4;
-      const uint4* sB = sA + IMG_U4;
-      if (kt > 0) wait_vm(2 + 4 * pi23);       // chunk 2 of K-tile kt (issued in phase 0 of kt-1)
-      read_a(sA, 0);
-      read_b(sB, 0);
-      if (i01) issue_chunk(2, b01, t01m, t01n, k01);
-      barrier();
-      mfma_q(0, 0);
-      barrier();
-      if (kt > 0) wait_vm(4 * pi23 + 2 * i01);  // chunk 3 of K-tile kt
-      read_b(sB, 1);
-      if (i01) issue_chunk(3, b01, t01m, t01n, k01);
-      barrier();
-      mfma_q(0, 1);
-      barrier();
-      read_a(sA, 1);
-      if (i23) issue_chunk(0, b23, t23m, t23n, k23);
-      barrier();
-      mfma_q(1, 1);
-      barrier();
-      if (kt + 1 < nk) wait_vm(4 * i01 + 2 * i23);   // chunks 0, 1 of K-tile kt+1
-      if (i23) issue_chunk(1, b23, t23m, t23n, k23);
-      barrier();
-      mfma_q(1, 0);
-      barrier();
-    };
-    int pi23 = 1;   // K-tile kt-1 issued its phase 2 / 3 chunks (kt = 0: K-tile 1's, above)
-    for (int64_t kt = 0; kt < nk; ++kt) {
-      const bool x1 = kt + 1 < nk, x2 = kt + 2 < nk;
-      const int i01 = x1 || pf ? 1 : 0;                 // K-tile kt+1 or the next tile's K-tile 0
-      const int i23 = x2 || (kt + 2 == nk && pf) ? 1 : 0;
-      ktile(kt, pi23, i01, i23, x1 ? (int)((kt + 1) & 1) : 0, x1 ? m0 : m1, x1 ? n0 : n1, x1 ? (kt + 1) * TK : 0,
-            x2 ? (int)(kt & 1) : 0, x2 ? m0 : m1, x2 ? n0 : n1, x2 ? (kt + 2) * TK : 0);
-      pi23 = i23;
-    }
-#else
     // one K-tile: 4 quadrant phases; `issue`: DMA chunk j of the K-tile at (tm0, tn0, koff)
     // into buffer nbuf in phase j (the next K-tile, or the next tile's K-tile 0)
     auto ktile = [&](int64_t kt, bool issue, int nbuf, int64_t tm0, int64_t tn0, int64_t koff) {
@@ -1270,7 +1190,6 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     for (int64_t kt = 0; kt + 1 < nk; ++kt) ktile(kt, true, (int)((kt + 1) & 1), m0, n0, (kt + 1) * TK);
     // the last K-tile: the next tile's K-tile 0 into buffer 0 (nk is even) when prefetching
     ktile(nk - 1, pf, 0, m1, n1, 0);
-#endif
     if (!grp1) barrier();         // waves 0-3 match the other half's barrier count
 #ifdef LLP_DIAG_EPI_SKIP
     // diagnostic build (tools/gemm_epi_cost.py): no epilogue at all, the accumulators kept live
@@ -1279,8 +1198,6 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
 #pragma unroll
       for (int b = 0; b < 8; ++b) asm volatile("" ::"v"(acc[a][b]));
     if (!pf) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's K-tile 0 (deep schedule)
-    barrier();
     t = t_next; m0 = m1; n0 = n1;
     continue;
 #endif
@@ -1354,11 +1271,6 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef LLP_PP8P_SHALLOW
-      // the next tile's K-tile 0 (issued in the last two K-tiles; nothing younger in flight
-      // yet): waited for here, before this epilogue's stores join the count
-      if (h == 0 && pf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
       barrier();
       // phase 2: all threads, staged rows rl0 + 16 i (i < 8) of this round
       const char* rb = stg + rl0 * ROWB + c * 16;
@@ -1432,9 +1344,7 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     // flight through the next tile's first two waits measured 1 % SLOWER on the collab
     // step, 3 interleaved rounds each: the stores then compete with that K-tile's DMA.)
     t = t_next; m0 = m1; n0 = n1;
-#ifdef LLP_PP8P_SHALLOW
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-#endif
   }
 }
 

@@ -119,39 +119,40 @@ __device__ __forceinline__ int64_t llp_xcd_block(int64_t bid, int64_t nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-// One workgroup's agent-scope arrival on a launch-wide ticket (cdna_hip_programming.md §5 "In-launch
-// split-K reduction", Guideline 16): every store of this workgroup that the last arriver reads must
-// have been made by its thread 0 (drained and released here).  Returns true in the LAST workgroup
-// to arrive, which has acquired and returned the ticket to zero (so a ticket zeroed once at
-// allocation stays valid call after call, graph replays included).  Called by every thread.
-__device__ __forceinline__ bool llp_arrive_last(uint32_t* ticket, uint32_t n_blocks) {
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == n_blocks - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  return last != 0;
+// Hand-offs inside one launch (cdna_hip_programming.md Guideline 16, the write-through form): a
+// word another workgroup of the launch reads is stored with llp_store_handed (an agent-scope
+// atomic store: write-through, sc1) and read with llp_load_handed (an sc1 load), so no release
+// or acquire fence is needed -- an agent-scope release fence in every workgroup (an L2
+// write-back each) cost 0.4 ms over the 16k workgroups of a one-launch Adam.
+__device__ __forceinline__ void llp_store_handed(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-// a 32-bit word another workgroup of this launch stored: a vector load behind the acquire
-// (never the scalar path, Guideline 16 Pitfall 6)
 __device__ __forceinline__ float llp_load_handed(const float* p) {
   return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// One workgroup's arrival on a launch-wide ticket: returns true in the LAST workgroup to
+// arrive, which has returned the ticket to zero (so a ticket zeroed once at allocation stays
+// valid call after call, graph replays included).  Every word this workgroup hands to the
+// last arriver must have been stored by its thread 0 with llp_store_handed; thread 0 drains
+// its stores (vmcnt(0)) before the ticket add.  Called by every thread.
+__device__ __forceinline__ bool llp_arrive_last(uint32_t* ticket, uint32_t n_blocks) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == n_blocks - 1;
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last != 0;
+}
+
 // ---------------------------------------------------------------- single-pass scan (decoupled look-back)
 // Workgroup b of a launch publishes its aggregate, looks back over its predecessors' published
-// aggregates / inclusive prefixes (64 per window, one wave) and publishes its inclusive prefix;
+// aggregates / inclusive prefixes (64 per window, one wave) and publishes its inclusive prefix
+// (values and flags are agent-scope atomic stores and loads: write-through, no fences);
 // returns its exclusive prefix to every thread.  flags[b] = (epoch << 2) | status (1 aggregate,
 // 2 inclusive): the epoch tags one call, so the flags never need resetting (the caller advances
 // the epoch once per call).  Waits only on lower-numbered workgroups, which the dispatcher starts
@@ -170,7 +171,7 @@ __device__ __forceinline__ uint32_t llp_lb_wait(const uint32_t* flag, uint32_t e
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the value loads below
   return f & 3u;
 }
 
@@ -182,7 +183,7 @@ __device__ __forceinline__ unsigned long long llp_lookback_u64(uint32_t* flags, 
   const int t = threadIdx.x;
   if (t == 0) {
     __hip_atomic_store(b == 0 ? &incl[0] : &agg[b], blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-through value before its flag
     __hip_atomic_store(&flags[b], (epoch << 2) | (b == 0 ? LLP_LB_INC : LLP_LB_AGG), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     if (b == 0) lb_excl = 0ull;
@@ -209,7 +210,7 @@ __device__ __forceinline__ unsigned long long llp_lookback_u64(uint32_t* flags, 
     if (t == 0) {
       lb_excl = acc;
       __hip_atomic_store(&incl[b], acc + blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&flags[b], (epoch << 2) | LLP_LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -129,9 +129,9 @@ __device__ __forceinline__ void llp_anchor_block(int64_t blk, int64_t B, int64_t
       k += red[i][0];
       r += red[i][1];
     }
-    partial[blk * 3 + 0] = 0.f;
-    partial[blk * 3 + 1] = k;
-    partial[blk * 3 + 2] = r;
+    llp_store_handed(partial + blk * 3 + 0, 0.f);   // (read by the last workgroup of the launch)
+    llp_store_handed(partial + blk * 3 + 1, k);
+    llp_store_handed(partial + blk * 3 + 2, r);
   }
 }
 
@@ -170,9 +170,9 @@ __device__ __forceinline__ void bce_block(int64_t blk, int64_t n, int64_t n_pos,
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
   __syncthreads();
   if (threadIdx.x == 0) {
-    partial[blk * 3 + 0] = (red[0] + red[1] + red[2] + red[3]) / (float)n_total;
-    partial[blk * 3 + 1] = 0.f;
-    partial[blk * 3 + 2] = 0.f;
+    llp_store_handed(partial + blk * 3 + 0, (red[0] + red[1] + red[2] + red[3]) / (float)n_total);
+    llp_store_handed(partial + blk * 3 + 1, 0.f);
+    llp_store_handed(partial + blk * 3 + 2, 0.f);
   }
 }
 

@@ -971,7 +971,7 @@ class DistillEngine(EngineBase):
             dfull = self._buf("owner_dfull", (B * C,), torch.float32)
             K.llp_loss(B, C, full[0], full[1], n_lab_loc, n_pos, logit[n_ctx:], B, P + n_neg, float(a.margin), 1.0,
                        float(a.True_label), float(a.LLP_D), float(a.LLP_R), dfull, dlogit[n_ctx:], self.terms, ws,
-                       term_range=(rank * B // world, (rank + 1) * B // world))
+                       term_range=(rank * B // world, (rank + 1) * B // world), ticket=self.loss_ticket)
             K.gather_i32(own["sel"][lo:lo + n_ctx], dfull.view(torch.int32), dlogit[:n_ctx].view(torch.int32))
         else:
             K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin),
