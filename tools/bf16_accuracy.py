@@ -103,16 +103,25 @@ def compare(scale=0.1, link_batch=8192, epochs=8, seed=0, hidden=1024, eval_ever
             "epochs": epochs, "runs": runs, "final": last, "bf16_minus_fp32": diff}
 
 
-def paired(runs, k="Hits@20", last=3):
-    """Paired bf16 - fp32 difference of Hits@K (percentage points) per seed: each run's value is
-    the mean of its last ``last`` checkpoints; returns per split the per-seed differences, their
-    mean, the standard error of the mean, and the fp32 runs' own seed-to-seed SD."""
+def _run_value(hist, k, split, rule, last):
+    """One run's Hits@K (percentage points): rule "best_valid" -- the reference Logger's
+    ``Highest Valid`` and ``Final Test`` (the checkpoint of the highest valid Hits@K, its valid or
+    test value; src/logger.py); "last" -- the mean of the last ``last`` checkpoints."""
+    if rule == "best_valid":
+        i = int(np.argmax([h["hits"][k]["valid"] for h in hist]))
+        return 100 * float(hist[i]["hits"][k][split])
+    return 100 * float(np.mean([h["hits"][k][split] for h in hist[-last:]]))
+
+
+def paired(runs, k="Hits@20", last=3, rule="best_valid"):
+    """Paired bf16 - fp32 difference of Hits@K (percentage points) per seed (each run's value by
+    _run_value's rule); returns per split the per-seed differences, their mean, the standard
+    error of the mean, |mean| + 2 SE, and the fp32 runs' own seed-to-seed SD."""
     out = {}
     for split in ("valid", "test"):
         d, f = [], []
         for r in runs:
-            v = {dt: 100 * float(np.mean([h["hits"][k][split] for h in r["runs"][dt]["history"][-last:]]))
-                 for dt in ("fp32", "bf16")}
+            v = {dt: _run_value(r["runs"][dt]["history"], k, split, rule, last) for dt in ("fp32", "bf16")}
             d.append(v["bf16"] - v["fp32"])
             f.append(v["fp32"])
         d = np.asarray(d)
@@ -140,7 +149,8 @@ def main():
                     communities=opt.communities)
         runs.append(r)
         print(json.dumps(r), flush=True)
-    summary = {k: paired(runs, k, opt.last) for k in ("Hits@20", "Hits@50")}
+    summary = {rule: {k: paired(runs, k, opt.last, rule) for k in ("Hits@20", "Hits@50")}
+               for rule in ("best_valid", "last")}
     print(json.dumps({"paired_bf16_minus_fp32": summary, "scale": opt.scale, "epochs": opt.epochs,
                       "eval_every": opt.eval_every, "last_checkpoints": opt.last}), flush=True)
 
