@@ -21,6 +21,9 @@ extern "C" {
 #endif
 
 #define LLP_OK 0
+/* A ticket block (the one-launch loss, gradient norm, compaction and dense-negative scans):
+ * LLP_TICKET_WORDS uint32, zero before the first call, returned to zero by every call. */
+#define LLP_TICKET_WORDS 2080
 #define LLP_E_ARG 10001
 #define LLP_E_WORKSPACE 10002
 
@@ -197,9 +200,8 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
  * logit of row m = *bias + sum_t part[t * ld + m], written to s_logit[m] (m < B*C) and
  * out_logit[m - B*C]; NULL: the logits are read from those buffers.  t_head (may be NULL):
  * the teacher predictor's partials over the B*C context rows; t_prob[m] = sigmoid(logit),
- * written.  ticket (may be NULL: a separate finalize launch follows): one uint32, zero
- * before the first call; the workgroup that arrives last on it sums the partials of
- * terms_out and returns it to zero.  Replaces src/main.py:103-130 (head, sigmoid, losses). */
+ * written.  ticket (may be NULL: a separate finalize launch follows): a ticket block
+ * (LLP_TICKET_WORDS); the workgroup that arrives last sums the partials of terms_out.  Replaces src/main.py:103-130 (head, sigmoid, losses). */
 typedef struct llp_head_parts {
   const float* part;   /* [parts][ld] f32 */
   const float* bias;   /* [1] or NULL */
@@ -517,16 +519,16 @@ int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64_t max_nume
 int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
                   float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
                   void* stream);
-/* The same two calls in ONE launch each (ticket: one uint32, zero before the first call,
- * returned to zero by each call; NULL = the two-launch forms above): the gradient norm's
- * finalize runs in the last workgroup to arrive, and Adam writes both shadows in its own
- * pass (transposed ones through 32 x 32 LDS tiles) with the step counter advanced by its
- * last workgroup.  Results bit-identical to the two-launch forms. */
+/* The same two calls in ONE launch each.  llp_grad_sumsq_t (ticket: a ticket block of
+ * LLP_TICKET_WORDS; NULL = the two-launch form): the finalize runs in the last workgroup to
+ * arrive.  llp_adam_step_t: Adam writes both shadows in its own pass (transposed ones through
+ * 32 x 32 LDS tiles) and reads *step WITHOUT advancing it: the caller advances it after the
+ * launch (llp_step_end2).  Results bit-identical to the two-launch forms. */
 int llp_grad_sumsq_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int n_groups,
                      float* sumsq, uint32_t* ticket, void* workspace, int64_t workspace_bytes, void* stream);
 int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
-                    float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
-                    uint32_t* ticket, void* stream);
+                    float max_norm, float lr, float beta1, float beta2, float eps, const int64_t* step,
+                    void* stream);
 /* Refresh bf16 shadows from masters (after loading weights). */
 int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream);
 
@@ -539,6 +541,9 @@ int llp_increment(int64_t* ctr, void* stream);
  * epoch's total_loss += loss.item() * num_examples, src/main.py:140-141) and
  * *step_ctr += 1 (the device step counter that keys every Philox stream). */
 int llp_step_end(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, void* stream);
+/* llp_step_end that also advances the Adam step counter *adam_step (after llp_adam_step_t). */
+int llp_step_end2(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, int64_t* adam_step,
+                  void* stream);
 /* Zero `bytes` bytes at p by a kernel (no memset node: a captured hipMemsetAsync node
  * was measured not to do its work on replay). */
 int llp_zero(void* p, int64_t bytes, void* stream);

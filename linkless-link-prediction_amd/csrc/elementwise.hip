@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) llp_store_handed(partial + blockIdx.y * max_chunks + blockIdx.x, red[0] + red[1] + red[2] + red[3]);
-  if (llp_arrive_last(ticket, gridDim.x * gridDim.y))
+  if (llp_arrive_last_tree(ticket, gridDim.x * gridDim.y))
     grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
@@ -477,12 +477,11 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
 // in 32 x 32 tiles (thread t: row t / 8, columns 4 (t % 8) ..): Adam per element exactly as
 // adam_kernel, the row-major shadow written from registers and the transposed one through an
 // LDS tile; other tensors take adam_kernel's 1,024-element chunks.  Grid-strided over each
-// tensor's tiles / chunks.  The Adam step counter is advanced by the launch's last workgroup
-// (every workgroup has read it before its ticket add; ticket zero on entry, left zero).
+// tensor's tiles / chunks.  The Adam step counter is read, not advanced (llp_step_end2 follows).
 __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* __restrict__ descs,
                                                          const float* __restrict__ sumsq, float max_norm, float lr,
-                                                         float beta1, float beta2, float eps, int64_t* step,
-                                                         uint32_t* ticket) {
+                                                         float beta1, float beta2, float eps,
+                                                         const int64_t* __restrict__ step) {
   __shared__ float tile[32][33];
   const llp_tensor_desc d = descs[blockIdx.y];
   float coef = 1.f;
@@ -606,8 +605,6 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
       }
     }
   }
-  __syncthreads();   // every wave of this workgroup past its use of *step
-  if (llp_arrive_last(ticket, gridDim.x * gridDim.y) && threadIdx.x == 0) *step += 1;
 }
 
 __global__ __launch_bounds__(256) void shadow_kernel(const llp_tensor_desc* __restrict__ descs) {
@@ -633,10 +630,11 @@ __global__ void convert_kernel(int src_bf16, int dst_bf16, int64_t n, const void
 }
 
 __global__ void accumulate_kernel(int64_t n, const float* __restrict__ src, float weight, double* __restrict__ dst,
-                                  int64_t* __restrict__ ctr) {
+                                  int64_t* __restrict__ ctr, int64_t* __restrict__ ctr2) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) dst[i] += (double)src[i] * (double)weight;
   if (ctr && i == 0) *ctr += 1;
+  if (ctr2 && i == 0) *ctr2 += 1;
 }
 
 int64_t max_chunks_of(int64_t max_numel) { return (max_numel + OPT_CHUNK - 1) / OPT_CHUNK; }
@@ -771,22 +769,11 @@ extern "C" int llp_grad_sumsq(const llp_tensor_desc* descs, int n_tensors, int64
 }
 
 extern "C" int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
-                               float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
-                               uint32_t* ticket, void* stream) {
-  LLP_CHECK_ARG(descs && step, "llp_adam_step: null pointer");
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t mc = max_chunks_of(max_numel);
-  if (ticket) {   // one launch: Adam, both shadows, the step counter by the last workgroup
-    hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0,
-                       s, descs, sumsq, max_norm, lr, beta1, beta2, eps, step, ticket);
-    LLP_LAUNCH_CHECK();
-    return LLP_OK;
-  }
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0, s, descs,
-                     sumsq, max_norm, lr,
-                     beta1, beta2, eps, (const int64_t*)step);
-  LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, step);
+                               float max_norm, float lr, float beta1, float beta2, float eps, const int64_t* step,
+                               void* stream) {
+  LLP_CHECK_ARG(descs && step, "llp_adam_step_t: null pointer");
+  hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0,
+                     (hipStream_t)stream, descs, sumsq, max_norm, lr, beta1, beta2, eps, step);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
@@ -794,7 +781,15 @@ extern "C" int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int6
 extern "C" int llp_adam_step(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
                              float max_norm, float lr, float beta1, float beta2, float eps, int64_t* step,
                              void* stream) {
-  return llp_adam_step_t(descs, n_tensors, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, nullptr, stream);
+  LLP_CHECK_ARG(descs && step, "llp_adam_step: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t mc = max_chunks_of(max_numel);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0, s, descs,
+                     sumsq, max_norm, lr, beta1, beta2, eps, (const int64_t*)step);
+  LLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(shadow_t_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs, step);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
 }
 
 extern "C" int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream) {
@@ -822,7 +817,7 @@ extern "C" int llp_convert(int src_dtype, int dst_dtype, int64_t n, const void* 
 extern "C" int llp_accumulate(int64_t n, const float* src, float weight, double* dst, void* stream) {
   LLP_CHECK_ARG(src && dst, "llp_accumulate: null pointer");
   hipLaunchKernelGGL(accumulate_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, n, src, weight,
-                     dst, nullptr);
+                     dst, (int64_t*)nullptr, (int64_t*)nullptr);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }
@@ -854,7 +849,16 @@ extern "C" int llp_zero(void* p, int64_t bytes, void* stream) {
 extern "C" int llp_step_end(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, void* stream) {
   LLP_CHECK_ARG(loss && loss_sum && step_ctr, "llp_step_end: null pointer");
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (int64_t)1, loss, weight, loss_sum,
-                     step_ctr);
+                     step_ctr, (int64_t*)nullptr);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_step_end2(const float* loss, float weight, double* loss_sum, int64_t* step_ctr, int64_t* adam_step,
+                             void* stream) {
+  LLP_CHECK_ARG(loss && loss_sum && step_ctr && adam_step, "llp_step_end2: null pointer");
+  hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (int64_t)1, loss, weight, loss_sum,
+                     step_ctr, adam_step);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void llp_loss_kernel(LossArgs a) {
     bce_block(blk - a.nba, a.n_lab, a.n_pos, a.out_logit, a.hs, a.lab_row0, a.n_lab_total, a.neg_count,
               a.neg_offset, a.pos_total, a.w_label, a.loss_scale, a.dlogit_lab, a.partial + a.nba * 3);
   if (!a.ticket) return;
-  if (!llp_arrive_last(a.ticket, (uint32_t)(a.nba + a.nbl))) return;
+  if (!llp_arrive_last_tree(a.ticket, (uint32_t)(a.nba + a.nbl))) return;
   loss_finalize_block<true>(a.partial, a.nba + a.nbl, a.w_label, a.w_d, a.w_r, a.terms, a.accumulate);
 }
 

@@ -205,10 +205,10 @@ class EngineBase:
         self.rank = dist.get_rank(group) if self.world > 1 else 0
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)   # RNG stream counter
         self.terms = torch.zeros(8, dtype=torch.float32, device=self.dev)
-        # last-arriver tickets of the one-launch loss, gradient norm and Adam (llp_llp_loss_heads,
-        # llp_grad_sumsq_t, llp_adam_step_t): zero, and left zero by every call
-        self.tickets = torch.zeros(4, dtype=torch.int32, device=self.dev)
-        self.loss_ticket = self.tickets[0:1]
+        # last-arriver ticket blocks of the one-launch loss and gradient norm (llp_llp_loss_heads,
+        # llp_grad_sumsq_t): zero, and left zero by every call
+        self.loss_ticket = K.ticket_block(self.dev)
+        self.sumsq_ticket = K.ticket_block(self.dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self._bufs = {}
         self._shadows = {}
@@ -667,10 +667,11 @@ class EngineBase:
             self._collective(lambda: self._finish_allreduce(rest))
         g = self.optimizer.param_groups[0]
         K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq,
-                     ticket=self.tickets[1:2])
+                     ticket=self.sumsq_ticket)
         b1, b2 = g["betas"]
+        # the one-launch Adam reads the step counter; the step-end launch advances it
         K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
-                    float(b2), float(g["eps"]), self.adam_step, ticket=self.tickets[2:3])
+                    float(b2), float(g["eps"]), self.adam_step, fused=True)
 
     # ------------------------------------------------------------------ epoch bookkeeping
     def begin_epoch(self):
@@ -996,7 +997,7 @@ class DistillEngine(EngineBase):
         self._student_backward(dh, rows_s, gather_s, acts, p_drop, count=n_u, x_rows=x_rows, norm_count=R1_total,
                                norm_sync=True)
         self._allreduce_and_update()
-        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
+        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr, adam_step=self.adam_step)
 
     def _owner_assign(self, B, C, C1, P, n_neg, target, rank, world):
         """This rank's pairs under the owner decomposition (llp_pair_owner_assign): categories
@@ -1259,7 +1260,7 @@ class DistillEngine(EngineBase):
         self._student_backward(dh, n_rows, None, acts, p_drop, x_rows=None if shard is None else x_loc,
                                norm_count=n_rows)
         self._allreduce_and_update()
-        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr)
+        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr, adam_step=self.adam_step)
         return n_neg if cnt is None else cnt
 
     def _fb_shard(self, p_drop, grouped):

@@ -127,12 +127,13 @@ _SIGS = {
     "llp_grad_sumsq": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
     "llp_adam_step": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "llp_grad_sumsq_t": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "llp_adam_step_t": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp]),
+    "llp_adam_step_t": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "llp_refresh_shadows": (c_int, [c_vp, c_int, c_i64, c_vp]),
     "llp_convert": (c_int, [c_int, c_int, c_i64, c_vp, c_vp, c_vp]),
     "llp_accumulate": (c_int, [c_i64, c_vp, c_f32, c_vp, c_vp]),
     "llp_increment": (c_int, [c_vp, c_vp]),
     "llp_step_end": (c_int, [c_vp, c_f32, c_vp, c_vp, c_vp]),
+    "llp_step_end2": (c_int, [c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     "llp_zero": (c_int, [c_vp, c_i64, c_vp]),
     "llp_hadamard_rows": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_relu_bwd": (c_int, [c_int, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
@@ -665,18 +666,32 @@ def grad_sumsq_ws_bytes(n, max_numel):
     return load().llp_grad_sumsq_workspace_bytes(n, max_numel)
 
 
+TICKET_WORDS = 2080   # LLP_TICKET_WORDS (include/llp_hip.h)
+
+
+def ticket_block(dev):
+    """A ticket block for the one-launch loss / gradient norm: zero, left zero by every call."""
+    return torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)
+
+
 def grad_sumsq(descs_dev, n, max_numel, n_groups, sumsq, ws, ticket=None):
-    """ticket (int32 device word, zero, left zero): one launch (the finalize in its last workgroup)."""
+    """ticket (a ticket_block): one launch (the finalize in its last workgroup)."""
     L = lib()
+    assert ticket is None or ticket.numel() >= TICKET_WORDS
     check(L.llp_grad_sumsq_t(descs_dev.data_ptr(), n, max_numel, n_groups, sumsq.data_ptr(), ptr(ticket),
                              ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_grad_sumsq")
 
 
-def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, ticket=None):
-    """ticket: one launch (both shadows in the Adam pass, the step advanced by its last workgroup)."""
+def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, fused=False):
+    """fused: one launch (both shadows in the Adam pass) that reads *step without advancing it
+    (step_end(..., adam_step=step) advances it); otherwise Adam + shadow pass, step advanced."""
     L = lib()
-    check(L.llp_adam_step_t(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
-                            step.data_ptr(), ptr(ticket), stream_ptr()), "llp_adam_step")
+    if fused:
+        check(L.llp_adam_step_t(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
+                                step.data_ptr(), stream_ptr()), "llp_adam_step_t")
+    else:
+        check(L.llp_adam_step(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
+                              step.data_ptr(), stream_ptr()), "llp_adam_step")
 
 
 def refresh_shadows(descs_dev, n, max_numel):
@@ -701,9 +716,14 @@ def zero_(t):
     check(L.llp_zero(t.data_ptr(), t.numel() * t.element_size(), stream_ptr()), "llp_zero")
 
 
-def step_end(loss, weight, loss_sum, ctr):
+def step_end(loss, weight, loss_sum, ctr, adam_step=None):
     L = lib()
-    check(L.llp_step_end(loss.data_ptr(), weight, loss_sum.data_ptr(), ctr.data_ptr(), stream_ptr()), "llp_step_end")
+    if adam_step is not None:
+        check(L.llp_step_end2(loss.data_ptr(), weight, loss_sum.data_ptr(), ctr.data_ptr(), adam_step.data_ptr(),
+                              stream_ptr()), "llp_step_end2")
+    else:
+        check(L.llp_step_end(loss.data_ptr(), weight, loss_sum.data_ptr(), ctr.data_ptr(), stream_ptr()),
+              "llp_step_end")
 
 
 def increment(ctr):

@@ -322,8 +322,7 @@ class TeacherEngine(EngineBase):
             self._hadamard_bwd_nodes(R, tgt, None, dlogit, h, self._dh_slot())
         self._encode_backward()
         self._allreduce_and_update()
-        K.accumulate(self.terms[:1], float(P_total), self.loss_sum)
-        K.increment(self.step_ctr)
+        K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr, adam_step=self.adam_step)
         return n_neg if cnt is None else cnt
 
     @torch.no_grad()

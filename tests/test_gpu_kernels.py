@@ -389,7 +389,7 @@ def test_llp_loss_heads_one_launch(B, C, n_lab, parts, dense):
     tb = torch.randn(1, generator=g).to(DEV)
     cnt = torch.tensor([n_lab - n_pos - 3], dtype=torch.int32, device=DEV) if dense else None
     ws = torch.empty(k.llp_loss_ws_bytes(B, n_lab) // 4 + 16, device=DEV)
-    ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ticket = k.ticket_block(DEV)
     for it in range(3):
         # reference: the heads finished by their own launches, the loss in three
         logit1 = torch.empty(max(R, 1), device=DEV)
@@ -413,7 +413,7 @@ def test_llp_loss_heads_one_launch(B, C, n_lab, parts, dense):
         assert torch.equal(tprob1[:B * C], tprob2[:B * C]), it
         assert torch.equal(d1[:R], d2[:R]), it
         assert torch.equal(t1, t2), it
-        assert int(ticket.item()) == 0
+        assert int(ticket.abs().sum()) == 0
         sp.mul_(1.1)
 
 
@@ -554,9 +554,10 @@ def test_clip_and_adam_match_oracle(case, nan_group, fused):
     """grad_sumsq (chunk partials + one-pass finalize) + clip per group + Adam
     against the oracle's clip_grad_norm_ / Adam (src/main.py:132-138); a NaN
     gradient turns its group's clip coefficient into NaN, as torch.clamp does.
-    fused: the one-launch forms (llp_grad_sumsq_t / llp_adam_step_t with tickets)."""
+    fused: the one-launch forms (llp_grad_sumsq_t with a ticket block, llp_adam_step_t with the
+    step counter advanced after it, as llp_step_end2 does)."""
     k = K()
-    tickets = torch.zeros(2, dtype=torch.int32, device=DEV) if fused else None
+    tickets = k.ticket_block(DEV) if fused else None
     spec = _ADAM_CASES[case]
     g = torch.Generator().manual_seed(9 + len(spec))
     shapes = [sh for sh, _, _ in spec]
@@ -596,9 +597,11 @@ def test_clip_and_adam_match_oracle(case, nan_group, fused):
         gs = [x * (it + 1) for x in grads]
         for i in range(len(dp)):
             dg[i].copy_(gs[i].to(DEV))
-        k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets[0:1] if fused else None)
-        k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step,
-                    ticket=tickets[1:2] if fused else None)
+        k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets)
+        k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step, fused=fused)
+        if fused:
+            assert step.item() == it        # read, not advanced
+            step += 1
         assert step.item() == it + 1       # one increment per adam_step
         assert not fused or int(tickets.abs().sum()) == 0
         clipped = []
@@ -626,7 +629,8 @@ def test_clip_and_adam_match_oracle(case, nan_group, fused):
 
 def test_clip_and_adam_one_launch_bit_identical():
     """The one-launch norm and Adam (tickets) give the two-launch forms' parameters, moments,
-    gradients, bf16 shadows and transposed shadows bit for bit (big case, 3 steps)."""
+    gradients, bf16 shadows and transposed shadows bit for bit (big case, 3 steps; the fused
+    form's step counter advanced by llp_step_end2, as the engines do)."""
     k = K()
     spec = _ADAM_CASES["big"]
     g = torch.Generator().manual_seed(77)
@@ -657,14 +661,19 @@ def test_clip_and_adam_one_launch_bit_identical():
         sumsq = torch.zeros(n_groups, device=DEV)
         ws = torch.empty(k.grad_sumsq_ws_bytes(len(dp), max_numel) // 4 + 16, device=DEV)
         step = torch.zeros(1, dtype=torch.int64, device=DEV)
-        tickets = torch.zeros(2, dtype=torch.int32, device=DEV)
+        tickets = k.ticket_block(DEV)
+        loss, loss_sum = torch.ones(1, device=DEV), torch.zeros(1, dtype=torch.float64, device=DEV)
+        ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
         for it in range(3):
             for i in range(len(dp)):
                 dg[i].copy_((grads[i] * (it + 1)).to(DEV))
-            k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets[0:1] if fused else None)
-            k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step,
-                        ticket=tickets[1:2] if fused else None)
+            k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets if fused else None)
+            k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step, fused=fused)
+            if fused:
+                k.step_end(loss, 2.0, loss_sum, ctr, adam_step=step)
         torch.cuda.synchronize()
+        assert not fused or (int(ctr.item()) == 3 and float(loss_sum.item()) == 6.0
+                             and int(tickets.abs().sum()) == 0)
         runs.append((dp, dg, m, v, [x for x in sh if x is not None], sumsq, int(step.item())))
     for a, b in zip(runs[0][:5], runs[1][:5]):
         for x, y in zip(a, b):
