@@ -283,54 +283,107 @@ __device__ __forceinline__ void put_elem(void* base, int64_t i, float v, int dt)
     reinterpret_cast<float*>(base)[i] = v;
 }
 
+// one thread's share of a chunk's sum of squares: its OPT_CHUNK / 256 loads issued together
+// (a loop that waits on each is latency-bound: 18 us for the 2.3 M-parameter physics student),
+// summed in element order (the order fixes the result; both norm kernels use this)
+__device__ __forceinline__ float chunk_sumsq(const float* __restrict__ grad, int64_t e0, int64_t e1) {
+  constexpr int PER = OPT_CHUNK / 256;
+  float x[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int64_t e = e0 + threadIdx.x + 256 * k;
+    x[k] = e < e1 ? grad[e] : 0.f;
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (e0 + threadIdx.x + 256 * k < e1) acc += x[k] * x[k];
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void grad_sumsq_kernel(const llp_tensor_desc* __restrict__ descs, int64_t max_chunks,
                                                          float* __restrict__ partial) {
   __shared__ float red[4];
   const llp_tensor_desc d = descs[blockIdx.y];
   const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
   float acc = 0.f;
-  if (e0 < d.numel) {
-    const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-      const float g = d.grad[e];
-      acc += g * g;
-    }
-  }
+  if (e0 < d.numel) acc = chunk_sumsq(d.grad, e0, min(d.numel, e0 + OPT_CHUNK));
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) partial[blockIdx.y * max_chunks + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// chunks of the gradient norm in tensor t
+__device__ __forceinline__ uint32_t sumsq_chunks(const llp_tensor_desc* __restrict__ descs, int t) {
+  return (uint32_t)((descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK);
+}
+
 template <bool HANDOFF>
 __device__ __forceinline__ void grad_sumsq_finalize_block(const llp_tensor_desc* __restrict__ descs, int n_tensors,
                                                           int64_t max_chunks, const float* partial, int n_groups,
                                                           float* __restrict__ sumsq) {
-  // one block, one pass: thread i sums (in double) the chunk partials i, i+256, ... of
-  // every tensor into its group's register, then a fixed LDS tree per group
-  // (deterministic; was one block-wide reduction per tensor)
+  // one block, one pass over every tensor's chunk partials at once (n_tensors <= 256): thread t
+  // holds tensor t's chunk count, a block scan gives each tensor's first flat index, and thread i
+  // sums (in double) the flat partials i, i+256, .. into its group's register, then a fixed LDS
+  // tree per group (deterministic).  A loop over tensors waited one memory round trip each.
   __shared__ double red[8][256];
+  __shared__ uint32_t pre[257];
+  __shared__ int grp[256];
+  __shared__ uint32_t wtot[4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  uint32_t v = 0;
+  if (tid < n_tensors) {
+    v = sumsq_chunks(descs, tid);
+    grp[tid] = descs[tid].group;
+  }
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) wtot[tid >> 6] = v;
+  __syncthreads();
+  for (int w = 0; w < (tid >> 6); ++w) v += wtot[w];
+  pre[tid + 1] = v;
+  if (tid == 0) pre[0] = 0;
+  __syncthreads();
+  const uint32_t total = pre[n_tensors];
   double gs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int t = 0; t < n_tensors; ++t) {
-    const int gidx = descs[t].group;
-    const int64_t nch = (descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK;
-    double ts = 0.0;
-    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x)
-      ts += (double)(HANDOFF ? llp_load_handed(partial + t * max_chunks + c) : partial[t * max_chunks + c]);
+  for (uint32_t j0 = 0; j0 < total; j0 += 4 * 256) {
+    float x[4];
+    int gi[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k == gidx) gs[k] += ts;
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t j = j0 + tid + 256 * u;
+      x[u] = 0.f;
+      gi[u] = -1;
+      if (j < total) {
+        int lo = 0, hi = n_tensors - 1;   // the last tensor whose first flat index is <= j
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pre[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        const float* src = partial + lo * max_chunks + (j - pre[lo]);
+        x[u] = HANDOFF ? llp_load_handed(src) : *src;
+        gi[u] = grp[lo];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k == gi[u]) gs[k] += (double)x[u];
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) red[k][threadIdx.x] = gs[k];
+  for (int k = 0; k < 8; ++k) red[k][tid] = gs[k];
   __syncthreads();
   for (int st = 128; st > 0; st >>= 1) {
-    if ((int)threadIdx.x < st)
+    if (tid < st)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + st];
+      for (int k = 0; k < 8; ++k) red[k][tid] += red[k][tid + st];
     __syncthreads();
   }
-  if ((int)threadIdx.x < n_groups) sumsq[threadIdx.x] = (float)red[threadIdx.x][0];
+  if (tid < n_groups) sumsq[tid] = (float)red[tid][0];
 }
 
 __global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc* __restrict__ descs, int n_tensors,
@@ -339,7 +392,10 @@ __global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc
   grad_sumsq_finalize_block<false>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
-// grad_sumsq_kernel with the finalize in the launch's last workgroup (ticket: zero, left zero)
+// grad_sumsq_kernel with the finalize in the launch's last workgroup (ticket block: zero, left
+// zero).  Only the workgroups that own a chunk arrive (the grid is max_chunks x n_tensors, most
+// of it idle past the small tensors' ends): arrival index = the chunks of the tensors before
+// this one + this chunk.
 __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_desc* __restrict__ descs,
                                                                int n_tensors, int64_t max_chunks, float* partial,
                                                                int n_groups, float* __restrict__ sumsq,
@@ -347,19 +403,27 @@ __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_
   __shared__ float red[4];
   const llp_tensor_desc d = descs[blockIdx.y];
   const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
-  float acc = 0.f;
-  if (e0 < d.numel) {
-    const int64_t e1 = min(d.numel, e0 + OPT_CHUNK);
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-      const float g = d.grad[e];
-      acc += g * g;
+  if (e0 >= d.numel) return;
+  // this arrival's index and the number of arrivals: every wave reads the descriptors in
+  // parallel (one round trip per 64 tensors) and sums them across its lanes
+  uint32_t before = 0, total = 0;
+  for (int t0 = 0; t0 < n_tensors; t0 += 64) {
+    const int t = t0 + (threadIdx.x & 63);
+    const uint32_t nch = t < n_tensors ? sumsq_chunks(descs, t) : 0u;
+    uint32_t bb = t < (int)blockIdx.y ? nch : 0u, tt = nch;
+    for (int o = 32; o > 0; o >>= 1) {
+      bb += __shfl_xor(bb, o, 64);
+      tt += __shfl_xor(tt, o, 64);
     }
+    before += bb;
+    total += tt;
   }
+  float acc = chunk_sumsq(d.grad, e0, min(d.numel, e0 + OPT_CHUNK));
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) llp_store_handed(partial + blockIdx.y * max_chunks + blockIdx.x, red[0] + red[1] + red[2] + red[3]);
-  if (llp_arrive_last_tree(ticket, gridDim.x * gridDim.y))
+  if (llp_arrive_last_tree(ticket, before + blockIdx.x, total))
     grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
@@ -474,16 +538,23 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
 }
 
 // adam_kernel and shadow_t_kernel in one launch.  A tensor with a transposed shadow is walked
-// in 32 x 32 tiles (thread t: row t / 8, columns 4 (t % 8) ..): Adam per element exactly as
-// adam_kernel, the row-major shadow written from registers and the transposed one through an
-// LDS tile; other tensors take adam_kernel's 1,024-element chunks.  Grid-strided over each
-// tensor's tiles / chunks.  The Adam step counter is read, not advanced (llp_step_end2 follows).
+// in 64 x 64 tiles on shadow_t_kernel's mapping (lane l of wave w: column c0 + l, rows w, w + 4,
+// ..): every load and store of the Adam pass is lane-contiguous whatever the row width and
+// alignment (the physics input weight is 8,415 wide), the row-major shadow is written from
+// registers and the transposed one through the LDS tile.  Other tensors take adam_kernel's
+// 1,024-element chunks.  Grid-strided over each tensor's tiles / chunks.  The Adam step counter
+// is read, not advanced (llp_step_end2 follows).
 __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* __restrict__ descs,
                                                          const float* __restrict__ sumsq, float max_norm, float lr,
                                                          float beta1, float beta2, float eps,
                                                          const int64_t* __restrict__ step) {
-  __shared__ float tile[32][33];
+  __shared__ float tile[64][65];
   const llp_tensor_desc d = descs[blockIdx.y];
+  // most of the grid (max chunks x tensors) owns nothing: leave before the double pow below
+  // (every thread of ~21k idle workgroups evaluating it cost ~40 us of the physics step)
+  if (d.shadow_t ? (int64_t)blockIdx.x >= ((d.rows + 63) / 64) * ((d.cols + 63) / 64)
+                 : (int64_t)blockIdx.x * ADAM_CHUNK >= d.numel)
+    return;
   float coef = 1.f;
   if (sumsq) {
     const float total = sqrtf(sumsq[d.group]);
@@ -497,62 +568,46 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
   if (d.shadow_t) {
     const int64_t rows = d.rows, cols = d.cols;
     const int64_t ldt = d.shadow_t_ld ? d.shadow_t_ld : rows;
-    const int64_t tr = (rows + 31) / 32, tc = (cols + 31) / 32;
-    const int r = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;
-    const bool vec = (cols & 3) == 0 &&
-                     ((((uintptr_t)d.grad) | ((uintptr_t)d.exp_avg) | ((uintptr_t)d.exp_avg_sq) | ((uintptr_t)d.param)) &
-                      15) == 0;
+    const int64_t lds = d.shadow_ld ? d.shadow_ld : cols;
+    const int64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int64_t ti = blockIdx.x; ti < tr * tc; ti += gridDim.x) {
-      const int64_t r0 = (ti / tc) * 32, c0 = (ti % tc) * 32;
-      const int64_t gr = r0 + r, gc = c0 + c4;
-      float pv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (gr < rows) {
-        const int64_t e = gr * cols + gc;
-        if (vec && gc + 3 < cols) {
-          float4 g = *reinterpret_cast<const float4*>(d.grad + e);
-          if (coef != 1.f) {
-            g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
-            *reinterpret_cast<float4*>(d.grad + e) = g;
-          }
-          float4 m = *reinterpret_cast<const float4*>(d.exp_avg + e);
-          float4 v = *reinterpret_cast<const float4*>(d.exp_avg_sq + e);
-          float4 p = *reinterpret_cast<const float4*>(d.param + e);
-          p.x = adam_elem(g.x, m.x, v.x, p.x, beta1, beta2, eps, bc2s, step_size);
-          p.y = adam_elem(g.y, m.y, v.y, p.y, beta1, beta2, eps, bc2s, step_size);
-          p.z = adam_elem(g.z, m.z, v.z, p.z, beta1, beta2, eps, bc2s, step_size);
-          p.w = adam_elem(g.w, m.w, v.w, p.w, beta1, beta2, eps, bc2s, step_size);
-          *reinterpret_cast<float4*>(d.exp_avg + e) = m;
-          *reinterpret_cast<float4*>(d.exp_avg_sq + e) = v;
-          *reinterpret_cast<float4*>(d.param + e) = p;
-          pv[0] = p.x; pv[1] = p.y; pv[2] = p.z; pv[3] = p.w;
-        } else {
+      const int64_t r0 = (ti / tc) * 64, c0 = (ti % tc) * 64;
+      const int64_t c = c0 + tx;
+      // every load of the tile issued before the first store (the stores may alias later
+      // loads as far as the compiler knows, which kept it to one row's round trip at a time)
+      float gv[16], mv[16], vv[16], pv[16];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (gc + i >= cols) break;
-            const float g = d.grad[e + i] * coef;
-            if (coef != 1.f) d.grad[e + i] = g;
-            float m = d.exp_avg[e + i], v = d.exp_avg_sq[e + i];
-            pv[i] = adam_elem(g, m, v, d.param[e + i], beta1, beta2, eps, bc2s, step_size);
-            d.exp_avg[e + i] = m;
-            d.exp_avg_sq[e + i] = v;
-            d.param[e + i] = pv[i];
-          }
-        }
-        if (d.shadow) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (gc + i < cols) put_elem(d.shadow, shadow_index(d, e + i), pv[i], d.shadow_dtype);
-        }
+      for (int k = 0; k < 16; ++k) {
+        const int64_t r = r0 + ty + 4 * k, e = r * cols + c;
+        const bool ok = r < rows && c < cols;
+        gv[k] = ok ? d.grad[e] : 0.f;
+        mv[k] = ok ? d.exp_avg[e] : 0.f;
+        vv[k] = ok ? d.exp_avg_sq[e] : 0.f;
+        pv[k] = ok ? d.param[e] : 0.f;
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) tile[r][c4 + i] = pv[i];
+      for (int k = 0; k < 16; ++k) {
+        const int i = ty + 4 * k;
+        const int64_t r = r0 + i;
+        float pnew = 0.f;
+        if (r < rows && c < cols) {
+          const int64_t e = r * cols + c;
+          const float g = gv[k] * coef;
+          if (coef != 1.f) d.grad[e] = g;
+          pnew = adam_elem(g, mv[k], vv[k], pv[k], beta1, beta2, eps, bc2s, step_size);
+          d.exp_avg[e] = mv[k];
+          d.exp_avg_sq[e] = vv[k];
+          d.param[e] = pnew;
+          if (d.shadow) put_elem(d.shadow, r * lds + c, pnew, d.shadow_dtype);
+        }
+        tile[i][tx] = pnew;
+      }
       __syncthreads();
-      // transposed: thread t writes shadow_t row c0 + t / 8, columns r0 + 4 (t % 8) ..
-      const int64_t oc = c0 + r;
-      if (oc < cols) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (r0 + c4 + i < rows) put_elem(d.shadow_t, oc * ldt + r0 + c4 + i, tile[c4 + i][r], d.shadow_dtype);
+#pragma unroll 4
+      for (int i = ty; i < 64; i += 4) {   // output row = column c0 + i, output col = r0 + tx
+        const int64_t oc = c0 + i, orow = r0 + tx;
+        if (oc < cols && orow < rows) put_elem(d.shadow_t, oc * ldt + orow, tile[tx][i], d.shadow_dtype);
       }
       __syncthreads();
     }
@@ -743,6 +798,7 @@ extern "C" int llp_grad_sumsq_t(const llp_tensor_desc* descs, int n_tensors, int
                                 void* stream) {
   LLP_CHECK_ARG(descs && sumsq && workspace, "llp_grad_sumsq: null pointer");
   LLP_CHECK_ARG(n_groups >= 1 && n_groups <= 8, "llp_grad_sumsq: n_groups in [1,8]");
+  LLP_CHECK_ARG(n_tensors >= 1 && n_tensors <= 256, "llp_grad_sumsq: n_tensors in [1,256]");
   LLP_CHECK_ARG(workspace_bytes >= llp_grad_sumsq_workspace_bytes(n_tensors, max_numel),
                 "llp_grad_sumsq: workspace too small");
   hipStream_t s = (hipStream_t)stream;

@@ -135,17 +135,17 @@ __device__ __forceinline__ float llp_load_handed(const float* p) {
 // One workgroup's arrival on a launch-wide ticket block (LLP_TICKET_WORDS uint32, include/llp_hip.h):
 // returns true in the LAST workgroup to arrive.  Two levels, so the arrivals do not all
 // serialise on one word (thousands of adds on a single address cost 0.2 ms in a one-launch
-// Adam): workgroup b adds to sub-ticket b % 64, the last arriver there adds to the main word.
+// Adam): arrival b (0 .. n_blocks-1, dense: each arriving workgroup passes its own) adds to
+// sub-ticket b % 64, the last arriver there adds to the main word.
 // Each word is returned to zero by its last arriver, so a block zeroed once at allocation stays
 // valid call after call, graph replays included.  Every word this workgroup hands to the last
 // arriver must have been stored by its thread 0 with llp_store_handed; thread 0 drains its
 // stores (vmcnt(0)) before its add.  Called by every thread.
 constexpr int LLP_TICKET_SUBS = 64, LLP_TICKET_STRIDE = 32;   // sub-tickets 128 B apart
 
-__device__ __forceinline__ bool llp_arrive_last_tree(uint32_t* tk, uint32_t n_blocks) {
+__device__ __forceinline__ bool llp_arrive_last_tree(uint32_t* tk, uint32_t b, uint32_t n_blocks) {
   __shared__ int last;
   if (threadIdx.x == 0) {
-    const uint32_t b = blockIdx.x + blockIdx.y * gridDim.x;
     const uint32_t sub = b % LLP_TICKET_SUBS;
     const uint32_t n_sub = (n_blocks - sub + LLP_TICKET_SUBS - 1) / LLP_TICKET_SUBS;   // arrivals on it
     const uint32_t n_main = n_blocks < (uint32_t)LLP_TICKET_SUBS ? n_blocks : (uint32_t)LLP_TICKET_SUBS;

@@ -182,13 +182,25 @@ __device__ __forceinline__ void loss_finalize_block(const float* partial, int64_
                                                     float w_r, float* __restrict__ terms, int accumulate) {
   __shared__ double red[3][256];
   double a[3] = {0, 0, 0};
-  for (int64_t i = threadIdx.x; i < nblocks; i += blockDim.x)
-    for (int k = 0; k < 3; ++k) {
-      // partials of other workgroups of this launch: vector loads behind the acquire (never the
-      // scalar path, cdna_hip_programming.md Guideline 16 Pitfall 6)
-      const float v = HANDOFF ? llp_load_handed(partial + i * 3 + k) : partial[i * 3 + k];
-      a[k] += (double)v;
+  // partials of other workgroups of this launch (write-through loads, never the scalar path):
+  // eight blocks' worth issued before any is summed -- the compiler does not batch atomic loads
+  // across iterations, and one round trip per block cost ~20 us of the physics step
+  constexpr int U = 8;
+  for (int64_t i0 = threadIdx.x; i0 < nblocks; i0 += (int64_t)U * blockDim.x) {
+    float v[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        v[u][k] = i < nblocks ? (HANDOFF ? llp_load_handed(partial + i * 3 + k) : partial[i * 3 + k]) : 0.f;
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + (int64_t)u * blockDim.x < nblocks)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a[k] += (double)v[u][k];
+  }
   for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = a[k];
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
@@ -223,9 +235,9 @@ struct LossArgs {
 // The whole loss in one launch: blocks [0, nba) are the anchors' (llp_anchor_block), the
 // rest the label rows' (bce_block); the workgroup that arrives last on the ticket sums every
 // block's partials (the same tree as loss_finalize_kernel) and returns the ticket to zero.
-// Hand-off: each block's partials are stored by one lane, drained (vmcnt(0)), published by an
-// agent-scope release before the relaxed ticket add; the last arriver acquires (agent) before
-// it reads them (cdna_hip_programming.md §5 "In-launch split-K reduction", Guideline 16).
+// Hand-off: each block's partials are stored by one lane with write-through atomic stores and
+// drained (vmcnt(0)) before its ticket add; the last arriver reads them with write-through
+// atomic loads (llp_common.h: llp_store_handed / llp_arrive_last_tree / llp_load_handed).
 template <int CMAX>
 __global__ __launch_bounds__(256) void llp_loss_kernel(LossArgs a) {
   const int64_t blk = blockIdx.x;
@@ -236,7 +248,7 @@ __global__ __launch_bounds__(256) void llp_loss_kernel(LossArgs a) {
     bce_block(blk - a.nba, a.n_lab, a.n_pos, a.out_logit, a.hs, a.lab_row0, a.n_lab_total, a.neg_count,
               a.neg_offset, a.pos_total, a.w_label, a.loss_scale, a.dlogit_lab, a.partial + a.nba * 3);
   if (!a.ticket) return;
-  if (!llp_arrive_last_tree(a.ticket, (uint32_t)(a.nba + a.nbl))) return;
+  if (!llp_arrive_last_tree(a.ticket, blockIdx.x, (uint32_t)(a.nba + a.nbl))) return;
   loss_finalize_block<true>(a.partial, a.nba + a.nbl, a.w_label, a.w_d, a.w_r, a.terms, a.accumulate);
 }
 
