@@ -140,6 +140,24 @@ int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q,
                 float* C, int64_t ldc, int accumulate, float* colsum_a,
                 void* workspace, int64_t workspace_bytes, void* stream);
 
+/* Sparse-input first Linear (src/models.py:48 on bag-of-words x, e.g. coauthor-physics' 8,415
+ * binary keywords at ~0.5 % density; csrc/spmm.hip).  x is held as CSR (rowptr[N+1], colidx,
+ * val; val NULL = all ones) and, per student slice, as CSC (colptr[F+1], rowidx ascending within
+ * a column, local to the slice).  Wt is the bf16 transposed weight [F, H] (row stride ldw).
+ *   llp_spmm_rows: Y[r, :] = act(sum_{k in CSR row row0 + r} val[k] * Wt[colidx[k], :] + bias)
+ *                  for r < rows, bf16 out (RNE), act NONE or RELU, optional ReLU bit mask as
+ *                  llp_gemm_nt writes it (the next layer's ReLU-backward GEMM reads it).
+ *   llp_spmm_tn:   dW[o, f] (+)= sum_{k in CSC column f} val[k] * dY[rowidx[k], o]: the
+ *                  weight gradient of the same Linear (f32, row stride ldw >= F); the bias
+ *                  gradient is llp_colsum of dY.
+ * f32 sums in index order: deterministic, equal to llp_gemm_nt / llp_gemm_tn on the dense x up
+ * to the order of the f32 sums.  H <= 1024 (H % 8 == 0 forward, % 4 backward). */
+int llp_spmm_rows(int64_t rows, int64_t row0, int64_t H, const int32_t* rowptr, const int32_t* colidx,
+                  const float* val, const void* Wt, int64_t ldw, const float* bias, int act, void* Y,
+                  int64_t ldy, void* mask_out, int64_t ld_mask, void* stream);
+int llp_spmm_tn(int64_t F, int64_t H, const int32_t* colptr, const int32_t* rowidx, const float* val,
+                const void* dY, int64_t ldy, float* dW, int64_t ldw, int accumulate, void* stream);
+
 /* Column sums: out[n] (+)= sum_m Y[m,n] (bias gradient).  Deterministic. */
 int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N);
 int llp_colsum(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy, float* out, int accumulate,

@@ -38,6 +38,9 @@ DENSE_NEG_STREAM = STREAMS_PER_STEP - 2
 MAX_RW_STEP = STREAMS_PER_STEP - 3          # walks + negatives below DENSE_NEG_STREAM
 # dropout Philox keys (EngineBase._dropout): one per module, one stream per layer and step
 DROP_ENCODER, DROP_PREDICTOR, DROP_TEACHER_PRED = 0, 1, 2
+# x at most this dense runs the full-batch student's first layer sparse (llp_spmm_rows): a
+# gathered 512-B weight row per nonzero against a dense 256-wide MFMA pass over every column
+SPARSE_X_MAX_DENSITY = 0.05
 _MAX_DROPOUT_LAYERS = STREAMS_PER_STEP - 1
 
 _DT = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
@@ -702,7 +705,7 @@ class DistillEngine(EngineBase):
 
     def __init__(self, model, predictor, teacher_predictor, x, t_h, row, col, num_nodes, args, optimizer,
                  dtype="bf16", seed=0, rw_sorted=False, group=None, device=None, dedup=True, shard_student=True,
-                 owner_pairs=True, owner_locality=True):
+                 owner_pairs=True, owner_locality=True, sparse_input=True):
         self._init_device(x.device, device, dtype, seed, group, "DistillEngine")
         # run the dropout-free student on unique nodes (step_minibatch); the unique
         # count stays on the device, so this path is hipGraph-capturable too
@@ -728,7 +731,14 @@ class DistillEngine(EngineBase):
         # ---------------- parameters
         self.model, self.predictor, self.tpred = model, predictor, teacher_predictor
         stu = list(model.layers)
-        self.stu = [_Linear(l, self.dtype, need_t=(i > 0), need_c=True) for i, l in enumerate(stu)]
+        # bag-of-words inputs (coauthor-physics: 8,415 binary keywords, ~0.5 % nonzero): the full-batch
+        # student's first layer gathers rows of its transposed bf16 weight by x's nonzeros
+        # (llp_spmm_rows / llp_spmm_tn, csrc/spmm.hip) instead of dense MFMA tiles over zeros
+        H0 = stu[0].out_features
+        self.sparse_x = (bool(sparse_input) and self.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[1] >= 256
+                         and H0 % 8 == 0 and H0 <= 1024
+                         and float(torch.count_nonzero(x)) <= SPARSE_X_MAX_DENSITY * x.numel())
+        self.stu = [_Linear(l, self.dtype, need_t=(i > 0 or self.sparse_x), need_c=True) for i, l in enumerate(stu)]
         # bf16: the input width is zero-padded to a multiple of 64 (x and the first layer's compute
         # copy) so that the first layer runs on the 256-tile MFMA kernels (cora 1,433 -> 1,472,
         # coauthor-physics 8,415 -> 8,448, ...); padded columns are 0 in both, the products exact
@@ -764,6 +774,7 @@ class DistillEngine(EngineBase):
             self.x[:, :F_in].copy_(x.to(self.dev))
         else:
             self.x = x.to(self.dev).to(self.dtype).contiguous()
+        self.xs = K.SparseRows(x.to(self.dev)) if self.sparse_x else None
         self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
         self._neg_rc = (np.asarray(row), np.asarray(col))
         self._neg_keys = None
@@ -1149,8 +1160,11 @@ class DistillEngine(EngineBase):
                 dst = self._buf(f"Y{l}", (n_loc, lin.out_f), dt)
             else:
                 dst = out
-            splits = self._splitk_plan(n_rows, lin.out_f, lin.k_in) if (p_drop == 0.0 or normed) else 1
-            if splits > 1:   # few output tiles over a long K (the first layer at 8,448 features)
+            sparse = l == 0 and self.xs is not None and (p_drop == 0.0 or normed)
+            splits = self._splitk_plan(n_rows, lin.out_f, lin.k_in) if (p_drop == 0.0 or normed) and not sparse else 1
+            if sparse:       # bag-of-words x: gather W^T rows by its nonzeros (no dropout here)
+                K.spmm_rows(self.xs, n_rows, r0, lin.Wt, lin.b, dst, act=act, mask=hm)
+            elif splits > 1:   # few output tiles over a long K (the first layer at 8,448 features)
                 ws = self._ws("ws_splitk", K.gemm_nt_splitk_ws_bytes(n_rows, lin.out_f, splits))
                 K.gemm_nt_splitk(A, K.operand(lin.Wcomp), n_rows, lin.out_f, lin.k_in, dst, splits, ws, bias=lin.b,
                                  act=act, mask=hm)
@@ -1257,8 +1271,9 @@ class DistillEngine(EngineBase):
             else:
                 dh = self._buf("gS0", (N, H), dt)
                 K.convert(dh32, dh)
+        sp = (r0, n_rows) if self.xs is not None and (p_drop == 0.0 or bool(self.stu_norms)) else None
         self._student_backward(dh, n_rows, None, acts, p_drop, x_rows=None if shard is None else x_loc,
-                               norm_count=n_rows)
+                               norm_count=n_rows, sparse_rows=sp)
         self._allreduce_and_update()
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr, adam_step=self.adam_step)
         return n_neg if cnt is None else cnt
@@ -1402,11 +1417,13 @@ class DistillEngine(EngineBase):
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
     def _student_backward(self, dh, R1, target, acts, p_drop, count=None, x_rows=None, norm_count=0.0,
-                          norm_sync=False):
+                          norm_sync=False, sparse_rows=None):
         """count: int32 device row count (unique-node student) or None.  dh lives in
         buffer 'gS0'.  x_rows: x[target] materialised by the forward (else the first
         layer's input is gathered).  norm_count / norm_sync: BatchNorm's batch row count
-        and whether its sums are all-reduced across ranks (_norm_backward)."""
+        and whether its sums are all-reduced across ranks (_norm_backward).  sparse_rows:
+        (first row, rows) of the sparse x the forward's first layer ran on (llp_spmm_rows):
+        its weight gradient by llp_spmm_tn over the same rows, the bias gradient by llp_colsum."""
         dt, dc = self.dtype, self.dc
         alpha = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
         names = ["gS0", "gS1"]
@@ -1420,6 +1437,10 @@ class DistillEngine(EngineBase):
                 A_in = K.operand(x_rows, count=count)
             else:
                 A_in = K.operand(self.x, target, count=count)
+            if l == 0 and sparse_rows is not None:
+                K.spmm_tn(self.xs, sparse_rows[0], sparse_rows[1], gcur, lin.lin.weight.grad)
+                K.colsum(gcur, R1, lin.out_f, lin.lin.bias.grad, self._ws("ws_colsum", K.colsum_ws_bytes(R1, lin.out_f)))
+                continue
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
             dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad

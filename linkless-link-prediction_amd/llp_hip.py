@@ -66,6 +66,9 @@ _SIGS = {
                             c_vp, c_vp, c_i64, c_vp]),
     "llp_colsum_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_colsum": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp]),
+    "llp_spmm_rows": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp,
+                              c_i64, c_vp]),
+    "llp_spmm_tn": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
     "llp_head_fwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_head_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_head_bwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_vp, c_i64, c_vp, c_vp,
@@ -293,6 +296,62 @@ def colsum(Y, M, N, out, ws, accumulate=False):
     L = lib()
     check(L.llp_colsum(dtype_code(Y.dtype), M, N, Y.data_ptr(), Y.stride(0), out.data_ptr(), int(accumulate),
                        ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_colsum")
+
+
+class SparseRows:
+    """A constant sparse matrix x [N, F] on the device for llp_spmm_rows / llp_spmm_tn: CSR
+    (rowptr, colidx, val; val None when every stored value is 1) and, per row slice, its CSC
+    (csc(r0, n): colptr, rowidx local to the slice, ascending within a column, val).  Built once
+    from the dense x with torch (setup plumbing, not the step)."""
+
+    def __init__(self, x):
+        assert x.dim() == 2
+        self.N, self.F = x.shape
+        nz = torch.nonzero(x)                                   # row-major order: rows, then columns
+        self.nnz = int(nz.shape[0])
+        assert self.nnz < 2 ** 31
+        counts = torch.bincount(nz[:, 0], minlength=self.N)
+        self.rowptr = torch.zeros(self.N + 1, dtype=torch.int64, device=x.device)
+        self.rowptr[1:] = torch.cumsum(counts, 0)
+        self.rowptr_host = self.rowptr.cpu()
+        self.rowptr = self.rowptr.to(torch.int32)
+        self.colidx = nz[:, 1].to(torch.int32).contiguous()
+        v = x[nz[:, 0], nz[:, 1]].float().contiguous()
+        self.val = None if bool((v == 1).all()) else v
+        self._csc = {}
+
+    def csc(self, r0, n):
+        key = (int(r0), int(n))
+        c = self._csc.get(key)
+        if c is None:
+            k0, k1 = int(self.rowptr_host[r0]), int(self.rowptr_host[r0 + n])
+            rows = torch.repeat_interleave(torch.arange(n, device=self.colidx.device, dtype=torch.int32),
+                                           (self.rowptr[r0 + 1:r0 + n + 1] - self.rowptr[r0:r0 + n]).long())
+            cols = self.colidx[k0:k1].long()
+            order = torch.sort(cols, stable=True).indices        # ascending rows kept within a column
+            colptr = torch.zeros(self.F + 1, dtype=torch.int64, device=cols.device)
+            colptr[1:] = torch.cumsum(torch.bincount(cols, minlength=self.F), 0)
+            c = (colptr.to(torch.int32), rows[order].contiguous(),
+                 None if self.val is None else self.val[k0:k1][order].contiguous())
+            self._csc[key] = c
+        return c
+
+
+def spmm_rows(xs, rows, row0, Wt, bias, Y, act=ACT_NONE, mask=None):
+    """Y[:rows] = act(x[row0:row0+rows] @ Wt + bias) (llp_spmm_rows); Wt bf16 [F, H]."""
+    L = lib()
+    H = Wt.shape[1]
+    check(L.llp_spmm_rows(rows, row0, H, xs.rowptr.data_ptr(), xs.colidx.data_ptr(), ptr(xs.val), Wt.data_ptr(),
+                          Wt.stride(0), ptr(bias), act, Y.data_ptr(), Y.stride(0), ptr(mask),
+                          mask.stride(0) if mask is not None else 0, stream_ptr()), "llp_spmm_rows")
+
+
+def spmm_tn(xs, r0, n, dY, dW, accumulate=False):
+    """dW (+)= dY[:n]^T @ x[r0:r0+n] (llp_spmm_tn); dW f32 [H, F] (row stride >= F)."""
+    L = lib()
+    colptr, rowidx, val = xs.csc(r0, n)
+    check(L.llp_spmm_tn(xs.F, dY.shape[1], colptr.data_ptr(), rowidx.data_ptr(), ptr(val), dY.data_ptr(),
+                        dY.stride(0), dW.data_ptr(), dW.stride(0), int(accumulate), stream_ptr()), "llp_spmm_tn")
 
 
 def head_fwd(Z, R, H, w, b, logit=None, prob=None, Z2=None, iz=None, iz2=None):

@@ -1,0 +1,119 @@
+"""Sparse-input first layer (csrc/spmm.hip: llp_spmm_rows / llp_spmm_tn) against a numpy
+restatement of nn.Linear on the sparse x (src/models.py:48) that sums in the kernels' index
+order: bit for bit, ReLU bit masks included.  Binary values (bag-of-words) and small-integer
+values (every fma exact in f64, rounded once to f32 as fmaf does)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def K():
+    import llp_hip
+    return llp_hip
+
+
+def _bf16_round(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
+
+
+def _x(N, F, dens, values, seed):
+    rng = np.random.default_rng(seed)
+    x = (rng.random((N, F)) < dens).astype(np.float32)
+    x[N // 3] = 0                                # an empty row
+    if values:
+        x *= rng.choice(np.array([0.5, 2.0, 3.0], np.float32), size=(N, F))
+    return x
+
+
+def _fma_seq(acc, v, w):
+    """acc (f32) <- fmaf(v, w, acc), elementwise: exact in f64 for these operands, one rounding."""
+    return (acc.astype(np.float64) + np.float64(v) * w.astype(np.float64)).astype(np.float32)
+
+
+@pytest.mark.parametrize("H", [256, 64, 520])
+@pytest.mark.parametrize("values", [False, True])
+@pytest.mark.parametrize("relu", [False, True])
+def test_spmm_rows_bit_exact(H, values, relu):
+    k = K()
+    N, F = 203, 700
+    x = _x(N, F, 0.02, values, H + values)
+    g = torch.Generator().manual_seed(5)
+    Wt = (torch.randn(F, H, generator=g) * 0.2).to(torch.bfloat16)
+    bias = torch.randn(H, generator=g) * 0.1
+    xs = k.SparseRows(torch.from_numpy(x).to(DEV))
+    assert (xs.val is None) == (not values)
+    r0, rows = 17, 150
+    Y = torch.full((rows + 3, H), 7.0, dtype=torch.bfloat16, device=DEV)
+    mask = torch.full((rows, H // 8), 0xAB, dtype=torch.uint8, device=DEV) if relu and H % 8 == 0 else None
+    Wt_d = Wt.to(DEV)
+    k.spmm_rows(xs, rows, r0, Wt_d, bias.to(DEV), Y, act=k.ACT_RELU if relu else k.ACT_NONE, mask=mask)
+    torch.cuda.synchronize()
+    Wf = Wt.float().numpy()
+    ref = np.zeros((rows, H), np.float32)
+    for r in range(rows):
+        acc = np.zeros(H, np.float32)
+        for c in np.nonzero(x[r0 + r])[0]:
+            acc = _fma_seq(acc, x[r0 + r, c], Wf[c])
+        ref[r] = acc + bias.numpy()
+    refb = _bf16_round(ref)
+    if relu:
+        refb = torch.where(refb.view(torch.int16) < 0, torch.zeros_like(refb), refb)
+    got = Y[:rows].cpu()
+    assert torch.equal(got.view(torch.int16), refb.view(torch.int16))
+    assert torch.equal(Y[rows:].cpu().float(), torch.full((3, H), 7.0))     # rows past `rows` untouched
+    if mask is not None:
+        nz = (refb.view(torch.int16) != 0).numpy().reshape(rows, H // 8, 8)
+        ref_mask = (nz * (1 << np.arange(8))).sum(-1).astype(np.uint8)
+        assert np.array_equal(mask.cpu().numpy(), ref_mask)
+
+
+@pytest.mark.parametrize("H", [256, 128, 1024])
+@pytest.mark.parametrize("values", [False, True])
+def test_spmm_tn_bit_exact(H, values):
+    k = K()
+    N, F = 240, 333
+    x = _x(N, F, 0.03, values, 7 * H + values)
+    g = torch.Generator().manual_seed(11)
+    xs = k.SparseRows(torch.from_numpy(x).to(DEV))
+    r0, n = 30, 180
+    dY = (torch.randn(n, H, generator=g) * 0.3).to(torch.bfloat16)
+    dW = torch.full((H, F + 5), 3.0, device=DEV)[:, :F]     # row stride F + 5
+    for accumulate in (False, True):
+        k.spmm_tn(xs, r0, n, dY.to(DEV), dW, accumulate=accumulate)
+    torch.cuda.synchronize()
+    dYf = dY.float().numpy()
+    ref = np.zeros((F, H), np.float32)
+    for f in range(F):
+        acc = np.zeros(H, np.float32)
+        for r in np.nonzero(x[r0:r0 + n, f])[0]:                # ascending rows of the slice
+            acc = _fma_seq(acc, x[r0 + r, f], dYf[r])
+        ref[f] = acc
+    got = dW.cpu().numpy()
+    assert np.array_equal(got, (ref.T + ref.T).astype(np.float32))   # second call accumulated once more
+
+
+def test_spmm_csc_slices():
+    """SparseRows.csc: per-slice column lists (local rows, ascending) reproduce the slice."""
+    k = K()
+    x = _x(97, 50, 0.1, True, 3)
+    xs = k.SparseRows(torch.from_numpy(x).to(DEV))
+    for r0, n in [(0, 97), (10, 40), (96, 1)]:
+        colptr, rowidx, val = xs.csc(r0, n)
+        dense = np.zeros((n, 50), np.float32)
+        cp, ri, vv = colptr.cpu().numpy(), rowidx.cpu().numpy(), val.cpu().numpy()
+        for f in range(50):
+            rows = ri[cp[f]:cp[f + 1]]
+            assert np.all(np.diff(rows) > 0)
+            dense[rows, f] = vv[cp[f]:cp[f + 1]]
+        assert np.array_equal(dense, x[r0:r0 + n])
+
+
+def test_spmm_rejects_bad_shapes():
+    k = K()
+    xs = k.SparseRows(torch.from_numpy(_x(8, 300, 0.05, False, 1)).to(DEV))
+    Wt = torch.zeros(300, 12, dtype=torch.bfloat16, device=DEV)        # H % 8 != 0
+    with pytest.raises(RuntimeError):
+        k.spmm_rows(xs, 8, 0, Wt, None, torch.zeros(8, 12, dtype=torch.bfloat16, device=DEV))

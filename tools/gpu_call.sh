@@ -98,6 +98,12 @@ for RA in "$@"; do
       cat $O/phys1g.json $O/phys4g.json
       timeout -k 10 300 $PROF -d $O/phys_t1 -o t -- python tools/physics_bench.py --steps 10 --dtype bf16 --graph > $O/phys_t1.log 2>&1 || fail phys-t1 $O/phys_t1.log
       timeout -k 10 300 $PROF -d $O/phys_t4 -o t -- python tools/physics_bench.py --steps 10 --dtype bf16 --emulate-ranks 4 --graph > $O/phys_t4.log 2>&1 || fail phys-t4 $O/phys_t4.log ;;
+    physics-ab)     # sparse vs dense first student layer, graph replays, 1 rank and rank 0 of 4, twice
+      for i in 1 2; do for E in "" "--emulate-ranks 4"; do for D in "" "--dense-input"; do
+        timeout -k 10 300 python tools/physics_bench.py --steps 20 --dtype bf16 --graph $E $D > $O/phys_ab.tmp 2> $O/phys_ab.err || fail physics-ab $O/phys_ab.err
+        echo "{\"args\": \"$E $D\", \"run\": $(head -1 $O/phys_ab.tmp)}" >> $O/phys_ab.jsonl
+      done; done; done
+      cut -c1-200 $O/phys_ab.jsonl ;;
     bf16-accuracy)  # paired bf16 - fp32 Hits@K over seeds (tools/bf16_accuracy.py)
       timeout -k 10 1000 python tools/bf16_accuracy.py ${ACC_ARGS:-} > $O/bf16_accuracy.jsonl 2> $O/bf16_accuracy.err || fail bf16-accuracy $O/bf16_accuracy.err
       tail -5 $O/bf16_accuracy.jsonl ;;

@@ -82,6 +82,11 @@ def main():
     out.append(("adam one launch", us, adam_bytes))
     us = timed(lambda: K.adam_step(dd, n, max_numel, sumsq, 1e9, 1e-3, 0.9, 0.999, 1e-8, step), args.reps)
     out.append(("adam two launches", us, adam_bytes))
+    w1 = K.descs_to_device(descs[:1], dev)    # the input weight alone: a grid with no idle tensors
+    us = timed(lambda: K.adam_step(w1, 1, max_numel, sumsq, 1e9, 1e-3, 0.9, 0.999, 1e-8, step, fused=True), args.reps)
+    out.append(("adam one launch, input weight alone", us, 28 * descs[0].numel + 4 * descs[0].numel))
+    us = timed(lambda: K.grad_sumsq(w1, 1, max_numel, 1, sumsq, ws, ticket=ticket), args.reps)
+    out.append(("grad_sumsq one launch, input weight alone", us, 4 * descs[0].numel))
     src = torch.empty(adam_bytes // 8, dtype=torch.float32, device=dev)
     dst = torch.empty_like(src)
     us = timed(lambda: dst.copy_(src), args.reps)

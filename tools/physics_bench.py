@@ -55,7 +55,7 @@ def _hb_two_kernel(self, R, tgt, dZ, drow, h, out):
     K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, out, count=n_u, out_rows=uniq)
 
 
-def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False):
+def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False, sparse_input=True):
     dev = torch.device("cuda", 0)
     a = physics_args()
     td = split[0]                                     # training_data: old nodes, old-old edges
@@ -73,7 +73,7 @@ def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False):
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
     row, col = td.edge_index
     eng = llp_engine.DistillEngine(model, pred, tpred, td.x.to(dev), t_h.to(dev), row.numpy(), col.numpy(), N, a,
-                                   opt, dtype=dtype, seed=11, shard_student=shard_student)
+                                   opt, dtype=dtype, seed=11, shard_student=shard_student, sparse_input=sparse_input)
     if emulate and shard_student:
         eng.emulate_shard = (0, emulate)      # rank 0's slice of the node-sharded student (default)
     pairs = td.edge_index.t().to(torch.int32).to(dev).contiguous()      # pos_train_edge (src/main.py:153)
@@ -118,7 +118,7 @@ def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False):
             "emulated_ranks": emulate or None, "fb_shard": eng.emulate_shard is not None, "N_old": N, "F": F, "E_train_directed": E, "anchors_per_step": B_full,
             "contexts_per_anchor": a.rw_step * a.hops * (1 + a.ns_rate), "edges_per_step": P_full,
             "steps_per_epoch": -(-E // P_full), "loss": loss, "hipgraph": replay is not None,
-            "host_issue_ms_per_step": t_issue * 1e3}
+            "host_issue_ms_per_step": t_issue * 1e3, "sparse_first_layer": eng.xs is not None}
 
 
 def main():
@@ -131,6 +131,8 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay a hipGraph of the step (capture_fullbatch); eager measured faster, "
                          "profiles/r03_physics_devcount_graph_ab.txt")
+    ap.add_argument("--dense-input", action="store_true",
+                    help="A/B: the first student layer as dense GEMMs over x (not llp_spmm_rows / llp_spmm_tn)")
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "llp_physics"))
     ap.add_argument("--no-edge-table", action="store_true",
                     help="A/B: the dense negative sampler's membership test by binary search of the sorted keys")
@@ -149,7 +151,7 @@ def main():
            "split_s": prep, "runs": []}
     for dt in opt.dtype.split(","):
         out["runs"].append(run(dt, opt.steps, opt.warmup, opt.emulate_ranks, split, not opt.replicated,
-                               opt.graph))
+                               opt.graph, not opt.dense_input))
         print(json.dumps(out["runs"][-1]), flush=True)
     print(json.dumps(out), flush=True)
 
