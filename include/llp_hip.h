@@ -150,13 +150,21 @@ int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q,
  *   llp_spmm_tn:   dW[o, f] (+)= sum_{k in CSC column f} val[k] * dY[rowidx[k], o]: the
  *                  weight gradient of the same Linear (f32, row stride ldw >= F); the bias
  *                  gradient is llp_colsum of dY.
- * f32 sums in index order: deterministic, equal to llp_gemm_nt / llp_gemm_tn on the dense x up
- * to the order of the f32 sums.  H <= 1024 (H % 8 == 0 forward, % 4 backward). */
+ * f32 sums in a fixed order (forward: 4 interleaved streams of the row's nonzeros, summed
+ * (s0+s1)+(s2+s3); backward: 8 interleaved streams, butterfly-summed, over a column's nonzeros
+ * or, for a heavy column, over each of 4 contiguous quarters, then (q0+q1)+(q2+q3)): deterministic, equal to llp_gemm_nt /
+ * llp_gemm_tn on the dense x up to the order of the f32 sums.  H <= 4096, H % 8 == 0, 16-B
+ * aligned rows of Wt, Y and dY.  Column slices go to XCDs by workgroup index (csrc/spmm.hip). */
 int llp_spmm_rows(int64_t rows, int64_t row0, int64_t H, const int32_t* rowptr, const int32_t* colidx,
                   const float* val, const void* Wt, int64_t ldw, const float* bias, int act, void* Y,
                   int64_t ldy, void* mask_out, int64_t ld_mask, void* stream);
 int llp_spmm_tn(int64_t F, int64_t H, const int32_t* colptr, const int32_t* rowidx, const float* val,
-                const void* dY, int64_t ldy, float* dW, int64_t ldw, int accumulate, void* stream);
+                const int32_t* perm, int64_t n_heavy, const void* dY, int64_t ldy, float* dW, int64_t ldw,
+                int accumulate, void* stream);
+/* llp_spmm_tn's schedule: perm = the features by nonzero count, most first (ties by index); the
+ * first n_heavy (>= llp_spmm_heavy_nnz() nonzeros) take a workgroup each, split in quarters
+ * summed (q0+q1)+(q2+q3); the rest one wave each. */
+int llp_spmm_heavy_nnz(void);
 
 /* Column sums: out[n] (+)= sum_m Y[m,n] (bias gradient).  Deterministic. */
 int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N);

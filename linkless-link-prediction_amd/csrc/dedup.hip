@@ -721,7 +721,9 @@ __global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __rest
 // calls: zero at the first call (a zeroing launch when the caller does not vouch for it), left so
 // by every call (counts reset by the scan, the ticket by its last workgroup, the flags tagged with a
 // per-call epoch that the last workgroup advances).
-constexpr int LB_T = 256, LB_I = 8, LB_B = LB_T * LB_I;   // nodes per scan block: 2,048
+// nodes per scan block: 512 (61 workgroups at coauthor-physics' 31,044 nodes, 461 at collab's
+// 235,868: the absent nodes' row zeroing, up to 16 MB, is spread over that many CUs)
+constexpr int LB_T = 256, LB_I = 2, LB_B = LB_T * LB_I;
 struct ScanArgs {
   int64_t N, R;
   int32_t* cnt;                 // [N] per-node counts (zeroed here after use)
@@ -736,6 +738,8 @@ struct ScanArgs {
 
 __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
   __shared__ unsigned long long ts[LB_T];
+  __shared__ int32_t absent[LB_B];   // this workgroup's absent nodes (local index), n_absent of them
+  __shared__ int n_absent;
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const uint32_t epoch = a.ctl[0] + 1u;   // read by every workgroup before its ticket add
@@ -758,6 +762,7 @@ __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
     __syncthreads();
   }
   const unsigned long long blk_sum = ts[LB_T - 1];
+  if (t == 0) n_absent = 0;
   const unsigned long long excl = llp_lookback_u64(a.flags, a.agg, a.incl, b, blk_sum, epoch, &a.ctl[2]);
   // compaction (compact_count_kernel's writes), counts back to zero, absent nodes' rows zeroed
   unsigned long long run = excl + ts[t] - s;
@@ -772,9 +777,6 @@ __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
         a.uidx[node] = slot;
         a.start[node] = st;
         a.cnt[node] = 0;
-      } else if (a.zero_rows) {
-        uint4* zr = reinterpret_cast<uint4*>(a.zero_rows + node * a.zero_ld);
-        for (int64_t w = 0; w < a.zero_u4; ++w) zr[w] = make_uint4(0u, 0u, 0u, 0u);
       }
       if (node == a.N - 1) {
         const int32_t U = slot + (c[i] > 0 ? 1 : 0);
@@ -785,6 +787,15 @@ __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
       }
     }
     run += v[i];
+    if (a.zero_rows && node < a.N && c[i] == 0) absent[atomicAdd(&n_absent, 1)] = t * LB_I + i;
+  }
+  if (a.zero_rows) {   // absent nodes' rows (few): consecutive threads on consecutive 16-B words
+    __syncthreads();
+    const int32_t wpr = (int32_t)a.zero_u4, total = n_absent * wpr;
+    for (int32_t q = t; q < total; q += LB_T) {
+      const int32_t n = absent[q / wpr], wd = q % wpr;
+      reinterpret_cast<uint4*>(a.zero_rows + (b * (int64_t)LB_B + n) * a.zero_ld)[wd] = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
   // the last workgroup advances the epoch (every workgroup read it above)
   if (llp_arrive_last(&a.ctl[1], gridDim.x) && t == 0)

@@ -208,10 +208,12 @@ __global__ __launch_bounds__(256) void neg_tile_scatter(int64_t M, int64_t num_n
 // (llp_neg_sample_dense2; the same outputs as llp_neg_sample_dense): the candidates' table and the
 // tile scan's look-back flags persist in the workspace with a per-call epoch instead of being
 // reset every call (neg_table_init), and the tile count / scan / scatter run as ONE pass with a
-// decoupled look-back.  Table entry = (epoch & 0xFFFFFF) << 40 | candidate value (values < 2^40):
-// an entry of another epoch is free; a stale entry that happens to carry the current tag is
-// only ever taken as occupied (a wasted slot) or as the same value, which the first-index word
-// (epoch << 32 | ~index, atomicMax) then claims correctly.
+// decoupled look-back.  Table entry = (epoch & 0xFFFFFF) << 40 | the index of the FIRST candidate
+// holding the slot's value (indices < 2^31); the value itself is read from cand[], which each
+// candidate stores write-through before its claim can be seen.  An entry of another epoch is free.
+// One atomic per candidate (the claim); a repeated value takes an atomicMin on the entry, so the
+// lowest index keeps it -- the first occurrence, as torch.unique-then-first does (the two-word
+// form took a second atomic, the first-index atomicMax, for every candidate).
 constexpr int64_t NEG2_VALUE_BITS = 40;
 constexpr uint64_t NEG2_VALUE_MASK = (1ull << NEG2_VALUE_BITS) - 1;
 
@@ -219,8 +221,8 @@ __global__ void neg_candidates2(int64_t M, int enumerate_all, uint64_t populatio
                                 const int64_t* __restrict__ step_ctr, int64_t stream_offset,
                                 const int64_t* __restrict__ edge_keys, int64_t n_keys,
                                 const uint64_t* __restrict__ edge_table, int64_t edge_table_size,
-                                int64_t* __restrict__ cand, int32_t* __restrict__ slot, uint64_t* __restrict__ tkeys,
-                                unsigned long long* __restrict__ tfirst, int64_t T, const uint32_t* __restrict__ ctl) {
+                                int64_t* cand, int32_t* __restrict__ slot, uint64_t* __restrict__ tkeys, int64_t T,
+                                const uint32_t* __restrict__ ctl) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= M) return;
   const uint32_t epoch = ctl[0] + 1u;
@@ -234,32 +236,36 @@ __global__ void neg_candidates2(int64_t M, int enumerate_all, uint64_t populatio
     const uint64_t hi = philox_u32(seed, stream, 2 * (uint64_t)i + 1);
     c = __umul64hi((hi << 32) | lo, population);
   }
-  cand[i] = (int64_t)c;
+  // write-through, drained before the claim below publishes this index
+  __hip_atomic_store((unsigned long long*)&cand[i], (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (edge_table ? in_table(edge_table, edge_table_size, c) : in_sorted(edge_keys, n_keys, (int64_t)c)) {
     slot[i] = -1;
     return;
   }
-  const unsigned long long mine = ((unsigned long long)epoch << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long mine = tag | (unsigned long long)i;
   uint32_t h = mix32(c) & (uint32_t)(T - 1);
   while (true) {
     unsigned long long e = __hip_atomic_load((unsigned long long*)&tkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((e & ~NEG2_VALUE_MASK) != tag) {   // free in this epoch: claim it
-      const unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[h], e, (unsigned long long)(tag | c));
-      if (prev != e) continue;   // taken meanwhile: look at the same slot again
-      e = tag | c;
+      const unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[h], e, mine);
+      if (prev == e) break;
+      continue;                            // taken meanwhile: look at the same slot again
     }
-    if ((e & NEG2_VALUE_MASK) == c) {
-      atomicMax(&tfirst[h], mine);
-      slot[i] = (int32_t)h;
-      return;
+    const unsigned long long cj = __hip_atomic_load((unsigned long long*)&cand[e & NEG2_VALUE_MASK], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    if (cj == c) {                         // the same value: the lower index keeps the slot
+      atomicMin((unsigned long long*)&tkeys[h], mine);
+      break;
     }
     h = (h + 1) & (uint32_t)(T - 1);
   }
+  slot[i] = (int32_t)h;
 }
 
 __global__ __launch_bounds__(256) void neg_compact2(int64_t M, int64_t num_nodes, int64_t num_neg,
                                                     const int64_t* __restrict__ cand, const int32_t* __restrict__ slot,
-                                                    const unsigned long long* __restrict__ tfirst,
+                                                    const uint64_t* __restrict__ tkeys,
                                                     uint32_t* flags, unsigned long long* agg, unsigned long long* incl,
                                                     uint32_t* ctl, int32_t* __restrict__ out, int64_t ld_out,
                                                     int32_t* __restrict__ count) {
@@ -274,8 +280,7 @@ __global__ __launch_bounds__(256) void neg_compact2(int64_t M, int64_t num_nodes
     v[k] = 0;
     if (i < M) {
       const int32_t s = slot[i];
-      v[k] = (s >= 0 && tfirst[s] == (((unsigned long long)epoch << 32) |
-                                      (unsigned long long)(0xFFFFFFFFu - (uint32_t)i))) ? 1 : 0;
+      v[k] = (s >= 0 && tkeys[s] == ((uint64_t)(epoch & 0xFFFFFFu) << NEG2_VALUE_BITS | (uint64_t)i)) ? 1 : 0;
     }
     mine += v[k];
   }
@@ -511,7 +516,7 @@ static int64_t al256b(int64_t b) { return (b + 255) & ~(int64_t)255; }
 static int64_t neg2_state_bytes(int64_t M) {
   const int64_t T = pow2_at_least(2 * (M > 0 ? M : 1));
   const int64_t ntiles = (M + NC_TILE - 1) / NC_TILE;
-  return al256b(T * 8) + al256b(T * 8) + al256b(ntiles * 4) + 256;
+  return al256b(T * 8) + al256b(ntiles * 4) + 256;
 }
 
 extern "C" int64_t llp_neg_sample_dense2_state_bytes(int64_t max_candidates) { return neg2_state_bytes(max_candidates); }
@@ -551,8 +556,6 @@ extern "C" int llp_neg_sample_dense2(int64_t num_nodes, const int64_t* edge_keys
   }
   uint64_t* tkeys = reinterpret_cast<uint64_t*>(w);
   w += al256b(T * 8);
-  unsigned long long* tfirst = reinterpret_cast<unsigned long long*>(w);
-  w += al256b(T * 8);
   uint32_t* flags = reinterpret_cast<uint32_t*>(w);
   w += al256b(ntiles * 4);
   uint32_t* ctl = reinterpret_cast<uint32_t*>(w);
@@ -570,10 +573,10 @@ extern "C" int llp_neg_sample_dense2(int64_t num_nodes, const int64_t* edge_keys
     return LLP_OK;
   }
   hipLaunchKernelGGL(neg_candidates2, dim3(ceil_div_u(M, 256)), dim3(256), 0, s, M, enumerate_all, population, seed,
-                     step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size, cand, slot, tkeys, tfirst,
-                     T, (const uint32_t*)ctl);
+                     step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size, cand, slot, tkeys, T,
+                     (const uint32_t*)ctl);
   LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(neg_compact2, dim3((unsigned)ntiles), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot, tfirst,
+  hipLaunchKernelGGL(neg_compact2, dim3((unsigned)ntiles), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot, tkeys,
                      flags, agg, incl, ctl, out, ld_out, count);
   LLP_LAUNCH_CHECK();
   return LLP_OK;

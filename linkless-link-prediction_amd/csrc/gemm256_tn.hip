@@ -535,9 +535,13 @@ int64_t llp_gemm_tn_256_splits(int64_t M, int64_t P, int64_t Q) {
   const int64_t target = llp_cu_count();   // one wave of workgroups, one per CU
   // whole waves only: tiles * splits <= CUs (33 tiles x 8 splits = 264 blocks ran as two
   // rounds on 256 CUs, the second one 8 blocks long -- the physics first layer's weight gradient)
-  int64_t splits = tiles >= target ? 1 : target / tiles;
-  const int64_t maxs = (M + TKM * 16 - 1) / (TKM * 16);   // >= 16 m-steps per split
-  if (splits > maxs) splits = maxs;
+  const int64_t wave = tiles >= target ? 1 : target / tiles;
+  // >= 16 m-steps per split; a short M (the physics student's 256 x 256 layer over a rank's
+  // 7,761 rows: 16 splits, 21.5 us) may go down to 4 m-steps while its f32 slabs stay <= 32 MB
+  const int64_t s16 = std::min<int64_t>(wave, (M + TKM * 16 - 1) / (TKM * 16));
+  int64_t splits = std::min<int64_t>(wave, (M + TKM * 4 - 1) / (TKM * 4));
+  const int64_t slab = P * Q * (int64_t)sizeof(float);
+  if (splits * slab > (32ll << 20)) splits = std::max<int64_t>(s16, (32ll << 20) / slab);
   return splits < 1 ? 1 : splits;
 }
 

@@ -68,7 +68,8 @@ _SIGS = {
     "llp_colsum": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp]),
     "llp_spmm_rows": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp,
                               c_i64, c_vp]),
-    "llp_spmm_tn": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
+    "llp_spmm_tn": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
+    "llp_spmm_heavy_nnz": (c_int, []),
     "llp_head_fwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_head_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_head_bwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_vp, c_i64, c_vp, c_vp,
@@ -329,10 +330,14 @@ class SparseRows:
                                            (self.rowptr[r0 + 1:r0 + n + 1] - self.rowptr[r0:r0 + n]).long())
             cols = self.colidx[k0:k1].long()
             order = torch.sort(cols, stable=True).indices        # ascending rows kept within a column
+            cnt = torch.bincount(cols, minlength=self.F)
             colptr = torch.zeros(self.F + 1, dtype=torch.int64, device=cols.device)
-            colptr[1:] = torch.cumsum(torch.bincount(cols, minlength=self.F), 0)
+            colptr[1:] = torch.cumsum(cnt, 0)
+            # llp_spmm_tn's schedule: most nonzeros first (ties by feature), the heavy ones counted
+            perm = torch.sort(-cnt, stable=True).indices
+            n_heavy = int((cnt >= load().llp_spmm_heavy_nnz()).sum())
             c = (colptr.to(torch.int32), rows[order].contiguous(),
-                 None if self.val is None else self.val[k0:k1][order].contiguous())
+                 None if self.val is None else self.val[k0:k1][order].contiguous(), perm.to(torch.int32), n_heavy)
             self._csc[key] = c
         return c
 
@@ -349,9 +354,10 @@ def spmm_rows(xs, rows, row0, Wt, bias, Y, act=ACT_NONE, mask=None):
 def spmm_tn(xs, r0, n, dY, dW, accumulate=False):
     """dW (+)= dY[:n]^T @ x[r0:r0+n] (llp_spmm_tn); dW f32 [H, F] (row stride >= F)."""
     L = lib()
-    colptr, rowidx, val = xs.csc(r0, n)
-    check(L.llp_spmm_tn(xs.F, dY.shape[1], colptr.data_ptr(), rowidx.data_ptr(), ptr(val), dY.data_ptr(),
-                        dY.stride(0), dW.data_ptr(), dW.stride(0), int(accumulate), stream_ptr()), "llp_spmm_tn")
+    colptr, rowidx, val, perm, n_heavy = xs.csc(r0, n)
+    check(L.llp_spmm_tn(xs.F, dY.shape[1], colptr.data_ptr(), rowidx.data_ptr(), ptr(val), perm.data_ptr(), n_heavy,
+                        dY.data_ptr(), dY.stride(0), dW.data_ptr(), dW.stride(0), int(accumulate), stream_ptr()),
+          "llp_spmm_tn")
 
 
 def head_fwd(Z, R, H, w, b, logit=None, prob=None, Z2=None, iz=None, iz2=None):

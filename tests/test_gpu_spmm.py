@@ -1,6 +1,6 @@
 """Sparse-input first layer (csrc/spmm.hip: llp_spmm_rows / llp_spmm_tn) against a numpy
-restatement of nn.Linear on the sparse x (src/models.py:48) that sums in the kernels' index
-order: bit for bit, ReLU bit masks included.  Binary values (bag-of-words) and small-integer
+restatement of nn.Linear on the sparse x (src/models.py:48) that sums in the kernels' order
+(interleaved streams, butterfly): bit for bit, ReLU bit masks included.  Binary values (bag-of-words) and small-integer
 values (every fma exact in f64, rounded once to f32 as fmaf does)."""
 import numpy as np
 import pytest
@@ -33,7 +33,21 @@ def _fma_seq(acc, v, w):
     return (acc.astype(np.float64) + np.float64(v) * w.astype(np.float64)).astype(np.float32)
 
 
-@pytest.mark.parametrize("H", [256, 64, 520])
+def _streams(idx, vals, rows_of, streams):
+    """The kernels' sum over one index list: stream s takes positions s, s + streams, .. (fmaf
+    in order), then the butterfly ((s0+s1)+(s2+s3)) .. in f32."""
+    parts = []
+    for s in range(streams):
+        acc = np.zeros(rows_of.shape[1], np.float32)
+        for j in range(s, len(idx), streams):
+            acc = _fma_seq(acc, vals[j], rows_of[idx[j]])
+        parts.append(acc)
+    while len(parts) > 1:
+        parts = [(parts[i] + parts[i + 1]).astype(np.float32) for i in range(0, len(parts), 2)]
+    return parts[0]
+
+
+@pytest.mark.parametrize("H", [256, 64, 520, 136])
 @pytest.mark.parametrize("values", [False, True])
 @pytest.mark.parametrize("relu", [False, True])
 def test_spmm_rows_bit_exact(H, values, relu):
@@ -54,10 +68,8 @@ def test_spmm_rows_bit_exact(H, values, relu):
     Wf = Wt.float().numpy()
     ref = np.zeros((rows, H), np.float32)
     for r in range(rows):
-        acc = np.zeros(H, np.float32)
-        for c in np.nonzero(x[r0 + r])[0]:
-            acc = _fma_seq(acc, x[r0 + r, c], Wf[c])
-        ref[r] = acc + bias.numpy()
+        cols = np.nonzero(x[r0 + r])[0]
+        ref[r] = _streams(cols, x[r0 + r, cols], Wf, 4) + bias.numpy()
     refb = _bf16_round(ref)
     if relu:
         refb = torch.where(refb.view(torch.int16) < 0, torch.zeros_like(refb), refb)
@@ -76,6 +88,7 @@ def test_spmm_tn_bit_exact(H, values):
     k = K()
     N, F = 240, 333
     x = _x(N, F, 0.03, values, 7 * H + values)
+    x[:, 5:40:3] = (np.random.default_rng(H).random((N, 12)) < 0.9) * (2.0 if values else 1.0)   # heavy columns
     g = torch.Generator().manual_seed(11)
     xs = k.SparseRows(torch.from_numpy(x).to(DEV))
     r0, n = 30, 180
@@ -86,11 +99,18 @@ def test_spmm_tn_bit_exact(H, values):
     torch.cuda.synchronize()
     dYf = dY.float().numpy()
     ref = np.zeros((F, H), np.float32)
+    heavy = k.load().llp_spmm_heavy_nnz()
+    n_heavy = 0
     for f in range(F):
-        acc = np.zeros(H, np.float32)
-        for r in np.nonzero(x[r0:r0 + n, f])[0]:                # ascending rows of the slice
-            acc = _fma_seq(acc, x[r0 + r, f], dYf[r])
-        ref[f] = acc
+        rws = np.nonzero(x[r0:r0 + n, f])[0]                   # ascending rows of the slice
+        if len(rws) >= heavy:                                    # four contiguous quarters
+            n_heavy += 1
+            q = [len(rws) * w // 4 for w in range(5)]
+            w = [_streams(rws[q[i]:q[i + 1]], x[r0 + rws[q[i]:q[i + 1]], f], dYf, 8) for i in range(4)]
+            ref[f] = ((w[0] + w[1]).astype(np.float32) + (w[2] + w[3]).astype(np.float32)).astype(np.float32)
+        else:
+            ref[f] = _streams(rws, x[r0 + rws, f], dYf, 8)
+    assert xs.csc(r0, n)[4] == n_heavy and 0 < n_heavy < F      # both schedules exercised
     got = dW.cpu().numpy()
     assert np.array_equal(got, (ref.T + ref.T).astype(np.float32))   # second call accumulated once more
 
@@ -101,7 +121,9 @@ def test_spmm_csc_slices():
     x = _x(97, 50, 0.1, True, 3)
     xs = k.SparseRows(torch.from_numpy(x).to(DEV))
     for r0, n in [(0, 97), (10, 40), (96, 1)]:
-        colptr, rowidx, val = xs.csc(r0, n)
+        colptr, rowidx, val, perm, n_heavy = xs.csc(r0, n)
+        cnt = np.diff(colptr.cpu().numpy())
+        assert np.array_equal(perm.cpu().numpy(), np.argsort(-cnt, kind="stable"))
         dense = np.zeros((n, 50), np.float32)
         cp, ri, vv = colptr.cpu().numpy(), rowidx.cpu().numpy(), val.cpu().numpy()
         for f in range(50):
@@ -117,3 +139,6 @@ def test_spmm_rejects_bad_shapes():
     Wt = torch.zeros(300, 12, dtype=torch.bfloat16, device=DEV)        # H % 8 != 0
     with pytest.raises(RuntimeError):
         k.spmm_rows(xs, 8, 0, Wt, None, torch.zeros(8, 12, dtype=torch.bfloat16, device=DEV))
+    Wt = torch.zeros(300, 20, dtype=torch.bfloat16, device=DEV)[:, :16]   # rows not 16-B aligned
+    with pytest.raises(RuntimeError):
+        k.spmm_rows(xs, 8, 0, Wt, None, torch.zeros(8, 16, dtype=torch.bfloat16, device=DEV))
