@@ -721,9 +721,13 @@ __global__ __launch_bounds__(256) void segsort_long_kernel(const int32_t* __rest
 // calls: zero at the first call (a zeroing launch when the caller does not vouch for it), left so
 // by every call (counts reset by the scan, the ticket by its last workgroup, the flags tagged with a
 // per-call epoch that the last workgroup advances).
-// nodes per scan block: 512 (61 workgroups at coauthor-physics' 31,044 nodes, 461 at collab's
-// 235,868: the absent nodes' row zeroing, up to 16 MB, is spread over that many CUs)
-constexpr int LB_T = 256, LB_I = 2, LB_B = LB_T * LB_I;
+// nodes per scan block LB_T * I: 512 up to 64k nodes (coauthor-physics' 31,044: 61 workgroups
+// instead of 16), 2,048 above (collab's 235,868: 116; at 512 per block its look-back over 461
+// workgroups cost 13.8 against 10.8 us, tools/dedup2_probe.py).  The workspace's look-back arrays
+// are sized for the smaller blocks.
+constexpr int LB_T = 256, LB_I_MIN = 2, LB_B_MIN = LB_T * LB_I_MIN;
+constexpr int64_t LB_SMALL_N = 65536;
+static int lb_items(int64_t num_nodes) { return num_nodes <= LB_SMALL_N ? 2 : 8; }
 struct ScanArgs {
   int64_t N, R;
   int32_t* cnt;                 // [N] per-node counts (zeroed here after use)
@@ -736,7 +740,9 @@ struct ScanArgs {
   char* zero_rows; int64_t zero_ld; int64_t zero_u4;   // optional: rows of absent nodes zeroed (16-B words)
 };
 
+template <int LB_I>
 __global__ __launch_bounds__(LB_T) void dedup_scan_kernel(ScanArgs a) {
+  constexpr int LB_B = LB_T * LB_I;
   __shared__ unsigned long long ts[LB_T];
   __shared__ int32_t absent[LB_B];   // this workgroup's absent nodes (local index), n_absent of them
   __shared__ int n_absent;
@@ -957,14 +963,14 @@ extern "C" int llp_dedup_rows(int64_t num_nodes, int64_t R, const int32_t* targe
 
 // workspace of llp_dedup_rows2: [state: counts | look-back flags | control words] then scratch
 static int64_t dedup2_state_bytes(int64_t num_nodes) {
-  const int64_t nb = (num_nodes + LB_B - 1) / LB_B;
+  const int64_t nb = (num_nodes + LB_B_MIN - 1) / LB_B_MIN;
   return al256((num_nodes + 1) * 4) + al256(nb * 4) + 256;
 }
 
 extern "C" int64_t llp_dedup_rows2_state_bytes(int64_t num_nodes) { return dedup2_state_bytes(num_nodes); }
 
 extern "C" int64_t llp_dedup_rows2_workspace_bytes(int64_t num_nodes, int64_t R) {
-  const int64_t nb = (num_nodes + LB_B - 1) / LB_B;
+  const int64_t nb = (num_nodes + LB_B_MIN - 1) / LB_B_MIN;   // look-back arrays: the most blocks
   return dedup2_state_bytes(num_nodes) + 2 * al256(nb * 8) + 2 * al256((num_nodes + 1) * 4) + 2 * al256(R * 4) + 512;
 }
 
@@ -979,7 +985,7 @@ extern "C" int llp_dedup_rows2(int64_t num_nodes, int64_t R, const int32_t* targ
   LLP_CHECK_ARG(!zero_rows || (zero_row_bytes % 16 == 0 && zero_ld_bytes % 16 == 0 && ((uintptr_t)zero_rows & 15) == 0),
                 "llp_dedup_rows2: zero_rows must be 16-B aligned rows of a multiple of 16 bytes");
   char* w = reinterpret_cast<char*>(workspace);
-  const int64_t nb = (num_nodes + LB_B - 1) / LB_B;
+  const int64_t nb = (num_nodes + LB_B_MIN - 1) / LB_B_MIN;   // look-back arrays: the most blocks
   if (!state_clean) {   // first call on this workspace: the persistent state from zero
     const int64_t n32 = dedup2_state_bytes(num_nodes) / 4;
     hipLaunchKernelGGL(zero_u32_kernel, dim3(ceil_div_u(n32, 256)), dim3(256), 0, s, n32, (uint32_t*)w);
@@ -1014,7 +1020,10 @@ extern "C" int llp_dedup_rows2(int64_t num_nodes, int64_t R, const int32_t* targ
     hipLaunchKernelGGL(count_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, a.cnt, rank);
     LLP_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(dedup_scan_kernel, dim3((unsigned)nb), dim3(LB_T), 0, s, a);
+  const int li = lb_items(num_nodes);
+  const int64_t nbk = (num_nodes + LB_T * li - 1) / (LB_T * li);
+  if (li == 2) hipLaunchKernelGGL(dedup_scan_kernel<2>, dim3((unsigned)nbk), dim3(LB_T), 0, s, a);
+  else hipLaunchKernelGGL(dedup_scan_kernel<8>, dim3((unsigned)nbk), dim3(LB_T), 0, s, a);
   LLP_LAUNCH_CHECK();
   if (R == 0) return LLP_OK;
   hipLaunchKernelGGL(scatter_rank_kernel, dim3(ceil_div_u(R, 256)), dim3(256), 0, s, R, target, a.uidx, a.start,
