@@ -362,7 +362,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
   // bf16: the splits of one tile are adjacent in logical order (tile = lt / splits); f32: the
   // tiles of one split are (z = lt / ntile), so the workgroups an XCD runs together read the
   // same m rows of A and B (one HBM read, served from L2 to every tile of the split)
+#ifdef LLP_NO_L2_ORDER   // A/B build: the f32 splits adjacent too (tools/gpu_call.sh fp32-ab)
+  const int64_t tile = lt / splits, z = lt % splits;
+#else
   const int64_t tile = BF ? lt / splits : lt % ntile, z = BF ? lt % splits : lt / ntile;
+#endif
   const int64_t tp = tile / tilesQ, tq = tile % tilesQ;
   const int64_t p0 = tp * BM, q0 = tq * BN;
   if (p.m_dev) {   // live rows from the device count; the grid (splits) is the host M's
@@ -629,6 +633,9 @@ int64_t tn_splits(int dtype, int64_t M, int64_t P, int64_t Q) {
 static int64_t nt_groups(int64_t N, int64_t K, int es, int64_t tilesM) {
   const int64_t tilesN = (N + BN - 1) / BN;
   int64_t g = 1;
+#ifdef LLP_NO_L2_ORDER   // A/B build: one group, the round-3 walk
+  return g;
+#endif
   while (g * 2 <= tilesN && tilesN % (g * 2) == 0 && N * K * es / g > (2ll << 20) && tilesM >= 64) g *= 2;
   return g;
 }
