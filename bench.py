@@ -228,7 +228,7 @@ def evaluate(model, pred, data, dev):
             "hits_note": "after the timed steps from random init on synthetic data (not a converged model)"}
 
 
-SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_sage.json")
+SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r04_pmc_sage_orders.json")
 
 
 def practical_peak(dev, seconds=0.2, dtype="bf16"):
@@ -261,18 +261,21 @@ def practical_peak(dev, seconds=0.2, dtype="bf16"):
 
 def sage_aggregate(data, dev):
     """SAGE teacher's CSR mean aggregate (a11, src/sageconv_updated.py:65-81 / PyG SAGEConv mean)
-    at the collab shape, forward, F = 128 and 256, fp32 and bf16, event-timed live.
+    at the collab shape, forward, F = 128 and 256, fp32 and bf16, event-timed live, on the
+    graph in TeacherEngine's node order (llp_sage.locality_order: neighbour rows mostly hit L2).
     algorithmic bytes E*F*s + 4E + 4(N+1) + N*F*s (every neighbour row from memory, SURVEY
     §8d); compulsory bytes: x, col, rowptr read once, out written once; traffic: beyond-L2
-    counter bytes per launch from the committed PMC passes (profiles/r03_pmc_sage.json:
-    2 x FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits included, so an upper bound on HBM
-    bytes).  frac = traffic / time / 8 TB/s."""
+    counter bytes per launch from the committed PMC passes of the same order
+    (profiles/r04_pmc_sage_orders.json: 2 x FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits
+    included, so an upper bound on HBM bytes).  frac = traffic / time / 8 TB/s."""
     import llp_hip as K
     import llp_sage
-    g = llp_sage.Graph(data.edge_index, data.N, dev)
+    _, pi = llp_sage.locality_order(data.edge_index, data.N)
+    g = llp_sage.Graph(torch.from_numpy(pi[data.edge_index.numpy()]), data.N, dev)
     try:
         with open(SAGE_PMC_FILE) as f:
-            pmc = {(c["dtype"], c["F"], c["mode"]): c["counter_bytes"] for c in json.load(f)["configs"]}
+            pmc = {(c["dtype"], c["F"], c["mode"]): c["counter_bytes"] for c in json.load(f)["configs"]
+                   if c.get("order") == "locality"}
     except (OSError, ValueError, KeyError):
         pmc = {}
     out = []
@@ -294,8 +297,9 @@ def sage_aggregate(data, dev):
             comp = 2 * data.N * F_ * es + 4 * g.num_edges + 4 * (data.N + 1)
             traffic = pmc.get((dts, F_, "fwd"))
             tb = (traffic if traffic else algo) / (ms * 1e-3)
-            out.append({"kernel": "csr_agg_rows_kernel fwd", "dtype": dts, "F": F_, "N": data.N, "E": g.num_edges,
-                        "ms": ms, "achieved": tb / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            out.append({"kernel": "csr_agg_rows_kernel fwd", "order": "locality", "dtype": dts, "F": F_, "N": data.N,
+                        "E": g.num_edges, "ms": ms, "achieved": tb / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "traffic_over_compulsory": traffic / comp if traffic else None,
                         "frac": tb / 1e9 / PEAK_HBM_GBS, "traffic": traffic, "algorithmic_bytes": algo,
                         "algorithmic_frac": algo / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "compulsory_bytes": comp,
                         "compulsory_frac": comp / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS,

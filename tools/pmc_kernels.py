@@ -126,7 +126,8 @@ def sage(a):
         name = short(seg[0][0]) if seg else "?"
         e = entry(name, p["algorithmic_bytes"], [x[1] for x in seg], p["ms"] * 1e6,
                   "x rows re-read ~E/N times; the Infinity Cache serves most of them")
-        e.update({"dtype": p["dtype"], "F": p["F"], "mode": p["mode"], "compulsory_bytes": p["compulsory_bytes"],
+        e.update({"order": p.get("order", "id"), "dtype": p["dtype"], "F": p["F"], "mode": p["mode"],
+                  "compulsory_bytes": p["compulsory_bytes"], "counter_over_compulsory": e["counter_bytes"] / p["compulsory_bytes"],
                   "compulsory_frac": p["compulsory_bytes"] / (p["ms"] * 1e-3) / PEAK})
         res.append(e)
     out = {"workload": "SAGE mean aggregate over the synthetic ogbl-collab graph", "N": plan["N"], "E": plan["E"],
@@ -135,9 +136,9 @@ def sage(a):
            "durations": "HIP events in the same run (tools/sage_bench.py --agg-only)", "configs": res}
     json.dump(out, open(a.out, "w"), indent=1)
     for r in res:
-        print(f"{r['dtype']} F={r['F']} {r['mode']}: {r['avg_us']:6.1f} us  algo {r['algorithmic_TBs']:5.2f} TB/s "
+        print(f"{r['order']:8s} {r['dtype']} F={r['F']} {r['mode']}: {r['avg_us']:6.1f} us  algo {r['algorithmic_TBs']:5.2f} TB/s "
               f"counter {r['counter_bytes']/1e9:5.3f} GB {r['counter_TBs']:5.2f} TB/s "
-              f"({r['counter_over_algorithmic']:.2f} of algo)")
+              f"({r['counter_over_algorithmic']:.2f} of algo, {r['counter_over_compulsory']:.2f}x compulsory)")
 
 
 def main():
