@@ -600,12 +600,14 @@ def main():
             "loss": loss,
             "hipgraph": bool(graph is not None),
         }
-        if opt.dtype == "bf16" and not opt.no_practical_peak:
-            pp = practical_peak(dev)
+        if not opt.no_practical_peak:
+            pp = practical_peak(dev, dtype=opt.dtype)
+            ins, fn = (("v_mfma_f32_16x16x32_bf16", "llp_mfma_probe") if opt.dtype == "bf16"
+                       else ("v_mfma_f32_16x16x4_f32", "llp_mfma_probe_f32"))
             res["roofline"].update(practical_peak=pp, practical_frac=achieved / pp,
-                                   practical_note="bare v_mfma_f32_16x16x32_bf16 loop on random operands, every CU, "
-                                                  "timed here (llp_mfma_probe): the FLOP/s the chip sustains at the "
-                                                  "clock it holds under dense MFMA load")
+                                   practical_note=f"bare {ins} loop on random operands, every CU, timed here ({fn}): "
+                                                  "the FLOP/s the chip sustains at the clock it holds under dense "
+                                                  "MFMA load")
         if not opt.no_eval:
             res.update(evaluate(model, pred, data, dev))
         if world == 1 and not opt.no_shard8 and not opt.profile_kernels:

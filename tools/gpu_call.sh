@@ -53,7 +53,7 @@ for RA in "$@"; do
       timeout -k 10 180 rocprofv3 --kernel-trace -d $O/pmcm_trace -o run --output-format csv -- $S > $O/pmcm_trace.log 2>&1 || fail pmcm-trace $O/pmcm_trace.log ;;
     fp32)           # the collab step in fp32 (the reference's arithmetic): bench line, trace, dominant PMC
       F32="--dtype fp32 $LEAN --no-practical-peak"
-      timeout -k 10 300 python bench.py --steps 5 --warmup 2 $F32 > $O/fp32_bench.json 2> $O/fp32_bench.err || fail fp32-bench $O/fp32_bench.err
+      timeout -k 10 300 python bench.py --steps 5 --warmup 2 --dtype fp32 $LEAN > $O/fp32_bench.json 2> $O/fp32_bench.err || fail fp32-bench $O/fp32_bench.err
       cat $O/fp32_bench.json
       timeout -k 10 300 $PROF -d $O/fp32_trace -o t -- python bench.py --steps 4 --warmup 2 $F32 > $O/fp32_trace.log 2>&1 || fail fp32-trace $O/fp32_trace.log
       D="python bench.py --dominant-only 6 $F32"
