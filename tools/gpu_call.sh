@@ -39,6 +39,9 @@ for RA in "$@"; do
     bench-lean)     # the collab line alone
       timeout -k 10 300 python bench.py $LEAN > $O/bench_lean.json 2> $O/bench_lean.err || fail bench-lean $O/bench_lean.err
       cat $O/bench_lean.json ;;
+    smoke)          # __graft_entry__.smoke(): one small step on cuda:0 against the oracle
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+      tail -3 $O/smoke.log ;;
     trace)          # kernel trace + stats of the collab bench (hipGraph replay)
       timeout -k 10 300 $PROF -d $O/trace -o t -- python bench.py --steps 10 --warmup 3 $LEAN > $O/trace.log 2>&1 || fail trace $O/trace.log ;;
     pmc-dominant)   # FETCH / WRITE / SQ passes on the dominant GEMM alone
