@@ -109,7 +109,7 @@ def test_kd_terms_match_autograd():
         assert torch.allclose(dh.cpu().double(), hf.grad, atol=1e-7, rtol=1e-3)
 
 
-def _engine(case, dtype="fp32"):
+def _engine(case, dtype="fp32", **kw):
     import llp_engine
     import models
     a = case.args
@@ -127,7 +127,7 @@ def _engine(case, dtype="fp32"):
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=float(a.lr))
     ei = case.edge_index
     eng = llp_engine.DistillEngine(model, pred, tpred, case.x.to(DEV), case.t_h.to(DEV), ei[0].numpy(),
-                                   ei[1].numpy(), case.N, a, opt, dtype=dtype, seed=1)
+                                   ei[1].numpy(), case.N, a, opt, dtype=dtype, seed=1, **kw)
     return eng, model, pred
 
 
@@ -188,6 +188,40 @@ def test_fullbatch_device_negatives_and_bf16():
         assert F.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.97
 
 
+def test_fullbatch_sparse_first_layer_matches_dense():
+    """The bf16 engine's sparse first student layer (llp_spmm_rows / llp_spmm_tn on a
+    bag-of-words x) against the same engine on dense GEMMs, on a problem that
+    meets the path's conditions (x binary, 700 features, 1.5 % nonzero): the two differ only in
+    the order of the layer's f32 sums, so over two steps (device samples, PyG-dense negatives)
+    the loss terms agree to 1e-3 and every gradient to within bf16 rounding of the
+    activations (cosine > 0.999, max error 2 % of the largest entry)."""
+    _K()
+    N, pairs, ei, _, t_h, args, P = _dense_problem(N=300, n_und=1500, P=512, seed=3)
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(N, 700, generator=g) < 0.015).float()
+    anchors = torch.arange(0, N, 3, dtype=torch.int32).to(DEV)
+    links = torch.arange(P, dtype=torch.int32).remainder(pairs.size(0)).to(DEV)
+    pr = pairs.to(torch.int32).to(DEV).contiguous()
+    res = {}
+    for sparse in (True, False):
+        eng, model, pred = _dense_engine(N, ei, x, t_h, args, "bf16", sparse_input=sparse)
+        assert (eng.xs is not None) == sparse
+        out = []
+        for _ in range(2):
+            eng.step_fullbatch(anchors, links, pr)
+            torch.cuda.synchronize()
+            out.append((eng.terms.cpu().clone(), [p.grad.detach().cpu().clone() for p in
+                                                  list(model.parameters()) + list(pred.parameters())]))
+        res[sparse] = out
+    for (ts, gs), (td, gd) in zip(res[True], res[False]):
+        for i in range(4):
+            a, b = ts[i].item(), td[i].item()
+            assert abs(a - b) <= 1e-3 * max(abs(b), 1e-2), (i, a, b)
+        for a, b in zip(gs, gd):
+            assert F.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item() > 0.999
+            assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item() + 1e-7
+
+
 def _dense_problem(N=22, n_und=180, P=256, seed=0):
     """A graph so dense that PyG's sampler returns fewer negatives than asked for
     (N (N - 1) = 462 candidates, 240 of them edges, 256 asked)."""
@@ -205,7 +239,7 @@ def _dense_problem(N=22, n_und=180, P=256, seed=0):
     return N, pairs, ei, x, t_h, args, P
 
 
-def _dense_engine(N, ei, x, t_h, args, dtype="fp32"):
+def _dense_engine(N, ei, x, t_h, args, dtype="fp32", **kw):
     import llp_engine
     import models
     torch.manual_seed(4)
@@ -216,7 +250,7 @@ def _dense_engine(N, ei, x, t_h, args, dtype="fp32"):
         p.requires_grad = False
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=args.lr)
     eng = llp_engine.DistillEngine(model, pred, tpred, x.to(DEV), t_h.to(DEV), ei[0].numpy(), ei[1].numpy(), N, args,
-                                   opt, dtype=dtype, seed=9)
+                                   opt, dtype=dtype, seed=9, **kw)
     return eng, model, pred
 
 
