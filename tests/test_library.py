@@ -88,3 +88,34 @@ def test_splitk_plan_host_arithmetic():
     assert plan(1_000, 500, 2_048) == 1         # N not a multiple of 256
     assert plan(100, 256, 64 * 1000) == 16      # capped at 16 slabs
     assert llp_hip.gemm_nt_splitk_ws_bytes(7_761, 256, 8) == 8 * 7_761 * 256 * 4
+
+
+def test_sparse_rows_host_layout():
+    """llp_hip.SparseRows (the sparse first layer's host-side layout, built with torch on any
+    device; here the CPU): CSR of x, per-slice CSC with local rows ascending in each column,
+    the heavy-first feature order and heavy count llp_spmm_tn schedules by, and val = None
+    exactly when every stored value is 1."""
+    import numpy as np
+    import torch
+    import llp_hip
+    g = torch.Generator().manual_seed(2)
+    x = (torch.rand(90, 333, generator=g) < 0.03).float()
+    x[:, 7] = 1.0                                   # a column with a nonzero in every row
+    x[40] = 0.0                                     # an empty row
+    xs = llp_hip.SparseRows(x)
+    assert xs.val is None and xs.nnz == int((x != 0).sum())
+    rp, ci = xs.rowptr.numpy(), xs.colidx.numpy()
+    for r in range(90):
+        assert np.array_equal(ci[rp[r]:rp[r + 1]], np.nonzero(x[r].numpy())[0])
+    heavy = llp_hip.load().llp_spmm_heavy_nnz()
+    for r0, n in [(0, 90), (13, 50)]:
+        colptr, rowidx, val, perm, n_heavy = xs.csc(r0, n)
+        cp, ri = colptr.numpy(), rowidx.numpy()
+        cnt = np.diff(cp)
+        for f in range(333):
+            assert np.array_equal(ri[cp[f]:cp[f + 1]], np.nonzero(x[r0:r0 + n, f].numpy())[0])
+        assert np.array_equal(perm.numpy(), np.argsort(-cnt, kind="stable"))
+        assert n_heavy == int((cnt >= heavy).sum())
+        assert val is None
+    xv = x * 2.0
+    assert torch.equal(llp_hip.SparseRows(xv).val, torch.full((xs.nnz,), 2.0))
