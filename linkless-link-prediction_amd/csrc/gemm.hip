@@ -170,17 +170,20 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 }
 
 // ============================================================== NT kernel
-template <typename T, bool VEC>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
+// NW waves per 128 x 128 tile: 4 (2 x 2, 64 x 64 per wave) or 8 (2 x 4, 64 x 32 per wave: four
+// waves per SIMD at two workgroups per CU, to cover each other's K-tile boundary)
+template <typename T, bool VEC, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
   constexpr int E = Traits<T>::ELEMS;
   constexpr int BK = 8 * E;  // 8 chunks of 16 B per row
+  constexpr int NT = 64 * NW, WN = NW / 2, WC = BN / WN, JN = WC / 16, SI = (BM * 8) / NT;
   __shared__ uint4 smem[2 * (BM + BN) * 8];
   uint4* sA0 = smem;
   uint4* sB0 = smem + BM * 8;
   const int buf_stride = (BM + BN) * 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   p.M = rows_live(p.M, p.m_dev);
   const int64_t tilesN = (p.N + BN - 1) / BN;
   const int64_t tilesM = (p.M + BM - 1) / BM;
@@ -194,16 +197,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
   const int64_t tm = rem / tnG, tn = grp * tnG + rem % tnG;
   const int64_t m0 = tm * BM, n0 = tn * BN;
 
-  // staging assignment: chunk c = tid + 256*i -> row (tid>>3) + 32*i, kc = tid&7
+  // staging assignment: chunk c = tid + NT*i -> row (tid>>3) + (NT/8)*i, kc = tid&7
   const int kc = tid & 7;
-  const T* pa[4];
-  const T* pa2[4];
-  const T* pb[4];
-  const T* pb2[4];
-  bool va[4], vb[4];
+  const T* pa[SI];
+  const T* pa2[SI];
+  const T* pb[SI];
+  const T* pb2[SI];
+  bool va[SI], vb[SI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (tid >> 3) + 32 * i;
+  for (int i = 0; i < SI; ++i) {
+    const int r = (tid >> 3) + (NT / 8) * i;
     int64_t gm = m0 + r;
     va[i] = gm < p.M;
     gm = va[i] ? gm : (p.M - 1);
@@ -216,11 +219,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
     pb2[i] = row_ptr2<T>(p.B, gn);
   }
 
-  uint4 ra[4], rb[4];
+  uint4 ra[SI], rb[SI];
   auto gload = [&](int64_t kt) {
     const int64_t k0 = kt * BK + kc * E;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < SI; ++i) {
       ra[i] = load_chunk<T, VEC>(pa[i], pa2[i], k0, p.K, va[i]);
       rb[i] = load_chunk<T, VEC>(pb[i], pb2[i], k0, p.K, vb[i]);
     }
@@ -229,18 +232,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
     uint4* sA = sA0 + buf * buf_stride;
     uint4* sB = sB0 + buf * buf_stride;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = (tid >> 3) + 32 * i;
+    for (int i = 0; i < SI; ++i) {
+      const int r = (tid >> 3) + (NT / 8) * i;
       sA[r * 8 + (kc ^ (r & 7))] = ra[i];
       sB[r * 8 + (kc ^ (r & 7))] = rb[i];
     }
   };
 
-  float4_t acc[4][4];
+  float4_t acc[4][JN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   const int64_t nk = (p.K + BK - 1) / BK;
   gload(0);
@@ -256,41 +259,47 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        short8 af[4], bfr[4];
+        short8 af[4], bfr[JN];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = wm * 64 + i * 16 + li;
           uint4 v = sA[r * 8 + ((g + 4 * s) ^ (r & 7))];
           af[i] = *reinterpret_cast<short8*>(&v);
-          const int c = wn * 64 + i * 16 + li;
+        }
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int c = wn * WC + j * 16 + li;
           uint4 w = sB[c * 8 + ((g + 4 * s) ^ (c & 7))];
-          bfr[i] = *reinterpret_cast<short8*>(&w);
+          bfr[j] = *reinterpret_cast<short8*>(&w);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < JN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     } else {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        float4_t af[4], bfr[4];
+        float4_t af[4], bfr[JN];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = wm * 64 + i * 16 + li;
           uint4 v = sA[r * 8 + ((kb * 4 + g) ^ (r & 7))];
           af[i] = *reinterpret_cast<float4_t*>(&v);
-          const int c = wn * 64 + i * 16 + li;
+        }
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int c = wn * WC + j * 16 + li;
           uint4 w = sB[c * 8 + ((kb * 4 + g) ^ (c & 7))];
-          bfr[i] = *reinterpret_cast<float4_t*>(&w);
+          bfr[j] = *reinterpret_cast<float4_t*>(&w);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < JN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][t], bfr[j][t], acc[i][j], 0, 0, 0);
       }
     }
@@ -298,11 +307,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_nt_kernel(NTParams p) {
     __syncthreads();
   }
 
-  // epilogue: acc[i][j][r] -> row m0 + wm*64 + i*16 + g*4 + r, col n0 + wn*64 + j*16 + li
+  // epilogue: acc[i][j][r] -> row m0 + wm*64 + i*16 + g*4 + r, col n0 + wn*WC + j*16 + li
   const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = n0 + wn * 64 + j * 16 + li;
+  for (int j = 0; j < JN; ++j) {
+    const int64_t col = n0 + wn * WC + j * 16 + li;
     if (col >= p.N) continue;
     const float bias = p.bias ? p.bias[col] : 0.f;
 #pragma unroll
@@ -703,10 +712,17 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, false>), grid, dim3(NTHREADS), 0, s, p);
   } else {
+#ifdef LLP_F32_NT_8W   // A/B build: eight waves per f32 tile
+    llp::note_kernel(vec ? "gemm_nt_kernel<f32, vec, 8 waves> (128x128, v_mfma_f32_16x16x4_f32)"
+                         : "gemm_nt_kernel<f32, 8 waves> (128x128, v_mfma_f32_16x16x4_f32)");
+    if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true, 8>), grid, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((gemm_nt_kernel<float, false, 8>), grid, dim3(512), 0, s, p);
+#else
     llp::note_kernel(vec ? "gemm_nt_kernel<f32, vec> (128x128, v_mfma_f32_16x16x4_f32)"
                          : "gemm_nt_kernel<f32> (128x128, v_mfma_f32_16x16x4_f32)");
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<float, false>), grid, dim3(NTHREADS), 0, s, p);
+#endif
   }
   LLP_LAUNCH_CHECK();
   return LLP_OK;

@@ -62,10 +62,10 @@ for RA in "$@"; do
       D="python bench.py --dominant-only 6 $F32"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/fp32_pmc_fetch -o p --output-format csv -- $D > $O/fp32_pmc_fetch.log 2>&1 || fail fp32-fetch $O/fp32_pmc_fetch.log
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/fp32_pmc_write -o p --output-format csv -- $D > $O/fp32_pmc_write.log 2>&1 || fail fp32-write $O/fp32_pmc_write.log ;;
-    fp32-ab)        # fp32 collab step: L2 tile orders (default) against LLP_LIB=tools/bin/no_l2_order.so, 3 rounds
+    fp32-ab)        # fp32 collab step: default build against LLP_LIB=${AB_LIB:-tools/bin/no_l2_order.so}, 3 rounds
       F32="--dtype fp32 $LEAN --no-practical-peak --steps 5 --warmup 2"
       for i in 1 2 3; do
-        for L in linkless-link-prediction_amd/libllp_hip.so tools/bin/no_l2_order.so; do
+        for L in linkless-link-prediction_amd/libllp_hip.so ${AB_LIB:-tools/bin/no_l2_order.so}; do
           LLP_LIB=$L timeout -k 10 300 python bench.py $F32 > $O/fp32_ab.tmp 2> $O/fp32_ab.err || fail fp32-ab $O/fp32_ab.err
           echo "{\"lib\": \"$L\", \"run\": $(tail -1 $O/fp32_ab.tmp)}" >> $O/fp32_ab.jsonl
         done
