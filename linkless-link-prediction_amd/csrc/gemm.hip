@@ -351,10 +351,12 @@ __global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
 // f32 : BKm = 32; LDS image [m][128 + 16 pad] floats; ds_read_b32.
 __device__ __forceinline__ int tr_swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
 
-template <typename T, bool VEC>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
+template <typename T, bool VEC, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void gemm_tn_kernel(TNParams p) {
   constexpr int E = Traits<T>::ELEMS;
   constexpr bool BF = sizeof(T) == 2;
+  static_assert(!BF || NW == 4, "the bf16 TN fragment path is written for four waves");
+  constexpr int NT = 64 * NW, WN = NW / 2, WC = BN / WN, JN = WC / 16;
   constexpr int BKM = BF ? 64 : 32;
   constexpr int CPR = BF ? 16 : 32;               // 16-B chunks per 128-col row
   constexpr int ROWU4 = BF ? 16 : 36;             // uint4 per LDS row (f32 padded by 16 floats)
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
   __shared__ uint4 smem[2 * 2 * TILE_U4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wp = wave >> 1, wq = wave & 1;
+  const int wp = wave / WN, wq = wave % WN;
   const int64_t tilesQ = (p.Q + BN - 1) / BN;
   const int64_t tilesP = (p.P + BM - 1) / BM;
   const int64_t ntile = tilesP * tilesQ;
@@ -386,15 +388,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
   const int64_t mbeg = z * p.mchunk;
   const int64_t mend = min(p.M, mbeg + p.mchunk);
 
-  // staging: chunk c = tid + 256*i -> m row c / CPR, chunk (c % CPR)
-  constexpr int ROWS_PER_PASS = NTHREADS / CPR;  // 16 (bf16) or 8 (f32)
+  // staging: chunk c = tid + NT*i -> m row c / CPR, chunk (c % CPR)
+  constexpr int ROWS_PER_PASS = NT / CPR;  // 16 (bf16) or 8 / 16 (f32, 4 / 8 waves)
+  constexpr int SI = BKM * CPR / NT;
   const int cc = tid % CPR;
   const int rr = tid / CPR;
 
-  uint4 ra[4], rb[4];
+  uint4 ra[SI], rb[SI];
   auto gload = [&](int64_t mt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < SI; ++i) {
       const int64_t m = mt + rr + ROWS_PER_PASS * i;
       const bool v = m < mend;
       const int64_t mm = v ? m : mbeg;
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
     uint4* sA = smem + buf * 2 * TILE_U4;
     uint4* sB = sA + TILE_U4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < SI; ++i) {
       const int r = rr + ROWS_PER_PASS * i;
       const int ch = BF ? tr_swz(r, cc) : cc;
       sA[r * ROWU4 + ch] = ra[i];
@@ -419,11 +422,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
     }
   };
 
-  float4_t acc[4][4];
+  float4_t acc[4][JN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   if (mbeg < mend) {
     const int64_t nsteps = (mend - mbeg + BKM - 1) / BKM;
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < JN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
       } else {
@@ -474,16 +477,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
 #pragma unroll
         for (int t = 0; t < BKM / 4; ++t) {
           const int row = 4 * t + g;
-          float af[4], bfr[4];
+          float af[4], bfr[JN];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            af[i] = fA[row * (ROWU4 * 4) + wp * 64 + i * 16 + li];
-            bfr[i] = fB[row * (ROWU4 * 4) + wq * 64 + i * 16 + li];
-          }
+          for (int i = 0; i < 4; ++i) af[i] = fA[row * (ROWU4 * 4) + wp * 64 + i * 16 + li];
+#pragma unroll
+          for (int j = 0; j < JN; ++j) bfr[j] = fB[row * (ROWU4 * 4) + wq * WC + j * 16 + li];
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < JN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
       }
@@ -495,8 +497,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_tn_kernel(TNParams p) {
   const int g = lane >> 4, li = lane & 15;
   float* out = p.ws + z * p.P * p.Q;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = q0 + wq * 64 + j * 16 + li;
+  for (int j = 0; j < JN; ++j) {
+    const int64_t col = q0 + wq * WC + j * 16 + li;
     if (col >= p.Q) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -712,17 +714,12 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, false>), grid, dim3(NTHREADS), 0, s, p);
   } else {
-#ifdef LLP_F32_NT_8W   // A/B build: eight waves per f32 tile
+    // eight waves per f32 tile (four per SIMD): 105.3 -> 97.5 ms per fp32 collab step, dominant
+    // launch 4.28 -> 3.86 ms (profiles/r04_fp32_8w_ab.jsonl); bf16 keeps four (its 256 path rules)
     llp::note_kernel(vec ? "gemm_nt_kernel<f32, vec, 8 waves> (128x128, v_mfma_f32_16x16x4_f32)"
                          : "gemm_nt_kernel<f32, 8 waves> (128x128, v_mfma_f32_16x16x4_f32)");
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true, 8>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<float, false, 8>), grid, dim3(512), 0, s, p);
-#else
-    llp::note_kernel(vec ? "gemm_nt_kernel<f32, vec> (128x128, v_mfma_f32_16x16x4_f32)"
-                         : "gemm_nt_kernel<f32> (128x128, v_mfma_f32_16x16x4_f32)");
-    if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true>), grid, dim3(NTHREADS), 0, s, p);
-    else hipLaunchKernelGGL((gemm_nt_kernel<float, false>), grid, dim3(NTHREADS), 0, s, p);
-#endif
   }
   LLP_LAUNCH_CHECK();
   return LLP_OK;
@@ -903,8 +900,13 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     if (vec) hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, true>), g2, dim3(NTHREADS), 0, s, pp);
     else hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, false>), g2, dim3(NTHREADS), 0, s, pp);
   } else {
+#ifdef LLP_F32_TN_8W   // A/B build: eight waves per f32 TN tile (as the f32 NT kernel)
+    if (vec) hipLaunchKernelGGL((gemm_tn_kernel<float, true, 8>), g2, dim3(512), 0, s, pp);
+    else hipLaunchKernelGGL((gemm_tn_kernel<float, false, 8>), g2, dim3(512), 0, s, pp);
+#else
     if (vec) hipLaunchKernelGGL((gemm_tn_kernel<float, true>), g2, dim3(NTHREADS), 0, s, pp);
     else hipLaunchKernelGGL((gemm_tn_kernel<float, false>), g2, dim3(NTHREADS), 0, s, pp);
+#endif
   }
   LLP_LAUNCH_CHECK();
   slab_reduce(reinterpret_cast<const float*>(workspace), splits, P, Q, C, ldc, accumulate, s);
