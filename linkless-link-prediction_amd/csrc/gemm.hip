@@ -900,13 +900,10 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     if (vec) hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, true>), g2, dim3(NTHREADS), 0, s, pp);
     else hipLaunchKernelGGL((gemm_tn_kernel<bf16_t, false>), g2, dim3(NTHREADS), 0, s, pp);
   } else {
-#ifdef LLP_F32_TN_8W   // A/B build: eight waves per f32 TN tile (as the f32 NT kernel)
+    // eight waves per f32 tile, as the f32 NT kernel: fp32 collab step 97.3 -> 95.3 ms
+    // (profiles/r04_fp32_tn8w_ab.jsonl)
     if (vec) hipLaunchKernelGGL((gemm_tn_kernel<float, true, 8>), g2, dim3(512), 0, s, pp);
     else hipLaunchKernelGGL((gemm_tn_kernel<float, false, 8>), g2, dim3(512), 0, s, pp);
-#else
-    if (vec) hipLaunchKernelGGL((gemm_tn_kernel<float, true>), g2, dim3(NTHREADS), 0, s, pp);
-    else hipLaunchKernelGGL((gemm_tn_kernel<float, false>), g2, dim3(NTHREADS), 0, s, pp);
-#endif
   }
   LLP_LAUNCH_CHECK();
   slab_reduce(reinterpret_cast<const float*>(workspace), splits, P, Q, C, ldc, accumulate, s);

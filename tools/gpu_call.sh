@@ -62,7 +62,8 @@ for RA in "$@"; do
       D="python bench.py --dominant-only 6 $F32"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/fp32_pmc_fetch -o p --output-format csv -- $D > $O/fp32_pmc_fetch.log 2>&1 || fail fp32-fetch $O/fp32_pmc_fetch.log
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/fp32_pmc_write -o p --output-format csv -- $D > $O/fp32_pmc_write.log 2>&1 || fail fp32-write $O/fp32_pmc_write.log ;;
-    fp32-ab)        # fp32 collab step: default build against LLP_LIB=${AB_LIB:-tools/bin/no_l2_order.so}, 3 rounds
+    fp32-ab)        # fp32 collab step: default build against LLP_LIB=$AB_LIB (a build_lib.build_variant output,
+                    # e.g. -DLLP_NO_L2_ORDER -> tools/bin/no_l2_order.so, the default), 3 rounds
       F32="--dtype fp32 $LEAN --no-practical-peak --steps 5 --warmup 2"
       for i in 1 2 3; do
         for L in linkless-link-prediction_amd/libllp_hip.so ${AB_LIB:-tools/bin/no_l2_order.so}; do
