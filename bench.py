@@ -405,12 +405,17 @@ def physics_production_step(dtype):
                                        synthetic=True)
     r1 = physics_bench.run(dtype, 10, 2, 0, split)
     r4 = physics_bench.run(dtype, 10, 2, 4, split)
+    r1g = physics_bench.run(dtype, 10, 2, 0, split, graph=True)
+    r4g = physics_bench.run(dtype, 10, 2, 4, split, graph=True)
     return {"config": "coauthor-physics production LLP (N_old=%d, F=%d, H=256, L=2, C=%d, 65,536 edges/step)"
                       % (r1["N_old"], r1["F"], r1["contexts_per_anchor"]),
             "dtype": dtype, "ms_per_step": r1["ms_per_step"], "edges_per_s": r1["edges_per_s"],
             "rank0_ms_per_step_at_4_ranks": r4["ms_per_step"], "hipgraph": r1["hipgraph"],
-            "note": "eager steps with no host sync (the dense negatives' count stays on the device; a hipGraph "
-                    "replay measured 1 % slower); rank 0 of 4 runs its slice of the node-sharded student"}
+            "ms_per_step_graph": r1g["ms_per_step"], "rank0_ms_per_step_at_4_ranks_graph": r4g["ms_per_step"],
+            "sparse_first_layer": r1["sparse_first_layer"],
+            "note": "eager steps with no host sync (the dense negatives' count stays on the device), and the same "
+                    "steps replayed from a hipGraph (capture_fullbatch); rank 0 of 4 runs its slice of the "
+                    "node-sharded student"}
 
 
 def main():
