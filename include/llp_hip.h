@@ -207,9 +207,10 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
                  float w_label, float w_d, float w_r, float loss_scale,
                  float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
                  const int32_t* neg_count, int64_t neg_offset, double pos_total,
-                 int64_t term_b0, int64_t term_b1,
                  void* workspace, int64_t workspace_bytes, void* stream);
-/* [term_b0, term_b1): the anchors whose KL / rank terms enter terms_out (every anchor's
+/* llp_llp_loss with a term range (round 4; llp_llp_loss keeps its round-3 signature and
+ * reports every anchor, [0, B)).
+ * [term_b0, term_b1): the anchors whose KL / rank terms enter terms_out (every anchor's
  * gradient is written): with the owner decomposition every rank evaluates the loss of
  * all B anchors on the all-reduced logits and reports the terms of its own slice
  * (llp_pair_owner_assign); [0, B) otherwise.
@@ -219,6 +220,14 @@ int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob
  * [neg_offset, ...) of the whole batch's negatives; a slot at or past *neg_count is inert
  * (zero gradient, no loss), and the BCE mean runs over pos_total + *neg_count labels
  * (n_lab_total unused). */
+int llp_llp_loss_range(int64_t B, int64_t C, const float* s_logit, const float* t_prob,
+                       int64_t n_lab, int64_t n_pos, const float* out_logit,
+                       double B_total, double n_lab_total, float margin, float T,
+                       float w_label, float w_d, float w_r, float loss_scale,
+                       float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
+                       const int32_t* neg_count, int64_t neg_offset, double pos_total,
+                       int64_t term_b0, int64_t term_b1,
+                       void* workspace, int64_t workspace_bytes, void* stream);
 
 /* llp_llp_loss in ONE launch, with the Linear(H, 1) heads finished inside it
  * (llp_head_finish's fixed-order sum: bit-identical logits).  s_head (may be NULL): the

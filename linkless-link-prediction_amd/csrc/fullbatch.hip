@@ -304,9 +304,16 @@ __global__ __launch_bounds__(256) void neg_compact2(int64_t M, int64_t num_nodes
   }
   // the last workgroup: the count (the last tile's inclusive prefix) and the next call's epoch
   if (llp_arrive_last(&ctl[1], gridDim.x) && threadIdx.x == 0) {
-    const unsigned long long all = __hip_atomic_load(&incl[gridDim.x - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a failed look-back (ctl[2] set) left the last tile's prefix unpublished: no negatives
+    const bool failed = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    const unsigned long long all =
+        failed ? 0ull : __hip_atomic_load(&incl[gridDim.x - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *count = (int32_t)(all < (unsigned long long)num_neg ? all : (unsigned long long)num_neg);
-    __hip_atomic_store(&ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the table tags entries with the epoch's low 24 bits, and entries still zero from the initial
+    // clear carry tag 0: skip the epochs whose low 24 bits are 0, so no call ever reads those
+    // entries as claimed (the next call uses ctl[0] + 1)
+    const uint32_t next = ((epoch + 1u) & 0xFFFFFFu) == 0u ? epoch + 1u : epoch;
+    __hip_atomic_store(&ctl[0], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

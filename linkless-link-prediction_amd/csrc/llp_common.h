@@ -186,9 +186,14 @@ __device__ __forceinline__ bool llp_arrive_last(uint32_t* tk, uint32_t n_blocks)
 // returns its exclusive prefix to every thread.  flags[b] = (epoch << 2) | status (1 aggregate,
 // 2 inclusive): the epoch tags one call, so the flags never need resetting (the caller advances
 // the epoch once per call).  Waits only on lower-numbered workgroups, which the dispatcher starts
-// first on each XCD; spins are bounded (a publisher never seen sets *err and the result is
-// invalid, the launch does not hang).  u64 sums: any association gives the same result.
-constexpr uint32_t LLP_LB_AGG = 1u, LLP_LB_INC = 2u;
+// first on each XCD; spins are bounded.  A publisher never seen sets *err, and the workgroup
+// publishes LLP_LB_FAIL instead of its prefix, so its successors fail at once instead of spinning
+// out in turn; every failed workgroup gets the exclusive prefix 0, which keeps the callers'
+// prefix-indexed writes inside their buffers (a prefix is at most the total, so 0 plus the
+// workgroup's own part is too).  The results are then invalid but in bounds, and the caller
+// checks *err (llp_hip.py error_word, DistillEngine.check_device_errors).  u64 sums: any
+// association gives the same result.
+constexpr uint32_t LLP_LB_AGG = 1u, LLP_LB_INC = 2u, LLP_LB_FAIL = 3u;
 
 __device__ __forceinline__ uint32_t llp_lb_wait(const uint32_t* flag, uint32_t epoch, uint32_t* err) {
   uint32_t f = 0;
@@ -197,7 +202,7 @@ __device__ __forceinline__ uint32_t llp_lb_wait(const uint32_t* flag, uint32_t e
     if ((f >> 2) == (epoch & 0x3FFFFFFFu) && (f & 3u)) break;
     if (it > (1u << 22)) {
       __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return LLP_LB_INC;
+      return LLP_LB_FAIL;
     }
     __builtin_amdgcn_s_sleep(1);
   }
@@ -220,6 +225,7 @@ __device__ __forceinline__ unsigned long long llp_lookback_u64(uint32_t* flags, 
   }
   if (b > 0 && t < 64) {   // wave 0: 64 predecessors per window, nearest first
     unsigned long long acc = 0;
+    bool failed = false;
     for (int64_t j0 = b - 1;; j0 -= 64) {
       const int64_t j = j0 - t;
       uint32_t st = 0;
@@ -227,6 +233,10 @@ __device__ __forceinline__ unsigned long long llp_lookback_u64(uint32_t* flags, 
       if (j >= 0) {
         st = llp_lb_wait(&flags[j], epoch, err);
         val = __hip_atomic_load(st == LLP_LB_INC ? &incl[j] : &agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (__ballot(j >= 0 && st == LLP_LB_FAIL)) {   // a predecessor timed out or failed: so does this one
+        failed = true;
+        break;
       }
       // the nearest predecessor holding an inclusive prefix (workgroup 0 always does) ends it
       const unsigned long long inc_mask = __ballot(j >= 0 && st == LLP_LB_INC);
@@ -238,10 +248,13 @@ __device__ __forceinline__ unsigned long long llp_lookback_u64(uint32_t* flags, 
       if (inc_mask || j0 - 64 < 0) break;
     }
     if (t == 0) {
-      lb_excl = acc;
-      __hip_atomic_store(&incl[b], acc + blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&flags[b], (epoch << 2) | LLP_LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lb_excl = failed ? 0ull : acc;
+      if (!failed) {
+        __hip_atomic_store(&incl[b], acc + blk_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(&flags[b], (epoch << 2) | (failed ? LLP_LB_FAIL : LLP_LB_INC), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();

@@ -563,12 +563,25 @@ extern "C" int llp_llp_loss_heads(int64_t B, int64_t C, float* s_logit, float* t
   return LLP_OK;
 }
 
+// the round-3 signature (every anchor's terms reported), kept for existing callers
 extern "C" int llp_llp_loss(int64_t B, int64_t C, const float* s_logit, const float* t_prob, int64_t n_lab,
                             int64_t n_pos, const float* out_logit, double B_total, double n_lab_total, float margin,
                             float T, float w_label, float w_d, float w_r, float loss_scale, float* dlogit_ctx,
                             float* dlogit_lab, float* terms_out, int accumulate, const int32_t* neg_count,
-                            int64_t neg_offset, double pos_total, int64_t term_b0, int64_t term_b1,
-                            void* workspace, int64_t workspace_bytes, void* stream) {
+                            int64_t neg_offset, double pos_total, void* workspace, int64_t workspace_bytes,
+                            void* stream) {
+  return llp_llp_loss_heads(B, C, const_cast<float*>(s_logit), const_cast<float*>(t_prob), n_lab, n_pos,
+                            const_cast<float*>(out_logit), B_total, n_lab_total, margin, T, w_label, w_d, w_r,
+                            loss_scale, dlogit_ctx, dlogit_lab, terms_out, accumulate, neg_count, neg_offset,
+                            pos_total, 0, B, nullptr, nullptr, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int llp_llp_loss_range(int64_t B, int64_t C, const float* s_logit, const float* t_prob, int64_t n_lab,
+                                  int64_t n_pos, const float* out_logit, double B_total, double n_lab_total,
+                                  float margin, float T, float w_label, float w_d, float w_r, float loss_scale,
+                                  float* dlogit_ctx, float* dlogit_lab, float* terms_out, int accumulate,
+                                  const int32_t* neg_count, int64_t neg_offset, double pos_total, int64_t term_b0,
+                                  int64_t term_b1, void* workspace, int64_t workspace_bytes, void* stream) {
   return llp_llp_loss_heads(B, C, const_cast<float*>(s_logit), const_cast<float*>(t_prob), n_lab, n_pos,
                             const_cast<float*>(out_logit), B_total, n_lab_total, margin, T, w_label, w_d, w_r,
                             loss_scale, dlogit_ctx, dlogit_lab, terms_out, accumulate, neg_count, neg_offset,

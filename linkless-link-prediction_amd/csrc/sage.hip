@@ -191,6 +191,96 @@ __global__ __launch_bounds__(256) void csr_agg_rows_kernel(int64_t n_rows, const
   *dst = V16<T>::pack(acc);
 }
 
+// Rows of NCH <= 64 16-B chunks with the block's CSR slice staged in LDS (round 5).  The rows-per-wave
+// kernel above walked each row behind a dependent chain: rowptr, then per UNR neighbours a col[]
+// load and only then the neighbour rows, so at the collab degree (~10) a wave waited out ~7 global
+// latencies and the aggregate ran at 3.1-3.9 TB/s counted.  Here a workgroup owns
+// TR = 4 * RPW consecutive rows: it loads their rowptr slice, then the whole col[] slice (and for the
+// degree-weighted modes the per-neighbour weights) with one coalesced pass into LDS, and every lane
+// then issues its row's neighbour loads UNR at a time with nothing in front of them but an LDS read.
+// Three global latencies per row tile instead of 2 + 2 * deg / UNR.  Rows whose slice overflows the
+// LDS capacity (hubs) read the excess indices from global memory.  Per-row accumulation in
+// neighbour order, the same arithmetic as csr_agg_rows_kernel: bit-identical outputs.
+constexpr int AGG_CAP = 1024;   // staged col[] entries per workgroup (4 KiB, + 4 KiB of weights)
+#ifndef AGG_UNR
+#define AGG_UNR 8               // neighbour rows in flight per lane
+#endif
+
+template <typename T, int NCH, int UNR>
+__global__ __launch_bounds__(256) void csr_agg_lds_kernel(int64_t n_rows, const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col, const T* __restrict__ x,
+                                                          int64_t ldx, const float* __restrict__ inv_deg, int mode,
+                                                          const float* __restrict__ bias, T* __restrict__ out,
+                                                          int64_t ldo, int accumulate) {
+  constexpr int E = V16<T>::E;
+  constexpr int RPW = 64 / NCH;
+  constexpr int TR = 4 * RPW;   // rows per workgroup
+  __shared__ int32_t s_ptr[TR + 1];
+  __shared__ int32_t s_col[AGG_CAP];
+  __shared__ float s_w[AGG_CAP];
+  const int t = threadIdx.x;
+  // each XCD a contiguous range of row tiles (locality-ordered graphs: neighbour rows hit its L2)
+  const int64_t r0 = llp_xcd_block(blockIdx.x, gridDim.x) * TR;
+  if (t <= TR) s_ptr[t] = rowptr[min(r0 + t, n_rows)];
+  __syncthreads();
+  const int32_t base = s_ptr[0];
+  const int32_t n_e = s_ptr[TR] - base;
+  const int32_t n_st = min(n_e, AGG_CAP);
+  for (int32_t i = t; i < n_st; i += 256) {
+    const int32_t c = col[base + i];
+    s_col[i] = c;
+    if (mode) s_w[i] = inv_deg[c];
+  }
+  __syncthreads();
+  const int lane = t & 63;
+  const int rl = lane / NCH, ch = lane % NCH;
+  const int lr = (t >> 6) * RPW + rl;
+  const int64_t row = r0 + lr;
+  if (row >= n_rows) return;
+  const int32_t beg = s_ptr[lr] - base, end = s_ptr[lr + 1] - base;
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  const T* xc = x + ch * E;
+  for (int32_t e = beg; e < end; e += UNR) {
+    int32_t j[UNR];
+    float wt[UNR];
+    bool v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int32_t q = e + k;
+      v[k] = q < end;
+      const bool st = q < AGG_CAP;
+      j[k] = v[k] ? (st ? s_col[q] : col[base + q]) : 0;
+      wt[k] = 1.f;
+      if (mode && v[k]) wt[k] = st ? s_w[q] : inv_deg[j[k]];
+    }
+    uint4 r[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k)
+      r[k] = v[k] ? *reinterpret_cast<const uint4*>(xc + (int64_t)j[k] * ldx) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < UNR; ++k)
+      if (v[k]) V16<T>::add(acc, r[k], wt[k]);
+  }
+  const float sc = mode == 0 ? 1.f / (float)max(end - beg, 1) : (mode == 2 ? inv_deg[row] : 1.f);
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] *= sc;
+  if (bias)
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += bias[ch * E + i];
+  uint4* dst = reinterpret_cast<uint4*>(out + row * ldo + ch * E);
+  if (accumulate) {
+    float prev[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) prev[i] = 0.f;
+    V16<T>::add(prev, *dst, 1.f);
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] += prev[i];
+  }
+  *dst = V16<T>::pack(acc);
+}
+
 // Scalar fallback for feature widths that are not a multiple of the vector.
 template <typename T>
 __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int64_t F,
@@ -249,10 +339,17 @@ static int csr_aggregate_launch(int dtype, int64_t n_rows, int64_t F, const int3
     };
     auto pick = [&](auto* xx, auto* oo) {
       using TT = std::remove_const_t<std::remove_pointer_t<decltype(xx)>>;
+#ifdef LLP_AGG_ROWS_DIRECT   // A/B build: the round-4 kernel (col[] read behind each row walk)
       if (nch == 8) go(csr_agg_rows_kernel<TT, 8, 4>, xx, oo);
       else if (nch == 16) go(csr_agg_rows_kernel<TT, 16, 4>, xx, oo);
       else if (nch == 32) go(csr_agg_rows_kernel<TT, 32, 4>, xx, oo);
       else go(csr_agg_rows_kernel<TT, 64, 4>, xx, oo);
+#else
+      if (nch == 8) go(csr_agg_lds_kernel<TT, 8, AGG_UNR>, xx, oo);
+      else if (nch == 16) go(csr_agg_lds_kernel<TT, 16, AGG_UNR>, xx, oo);
+      else if (nch == 32) go(csr_agg_lds_kernel<TT, 32, AGG_UNR>, xx, oo);
+      else go(csr_agg_lds_kernel<TT, 64, AGG_UNR>, xx, oo);
+#endif
     };
     if (dtype == LLP_BF16) pick((const bf16_t*)x, (bf16_t*)out);
     else pick((const float*)x, (float*)out);

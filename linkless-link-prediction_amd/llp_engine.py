@@ -19,6 +19,7 @@ transposed copy, refreshed by the Adam kernel.
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 
@@ -135,6 +136,15 @@ def _norms_of(model, n_hidden, width):
 def _acc_dtype(t):
     """f32, or the tensor's own dtype when that is wider (gloo has no bf16 sums)."""
     return t.dtype if t.dtype in (torch.float32, torch.float64) else torch.float32
+
+
+def _resets_on_error(step):
+    """Engine step decorator: a step that raises resets the persistent device state
+    (EngineBase.reset_device_state) before the exception propagates."""
+    @functools.wraps(step)
+    def run(self, *args, **kw):
+        return self._guarded(lambda: step(self, *args, **kw))
+    return run
 
 
 class _SegmentedGraph:
@@ -417,7 +427,8 @@ class EngineBase:
             if population < (1 << 40):   # two launches, the sampler's state persisting between steps
                 d = self.__dict__.setdefault("_neg_wss", {})
                 if d.get("neg") is None or d["neg"].key != M:
-                    d["neg"] = K.StatefulWorkspace(K.neg_sample2_ws_bytes(M), M, self.dev)
+                    d["neg"] = K.StatefulWorkspace(K.neg_sample2_ws_bytes(M), M, self.dev,
+                                                   state_bytes=K.neg_sample2_state_bytes(M))
                 K.neg_sample_dense2(N, keys, P_total, ss, self.seed ^ 0x5EED, self.step_ctr, DENSE_NEG_STREAM, negg,
                                     cnt, d["neg"], edge_table=self._neg_table)
             else:
@@ -676,16 +687,63 @@ class EngineBase:
         K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
                     float(b2), float(g["eps"]), self.adam_step, fused=True)
 
+    # ------------------------------------------------------------------ device state
+    def _stateful_workspaces(self):
+        """Every workspace whose state persists between calls (dedup, dense negatives)."""
+        out = list(self.__dict__.get("_dedup_wss", {}).values())
+        out += [w for w in self.__dict__.get("_neg_wss", {}).values() if w is not None]
+        return out
+
+    def check_device_errors(self):
+        """Raise if a single-pass scan of this engine (the dedup compaction, the dense negatives'
+        compaction) timed out in its look-back since the last check: that call's outputs were
+        invalid (in bounds, csrc/llp_common.h).  One host read; end_epoch calls it."""
+        words = [w.error_word() for w in self._stateful_workspaces()]
+        words = [w for w in words if w is not None]
+        if not words:
+            return
+        errs = torch.stack(words).tolist()
+        if any(errs):
+            self.reset_device_state()
+            raise RuntimeError("a device look-back scan timed out (dedup / dense-negative compaction); the "
+                               "affected steps are invalid. The engine's persistent device state was reset.")
+
+    def reset_device_state(self):
+        """Return every piece of persistent device state to zero: the last-arriver ticket
+        blocks of the one-launch loss and gradient norm, and the dedup / dense-negative
+        workspaces' state (counts, look-back flags, control and error words).  For use after
+        a step raised or a launch aborted part-way, which can leave a ticket or a count
+        non-zero; zero is the state every call starts from, so captured graphs stay valid."""
+        self.loss_ticket.zero_()
+        self.sumsq_ticket.zero_()
+        for w in self._stateful_workspaces():
+            w.reset()
+
+    def _guarded(self, step):
+        """Run one step; if it raises (outside a capture), reset the persistent device state."""
+        try:
+            return step()
+        except BaseException:
+            if not torch.cuda.is_current_stream_capturing():
+                try:
+                    torch.cuda.synchronize(self.dev)
+                    self.reset_device_state()
+                except Exception:
+                    pass
+            raise
+
     # ------------------------------------------------------------------ epoch bookkeeping
     def begin_epoch(self):
         self.loss_sum.zero_()
 
     def end_epoch(self, total_examples):
-        """Returns total_loss / total_examples (src/main.py:141-144); one host sync."""
+        """Returns total_loss / total_examples (src/main.py:141-144); one host sync.  Raises
+        if a device scan failed during the epoch (check_device_errors)."""
         tot = self.loss_sum
         if self.world > 1:
             tot = tot.clone()
             dist.all_reduce(tot, group=self.group)
+        self.check_device_errors()
         steps = int(self.adam_step.item())
         for p in self.all_params:
             self.optimizer.state[p]["step"] = torch.tensor(float(steps))
@@ -837,6 +895,7 @@ class DistillEngine(EngineBase):
             return self.rank, self.world
         return self.emulate_pairs
 
+    @_resets_on_error
     def step_minibatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
                        samples=None, neg=None, kernel_events=None, dense_negatives=False):
         """One link batch of train_minibatch (src/main.py:73-143).
@@ -944,6 +1003,13 @@ class DistillEngine(EngineBase):
         self._rows_dev = n_u
         self._rows_host = rows_s
 
+        t_r = self._buf("t_r", (max(n_ctx, 1),), torch.float32)[:n_ctx]
+        if owner:
+            # ---- a6 first (src/main.py:104,106): the frozen teacher's probabilities depend only on
+            # the sampled pairs, so their grid slice is reduce-scattered under the student forward
+            self._teacher_forward(n_ctx, target[:n_ctx], target[R2:R2 + n_ctx], t_r)
+            t_slice = self._owner_grid_scatter("t", B, C, world, rank, own, None, t_r, n_ctx)
+
         # ---- a4: student MLP over the gathered rows (src/main.py:95-96)
         R1_total = B_total * C1 + 2 * (P_total + n_neg_total)    # this_target rows of the whole batch
         acts, x_rows = self._student_forward(rows_s, gather_s, n_u, p_drop, R1_total, kernel_events)
@@ -958,10 +1024,7 @@ class DistillEngine(EngineBase):
         self._dbg_cut("predictor forward")
 
         # ---- a6: frozen teacher predictor on the same context pairs (src/main.py:104,106)
-        t_r = self._buf("t_r", (max(n_ctx, 1),), torch.float32)[:n_ctx]
-        if owner:
-            self._teacher_forward(n_ctx, target[:n_ctx], target[R2:R2 + n_ctx], t_r)
-        else:
+        if not owner:
             self._teacher_forward(B * C, t_ia, t_ib, t_r, defer_head=True)
 
         # ---- a7-a9: fused LLP_D + LLP_R + BCE and d(loss)/d(logit) (src/main.py:107-130)
@@ -971,19 +1034,24 @@ class DistillEngine(EngineBase):
         dlogit = self._buf("dlogit", (R2,), torch.float32)
         ws = self._ws("ws_loss", K.llp_loss_ws_bytes(B, n_lab_loc))
         if owner:
-            # every anchor's KL / rank needs all C of its logits: this rank's context logits and
-            # teacher probabilities go into the [B, C] grid (zeros elsewhere), one SUM all-reduce
-            # completes it, every rank evaluates the anchors' loss and keeps its pairs' gradients
-            # (the anchors' terms are reported by the rank of their slice, the BCE by each rank)
+            # every anchor's KL / rank needs all C of its logits.  The [B, C] grid of context logits
+            # (this rank's pairs scattered in, zeros elsewhere) is reduce-scattered by anchor slices
+            # of Bc = ceil(B / W) anchors, each rank evaluates the KL / rank loss of ITS slice (and
+            # the BCE of its label pairs), and the slices' d(logit) are all-gathered back, from
+            # which each rank takes its own pairs' entries.  The teacher's grid went the same way
+            # before the student forward (t_slice above).  Per step: 2 x 1.9 MB reduce-scatter and
+            # 1.9 MB all-gather at the collab shape, against one 3.8 MB all-reduce and the loss of
+            # all B anchors on every rank in round 4
             lo = own["ctx_lo"]
-            full = self._buf("owner_full", (2, B * C), torch.float32)
-            K.pair_owner_scatter(B * C, own["gpos"], lo, lo + n_ctx, logit, t_r, full[0], full[1])
-            if self.world > 1:
-                self._collective(lambda: dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group))
-            dfull = self._buf("owner_dfull", (B * C,), torch.float32)
-            K.llp_loss(B, C, full[0], full[1], n_lab_loc, n_pos, logit[n_ctx:], B, P + n_neg, float(a.margin), 1.0,
-                       float(a.True_label), float(a.LLP_D), float(a.LLP_R), dfull, dlogit[n_ctx:], self.terms, ws,
-                       term_range=(rank * B // world, (rank + 1) * B // world), ticket=self.loss_ticket)
+            Bc = -(-B // world)
+            B_loc = max(0, min(Bc, B - rank * Bc))
+            s_slice = self._owner_grid_scatter("s", B, C, world, rank, own, logit, None, n_ctx)
+            dslice = self._buf("owner_dslice", (Bc * C,), torch.float32)
+            K.llp_loss(B_loc, C, s_slice, t_slice, n_lab_loc, n_pos, logit[n_ctx:], B, P + n_neg, float(a.margin),
+                       1.0, float(a.True_label), float(a.LLP_D), float(a.LLP_R), dslice, dlogit[n_ctx:], self.terms,
+                       ws, ticket=self.loss_ticket)
+            dfull = self._buf("owner_dfull", (world * Bc * C,), torch.float32)
+            self._collective(lambda: self._all_gather_rows(dfull, dslice, world, rank))
             K.gather_i32(own["sel"][lo:lo + n_ctx], dfull.view(torch.int32), dlogit[:n_ctx].view(torch.int32))
         else:
             K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin),
@@ -1032,6 +1100,35 @@ class DistillEngine(EngineBase):
                             owner_tab=self._owner_table(world))
         return {"R2": R2, "ctx": caps[0], "pos": caps[1], "neg": caps[2], "rows": rows, "sel": sel,
                 "gpos": gpos, "ctx_lo": rank * ns[0] // world}
+
+    def _owner_grid_scatter(self, which, B, C, world, rank, own, s_loc, t_loc, n_ctx):
+        """This rank's context-pair values (student logits ``s_loc`` or teacher probabilities
+        ``t_loc``) scattered into the [world * Bc, C] grid of the whole batch (zeros elsewhere;
+        Bc = ceil(B / world), the padded tail stays zero), then reduce-scattered: returns this
+        rank's [Bc * C] slice (anchors [rank * Bc, ...)), the SUM over ranks, which is exact as
+        each entry has one owner.  The teacher's ("t") is issued asynchronously on RCCL's stream
+        and waited for by the student's ("s"), so it runs under the student forward."""
+        Bc = -(-B // world)
+        key = ("owner_grid", which, world * Bc * C)
+        if key not in self._bufs:       # zero once: the scatter writes [0, B*C) every step
+            self._bufs[key] = torch.zeros(world * Bc * C, dtype=torch.float32, device=self.dev)
+        full = self._bufs[key]
+        lo = own["ctx_lo"]
+        K.pair_owner_scatter(B * C, own["gpos"], lo, lo + n_ctx, s_loc, t_loc, full if s_loc is not None else None,
+                             full if t_loc is not None else None)
+        part = self._buf(f"owner_{which}slice", (Bc * C,), torch.float32)
+
+        def rs():
+            if which == "t" and self.world > 1 and dist.get_backend(self.group) == "nccl":
+                self._owner_work = dist.reduce_scatter_tensor(part, full, op=dist.ReduceOp.SUM, group=self.group,
+                                                              async_op=True)
+                return
+            self._reduce_scatter_rows(part, full, world, rank)
+            if which == "s" and getattr(self, "_owner_work", None) is not None:
+                self._owner_work.wait()          # the teacher's slice (stream-ordered, no host block)
+                self._owner_work = None
+        self._collective(rs)
+        return part
 
     def _owner_table(self, world):
         """Node -> owner rank for the owner decomposition (``owner_locality``): contiguous ranges
@@ -1098,6 +1195,7 @@ class DistillEngine(EngineBase):
         return any(n.batch for n in self.stu_norms)
 
     # ------------------------------------------------------------------ full-batch step
+    @_resets_on_error
     def step_fullbatch(self, anchors, link_ids, pairs, b_offset=0, p_offset=0, B_total=None, P_total=None,
                        samples=None, neg=None, dense_negatives=True):
         """One link batch of ``train`` (src/main.py:167-235): the student MLP runs

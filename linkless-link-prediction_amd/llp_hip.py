@@ -76,8 +76,10 @@ _SIGS = {
                              c_int, c_vp, c_i64, c_vp]),
     "llp_llp_loss_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_llp_loss": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32,
-                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64, c_vp, c_i64,
-                             c_vp]),
+                             c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_vp, c_i64, c_vp]),
+    "llp_llp_loss_range": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32,
+                                   c_f32, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64,
+                                   c_vp, c_i64, c_vp]),
     "llp_llp_loss_heads": (c_int, [c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_f64, c_f64, c_f32, c_f32, c_f32,
                                    c_f32, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_f64, c_i64, c_i64,
                                    c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
@@ -317,7 +319,9 @@ class SparseRows:
         self.rowptr_host = self.rowptr.cpu()
         self.rowptr = self.rowptr.to(torch.int32)
         self.colidx = nz[:, 1].to(torch.int32).contiguous()
-        v = x[nz[:, 0], nz[:, 1]].float().contiguous()
+        # rounded through bf16 as the dense first layer reads x (its bf16 copy): the sparse and the
+        # dense path then multiply the same values for non-binary features too
+        v = x[nz[:, 0], nz[:, 1]].to(torch.bfloat16).float().contiguous()
         self.val = None if bool((v == 1).all()) else v
         self._csc = {}
 
@@ -482,10 +486,19 @@ class DedupWorkspace:
     def fits(self, num_nodes, R):
         return int(num_nodes) == self.num_nodes and int(R) <= self.R
 
+    def _state_bytes(self):
+        return load().llp_dedup_rows2_state_bytes(self.num_nodes)
+
     def error_word(self):
-        """Word [2] of the control block (nonzero: a look-back timed out)."""
-        off = load().llp_dedup_rows2_state_bytes(self.num_nodes) - 256
-        return self.buf.view(-1)[off // 4 + 2].view(__import__("torch").int32)
+        """Word [2] of the control block (nonzero: a look-back timed out; that call's outputs are
+        invalid, though every write stayed in bounds)."""
+        off = self._state_bytes() - 256
+        return self.buf.view(-1)[off // 4 + 2].view(torch.int32)
+
+    def reset(self):
+        """Zero the persistent state (counts, look-back flags, control words) in place: valid for
+        calls already captured in a graph too (zero is the state every call starts from)."""
+        self.buf[:self._state_bytes() // 4].zero_()
 
 
 def dedup_rows2(num_nodes, R, target, uniq, pos, n_unique, seg_ptr, seg_rows, dws, zero_rows=None):
@@ -616,11 +629,27 @@ class StatefulWorkspace:
     two-launch dense sampler, ...): the first call clears it (state_clean = 0), later calls
     vouch for it."""
 
-    def __init__(self, nbytes, key, device):
+    def __init__(self, nbytes, key, device, state_bytes=None):
+        """state_bytes: the leading state's size (its last 256 bytes the control block, word [2]
+        the look-back error word), for error_word / reset; None: neither is available."""
         import torch
         self.key = key
         self.buf = torch.empty(int(nbytes) // 4 + 16, dtype=torch.float32, device=device)
         self.clean = False
+        self.state_bytes = None if state_bytes is None else int(state_bytes)
+
+    def error_word(self):
+        """Word [2] of the control block (nonzero: a look-back of some call timed out), or None."""
+        if self.state_bytes is None:
+            return None
+        return self.buf.view(-1)[(self.state_bytes - 256) // 4 + 2].view(torch.int32)
+
+    def reset(self):
+        """Zero the persistent state in place (valid for captured calls too)."""
+        if self.state_bytes is not None:
+            self.buf[:self.state_bytes // 4].zero_()
+        else:
+            self.clean = False
 
 
 def neg_sample_dense2(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr, stream_offset, out, count, sws,
@@ -638,6 +667,10 @@ def neg_sample_dense2(num_nodes, edge_keys, num_neg, sample_size, seed, step_ctr
 
 def neg_sample2_ws_bytes(max_candidates):
     return load().llp_neg_sample_dense2_workspace_bytes(max_candidates)
+
+
+def neg_sample2_state_bytes(max_candidates):
+    return load().llp_neg_sample_dense2_state_bytes(max_candidates)
 
 
 def edge_table_build(edge_keys):

@@ -40,7 +40,7 @@ import numpy as np
 import torch
 
 import llp_hip as K
-from llp_engine import DROP_ENCODER, EngineBase, _norms_of
+from llp_engine import DROP_ENCODER, EngineBase, _norms_of, _resets_on_error
 from llp_sage import GCNConv, Graph, SAGEConv_updated, locality_order
 
 
@@ -285,6 +285,7 @@ class TeacherEngine(EngineBase):
                           aux=L["X"], alpha=alpha)
 
     # ------------------------------------------------------------------ the step
+    @_resets_on_error
     def step(self, link_ids, pairs, p_offset=0, P_total=None, neg=None, dense_negatives=True):
         """One batch of train() (src/train_teacher_gnn.py:33-71).
 

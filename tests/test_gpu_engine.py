@@ -294,3 +294,46 @@ def test_engine_fp32_hidden_2048_matches_oracle():
         ok, err = _grad_close(p.grad.detach().cpu(), ref, 2e-4)
         assert ok, (tuple(p.shape), err)
     assert np.isfinite(t.numpy()).all()
+
+
+def test_engine_device_error_word_raises_and_resets():
+    """a look-back timeout in a single-pass compaction sets its workspace's error
+    word; end_epoch reads every such word, raises, and resets the persistent device state
+    (ticket blocks, dedup / negative-sampler state), after which steps run as from a fresh
+    engine."""
+    import types
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, F_, H, L = 3000, 128, 256, 3
+    args = types.SimpleNamespace(rw_step=3, hops=3, ns_rate=3, ps_method="nb", dropout=0.0, margin=0.01,
+                                 LLP_D=1.0, LLP_R=1.0, True_label=1.0, predictor="mlp", lr=0.001)
+    g = torch.Generator().manual_seed(0)
+    u = torch.randint(0, N, (20000,), generator=g)
+    v = torch.randint(0, N, (20000,), generator=g)
+    keep = u != v
+    pairs = torch.stack([u[keep], v[keep]], 1)
+    ei = torch.stack([pairs, pairs.flip(1)], 1).reshape(-1, 2).t()
+    x = torch.randn(N, F_, generator=g) * 0.3
+    t_h = torch.randn(N, 256, generator=g) * 0.3
+    anchors = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:300].to(torch.int32).to(DEV)
+    link = torch.randperm(pairs.size(0), generator=torch.Generator().manual_seed(2))[:2048].to(torch.int32).to(DEV)
+    pd = pairs.to(torch.int32).to(DEV)
+    res = []
+    for dirty in (False, True):
+        eng, model, pred = _make_engine("bf16", N, F_, H, L, 3, args, x, t_h, ei)
+        eng.begin_epoch()
+        eng.step_minibatch(anchors, link, pd)
+        eng.end_epoch(2048)
+        if dirty:
+            ws = eng._stateful_workspaces()
+            assert ws and all(w.error_word() is not None for w in ws)
+            ws[0].error_word().fill_(1)
+            eng.loss_ticket[5] = 7
+            with pytest.raises(RuntimeError, match="look-back"):
+                eng.end_epoch(2048)
+            assert int(eng.loss_ticket.abs().sum()) == 0 and int(ws[0].error_word()) == 0
+            eng.check_device_errors()            # clean now
+        eng.step_minibatch(anchors, link, pd)
+        torch.cuda.synchronize()
+        res.append(eng.terms.cpu().clone())
+    assert torch.equal(res[0], res[1])

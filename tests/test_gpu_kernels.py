@@ -535,6 +535,62 @@ def test_csr_mean_aggregate_fwd_bwd(dt, F_):
     assert torch.allclose(gx.float().cpu(), xg.grad, rtol=tol, atol=tol * 2)
 
 
+def _bf16_rne(a):
+    """f32 -> bf16 (round to nearest even) -> f32, in numpy."""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("F_", [64, 128, 256, 512])
+def test_csr_mean_aggregate_hubs_bit_exact(dt, F_):
+    """The LDS-staged aggregate (csr_agg_lds_kernel) with hub rows whose neighbour lists
+    overflow the workgroup's staged slice (AGG_CAP = 1,024 indices: the excess is read from
+    global memory), a tile whose rows together overflow it, empty rows and duplicate edges:
+    bit for bit the f32 neighbour-order sum times 1/deg, rounded once (PyG mean, Q2), which is
+    what the rows-per-wave kernel computed."""
+    import llp_sage
+    if dt == "fp32" and F_ == 512:
+        pytest.skip("128 chunks per row: the lane-group kernel (a different, fixed summation order)")
+    k = K()
+    rng = np.random.default_rng(F_ + (0 if dt == "fp32" else 1))
+    N = 3000
+    src = [rng.integers(0, N, 20000)]
+    dst = [rng.integers(0, N, 20000)]
+    for hub, deg in ((5, 2500), (6, 700), (7, 700), (1777, 4000)):   # 6, 7 share a tile: 1,400 > 1,024
+        src.append(rng.integers(0, N, deg))
+        dst.append(np.full(deg, hub))
+    src, dst = np.concatenate(src), np.concatenate(dst)
+    keep = (dst < 2000) | (dst > 2100)                     # rows 2000-2100 empty
+    ei = torch.from_numpy(np.stack([src[keep], dst[keep]]))
+    g = llp_sage.Graph(ei, N, DEV)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    x = torch.randn(N, F_).to(tdt)
+    out = torch.empty(N, F_, device=DEV, dtype=tdt)
+    k.csr_aggregate(N, F_, g.rowptr, g.col, x.to(DEV), None, 0, out)
+    rp, cl = g.rowptr.cpu().numpy(), g.col.cpu().numpy()
+    xf = x.float().numpy()
+    ref = np.zeros((N, F_), np.float32)
+    for r in range(N):
+        acc = np.zeros(F_, np.float32)
+        for e in range(rp[r], rp[r + 1]):
+            acc = acc + xf[cl[e]]
+        ref[r] = acc * (np.float32(1.0) / np.float32(max(rp[r + 1] - rp[r], 1)))
+    if dt == "bf16":
+        ref = _bf16_rne(ref)
+    assert np.array_equal(out.float().cpu().numpy(), ref)
+    assert int(np.diff(rp).max()) >= 4000
+    # degree-weighted (mode 1, the mean's backward over the transposed CSR) against the oracle
+    gout = torch.randn(N, F_).to(tdt)
+    gx = torch.empty(N, F_, device=DEV, dtype=tdt)
+    k.csr_aggregate(N, F_, g.rowptr_t, g.col_t, gout.to(DEV), g.inv_deg, 1, gx)
+    xg = x.float().clone().requires_grad_()
+    (O.sage_mean_aggregate(xg, ei[0], ei[1], N) * gout.float()).sum().backward()
+    tol = 1e-5 if dt == "fp32" else 1e-2
+    assert torch.allclose(gx.float().cpu(), xg.grad, rtol=tol, atol=tol * 2)
+
+
 # ------------------------------------------------------------------ clip + Adam
 # (shape, group, shadows) per tensor.  "big": one tensor of 275 chunks (> 256 finalize
 # threads, so threads sum several chunk partials), eight clip groups, bf16 shadow and

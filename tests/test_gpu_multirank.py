@@ -177,10 +177,11 @@ def test_two_ranks_segmented_graph_matches_eager(size, world):
         pytest.skip("no GPU")
     eager = _n_ranks(False, size, world)
     graph = _n_ranks(True, size, world)
-    # cuts: the context logits' all-reduce (owner decomposition), the predictor's all-reduce, one
-    # bucket per student layer but the first, the rest + clip/Adam
+    # cuts: the owner decomposition's teacher-grid reduce-scatter (async), logit-grid reduce-scatter
+    # and d(logit) all-gather, the predictor's all-reduce, one bucket per student layer but the
+    # first, the rest + clip/Adam
     assert graph["owner"]
-    assert graph["segments"] == 6
+    assert graph["segments"] == 8
     assert graph["loss"] == eager["loss"], (graph["loss"], eager["loss"])
     import numpy as np
     for a, b in zip(graph["grads"], eager["grads"]):
@@ -338,8 +339,8 @@ def test_two_ranks_norm_equal_one_rank(norm_type):
                                                ("fp32", 8, True), ("bf16", 8, True), ("fp32", 2, False)])
 def test_two_ranks_equal_one_rank(dtype, world, owner):
     """The minibatch step over 2, 4 and 8 gloo ranks on one GPU == the whole batch on one rank:
-    the owner decomposition (every pair on one rank, the context logits all-reduced; the
-    default) and the slice decomposition (owner_pairs=False: each rank its slice of anchors and
+    the owner decomposition (every pair on one rank, the context-logit grid reduce-scattered by
+    anchor slices, each rank's slice loss, d(logit) all-gathered; the default) and the slice decomposition (owner_pairs=False: each rank its slice of anchors and
     links, the path of steps with dropout or BatchNorm)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

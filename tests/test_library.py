@@ -119,3 +119,29 @@ def test_sparse_rows_host_layout():
         assert val is None
     xv = x * 2.0
     assert torch.equal(llp_hip.SparseRows(xv).val, torch.full((xs.nnz,), 2.0))
+
+
+def test_sparse_rows_values_rounded_like_the_dense_layer():
+    """the sparse first layer's values are x rounded through bf16, as the dense
+    first layer reads x (its bf16 copy), so both paths multiply the same numbers."""
+    import torch
+    import llp_hip
+    x = torch.zeros(4, 300)
+    x[0, 3] = 1.0 / 3.0
+    x[2, 17] = 0.1
+    x[3, 299] = 2.0
+    xs = llp_hip.SparseRows(x)
+    want = x[x != 0].to(torch.bfloat16).float()
+    assert torch.equal(xs.val, want)
+    assert not torch.equal(xs.val, x[x != 0])      # 1/3 and 0.1 are not exact in bf16
+
+
+def test_loss_entry_points_keep_the_round3_signature():
+    """llp_llp_loss has its round-3 argument list again (no term range); the term
+    range lives in llp_llp_loss_range."""
+    txt = open(HDR).read()
+    import re as _re
+    sig = _re.search(r"int llp_llp_loss\((.*?)\);", txt, _re.S).group(1)
+    assert "term_b0" not in sig and sig.count(",") == 24
+    rng = _re.search(r"int llp_llp_loss_range\((.*?)\);", txt, _re.S).group(1)
+    assert "term_b0" in rng and rng.count(",") == 26

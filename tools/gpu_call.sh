@@ -91,6 +91,15 @@ for RA in "$@"; do
       timeout -k 10 180 $A > $O/sage_plan.json 2> $O/sage_plan.err || fail sage-plan $O/sage_plan.err
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/sage_fetch -o run --output-format csv -- $A > $O/sage_fetch.log 2>&1 || fail sage-fetch $O/sage_fetch.log
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/sage_write -o run --output-format csv -- $A > $O/sage_write.log 2>&1 || fail sage-write $O/sage_write.log ;;
+    agg-ab)         # the aggregate in the teacher's order: the default library against each of $AB_LIBS
+                    # (space-separated build_variant outputs), 2 interleaved rounds
+      for i in 1 2; do
+        for L in linkless-link-prediction_amd/libllp_hip.so ${AB_LIBS:-}; do
+          LLP_LIB=$L timeout -k 10 180 python tools/sage_bench.py --agg-only --iters 20 --orders locality > $O/agg_ab.tmp 2> $O/agg_ab.err || fail agg-ab $O/agg_ab.err
+          echo "{\"lib\": \"$L\", \"run\": $(tail -1 $O/agg_ab.tmp)}" >> $O/agg_ab.jsonl
+        done
+      done
+      python tools/agg_ab_table.py $O/agg_ab.jsonl ;;
     emulate8)       # rank 0's shard of the collab step at 8 ranks: bench line and kernel trace
       timeout -k 10 300 python bench.py --steps 20 --warmup 3 --emulate-ranks 8 > $O/emu8.json 2> $O/emu8.err || fail emu8 $O/emu8.err
       cat $O/emu8.json
