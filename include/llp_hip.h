@@ -564,6 +564,21 @@ int llp_grad_sumsq_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_nu
 int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, const float* sumsq,
                     float max_norm, float lr, float beta1, float beta2, float eps, const int64_t* step,
                     void* stream);
+/* The one-launch forms on a COMPACT 1-D grid of n_work workgroups, one work item each (round 5):
+ * n_work = the sum over the table of llp_grad_sumsq_work_items(numel) (gradient norm) or of
+ * llp_adam_work_items(numel, rows, cols, shadow_t != NULL) (Adam), which the caller computes
+ * once from its tensors' shapes.  The 2-D grids of llp_grad_sumsq_t / llp_adam_step_t (max chunks
+ * x tensors) leave most workgroups idle past the small tensors' ends, and each idle one still
+ * loads its descriptor: ~20k in the coauthor-physics optimizer.  Same arithmetic, same order:
+ * bit-identical results.  llp_grad_sumsq_w requires the ticket block. */
+int64_t llp_grad_sumsq_work_items(int64_t numel);
+int64_t llp_adam_work_items(int64_t numel, int64_t rows, int64_t cols, int transposed_shadow);
+int llp_grad_sumsq_w(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int64_t n_work, int n_groups,
+                     float* sumsq, uint32_t* ticket, void* workspace, int64_t workspace_bytes, void* stream);
+int llp_adam_step_w(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int64_t n_work,
+                    const float* sumsq,
+                    float max_norm, float lr, float beta1, float beta2, float eps, const int64_t* step,
+                    void* stream);
 /* Refresh bf16 shadows from masters (after loading weights). */
 int llp_refresh_shadows(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, void* stream);
 

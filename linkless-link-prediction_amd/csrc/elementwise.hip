@@ -319,6 +319,46 @@ __device__ __forceinline__ uint32_t sumsq_chunks(const llp_tensor_desc* __restri
   return (uint32_t)((descs[t].numel + OPT_CHUNK - 1) / OPT_CHUNK);
 }
 
+// Compact grids (llp_grad_sumsq_w / llp_adam_step_w): workgroup w of a 1-D grid of n_work takes
+// work item w of the tensors' items laid end to end (tensor 0's items first).  Wave-parallel
+// prefix over the descriptors (one round trip per 64 tensors); every thread gets (t, blk, nblk).
+// The 2-D grids (max chunks x tensors) left most workgroups idle past the small tensors' ends,
+// and each idle one still paid a descriptor load: ~20k of them in the physics optimizer.
+template <typename BlocksOf>
+__device__ __forceinline__ void work_item(const llp_tensor_desc* __restrict__ descs, int n_tensors, uint32_t w,
+                                          BlocksOf blocks_of, int& t_out, int64_t& blk, int64_t& nblk) {
+  __shared__ int s_t;
+  __shared__ uint32_t s_base, s_n;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    uint32_t base = 0;
+    for (int t0 = 0; t0 < n_tensors; t0 += 64) {
+      const int t = t0 + lane;
+      const uint32_t nb = t < n_tensors ? blocks_of(descs[t]) : 0u;
+      uint32_t inc = nb;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      const uint32_t lo = base + inc - nb;
+      if (t < n_tensors && w >= lo && w < lo + nb) {
+        s_t = t;
+        s_base = lo;
+        s_n = nb;
+      }
+      base += __shfl(inc, 63, 64);
+    }
+  }
+  __syncthreads();
+  t_out = s_t;
+  blk = (int64_t)(w - s_base);
+  nblk = (int64_t)s_n;
+}
+
+__device__ __forceinline__ uint32_t sumsq_blocks(const llp_tensor_desc& d) {
+  return (uint32_t)((d.numel + OPT_CHUNK - 1) / OPT_CHUNK);
+}
+
 template <bool HANDOFF>
 __device__ __forceinline__ void grad_sumsq_finalize_block(const llp_tensor_desc* __restrict__ descs, int n_tensors,
                                                           int64_t max_chunks, const float* partial, int n_groups,
@@ -396,34 +436,49 @@ __global__ __launch_bounds__(256) void grad_sumsq_finalize(const llp_tensor_desc
 // zero).  Only the workgroups that own a chunk arrive (the grid is max_chunks x n_tensors, most
 // of it idle past the small tensors' ends): arrival index = the chunks of the tensors before
 // this one + this chunk.
+// n_work > 0: the compact 1-D grid of n_work workgroups (work_item), arrival index = blockIdx.x.
 __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_desc* __restrict__ descs,
                                                                int n_tensors, int64_t max_chunks, float* partial,
                                                                int n_groups, float* __restrict__ sumsq,
-                                                               uint32_t* ticket) {
+                                                               uint32_t* ticket, int64_t n_work) {
   __shared__ float red[4];
-  const llp_tensor_desc d = descs[blockIdx.y];
-  const int64_t e0 = (int64_t)blockIdx.x * OPT_CHUNK;
-  if (e0 >= d.numel) return;
-  // this arrival's index and the number of arrivals: every wave reads the descriptors in
-  // parallel (one round trip per 64 tensors) and sums them across its lanes
-  uint32_t before = 0, total = 0;
-  for (int t0 = 0; t0 < n_tensors; t0 += 64) {
-    const int t = t0 + (threadIdx.x & 63);
-    const uint32_t nch = t < n_tensors ? sumsq_chunks(descs, t) : 0u;
-    uint32_t bb = t < (int)blockIdx.y ? nch : 0u, tt = nch;
-    for (int o = 32; o > 0; o >>= 1) {
-      bb += __shfl_xor(bb, o, 64);
-      tt += __shfl_xor(tt, o, 64);
+  int t;
+  int64_t blk, nblk_unused;
+  uint32_t arrival, total;
+  if (n_work > 0) {
+    work_item(descs, n_tensors, blockIdx.x, [](const llp_tensor_desc& d) { return sumsq_blocks(d); }, t, blk,
+              nblk_unused);
+    arrival = blockIdx.x;
+    total = (uint32_t)n_work;
+  } else {
+    t = blockIdx.y;
+    blk = blockIdx.x;
+    if (blk * OPT_CHUNK >= descs[t].numel) return;
+    // this arrival's index and the number of arrivals: every wave reads the descriptors in
+    // parallel (one round trip per 64 tensors) and sums them across its lanes
+    uint32_t before = 0;
+    total = 0;
+    for (int t0 = 0; t0 < n_tensors; t0 += 64) {
+      const int tt_ = t0 + (threadIdx.x & 63);
+      const uint32_t nch = tt_ < n_tensors ? sumsq_chunks(descs, tt_) : 0u;
+      uint32_t bb = tt_ < t ? nch : 0u, tt = nch;
+      for (int o = 32; o > 0; o >>= 1) {
+        bb += __shfl_xor(bb, o, 64);
+        tt += __shfl_xor(tt, o, 64);
+      }
+      before += bb;
+      total += tt;
     }
-    before += bb;
-    total += tt;
+    arrival = before + (uint32_t)blk;
   }
+  const llp_tensor_desc d = descs[t];
+  const int64_t e0 = blk * OPT_CHUNK;
   float acc = chunk_sumsq(d.grad, e0, min(d.numel, e0 + OPT_CHUNK));
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) llp_store_handed(partial + blockIdx.y * max_chunks + blockIdx.x, red[0] + red[1] + red[2] + red[3]);
-  if (llp_arrive_last_tree(ticket, before + blockIdx.x, total))
+  if (threadIdx.x == 0) llp_store_handed(partial + t * max_chunks + blk, red[0] + red[1] + red[2] + red[3]);
+  if (llp_arrive_last_tree(ticket, arrival, total))
     grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
 }
 
@@ -544,17 +599,34 @@ __global__ __launch_bounds__(256) void shadow_t_kernel(const llp_tensor_desc* __
 // registers and the transposed one through the LDS tile.  Other tensors take adam_kernel's
 // 1,024-element chunks.  Grid-strided over each tensor's tiles / chunks.  The Adam step counter
 // is read, not advanced (llp_step_end2 follows).
+__device__ __forceinline__ uint32_t adam_blocks(const llp_tensor_desc& d) {
+  return d.shadow_t ? (uint32_t)(((d.rows + 63) / 64) * ((d.cols + 63) / 64))
+                    : (uint32_t)((d.numel + ADAM_CHUNK - 1) / ADAM_CHUNK);
+}
+
+// n_work > 0: the compact 1-D grid (work_item), one tile / chunk per workgroup; otherwise the
+// 2-D grid max chunks x tensors, grid-strided.
 __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* __restrict__ descs,
                                                          const float* __restrict__ sumsq, float max_norm, float lr,
                                                          float beta1, float beta2, float eps,
-                                                         const int64_t* __restrict__ step) {
+                                                         const int64_t* __restrict__ step, int n_tensors,
+                                                         int64_t n_work) {
   __shared__ float tile[64][65];
-  const llp_tensor_desc d = descs[blockIdx.y];
-  // most of the grid (max chunks x tensors) owns nothing: leave before the double pow below
+  int t;
+  int64_t blk0, bstride;
+  if (n_work > 0) {
+    int64_t nblk;
+    work_item(descs, n_tensors, blockIdx.x, [](const llp_tensor_desc& d) { return adam_blocks(d); }, t, blk0, nblk);
+    bstride = nblk;        // one item: the grid-strided loops below run once
+  } else {
+    t = blockIdx.y;
+    blk0 = blockIdx.x;
+    bstride = gridDim.x;
+  }
+  const llp_tensor_desc d = descs[t];
+  // most of the 2-D grid (max chunks x tensors) owns nothing: leave before the double pow below
   // (every thread of ~21k idle workgroups evaluating it cost ~40 us of the physics step)
-  if (d.shadow_t ? (int64_t)blockIdx.x >= ((d.rows + 63) / 64) * ((d.cols + 63) / 64)
-                 : (int64_t)blockIdx.x * ADAM_CHUNK >= d.numel)
-    return;
+  if (d.shadow_t ? blk0 >= ((d.rows + 63) / 64) * ((d.cols + 63) / 64) : blk0 * ADAM_CHUNK >= d.numel) return;
   float coef = 1.f;
   if (sumsq) {
     const float total = sqrtf(sumsq[d.group]);
@@ -571,7 +643,7 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
     const int64_t lds = d.shadow_ld ? d.shadow_ld : cols;
     const int64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int64_t ti = blockIdx.x; ti < tr * tc; ti += gridDim.x) {
+    for (int64_t ti = blk0; ti < tr * tc; ti += bstride) {
       const int64_t r0 = (ti / tc) * 64, c0 = (ti % tc) * 64;
       const int64_t c = c0 + tx;
       // every load of the tile issued before the first store (the stores may alias later
@@ -616,7 +688,7 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
                      ((((uintptr_t)d.grad) | ((uintptr_t)d.exp_avg) | ((uintptr_t)d.exp_avg_sq) | ((uintptr_t)d.param) |
                        (d.shadow ? (uintptr_t)d.shadow : 0)) & 15) == 0 &&
                      (d.shadow_ld == 0 || d.shadow_ld == d.cols);
-    for (int64_t e0 = (int64_t)blockIdx.x * ADAM_CHUNK; e0 < d.numel; e0 += (int64_t)gridDim.x * ADAM_CHUNK) {
+    for (int64_t e0 = blk0 * ADAM_CHUNK; e0 < d.numel; e0 += bstride * ADAM_CHUNK) {
       const int64_t e1 = min(d.numel, e0 + ADAM_CHUNK);
       if (vec) {
         for (int64_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
@@ -806,7 +878,7 @@ extern "C" int llp_grad_sumsq_t(const llp_tensor_desc* descs, int n_tensors, int
   // blocks past a tensor's numel exit immediately; x extent bounded by kMaxNumel
   if (ticket) {   // one launch: the last workgroup finalizes
     hipLaunchKernelGGL(grad_sumsq_fused_kernel, dim3((unsigned)mc, (unsigned)n_tensors), dim3(256), 0, s, descs,
-                       n_tensors, mc, (float*)workspace, n_groups, sumsq, ticket);
+                       n_tensors, mc, (float*)workspace, n_groups, sumsq, ticket, (int64_t)0);
     LLP_LAUNCH_CHECK();
     return LLP_OK;
   }
@@ -829,7 +901,52 @@ extern "C" int llp_adam_step_t(const llp_tensor_desc* descs, int n_tensors, int6
                                void* stream) {
   LLP_CHECK_ARG(descs && step, "llp_adam_step_t: null pointer");
   hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0,
-                     (hipStream_t)stream, descs, sumsq, max_norm, lr, beta1, beta2, eps, step);
+                     (hipStream_t)stream, descs, sumsq, max_norm, lr, beta1, beta2, eps, step, n_tensors, (int64_t)0);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+// The compact-grid forms: n_work = the number of work items (llp_adam_work_items /
+// llp_grad_sumsq_work_items over the table's shapes, which the caller knows); the same
+// arithmetic in the same order as llp_grad_sumsq_t / llp_adam_step_t (bit-identical).
+extern "C" int64_t llp_grad_sumsq_work_items(int64_t numel) { return (numel + OPT_CHUNK - 1) / OPT_CHUNK; }
+extern "C" int64_t llp_adam_work_items(int64_t numel, int64_t rows, int64_t cols, int transposed_shadow) {
+  return transposed_shadow ? ((rows + 63) / 64) * ((cols + 63) / 64) : (numel + ADAM_CHUNK - 1) / ADAM_CHUNK;
+}
+
+extern "C" int llp_grad_sumsq_w(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int64_t n_work,
+                                int n_groups, float* sumsq, uint32_t* ticket, void* workspace,
+                                int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(descs && sumsq && workspace && ticket, "llp_grad_sumsq_w: null pointer");
+  LLP_CHECK_ARG(n_groups >= 1 && n_groups <= 8, "llp_grad_sumsq_w: n_groups in [1,8]");
+  LLP_CHECK_ARG(n_tensors >= 1 && n_tensors <= 256 && n_work >= 1 && n_work < (1ll << 31),
+                "llp_grad_sumsq_w: n_tensors in [1,256], n_work >= 1");
+  LLP_CHECK_ARG(workspace_bytes >= llp_grad_sumsq_workspace_bytes(n_tensors, max_numel),
+                "llp_grad_sumsq_w: workspace too small");
+  const int64_t mc = max_chunks_of(max_numel);
+#ifdef LLP_OPT_2D_GRID   // A/B build: the 2-D grid of llp_grad_sumsq_t
+  return llp_grad_sumsq_t(descs, n_tensors, max_numel, n_groups, sumsq, ticket, workspace, workspace_bytes, stream);
+#endif
+  hipLaunchKernelGGL(grad_sumsq_fused_kernel, dim3((unsigned)n_work), dim3(256), 0, (hipStream_t)stream, descs,
+                     n_tensors, mc, (float*)workspace, n_groups, sumsq, ticket, n_work);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_adam_step_w(const llp_tensor_desc* descs, int n_tensors, int64_t max_numel, int64_t n_work,
+                               const float* sumsq,
+                               float max_norm, float lr, float beta1, float beta2, float eps, const int64_t* step,
+                               void* stream) {
+  LLP_CHECK_ARG(descs && step, "llp_adam_step_w: null pointer");
+  LLP_CHECK_ARG(n_tensors >= 1 && n_work >= 1 && n_work < (1ll << 31), "llp_adam_step_w: sizes");
+#ifdef LLP_OPT_2D_GRID   // A/B build: the 2-D grid of llp_adam_step_t
+  hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)adam_chunks_of(max_numel), (unsigned)n_tensors), dim3(256), 0,
+                     (hipStream_t)stream, descs, sumsq, max_norm, lr, beta1, beta2, eps, step, n_tensors, (int64_t)0);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+#endif
+  hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)n_work), dim3(256), 0, (hipStream_t)stream, descs, sumsq,
+                     max_norm, lr, beta1, beta2, eps, step, n_tensors, n_work);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

@@ -217,23 +217,29 @@ __global__ __launch_bounds__(256) void neg_tile_scatter(int64_t M, int64_t num_n
 constexpr int64_t NEG2_VALUE_BITS = 40;
 constexpr uint64_t NEG2_VALUE_MASK = (1ull << NEG2_VALUE_BITS) - 1;
 
-__global__ void neg_candidates2(int64_t M, int enumerate_all, uint64_t population, uint64_t seed,
+// Candidates [i_lo, i_hi).  gate (may be NULL): the whole launch does nothing when *gate >= num_neg
+// (the first round's candidates already hold enough negatives; llp_neg_sample_dense2 below).
+__global__ void neg_candidates2(int64_t i_lo, int64_t i_hi, int enumerate_all, uint64_t population, uint64_t seed,
                                 const int64_t* __restrict__ step_ctr, int64_t stream_offset,
                                 const int64_t* __restrict__ edge_keys, int64_t n_keys,
                                 const uint64_t* __restrict__ edge_table, int64_t edge_table_size,
                                 int64_t* cand, int32_t* __restrict__ slot, uint64_t* __restrict__ tkeys, int64_t T,
-                                const uint32_t* __restrict__ ctl) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= M) return;
+                                const uint32_t* __restrict__ ctl, const int32_t* __restrict__ gate, int64_t num_neg) {
+  if (gate && (int64_t)*gate >= num_neg) return;
+  const int64_t i = i_lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= i_hi) return;
   const uint32_t epoch = ctl[0] + 1u;
   const uint64_t tag = (uint64_t)(epoch & 0xFFFFFFu) << NEG2_VALUE_BITS;
   uint64_t c;
   if (enumerate_all) {
     c = (uint64_t)(i % (int64_t)population);
   } else {
+    // draws 2i and 2i + 1 are components of one Philox block (philox_u32: word idx & 3 of block
+    // idx >> 2), so one philox4 gives both
     const uint64_t stream = (uint64_t)(LLP_STREAMS_PER_STEP * (*step_ctr) + stream_offset);
-    const uint64_t lo = philox_u32(seed, stream, 2 * (uint64_t)i);
-    const uint64_t hi = philox_u32(seed, stream, 2 * (uint64_t)i + 1);
+    const uint4 x4 = philox4((uint64_t)i >> 1, stream, seed);
+    const uint64_t lo = (i & 1) ? x4.z : x4.x;
+    const uint64_t hi = (i & 1) ? x4.w : x4.y;
     c = __umul64hi((hi << 32) | lo, population);
   }
   // write-through, drained before the claim below publishes this index
@@ -263,15 +269,30 @@ __global__ void neg_candidates2(int64_t M, int enumerate_all, uint64_t populatio
   slot[i] = (int32_t)h;
 }
 
+// Tiles [tile_lo, tile_lo + gridDim.x) of the candidates [0, M); the look-back runs over the
+// global tile index, so a second launch continues the first one's prefix (same epoch: only the
+// launch with ``advance`` moves the epoch on).  gate as neg_candidates2 (the launch then only
+// arrives on its ticket and, with ``advance``, moves the epoch on).
 __global__ __launch_bounds__(256) void neg_compact2(int64_t M, int64_t num_nodes, int64_t num_neg,
                                                     const int64_t* __restrict__ cand, const int32_t* __restrict__ slot,
                                                     const uint64_t* __restrict__ tkeys,
                                                     uint32_t* flags, unsigned long long* agg, unsigned long long* incl,
                                                     uint32_t* ctl, int32_t* __restrict__ out, int64_t ld_out,
-                                                    int32_t* __restrict__ count) {
+                                                    int32_t* __restrict__ count, int64_t tile_lo, int advance,
+                                                    const int32_t* __restrict__ gate) {
   __shared__ int wsum[4];
+  __shared__ int gated;
   const uint32_t epoch = ctl[0] + 1u;
-  const int64_t b = blockIdx.x;
+  if (threadIdx.x == 0) gated = gate && (int64_t)*gate >= num_neg;
+  __syncthreads();
+  if (gated) {
+    if (llp_arrive_last(&ctl[1], gridDim.x) && threadIdx.x == 0 && advance) {
+      const uint32_t next = ((epoch + 1u) & 0xFFFFFFu) == 0u ? epoch + 1u : epoch;
+      __hip_atomic_store(&ctl[0], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  const int64_t b = tile_lo + blockIdx.x;
   const int64_t i0 = b * NC_TILE + 4 * threadIdx.x;
   int v[4], mine = 0;
 #pragma unroll
@@ -307,13 +328,16 @@ __global__ __launch_bounds__(256) void neg_compact2(int64_t M, int64_t num_nodes
     // a failed look-back (ctl[2] set) left the last tile's prefix unpublished: no negatives
     const bool failed = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     const unsigned long long all =
-        failed ? 0ull : __hip_atomic_load(&incl[gridDim.x - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        failed ? 0ull
+               : __hip_atomic_load(&incl[tile_lo + gridDim.x - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *count = (int32_t)(all < (unsigned long long)num_neg ? all : (unsigned long long)num_neg);
     // the table tags entries with the epoch's low 24 bits, and entries still zero from the initial
     // clear carry tag 0: skip the epochs whose low 24 bits are 0, so no call ever reads those
     // entries as claimed (the next call uses ctl[0] + 1)
-    const uint32_t next = ((epoch + 1u) & 0xFFFFFFu) == 0u ? epoch + 1u : epoch;
-    __hip_atomic_store(&ctl[0], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (advance) {
+      const uint32_t next = ((epoch + 1u) & 0xFFFFFFu) == 0u ? epoch + 1u : epoch;
+      __hip_atomic_store(&ctl[0], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -579,13 +603,37 @@ extern "C" int llp_neg_sample_dense2(int64_t num_nodes, const int64_t* edge_keys
     LLP_LAUNCH_CHECK();
     return LLP_OK;
   }
-  hipLaunchKernelGGL(neg_candidates2, dim3(ceil_div_u(M, 256)), dim3(256), 0, s, M, enumerate_all, population, seed,
-                     step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size, cand, slot, tkeys, T,
-                     (const uint32_t*)ctl);
+  // Round-gated: PyG's sampler stops after the first round of sample_size candidates whenever it
+  // holds num_neg valid ones, which at sample_size = 1.1 num_neg / prob is practically always.
+  // The first round's tiles are drawn and compacted first; the later rounds' launches read that
+  // count on the device and do nothing when it suffices (no host read, graph-capturable).  The
+  // result is the same as compacting all rounds at once: the first num_neg valid first
+  // occurrences in draw order (the later rounds' candidates come after, and their repeats of
+  // first-round values lose the slot to the lower index).  Round 1 ends on a tile boundary.
+  int64_t M1 = M;
+#ifndef LLP_NEG_ONE_PHASE   // A/B build: every round's candidates in one pass (round 4)
+  if (!enumerate_all && rounds > 1) {
+    M1 = (sample_size + NC_TILE - 1) / NC_TILE * NC_TILE;
+    if (M1 >= M) M1 = M;
+  }
+#endif
+  const int64_t nt1 = (M1 + NC_TILE - 1) / NC_TILE;
+  hipLaunchKernelGGL(neg_candidates2, dim3(ceil_div_u(M1, 256)), dim3(256), 0, s, (int64_t)0, M1, enumerate_all,
+                     population, seed, step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size, cand,
+                     slot, tkeys, T, (const uint32_t*)ctl, (const int32_t*)nullptr, num_neg);
   LLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(neg_compact2, dim3((unsigned)ntiles), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot, tkeys,
-                     flags, agg, incl, ctl, out, ld_out, count);
+  hipLaunchKernelGGL(neg_compact2, dim3((unsigned)nt1), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot, tkeys,
+                     flags, agg, incl, ctl, out, ld_out, count, (int64_t)0, M1 == M ? 1 : 0, (const int32_t*)nullptr);
   LLP_LAUNCH_CHECK();
+  if (M1 < M) {
+    hipLaunchKernelGGL(neg_candidates2, dim3(ceil_div_u(M - M1, 256)), dim3(256), 0, s, M1, M, enumerate_all,
+                       population, seed, step_ctr, stream_offset, edge_keys, n_keys, edge_table, edge_table_size,
+                       cand, slot, tkeys, T, (const uint32_t*)ctl, (const int32_t*)count, num_neg);
+    LLP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(neg_compact2, dim3((unsigned)(ntiles - nt1)), dim3(256), 0, s, M, num_nodes, num_neg, cand, slot,
+                       tkeys, flags, agg, incl, ctl, out, ld_out, count, nt1, 1, (const int32_t*)count);
+    LLP_LAUNCH_CHECK();
+  }
   return LLP_OK;
 }
 

@@ -9,7 +9,10 @@
 // once: HBM traffic = E*F*s (neighbours) + 4E (col) + 4(N+1) (rowptr) + N*F*s.
 #include "llp_common.h"
 
+#include <algorithm>
 #include <type_traits>
+
+int llp_cu_count();   // gemm256.hip
 
 namespace {
 
@@ -205,6 +208,12 @@ constexpr int AGG_CAP = 1024;   // staged col[] entries per workgroup (4 KiB, + 
 #ifndef AGG_UNR
 #define AGG_UNR 8               // neighbour rows in flight per lane
 #endif
+#ifndef AGG_PIPE_UNR
+#define AGG_PIPE_UNR 12         // the pipelined kernel's neighbour rows in flight per lane (collab degree ~10)
+#endif
+#ifndef AGG_WG_PER_CU
+#define AGG_WG_PER_CU 4
+#endif
 
 template <typename T, int NCH, int UNR>
 __global__ __launch_bounds__(256) void csr_agg_lds_kernel(int64_t n_rows, const int32_t* __restrict__ rowptr,
@@ -281,6 +290,113 @@ __global__ __launch_bounds__(256) void csr_agg_lds_kernel(int64_t n_rows, const 
   *dst = V16<T>::pack(acc);
 }
 
+// Rows of NCH <= 64 16-B chunks, persistent and software-pipelined per wave (round 5, second
+// form; measured SLOWER than csr_agg_lds_kernel and kept only as the LLP_AGG_PIPE A/B build:
+// bf16 F = 128 forward 67-78 against 58 us, profiles/r05_agg_ab.txt).  The LDS-staged kernel above still pays three serialized memory latencies per workgroup
+// of 4 * RPW rows (rowptr, then col[], then the neighbour rows) and its workgroups live one tile
+// each, so at the collab degree the aggregate stayed latency-bound (bf16 F = 128: 58 us, 0.28 of
+// HBM on compulsory bytes, profiles/r05_agg_ab.txt).  Here every wave walks many tiles of RPW
+// rows and keeps the index stages one and two tiles ahead: while it issues tile k's neighbour
+// loads it has tile k + 1's col[] slice and tile k + 2's rowptr values in flight, so a tile costs
+// about one memory latency.  The col[] slice lives in two registers per lane (128 entries; a
+// longer slice, i.e. a hub, reads the excess from global memory) and goes through the wave's own
+// 512 B of LDS, from which each lane picks its neighbour ids (the row walks diverge, and a
+// cross-lane read of an inactive lane's register is undefined).  Tiles are dealt per XCD in contiguous ranges (XCD x takes
+// tiles [x T / 8, (x + 1) T / 8), its waves round-robin inside), so the tiles in flight on an XCD
+// are neighbours in the (locality-ordered) graph.  Per-row accumulation in neighbour order, the
+// same arithmetic as the kernels above: bit-identical outputs.
+template <typename T, int NCH, int UNR>
+__global__ __launch_bounds__(256) void csr_agg_pipe_kernel(int64_t n_rows, const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ col, const T* __restrict__ x,
+                                                           int64_t ldx, const float* __restrict__ inv_deg, int mode,
+                                                           const float* __restrict__ bias, T* __restrict__ out,
+                                                           int64_t ldo, int accumulate, int64_t n_tiles) {
+  constexpr int E = V16<T>::E;
+  constexpr int RPW = 64 / NCH;
+  const int lane = threadIdx.x & 63;
+  const int rl = lane / NCH, ch = lane % NCH;
+  const int64_t xcd = blockIdx.x % 8, wg_x = blockIdx.x / 8;
+  const int64_t nwg_x = ((int64_t)gridDim.x - xcd + 7) / 8;
+  const int64_t W = nwg_x * 4;                                   // waves on this XCD
+  const int64_t t_lo = xcd * n_tiles / 8, t_hi = (xcd + 1) * n_tiles / 8;
+  int64_t t = t_lo + wg_x * 4 + (threadIdx.x >> 6);
+  auto load_rp = [&](int64_t tt) -> int32_t {
+    return (tt < t_hi && lane <= RPW) ? rowptr[min(tt * RPW + lane, n_rows)] : 0;
+  };
+  auto load_col = [&](int32_t rp, int32_t& ca, int32_t& cb, int32_t& base) {
+    base = __shfl(rp, 0, 64);
+    const int32_t len = __shfl(rp, RPW, 64) - base;
+    ca = lane < len ? col[base + lane] : 0;
+    cb = lane + 64 < len ? col[base + 64 + lane] : 0;
+  };
+  int32_t rp0 = load_rp(t), rp1 = load_rp(t + W);
+  int32_t ca0, cb0, base0;
+  load_col(rp0, ca0, cb0, base0);
+  const T* xc = x + ch * E;
+  __shared__ int32_t s_col[4][128];
+  int32_t* sc = s_col[threadIdx.x >> 6];
+  for (; t < t_hi; t += W) {
+    // this tile's col[] slice into the wave's LDS (every lane finished the previous tile's walk)
+    sc[lane] = ca0;
+    sc[64 + lane] = cb0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the index stages of the next tiles, issued before this tile's neighbour loads
+    const int32_t rp2 = load_rp(t + 2 * W);
+    int32_t ca1 = 0, cb1 = 0, base1 = 0;
+    if (t + W < t_hi) load_col(rp1, ca1, cb1, base1);
+    const int64_t row = t * RPW + rl;
+    const int32_t beg = __shfl(rp0, rl, 64) - base0, end = __shfl(rp0, rl + 1, 64) - base0;
+    float acc[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] = 0.f;
+    for (int32_t e = beg; e < end; e += UNR) {
+      int32_t j[UNR];
+      bool v[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int32_t q = e + k;
+        v[k] = q < end;
+        j[k] = v[k] ? (q < 128 ? sc[q] : col[base0 + q]) : 0;
+      }
+      uint4 r[UNR];
+      float wt[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        r[k] = v[k] ? *reinterpret_cast<const uint4*>(xc + (int64_t)j[k] * ldx) : make_uint4(0, 0, 0, 0);
+        wt[k] = (mode && v[k]) ? inv_deg[j[k]] : 1.f;
+      }
+#pragma unroll
+      for (int k = 0; k < UNR; ++k)
+        if (v[k]) V16<T>::add(acc, r[k], wt[k]);
+    }
+    if (row < n_rows) {
+      const float sc = mode == 0 ? 1.f / (float)max(end - beg, 1) : (mode == 2 ? inv_deg[row] : 1.f);
+#pragma unroll
+      for (int i = 0; i < E; ++i) acc[i] *= sc;
+      if (bias)
+#pragma unroll
+        for (int i = 0; i < E; ++i) acc[i] += bias[ch * E + i];
+      uint4* dst = reinterpret_cast<uint4*>(out + row * ldo + ch * E);
+      if (accumulate) {
+        float prev[E];
+#pragma unroll
+        for (int i = 0; i < E; ++i) prev[i] = 0.f;
+        V16<T>::add(prev, *dst, 1.f);
+#pragma unroll
+        for (int i = 0; i < E; ++i) acc[i] += prev[i];
+      }
+      *dst = V16<T>::pack(acc);
+    }
+    rp0 = rp1;
+    rp1 = rp2;
+    ca0 = ca1;
+    cb0 = cb1;
+    base0 = base1;
+  }
+}
+
 // Scalar fallback for feature widths that are not a multiple of the vector.
 template <typename T>
 __global__ __launch_bounds__(256) void csr_agg_scalar_kernel(int64_t n_rows, int64_t F,
@@ -339,12 +455,24 @@ static int csr_aggregate_launch(int dtype, int64_t n_rows, int64_t F, const int3
     };
     auto pick = [&](auto* xx, auto* oo) {
       using TT = std::remove_const_t<std::remove_pointer_t<decltype(xx)>>;
-#ifdef LLP_AGG_ROWS_DIRECT   // A/B build: the round-4 kernel (col[] read behind each row walk)
+#if defined(LLP_AGG_ROWS_DIRECT)   // A/B build: the round-4 kernel (col[] read behind each row walk)
       if (nch == 8) go(csr_agg_rows_kernel<TT, 8, 4>, xx, oo);
       else if (nch == 16) go(csr_agg_rows_kernel<TT, 16, 4>, xx, oo);
       else if (nch == 32) go(csr_agg_rows_kernel<TT, 32, 4>, xx, oo);
       else go(csr_agg_rows_kernel<TT, 64, 4>, xx, oo);
-#else
+#elif defined(LLP_AGG_PIPE)        // A/B build: persistent software-pipelined waves (slower)
+      const int64_t n_tiles = (n_rows + (64 / nch) - 1) / (64 / nch);
+      const int64_t cap = (int64_t)llp_cu_count() * AGG_WG_PER_CU;
+      const dim3 gp((unsigned)std::max<int64_t>(8, std::min<int64_t>((n_tiles + 3) / 4, cap)));
+      auto gop = [&](auto kern, auto* xx2, auto* oo2) {
+        hipLaunchKernelGGL(kern, gp, dim3(256), 0, s, n_rows, rowptr, col, xx2, ldx, inv_deg, mode, bias, oo2, ldo,
+                           accumulate, n_tiles);
+      };
+      if (nch == 8) gop(csr_agg_pipe_kernel<TT, 8, AGG_PIPE_UNR>, xx, oo);
+      else if (nch == 16) gop(csr_agg_pipe_kernel<TT, 16, AGG_PIPE_UNR>, xx, oo);
+      else if (nch == 32) gop(csr_agg_pipe_kernel<TT, 32, AGG_PIPE_UNR>, xx, oo);
+      else gop(csr_agg_pipe_kernel<TT, 64, AGG_PIPE_UNR>, xx, oo);
+#else                              // one LDS-staged tile per workgroup (the default)
       if (nch == 8) go(csr_agg_lds_kernel<TT, 8, AGG_UNR>, xx, oo);
       else if (nch == 16) go(csr_agg_lds_kernel<TT, 16, AGG_UNR>, xx, oo);
       else if (nch == 32) go(csr_agg_lds_kernel<TT, 32, AGG_UNR>, xx, oo);

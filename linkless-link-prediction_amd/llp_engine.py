@@ -303,6 +303,13 @@ class EngineBase:
                                       cols, grp, self.dc, ld, ld_t))
         self.n_desc = len(descs)
         self.max_numel = max(p.numel() for p in self.all_params)
+        # compact grids of the one-launch gradient norm and Adam (llp_grad_sumsq_w / llp_adam_step_w)
+        shapes = []
+        for p in self.all_params:
+            shadow_t = self._shadows.get(id(p), (None, None, 0, 0))[1]
+            rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+            shapes.append((p.numel(), rows, cols, shadow_t is not None))
+        self.n_work_sumsq, self.n_work_adam = K.work_items(shapes)
         self.descs_dev = K.descs_to_device(descs, self.dev)
         self.sumsq = torch.zeros(self.n_groups, dtype=torch.float32, device=self.dev)
         self.ws_sumsq = torch.empty(K.grad_sumsq_ws_bytes(self.n_desc, self.max_numel) // 4 + 1, dtype=torch.float32,
@@ -681,11 +688,11 @@ class EngineBase:
             self._collective(lambda: self._finish_allreduce(rest))
         g = self.optimizer.param_groups[0]
         K.grad_sumsq(self.descs_dev, self.n_desc, self.max_numel, self.n_groups, self.sumsq, self.ws_sumsq,
-                     ticket=self.sumsq_ticket)
+                     ticket=self.sumsq_ticket, n_work=self.n_work_sumsq)
         b1, b2 = g["betas"]
         # the one-launch Adam reads the step counter; the step-end launch advances it
         K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
-                    float(b2), float(g["eps"]), self.adam_step, fused=True)
+                    float(b2), float(g["eps"]), self.adam_step, fused=True, n_work=self.n_work_adam)
 
     # ------------------------------------------------------------------ device state
     def _stateful_workspaces(self):

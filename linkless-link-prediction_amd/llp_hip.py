@@ -135,6 +135,10 @@ _SIGS = {
     "llp_grad_sumsq_t": (c_int, [c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "llp_adam_step_t": (c_int, [c_vp, c_int, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "llp_refresh_shadows": (c_int, [c_vp, c_int, c_i64, c_vp]),
+    "llp_grad_sumsq_work_items": (c_i64, [c_i64]),
+    "llp_adam_work_items": (c_i64, [c_i64, c_i64, c_i64, c_int]),
+    "llp_grad_sumsq_w": (c_int, [c_vp, c_int, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "llp_adam_step_w": (c_int, [c_vp, c_int, c_i64, c_i64, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "llp_convert": (c_int, [c_int, c_int, c_i64, c_vp, c_vp, c_vp]),
     "llp_accumulate": (c_int, [c_i64, c_vp, c_f32, c_vp, c_vp]),
     "llp_increment": (c_int, [c_vp, c_vp]),
@@ -772,18 +776,37 @@ def ticket_block(dev):
     return torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)
 
 
-def grad_sumsq(descs_dev, n, max_numel, n_groups, sumsq, ws, ticket=None):
-    """ticket (a ticket_block): one launch (the finalize in its last workgroup)."""
+def work_items(shapes):
+    """(n_work of llp_grad_sumsq_w, n_work of llp_adam_step_w) for a descriptor table whose
+    tensors have ``shapes`` = [(numel, rows, cols, has_transposed_shadow), ...]."""
+    L = load()
+    return (sum(int(L.llp_grad_sumsq_work_items(int(n))) for n, _, _, _ in shapes),
+            sum(int(L.llp_adam_work_items(int(n), int(r), int(c), int(bool(t)))) for n, r, c, t in shapes))
+
+
+def grad_sumsq(descs_dev, n, max_numel, n_groups, sumsq, ws, ticket=None, n_work=0):
+    """ticket (a ticket_block): one launch (the finalize in its last workgroup); with n_work
+    (work_items) on the compact grid (llp_grad_sumsq_w)."""
     L = lib()
     assert ticket is None or ticket.numel() >= TICKET_WORDS
+    if n_work and ticket is not None:
+        check(L.llp_grad_sumsq_w(descs_dev.data_ptr(), n, max_numel, int(n_work), n_groups, sumsq.data_ptr(),
+                                 ticket.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()),
+              "llp_grad_sumsq_w")
+        return
     check(L.llp_grad_sumsq_t(descs_dev.data_ptr(), n, max_numel, n_groups, sumsq.data_ptr(), ptr(ticket),
                              ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_grad_sumsq")
 
 
-def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, fused=False):
+def adam_step(descs_dev, n, max_numel, sumsq, max_norm, lr, beta1, beta2, eps, step, fused=False, n_work=0):
     """fused: one launch (both shadows in the Adam pass) that reads *step without advancing it
-    (step_end(..., adam_step=step) advances it); otherwise Adam + shadow pass, step advanced."""
+    (step_end(..., adam_step=step) advances it), on the compact grid with n_work (work_items);
+    otherwise Adam + shadow pass, step advanced."""
     L = lib()
+    if fused and n_work:
+        check(L.llp_adam_step_w(descs_dev.data_ptr(), n, max_numel, int(n_work), ptr(sumsq), max_norm, lr, beta1, beta2, eps,
+                                step.data_ptr(), stream_ptr()), "llp_adam_step_w")
+        return
     if fused:
         check(L.llp_adam_step_t(descs_dev.data_ptr(), n, max_numel, ptr(sumsq), max_norm, lr, beta1, beta2, eps,
                                 step.data_ptr(), stream_ptr()), "llp_adam_step_t")

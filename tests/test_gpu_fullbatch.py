@@ -78,6 +78,42 @@ def test_neg_sample_dense_bit_exact(N, n_und, num_neg):
         assert np.array_equal(out2[:, :n2].cpu().numpy().astype(np.int64), exp), st
 
 
+def test_neg_sample_dense2_later_rounds_bit_exact():
+    """llp_neg_sample_dense2 is round-gated: the first round's candidates are drawn and compacted
+    first and the later rounds' launches do nothing when the first round holds num_neg valid
+    ones (the usual case, which the cases above hit).  Here the graph covers 80 % of the
+    population, so the first round falls short (975-1,002 of 1,200 at these draws) and the
+    later rounds run, continuing the first round's prefix: the oracle's draws bit for bit."""
+    K = _K()
+    N, num_neg = 100, 1200
+    g = np.random.default_rng(N)
+    u, v = np.meshgrid(np.arange(N), np.arange(N), indexing="ij")
+    m = u != v
+    u, v = u[m], v[m]
+    keep = g.random(u.size) < 0.8
+    ei = np.stack([u[keep], v[keep]], 0)
+    keys, n_idx = O.dense_neg_keys(ei, N)
+    ss = O.dense_neg_sample_size(n_idx, N, num_neg)
+    M = 3 * ss
+    assert N * (N - 1) > ss
+    seed, off = 77, 14
+    keys_d = torch.from_numpy(keys).to(DEV)
+    sws = K.StatefulWorkspace(K.neg_sample2_ws_bytes(M), M, DEV, state_bytes=K.neg_sample2_state_bytes(M))
+    table = K.edge_table_build(keys_d)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for st in range(3, 7):
+        ctr.fill_(st)
+        exp = O.negative_sampling_dense_philox(ei, N, num_neg, seed, O.STREAMS_PER_STEP * st + off)
+        out = torch.full((2, num_neg), -1, dtype=torch.int32, device=DEV)
+        cnt = torch.full((1,), -5, dtype=torch.int32, device=DEV)
+        K.neg_sample_dense2(N, None, num_neg, ss, seed, ctr, off, out, cnt, sws, edge_table=table)
+        torch.cuda.synchronize()
+        n = int(cnt.item())
+        assert n == exp.shape[1] == num_neg, (st, n, exp.shape)
+        assert np.array_equal(out[:, :n].cpu().numpy().astype(np.int64), exp), st
+    assert int(sws.error_word()) == 0
+
+
 def test_kd_terms_match_autograd():
     K = _K()
     torch.manual_seed(0)

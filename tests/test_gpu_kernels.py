@@ -686,7 +686,8 @@ def test_clip_and_adam_match_oracle(case, nan_group, fused):
 def test_clip_and_adam_one_launch_bit_identical():
     """The one-launch norm and Adam (tickets) give the two-launch forms' parameters, moments,
     gradients, bf16 shadows and transposed shadows bit for bit (big case, 3 steps; the fused
-    form's step counter advanced by llp_step_end2, as the engines do)."""
+    form's step counter advanced by llp_step_end2, as the engines do), on the 2-D grids and on
+    the compact grids of llp_grad_sumsq_w / llp_adam_step_w (round 5, the engines' default)."""
     k = K()
     spec = _ADAM_CASES["big"]
     g = torch.Generator().manual_seed(77)
@@ -697,7 +698,7 @@ def test_clip_and_adam_one_launch_bit_identical():
     grads = [torch.randn(*s, generator=g) * 3 for s in shapes]
     max_numel = max(p.numel() for p in params)
     runs = []
-    for fused in (False, True):
+    for fused, compact in ((False, False), (True, False), (True, True)):
         dp = [p.to(DEV).clone() for p in params]
         dg = [x.to(DEV).clone() for x in grads]
         m = [torch.zeros_like(p) for p in dp]
@@ -723,18 +724,21 @@ def test_clip_and_adam_one_launch_bit_identical():
         for it in range(3):
             for i in range(len(dp)):
                 dg[i].copy_((grads[i] * (it + 1)).to(DEV))
-            k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets if fused else None)
-            k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step, fused=fused)
+            nw_s, nw_a = k.work_items([(p.numel(), *((p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())),
+                                        bool(spec[i][2])) for i, p in enumerate(dp)]) if compact else (0, 0)
+            k.grad_sumsq(dd, len(dp), max_numel, n_groups, sumsq, ws, ticket=tickets if fused else None, n_work=nw_s)
+            k.adam_step(dd, len(dp), max_numel, sumsq, 1.0, 0.01, 0.9, 0.999, 1e-8, step, fused=fused, n_work=nw_a)
             if fused:
                 k.step_end(loss, 2.0, loss_sum, ctr, adam_step=step)
         torch.cuda.synchronize()
         assert not fused or (int(ctr.item()) == 3 and float(loss_sum.item()) == 6.0
                              and int(tickets.abs().sum()) == 0)
         runs.append((dp, dg, m, v, [x for x in sh if x is not None], sumsq, int(step.item())))
-    for a, b in zip(runs[0][:5], runs[1][:5]):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
-    assert torch.equal(runs[0][5], runs[1][5]) and runs[0][6] == runs[1][6] == 3
+    for r in runs[1:]:
+        for a, b in zip(runs[0][:5], r[:5]):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y)
+        assert torch.equal(runs[0][5], r[5]) and runs[0][6] == r[6] == 3
 
 
 # ------------------------------------------------------------------ unique-node compaction
