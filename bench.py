@@ -228,7 +228,7 @@ def evaluate(model, pred, data, dev):
             "hits_note": "after the timed steps from random init on synthetic data (not a converged model)"}
 
 
-SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r04_pmc_sage_orders.json")
+SAGE_PMC_FILE = os.path.join(REPO, "profiles", "r05_pmc_sage_orders.json")
 
 
 def practical_peak(dev, seconds=0.2, dtype="bf16"):
@@ -266,7 +266,7 @@ def sage_aggregate(data, dev):
     algorithmic bytes E*F*s + 4E + 4(N+1) + N*F*s (every neighbour row from memory, SURVEY
     §8d); compulsory bytes: x, col, rowptr read once, out written once; traffic: beyond-L2
     counter bytes per launch from the committed PMC passes of the same order
-    (profiles/r04_pmc_sage_orders.json: 2 x FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits
+    (profiles/r05_pmc_sage_orders.json: 2 x FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits
     included, so an upper bound on HBM bytes).  frac = traffic / time / 8 TB/s."""
     import llp_hip as K
     import llp_sage
@@ -297,7 +297,7 @@ def sage_aggregate(data, dev):
             comp = 2 * data.N * F_ * es + 4 * g.num_edges + 4 * (data.N + 1)
             traffic = pmc.get((dts, F_, "fwd"))
             tb = (traffic if traffic else algo) / (ms * 1e-3)
-            out.append({"kernel": "csr_agg_rows_kernel fwd", "order": "locality", "dtype": dts, "F": F_, "N": data.N,
+            out.append({"kernel": "csr_agg_lds_kernel fwd", "order": "locality", "dtype": dts, "F": F_, "N": data.N,
                         "E": g.num_edges, "ms": ms, "achieved": tb / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "traffic_over_compulsory": traffic / comp if traffic else None,
                         "frac": tb / 1e9 / PEAK_HBM_GBS, "traffic": traffic, "algorithmic_bytes": algo,

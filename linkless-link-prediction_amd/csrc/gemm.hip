@@ -172,20 +172,22 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 // ============================================================== NT kernel
 // NW waves per 128 x 128 tile: 4 (2 x 2, 64 x 64 per wave) or 8 (2 x 4, 64 x 32 per wave: four
 // waves per SIMD at two workgroups per CU, to cover each other's K-tile boundary)
-template <typename T, bool VEC, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
+// BNT: the tile's width (128, or 256 for the f32 wide form: each wave 64 x 64, the A row panel
+// re-read from L2 half as often; LDS 96 KB, one workgroup per CU).
+template <typename T, bool VEC, int NW = 4, int BNT = BN>
+__global__ __launch_bounds__(64 * NW, BNT == BN ? 2 : 1) void gemm_nt_kernel(NTParams p) {
   constexpr int E = Traits<T>::ELEMS;
   constexpr int BK = 8 * E;  // 8 chunks of 16 B per row
-  constexpr int NT = 64 * NW, WN = NW / 2, WC = BN / WN, JN = WC / 16, SI = (BM * 8) / NT;
-  __shared__ uint4 smem[2 * (BM + BN) * 8];
+  constexpr int NT = 64 * NW, WN = NW / 2, WC = BNT / WN, JN = WC / 16, SI = (BM * 8) / NT, SIB = (BNT * 8) / NT;
+  __shared__ uint4 smem[2 * (BM + BNT) * 8];
   uint4* sA0 = smem;
   uint4* sB0 = smem + BM * 8;
-  const int buf_stride = (BM + BN) * 8;
+  const int buf_stride = (BM + BNT) * 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   p.M = rows_live(p.M, p.m_dev);
-  const int64_t tilesN = (p.N + BN - 1) / BN;
+  const int64_t tilesN = (p.N + BNT - 1) / BNT;
   const int64_t tilesM = (p.M + BM - 1) / BM;
   if ((int64_t)blockIdx.x >= tilesM * tilesN) return;
   const int64_t lt = xcd_remap(blockIdx.x, tilesM * tilesN);
@@ -195,15 +197,15 @@ __global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
   const int64_t tnG = tilesN / p.ngroups, per = tilesM * tnG;
   const int64_t grp = lt / per, rem = lt % per;
   const int64_t tm = rem / tnG, tn = grp * tnG + rem % tnG;
-  const int64_t m0 = tm * BM, n0 = tn * BN;
+  const int64_t m0 = tm * BM, n0 = tn * BNT;
 
   // staging assignment: chunk c = tid + NT*i -> row (tid>>3) + (NT/8)*i, kc = tid&7
   const int kc = tid & 7;
   const T* pa[SI];
   const T* pa2[SI];
-  const T* pb[SI];
-  const T* pb2[SI];
-  bool va[SI], vb[SI];
+  const T* pb[SIB];
+  const T* pb2[SIB];
+  bool va[SI], vb[SIB];
 #pragma unroll
   for (int i = 0; i < SI; ++i) {
     const int r = (tid >> 3) + (NT / 8) * i;
@@ -212,6 +214,10 @@ __global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
     gm = va[i] ? gm : (p.M - 1);
     pa[i] = row_ptr<T>(p.A, gm);
     pa2[i] = row_ptr2<T>(p.A, gm);
+  }
+#pragma unroll
+  for (int i = 0; i < SIB; ++i) {
+    const int r = (tid >> 3) + (NT / 8) * i;
     int64_t gn = n0 + r;
     vb[i] = gn < p.N;
     gn = vb[i] ? gn : (p.N - 1);
@@ -219,14 +225,13 @@ __global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
     pb2[i] = row_ptr2<T>(p.B, gn);
   }
 
-  uint4 ra[SI], rb[SI];
+  uint4 ra[SI], rb[SIB];
   auto gload = [&](int64_t kt) {
     const int64_t k0 = kt * BK + kc * E;
 #pragma unroll
-    for (int i = 0; i < SI; ++i) {
-      ra[i] = load_chunk<T, VEC>(pa[i], pa2[i], k0, p.K, va[i]);
-      rb[i] = load_chunk<T, VEC>(pb[i], pb2[i], k0, p.K, vb[i]);
-    }
+    for (int i = 0; i < SI; ++i) ra[i] = load_chunk<T, VEC>(pa[i], pa2[i], k0, p.K, va[i]);
+#pragma unroll
+    for (int i = 0; i < SIB; ++i) rb[i] = load_chunk<T, VEC>(pb[i], pb2[i], k0, p.K, vb[i]);
   };
   auto lstore = [&](int buf) {
     uint4* sA = sA0 + buf * buf_stride;
@@ -235,6 +240,10 @@ __global__ __launch_bounds__(64 * NW, 2) void gemm_nt_kernel(NTParams p) {
     for (int i = 0; i < SI; ++i) {
       const int r = (tid >> 3) + (NT / 8) * i;
       sA[r * 8 + (kc ^ (r & 7))] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < SIB; ++i) {
+      const int r = (tid >> 3) + (NT / 8) * i;
       sB[r * 8 + (kc ^ (r & 7))] = rb[i];
     }
   };
@@ -641,6 +650,12 @@ int64_t tn_splits(int dtype, int64_t M, int64_t P, int64_t Q) {
 
 // Column groups of the 128x128 NT kernel's tile walk: B (N x K) split into groups of at most
 // 2 MB, half an XCD's 4 MB L2, when the row panels are many (each group then re-reads A once).
+static int64_t nt_groups_w(int64_t N, int64_t K, int es, int64_t tilesM, int64_t bn) {
+  const int64_t tilesN = (N + bn - 1) / bn;
+  int64_t g = 1;
+  while (g * 2 <= tilesN && tilesN % (g * 2) == 0 && N * K * es / g > (2ll << 20) && tilesM >= 64) g *= 2;
+  return g;
+}
 static int64_t nt_groups(int64_t N, int64_t K, int es, int64_t tilesM) {
   const int64_t tilesN = (N + BN - 1) / BN;
   int64_t g = 1;
@@ -716,6 +731,17 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   } else {
     // eight waves per f32 tile (four per SIMD): 105.3 -> 97.5 ms per fp32 collab step, dominant
     // launch 4.28 -> 3.86 ms (profiles/r04_fp32_8w_ab.jsonl); bf16 keeps four (its 256 path rules)
+#ifdef LLP_F32_NT_WIDE   // A/B build: 128 x 256 f32 tiles on LLP_F32_NT_WIDE (8 or 16) waves
+    if (vec && N % 256 == 0) {
+      NTParams pw = p;
+      pw.ngroups = nt_groups_w(N, K, es, (M + BM - 1) / BM, 256);
+      llp::note_kernel("gemm_nt_kernel<f32, vec, wide waves, 128x256> (v_mfma_f32_16x16x4_f32)");
+      hipLaunchKernelGGL((gemm_nt_kernel<float, true, LLP_F32_NT_WIDE, 256>),
+                         dim3((unsigned)(((M + BM - 1) / BM) * (N / 256))), dim3(64 * LLP_F32_NT_WIDE), 0, s, pw);
+      LLP_LAUNCH_CHECK();
+      return LLP_OK;
+    }
+#endif
     llp::note_kernel(vec ? "gemm_nt_kernel<f32, vec, 8 waves> (128x128, v_mfma_f32_16x16x4_f32)"
                          : "gemm_nt_kernel<f32, 8 waves> (128x128, v_mfma_f32_16x16x4_f32)");
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<float, true, 8>), grid, dim3(512), 0, s, p);

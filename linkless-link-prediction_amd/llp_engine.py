@@ -229,6 +229,10 @@ class EngineBase:
         self._seg = None        # _SegmentedGraph while a multi-rank step is being captured
         self._seg_debug = False  # extra segment cuts that sync and name the stage (capture_minibatch)
         self.emulate_shard = None   # (rank, world): time one rank's full-batch student slice (_fb_shard)
+        # full-batch step: the dense negatives beside the student forward and the frozen teacher beside the
+        # predictor forward, on a second stream (step_fullbatch); False: one stream
+        self.overlap_streams = True
+        self._side = None
         self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
 
     def _init_params(self, all_params, groups, optimizer):
@@ -693,6 +697,13 @@ class EngineBase:
         # the one-launch Adam reads the step counter; the step-end launch advances it
         K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
                     float(b2), float(g["eps"]), self.adam_step, fused=True, n_work=self.n_work_adam)
+
+    def _side_stream(self):
+        """The engine's second HIP stream (created once): forks / joins with the current stream
+        by events, so a hipGraph capture records the two branches."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
 
     # ------------------------------------------------------------------ device state
     def _stateful_workspaces(self):
@@ -1244,6 +1255,31 @@ class DistillEngine(EngineBase):
             else:
                 K.context_sampler(self.rowptr, self.col, N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                   self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
+        # ---- negatives (src/main.py:205-209) and the pair index.  PyG-dense ones keep their count on
+        # the device (label slots past it inert, no host read, so the step is graph-capturable) unless
+        # KD_LM, whose kernel takes the host count, needs it.  Without a host read they run on a side
+        # stream beside the student forward (overlap_streams): both are small launches on this path
+        # (the physics student at rank 0 of 4: 31-tile GEMMs), so the GPU has room for both
+        w_rm, w_lm = float(a.KD_RM), float(a.KD_LM)
+        BC = Bc * C
+        side = self._side_stream() if (self.overlap_streams and dense_negatives and neg is None and w_lm == 0.0) \
+            else None
+
+        def negatives_and_pairs():
+            negb, n_neg, n_neg_total, cnt = self._negatives(P, P_total, p_offset, neg, dense_negatives,
+                                                            device_count=w_lm == 0.0)
+            R2 = BC + P + n_neg
+            ia_ib = self._buf("fb_iab", (max(2 * R2, 1),), torch.int32)[:2 * R2]   # [ia | ib]: endpoint rows
+            K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia_ib[:R2],
+                              ia_ib[R2:], neg_count=cnt, neg_offset=p_offset)
+            return n_neg, n_neg_total, cnt, R2, ia_ib
+
+        main = torch.cuda.current_stream(self.dev)
+        if side is not None:
+            side.wait_stream(main)               # the samples
+            with torch.cuda.stream(side):
+                neg_res = negatives_and_pairs()
+
         # ---- a4: student MLP over all nodes (src/main.py:173), queued before the dense negatives'
         # count is read back (one host sync), so the GPU runs it while the host waits; at several ranks each rank
         # runs it on its own slice of the nodes and the slices are all-gathered (_fb_shard)
@@ -1283,6 +1319,14 @@ class DistillEngine(EngineBase):
                                    count=n_rows)
             acts.append(out)
             A = K.operand(out)
+        if side is not None:
+            main.wait_stream(side)               # joined before any collective cut (graph segments)
+        else:
+            neg_res = negatives_and_pairs()
+        n_neg, n_neg_total, cnt, R2, ia_ib = neg_res
+        n_lab = P + n_neg
+        n_lab_total = P_total + n_neg_total if cnt is None else 0.0
+        ia, ib = ia_ib[:R2], ia_ib[R2:]
         if shard is None:
             h = acts[-1]
         else:
@@ -1291,30 +1335,24 @@ class DistillEngine(EngineBase):
             self._collective(lambda: self._all_gather_rows(h_full, h_loc, s_world, s_rank))
             h = h_full[:N]
 
-        # ---- negatives (src/main.py:205-209).  PyG-dense ones keep their count on the device
-        # (label slots past it inert, no host read, so the step is graph-capturable) unless
-        # KD_LM, whose kernel takes the host count, needs it
-        w_rm, w_lm = float(a.KD_RM), float(a.KD_LM)
-        negb, n_neg, n_neg_total, cnt = self._negatives(P, P_total, p_offset, neg, dense_negatives,
-                                                        device_count=w_lm == 0.0)
-        n_lab = P + n_neg
-        n_lab_total = P_total + n_neg_total if cnt is None else 0.0
-        BC = Bc * C
-        R2 = BC + n_lab
-        ia_ib = self._buf("fb_iab", (max(2 * R2, 1),), torch.int32)[:2 * R2]   # [ia | ib]: endpoint rows
-        ia, ib = ia_ib[:R2], ia_ib[R2:]
-        K.fullbatch_pairs(Bc, C1, samp, pairs, link_ids, P, negb if n_neg > 0 else None, n_neg, ia, ib, neg_count=cnt,
-                          neg_offset=p_offset)
+        # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215); it needs
+        # only the pairs, so with the side stream it runs beside the predictor forward
+        R_t = R2 if float(a.KD_LM) != 0.0 else BC
+        t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
+        self._t_head = None
+        if side is not None and R_t > 0:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r, defer_head=R_t == BC)
+        t_head = self._t_head
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
         A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop, defer_head=True)
-
-        # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215)
-        R_t = R2 if float(a.KD_LM) != 0.0 else BC
-        t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
-        self._t_head = None
-        if R_t > 0:   # (KD_LM reads the label pairs' probabilities: finished here, not in the loss)
+        if side is not None and R_t > 0:
+            main.wait_stream(side)
+            self._t_head = t_head
+        elif R_t > 0:   # (KD_LM reads the label pairs' probabilities: finished here, not in the loss)
             self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r, defer_head=R_t == BC)
 
         # ---- a7-a9: LLP_D + LLP_R + BCE, then KD_RM / KD_LM (src/main.py:217-222)

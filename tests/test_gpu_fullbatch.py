@@ -345,3 +345,35 @@ def test_fullbatch_graph_replay_matches_eager(dtype):
     for a, b in zip(out[False][0], out[True][0]):
         assert torch.equal(a, b)
     assert torch.equal(out[False][1], out[True][1])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fullbatch_two_streams_bit_identical(dtype):
+    """DistillEngine.overlap_streams (the default): the dense negatives run beside the student
+    forward and the frozen teacher beside the predictor forward, on a second stream.  Two steps
+    give the one-stream engine's loss terms and parameters bit for bit, eagerly and from a
+    hipGraph (the capture records both branches)."""
+    _K()
+    case = G.load_case("fullbatch_production_small")
+    out = {}
+    for overlap, graph in ((False, False), (True, False), (True, True)):
+        eng, model, pred = _engine(case, dtype)
+        eng.overlap_streams = overlap
+        pairs = case.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+        st = case.steps[0]
+        a_buf = st.node_perm.to(torch.int32).to(DEV).clone()
+        l_buf = st.link_perm.to(torch.int32).to(DEV).clone()
+        eng.step_fullbatch(a_buf, l_buf, pairs)
+        if graph:
+            g = eng.capture_fullbatch(a_buf, l_buf, pairs)
+            g.replay()
+        else:
+            eng.step_fullbatch(a_buf, l_buf, pairs)
+        torch.cuda.synchronize()
+        out[(overlap, graph)] = ([p.detach().cpu().clone() for p in list(model.parameters()) + list(pred.parameters())],
+                                 eng.terms.cpu().clone())
+    ref = out[(False, False)]
+    for key in ((True, False), (True, True)):
+        for a, b in zip(ref[0], out[key][0]):
+            assert torch.equal(a, b), key
+        assert torch.equal(ref[1], out[key][1]), key

@@ -52,6 +52,10 @@ def main():
         for name, v in res.items():
             ms = sorted(v)[1]
             print(f"{opt.dtype} M={M:7d} {name:12s} {ms:.3f} ms {f / ms / 1e9:.0f} TF", flush=True)
+        K.gemm_nt(K.operand(A), K.operand(W), M, 1024, 1024, out, dc)
+        ref = torch.mm(A.float(), W.float().t())
+        err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+        print(f"{opt.dtype} M={M:7d} NT max rel error vs an f32 torch.mm: {err:.2e} ({K.last_gemm_kernel()})", flush=True)
 
 
 if __name__ == "__main__":

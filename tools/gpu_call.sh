@@ -30,6 +30,9 @@ for RA in "$@"; do
     tests-sel)      # a selection: tests-sel:tests/x.py::test_a,tests/y.py
       timeout -k 10 900 $PYT $ARGS -m gpu > $O/pytest_sel.log 2>&1 || fail tests-sel $O/pytest_sel.log
       tail -1 $O/pytest_sel.log ;;
+    fullsize-oracle) # the full-size oracle parity test with its printed per-tensor table (-s)
+      timeout -k 10 600 $PYT -s tests/test_gpu_fullsize_oracle.py -m gpu > $O/fullsize_oracle.log 2>&1 || fail fullsize-oracle $O/fullsize_oracle.log
+      grep -A14 "gradient max" $O/fullsize_oracle.log ;;
     tests-multirank)
       timeout -k 10 900 $PYT tests/test_gpu_multirank.py -q > $O/pytest_multirank.log 2>&1 || fail multirank $O/pytest_multirank.log
       tail -1 $O/pytest_multirank.log ;;
@@ -129,11 +132,13 @@ for RA in "$@"; do
     bf16-accuracy)  # paired bf16 - fp32 Hits@K over seeds (tools/bf16_accuracy.py)
       timeout -k 10 1000 python tools/bf16_accuracy.py ${ACC_ARGS:-} > $O/bf16_accuracy.jsonl 2> $O/bf16_accuracy.err || fail bf16-accuracy $O/bf16_accuracy.err
       tail -5 $O/bf16_accuracy.jsonl ;;
-    ab)             # same-box A/B of AB_SCRIPT (default: the lean collab bench) against LLP_LIB=$AB_LIB, 3 rounds
+    ab)             # same-box A/B of AB_SCRIPT (default: the lean collab bench) against LLP_LIB=$AB_LIB (default:
+                    # the same library) running AB_SCRIPT_VAR (default: AB_SCRIPT), 3 rounds
       S=${AB_SCRIPT:-"python bench.py $LEAN"}
+      SV=${AB_SCRIPT_VAR:-$S}
       for i in 1 2 3; do
         timeout -k 10 300 $S > $O/ab_base_$i.json 2> $O/ab_base_$i.err || fail ab-base $O/ab_base_$i.err
-        LLP_LIB=$AB_LIB timeout -k 10 300 $S > $O/ab_var_$i.json 2> $O/ab_var_$i.err || fail ab-var $O/ab_var_$i.err
+        LLP_LIB=${AB_LIB:-linkless-link-prediction_amd/libllp_hip.so} timeout -k 10 300 $SV > $O/ab_var_$i.json 2> $O/ab_var_$i.err || fail ab-var $O/ab_var_$i.err
       done
       tail -n 1 $O/ab_base_*.json $O/ab_var_*.json ;;
     *)

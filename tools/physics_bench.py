@@ -136,6 +136,9 @@ def main():
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "llp_physics"))
     ap.add_argument("--no-edge-table", action="store_true",
                     help="A/B: the dense negative sampler's membership test by binary search of the sorted keys")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="A/B: one stream (DistillEngine.overlap_streams = False): the dense negatives and the frozen "
+                         "teacher after the student / predictor forward instead of beside them")
     ap.add_argument("--hb-two-kernel", action="store_true",
                     help="A/B: the round-3 two-kernel Hadamard backward (profiles/r03_hb_fused_fb_ab.txt)")
     opt = ap.parse_args()
@@ -144,6 +147,13 @@ def main():
         llp_engine.K.neg_sample_dense = lambda *a, edge_table=None, **kw: _nsd(*a, **kw)
     if opt.hb_two_kernel:
         llp_engine.DistillEngine._hadamard_bwd_nodes = _hb_two_kernel
+    if opt.no_overlap:
+        _init = llp_engine.DistillEngine.__init__
+
+        def _init_one_stream(self, *a, **kw):
+            _init(self, *a, **kw)
+            self.overlap_streams = False
+        llp_engine.DistillEngine.__init__ = _init_one_stream
     t0 = time.perf_counter()
     split = llp_split.production_split("coauthor-physics", opt.data_dir, synthetic=True)
     prep = time.perf_counter() - t0
