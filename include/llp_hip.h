@@ -79,9 +79,12 @@ int llp_device_count(void);
  * type (aux_dtype LLP_MASK: aux is a ReLU bit mask, see enum llp_dtype; bf16
  * 256-tile path only).  bias (f32[N]) may be NULL. */
 /* Optional inverted dropout after the activation (F.dropout / nn.Dropout after
- * ReLU, src/models.py:52-53,144-145): element (m, n) is kept iff
- * u >= p with u = uniform draw #(m*N + n) of Philox stream
- * 64*(*step_ctr) + stream_offset; kept values are scaled by 1/(1-p).
+ * ReLU, src/models.py:52-53,144-145): element (m, n) is kept iff its keep
+ * draw (8 bits when p*256 is an integer, else 16; one Philox block per 16 or 8
+ * elements of a row, layout in csrc/llp_common.h drop_keep, oracle
+ * dropout_keep) in Philox stream 64*(*step_ctr) + stream_offset is >= the
+ * threshold p*256 (8-bit) or ceil(p*65536) (16-bit); kept values are scaled by
+ * 1/(1-p).
  * The backward needs no mask: LLP_ACT_RELU_BWD against the stored dropped
  * activation with alpha = 1/(1-p) is exact. */
 typedef struct llp_dropout {
@@ -606,7 +609,7 @@ int llp_zero(void* p, int64_t bytes, void* stream);
  * out = gprob * prob * (1 - prob)                 — torch.sigmoid backward (src/models.py:150) */
 int llp_relu_bwd(int dtype, int64_t n, const void* gy, const void* y, float alpha, void* out, void* stream);
 /* Strided [rows, cols] forms for the SAGE teacher's concatenated layouts:
- * y = dropout(act(x)) (act NONE/RELU; dropout draw #(r*cols+c), as the GEMM
+ * y = dropout(act(x)) (act NONE/RELU; dropout keep draw of (r, c), as the GEMM
  * epilogue; src/models.py:117-118) and out = alpha * gy * (y > 0). */
 int llp_act_2d(int dtype, int64_t rows, int64_t cols, const void* x, int64_t ldx, void* y, int64_t ldy,
                int act, const llp_dropout* dropout, void* stream);

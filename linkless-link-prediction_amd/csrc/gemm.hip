@@ -58,7 +58,7 @@ struct NTParams {
   int aux_bf16;
   float alpha;
   float drop_p;          // 0 = no dropout
-  uint32_t drop_thresh;  // keep iff (x >> 8) >= drop_thresh  (u >= p, u = (x>>8) 2^-24)
+  uint32_t drop_thresh;  // llp::drop_code(p): keep iff drop_keep(..) (llp_common.h)
   float drop_scale;      // 1 / (1 - p)
   uint64_t drop_seed;
   const int64_t* drop_ctr;
@@ -340,8 +340,7 @@ __global__ __launch_bounds__(64 * NW, BNT == BN ? 2 : 1) void gemm_nt_kernel(NTP
           v = a > 0.f ? v : 0.f;
         }
         if (p.drop_p > 0.f) {
-          const uint32_t x = philox_u32(p.drop_seed, dstream, (uint64_t)(row * p.N + col));
-          v = (x >> 8) >= p.drop_thresh ? v * p.drop_scale : 0.f;
+          v = drop_keep(p.drop_thresh, p.drop_seed, dstream, row, col, p.N) ? v * p.drop_scale : 0.f;
         }
         if (p.c_bf16)
           reinterpret_cast<bf16_t*>(p.C)[row * p.ldc + col] = f2bf(v);
@@ -695,7 +694,7 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   if (dropout && dropout->p > 0.f) {
     LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_gemm_nt: dropout p in (0,1) needs step_ctr");
     p.drop_p = dropout->p;
-    p.drop_thresh = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    p.drop_thresh = llp::drop_code(dropout->p);
     p.drop_scale = 1.f / (1.f - dropout->p);
     p.drop_seed = dropout->seed;
     p.drop_ctr = dropout->step_ctr;
@@ -826,7 +825,7 @@ extern "C" int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_opera
   if (dropout && dropout->p > 0.f) {
     LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_gemm_nt_head: dropout p in (0,1) needs step_ctr");
     dp = dropout->p;
-    dth = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    dth = llp::drop_code(dropout->p);
     ds = 1.f / (1.f - dropout->p);
     dseed = dropout->seed;
     dctr = dropout->step_ctr;

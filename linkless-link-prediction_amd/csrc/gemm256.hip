@@ -269,6 +269,13 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
   // ---------------- epilogue in registers: alpha, bias, ReLU, dropout
   const uint64_t dstream = p.drop_p > 0.f ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
   uint4* stg = smem;   // staged C tile: row-major [256][EPI_ROW_U4] uint4
+  // keep flags of this thread's 16 columns per row (one or two Philox blocks, drop_keep16)
+  uint32_t kb[8];
+#pragma unroll
+  for (int im = 0; im < 8; ++im)
+    kb[im] = p.drop_p > 0.f ? drop_keep16(p.drop_thresh, p.drop_seed, dstream, m0 + wm * 128 + im * 16 + li,
+                                          n0 + wn * 64 + g * 4, p.N)
+                            : 0u;
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn) {
     const int nl = wn * 64 + jn * 16 + g * 4;          // local column of element r = 0
@@ -287,12 +294,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_256(P256 p) {
         if (p.act == LLP_ACT_RELU) v[r] = __float_as_int(v[r]) < 0 ? 0.f : v[r];   // the lean epilogues' sign rule
       }
       if (p.drop_p > 0.f) {
-        // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
-        // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
-        const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
-        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
+        for (int r = 0; r < 4; ++r) v[r] = (kb[im] >> (4 * jn + r)) & 1u ? v[r] * p.drop_scale : 0.f;
       }
       const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -363,6 +366,10 @@ constexpr int EPI_HEAD_LEAN = 5;
 // [nkt*s/S, nkt*(s+1)/S) and stores its raw f32 accumulators to slab s at
 // head_part + s*M*N (row stride N); splitk_reduce_kernel applies the epilogue
 constexpr int EPI_PARTIAL = 6;
+// ReLU + dropout forward (pp8p only): EPI_FWD_RELU's epilogue with the keep draws
+// (drop_keep16, one or two Philox blocks per thread row) applied before the bf16 rounding,
+// and the ReLU mask of the dropped outputs; the values and bits of epilogue_t's dropout
+constexpr int EPI_FWD_DROP = 7;
 
 // MASK_LDS (TMv 256, NTHR 512 only): the ReLU-backward bit mask of the tile (256 rows x
 // 32 bytes) is read with ONE 16-byte load per thread into LDS at smem + head_off_u4 + 256
@@ -414,6 +421,13 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
   }
   uint4* stg = smem;
   float hp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // keep flags of this thread's 16 columns per row (one or two Philox blocks, drop_keep16)
+  uint32_t kb[8];
+#pragma unroll
+  for (int im = 0; im < 8; ++im)
+    kb[im] = drop ? drop_keep16(p.drop_thresh, p.drop_seed, dstream, m0 + wm * 128 + im * 16 + li,
+                                n0 + wn * 64 + g * 4, p.N)
+                  : 0u;
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn) {
     const int nl = wn * 64 + jn * 16 + g * 4;
@@ -445,12 +459,8 @@ __device__ __forceinline__ void epilogue_t(const P256& p, float4_t (&acc)[4][8],
         if (relu) v[r] = __float_as_int(v[r]) < 0 ? 0.f : v[r];
       }
       if (drop) {
-        // draws #idx..idx+3 (idx % 4 == 0: N % 8 == 0, nl % 4 == 0) are one Philox block:
-        // philox_u32(seed, stream, idx + r) == component r of philox4(idx >> 2, stream, seed)
-        const uint4 x4 = philox4((uint64_t)((m0 + ml) * p.N + n0 + nl) >> 2, dstream, p.drop_seed);
-        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (xs[r] >> 8) >= p.drop_thresh ? v[r] * p.drop_scale : 0.f;
+        for (int r = 0; r < 4; ++r) v[r] = (kb[im] >> (4 * jn + r)) & 1u ? v[r] * p.drop_scale : 0.f;
       }
       // explicit fma order: the head partial is bit-identical across kernel variants
       if (headw) hp[im] = head_dot4(hp[im], v, hw);
@@ -1017,9 +1027,11 @@ namespace {
 constexpr int PP_STAGE_U4 = 128 * EPI_ROW_U4;          // one 128-row half of the staged C tile
 template <int MODE>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
-  static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK || MODE == EPI_HEAD_LEAN,
+  static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK || MODE == EPI_HEAD_LEAN ||
+                    MODE == EPI_FWD_DROP,
                 "lean modes only");
-  constexpr bool RELU = MODE == EPI_FWD_RELU;
+  constexpr bool DROP = MODE == EPI_FWD_DROP;
+  constexpr bool RELU = MODE == EPI_FWD_RELU || DROP;
   constexpr bool BWD = MODE == EPI_BWD_MASK;
   constexpr bool HEAD = MODE == EPI_HEAD_LEAN;
   constexpr int IMG_U4 = 256 * 8;
@@ -1066,6 +1078,8 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   };
   int64_t t = blockIdx.x, m0 = 0, n0 = 0;
   if (!next_tile(t, m0, n0)) return;
+  // the dropout stream (a uniform load here, before any DMA is in flight)
+  const uint64_t dstream = DROP ? (uint64_t)(LLP_STREAMS_PER_STEP * (*p.drop_ctr) + p.drop_stream) : 0;
 
   // DMA in SADDR form: a wave-uniform base (the tile's row panel at the K-tile) and a per-lane
   // 32-bit byte offset computed per piece: row q64_row(..) + lane / 8 of the tile, clamped to
@@ -1250,6 +1264,28 @@ __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
     for (int h = 0; h < 2; ++h) {
       {   // phase 1: this wave's rows (4h + im') * 16 + li of its group's 128, im' < 4
         char* sb = stg + (ewm * 64 + eli) * ROWB + (ewn * 64 + eg * 4) * 2;
+        if (DROP) {   // row by row: the keep flags of the row's 16 columns, then its 4 column quads
+          const float dsc = p.drop_scale;
+#pragma unroll
+          for (int iq = 0; iq < 4; ++iq) {
+            const int im = 4 * h + iq;
+            const uint32_t kb = drop_keep16(p.drop_thresh, p.drop_seed, dstream, m0 + ewm * 128 + im * 16 + eli,
+                                            n0 + ewn * 64 + eg * 4, p.N);
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) {
+              // before the rounding, as epilogue_t (the ReLU after it: same values and bits)
+              float2_t v01 = float2_t{acc[jn][im][0], acc[jn][im][1]} + float2_t{bl[jn][0], bl[jn][1]};
+              float2_t v23 = float2_t{acc[jn][im][2], acc[jn][im][3]} + float2_t{bl[jn][2], bl[jn][3]};
+              const uint32_t k = kb >> (4 * jn);
+              v01[0] = k & 1u ? v01[0] * dsc : 0.f;
+              v01[1] = k & 2u ? v01[1] * dsc : 0.f;
+              v23[0] = k & 4u ? v23[0] * dsc : 0.f;
+              v23[1] = k & 8u ? v23[1] * dsc : 0.f;
+              *reinterpret_cast<uint2*>(sb + iq * 16 * ROWB + jn * 32) =
+                  make_uint2(relu_pk_bf16(pk_bf16(v01)), relu_pk_bf16(pk_bf16(v23)));
+            }
+          }
+        } else
 #pragma unroll
         for (int jn = 0; jn < 4; ++jn) {
           const float2_t b01 = {bl[jn][0], bl[jn][1]}, b23 = {bl[jn][2], bl[jn][3]};
@@ -1480,12 +1516,21 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   }
   const int mode = epi_mode_of(p);
 #ifndef LLP_GEMM_NO_PERSISTENT
+  // ReLU + dropout forward with an optional ReLU mask out (the teacher's hidden layers)
+  const bool drop_lean = mode == EPI_ANY && p.drop_p > 0.f && !head_w && C && act == LLP_ACT_RELU &&
+                         alpha == 1.f && !aux && !mask_in;
   // persistent form for the lean modes (plain operands, an even number of K-tiles): one
   // workgroup per CU walks its tiles with the next tile's first K-tile prefetched
   const bool lean_shapes = N % TN == 0 && !(ldc & 7) && !((uintptr_t)C & 15) &&
-                           (mode != EPI_FWD_RELU || !mask_out || (!(ld_mask & 3) && !((uintptr_t)mask_out & 3))) &&
+                           ((mode != EPI_FWD_RELU && !drop_lean) || !mask_out ||
+                            (!(ld_mask & 3) && !((uintptr_t)mask_out & 3))) &&
                            (mode != EPI_BWD_MASK || (!(ld_mask & 15) && !((uintptr_t)mask_in & 15))) &&
                            (!bias || !((uintptr_t)bias & 15));
+  if (drop_lean && lean_shapes && !A->idx && !B->idx && (K / TK) % 2 == 0 && tiles > 256) {
+    llp::note_kernel("gemm_nt_bf16_pp8p<EPI_FWD_DROP> (persistent)");
+    hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_FWD_DROP>), persistent_grid(tiles), block, 0, s, p);
+    return (int)hipGetLastError();
+  }
   if ((mode == EPI_FWD_RELU || mode == EPI_FWD_NONE || mode == EPI_BWD_MASK) && lean_shapes && !A->idx && !B->idx &&
       (K / TK) % 2 == 0 && tiles > 256) {
     const dim3 pgrid = persistent_grid(tiles);

@@ -384,6 +384,11 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
     for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
   const int q4 = li >> 2, pp = li & 3;
   const bool do_cs = p.ws_colsum != nullptr && q0 == 0 && wq == 0;
+  // waves 4-7 own the tile's columns q0 + 128 ..: with Q - q0 <= 128 (the first student layer's
+  // weight gradient at F = 128, the teacher's first layer) they hold only padding and skip their
+  // fragment reads and MFMAs, so each SIMD runs one wave's MFMAs (they still stage their DMA
+  // pieces and keep the barrier count)
+  const bool q_live = wq == 0 || q0 + 128 < p.Q;
   float4_t accb[4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) accb[b] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -461,14 +466,16 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
       if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
       else if (st + NS - 1 < nsteps) issue(st + NS - 1);
     }
-    if (st > 0) { mfma_half(0); mfma_half(1); }
+    if (st > 0 && q_live) { mfma_half(0); mfma_half(1); }
     if (STAG == 2) {
       if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
       else if (st + NS - 1 < nsteps) issue(st + NS - 1);
     }
-    read_p(sl);
-    read_q(sl, 0);
-    read_q(sl, 4);
+    if (q_live) {
+      read_p(sl);
+      read_q(sl, 0);
+      read_q(sl, 4);
+    }
   };
 
   if (nsteps > 0) {
@@ -484,8 +491,10 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
         body_stag(3, st + 3, true);
       }
       for (; st < nsteps; ++st) body_stag((int)(st % NS), st, false);
-      mfma_half(0);
-      mfma_half(1);
+      if (q_live) {
+        mfma_half(0);
+        mfma_half(1);
+      }
     } else if (do_cs) {
       for (; st < nsteady; st += NS) {
         body_plain(std::true_type{}, 0, st, true);

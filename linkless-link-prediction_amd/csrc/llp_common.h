@@ -14,6 +14,14 @@ extern thread_local char g_err[512];
 int set_error(int code, const char* fmt, ...);
 // records (thread-local) the name of the NT GEMM kernel a launch chose: llp_last_gemm_kernel()
 void note_kernel(const char* name);
+// dropout code of p in (0, 1): the keep threshold and draw width (see drop_keep below)
+inline uint32_t drop_code(float p) {
+  const double s = (double)p * 256.0;
+  if (s == (double)(int64_t)s) return 0x80000000u | (uint32_t)s;
+  const double t = (double)p * 65536.0;
+  const uint32_t ti = (uint32_t)t;
+  return (double)ti == t ? ti : ti + 1u;   // ceil
+}
 }  // namespace llp
 
 #define LLP_CHECK_ARG(cond, ...)                                        \
@@ -85,6 +93,65 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t stream, u
     case 2: return r.z;
     default: return r.w;
   }
+}
+
+// ---------------------------------------------------------------- dropout draws
+// One Philox block serves 16 (8-bit draws) or 8 (16-bit draws) elements of a row, laid
+// out so that the 256-tile GEMM epilogues' per-thread column sets (columns jn*16 + g*4 + r
+// of a 64-column group, jn, r < 4) take one or two blocks per row instead of one per four
+// elements (round 5: the teacher's dropout layers spent ~2/3 of their GEMM on Philox).
+// The drop code (llp::drop_code) is thr | (1 << 31) with 8-bit draws (p * 256 an integer,
+// e.g. 0.5: thr = p * 256 exactly), else ceil(p * 65536) with 16-bit draws; keep iff the
+// draw >= thr.  Element (r, c) of a [rows, N] tensor, NG = ceil(N / 64), q = c >> 6,
+// g = (c >> 2) & 3:
+//   8-bit:  block (r NG + q) 4 + g,                        word (c >> 4) & 3,                      byte c & 3
+//   16-bit: block ((r NG + q) 4 + g) 2 + ((c >> 5) & 1),  word ((c >> 4) & 1) 2 + ((c >> 1) & 1), half c & 1
+// Must match oracle/llp_oracle.py:dropout_keep bit for bit.
+constexpr uint32_t LLP_DROP_8BIT = 0x80000000u;
+__device__ __forceinline__ uint64_t drop_group(int64_t r, int64_t c, int64_t N) {
+  return (uint64_t)((r * ((N + 63) >> 6) + (c >> 6)) * 4 + ((c >> 2) & 3));
+}
+__device__ __forceinline__ uint32_t u4_word(const uint4& x, int w) {
+  return w == 0 ? x.x : w == 1 ? x.y : w == 2 ? x.z : x.w;
+}
+__device__ __forceinline__ bool drop_keep(uint32_t code, uint64_t seed, uint64_t stream, int64_t r, int64_t c,
+                                          int64_t N) {
+  const uint64_t grp = drop_group(r, c, N);
+  uint32_t u;
+  if (code & LLP_DROP_8BIT) {
+    u = (u4_word(philox4(grp, stream, seed), (int)((c >> 4) & 3)) >> (8 * (c & 3))) & 0xFFu;
+  } else {
+    const uint4 x = philox4(grp * 2 + ((c >> 5) & 1), stream, seed);
+    u = (u4_word(x, (int)(((c >> 4) & 1) * 2 + ((c >> 1) & 1))) >> (16 * (c & 1))) & 0xFFFFu;
+  }
+  return u >= (code & ~LLP_DROP_8BIT);
+}
+// keep flags of the 16 elements (jn, r) at columns c0 + 16 jn + r of row r (c0 = a 64-column
+// group's base + 4 g): bit 4 jn + r
+__device__ __forceinline__ uint32_t drop_keep16(uint32_t code, uint64_t seed, uint64_t stream, int64_t row,
+                                                int64_t c0, int64_t N) {
+  const uint64_t grp = drop_group(row, c0, N);
+  const uint32_t thr = code & ~LLP_DROP_8BIT;
+  uint32_t bits = 0;
+  if (code & LLP_DROP_8BIT) {
+    const uint4 x = philox4(grp, stream, seed);
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bits |= (((u4_word(x, jn) >> (8 * r)) & 0xFFu) >= thr ? 1u : 0u) << (4 * jn + r);
+  } else {
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const uint4 x = philox4(grp * 2 + jp, stream, seed);
+#pragma unroll
+      for (int j1 = 0; j1 < 2; ++j1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          bits |= (((u4_word(x, j1 * 2 + (r >> 1)) >> (16 * (r & 1))) & 0xFFFFu) >= thr ? 1u : 0u)
+                  << (4 * (2 * jp + j1) + r);
+    }
+  }
+  return bits;
 }
 
 // floor(u*n), u = (x>>8)*2^-24, exact integer form (oracle: uniform_index)

@@ -63,8 +63,9 @@ __global__ void sigmoid_bwd_kernel(int64_t n, const float* __restrict__ gprob, c
 
 unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384)); }
 
-// y = dropout(relu(x)) on a strided [rows, cols] view; draw #(r*cols + c) of
-// Philox stream LLP_STREAMS_PER_STEP*(*ctr) + stream_off, as the GEMM epilogue draws.
+// y = dropout(relu(x)) on a strided [rows, cols] view; the keep draw of element (r, c)
+// (drop_keep) of Philox stream LLP_STREAMS_PER_STEP*(*ctr) + stream_off, as the GEMM
+// epilogue draws.
 template <typename T>
 __global__ void act_2d_kernel(int64_t rows, int64_t cols, const T* __restrict__ x, int64_t ldx, T* __restrict__ y,
                               int64_t ldy, int relu, uint32_t thr, float scale, uint64_t seed,
@@ -77,7 +78,7 @@ __global__ void act_2d_kernel(int64_t rows, int64_t cols, const T* __restrict__ 
     // torch.relu propagates NaN (fmaxf would turn it into 0); bf16 follows the 256-tile GEMM
     // epilogues' sign-bit rule (a -NaN becomes 0 there)
     if (relu) v = sizeof(T) == 2 ? (__float_as_int(v) < 0 ? 0.f : v) : (v < 0.f ? 0.f : v);
-    if (thr) v = ((philox_u32(seed, stream, (uint64_t)i) >> 8) >= thr) ? v * scale : 0.f;
+    if (thr) v = drop_keep(thr, seed, stream, r, c, cols) ? v * scale : 0.f;
     stv<T>(y, r * ldy + c, v);
   }
 }
@@ -109,7 +110,7 @@ extern "C" int llp_act_2d(int dtype, int64_t rows, int64_t cols, const void* x, 
   int64_t off = 0;
   if (dropout && dropout->p > 0.f) {
     LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_act_2d: dropout p in (0,1) needs step_ctr");
-    thr = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    thr = llp::drop_code(dropout->p);
     scale = 1.f / (1.f - dropout->p);
     seed = dropout->seed;
     ctr = dropout->step_ctr;

@@ -42,8 +42,8 @@ __device__ __forceinline__ int64_t live_rows(int64_t M, const int32_t* m_dev) {
   return c < M ? (c > 0 ? c : 0) : M;
 }
 
-// dropout(relu(v)) of element (r, c): draw #(r*H + c) of the layer's Philox stream, as
-// the GEMM epilogue and llp_act_2d draw
+// dropout(relu(v)) of element (r, c) of an [M, H] tensor: its keep draw (drop_keep) of the
+// layer's Philox stream, as the GEMM epilogue and llp_act_2d draw
 struct Drop {
   uint32_t thr;
   float scale;
@@ -52,9 +52,10 @@ struct Drop {
   int64_t off;
 };
 
-__device__ __forceinline__ float relu_drop(float v, int relu, const Drop& d, uint64_t stream, uint64_t idx) {
+__device__ __forceinline__ float relu_drop(float v, int relu, const Drop& d, uint64_t stream, int64_t r, int64_t c,
+                                           int64_t H) {
   if (relu) v = fmaxf(v, 0.f);
-  if (d.thr) v = ((philox_u32(d.seed, stream, idx) >> 8) >= d.thr) ? v * d.scale : 0.f;
+  if (d.thr) v = drop_keep(d.thr, d.seed, stream, r, c, H) ? v * d.scale : 0.f;
   return v;
 }
 
@@ -168,7 +169,7 @@ __global__ void bn_apply_kernel(int64_t M, int64_t H, const T* __restrict__ y, i
     const float a = stats[H + c] * (gamma ? gamma[c] : 1.f);
     const float b = (beta ? beta[c] : 0.f) - stats[c] * a;
     const float v = fmaf(ldv<T>(y, r * ldy + c), a, b);
-    stv<T>(out, r * ldo + c, relu_drop(v, relu, d, stream, (uint64_t)i));
+    stv<T>(out, r * ldo + c, relu_drop(v, relu, d, stream, r, c, H));
   }
 }
 
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int64_t H, const
   for (int64_t c = lane; c < H; c += 64) {
     float v = (ldv<T>(yr, c) - mean) * rstd;
     v = fmaf(v, gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f);
-    stv<T>(out, r * ldo + c, relu_drop(v, relu, d, stream, (uint64_t)(r * H + c)));
+    stv<T>(out, r * ldo + c, relu_drop(v, relu, d, stream, r, c, H));
   }
 }
 
@@ -260,7 +261,7 @@ int make_drop(const llp_dropout* dropout, Drop& d, const char* fn) {
   d = Drop{0u, 1.f, 0ull, nullptr, 0};
   if (dropout && dropout->p > 0.f) {
     LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "%s: dropout p in (0,1) needs step_ctr", fn);
-    d.thr = (uint32_t)ceil((double)dropout->p * 16777216.0);
+    d.thr = llp::drop_code(dropout->p);
     d.scale = 1.f / (1.f - dropout->p);
     d.seed = dropout->seed;
     d.ctr = dropout->step_ctr;

@@ -235,10 +235,82 @@ def test_gemm_nt_dropout_is_deterministic_and_unbiased():
     assert torch.allclose(outs[0][kept], 2.0 * full[kept], rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("p", [0.5, 0.3])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_act_2d_dropout_keep_matches_oracle(p, dt):
+    """llp_act_2d's keep pattern is the oracle's dropout_keep bit for bit (8-bit draws at
+    p = 0.5, 16-bit at 0.3), on a width that is not a multiple of 64 and a strided view."""
+    k = K()
+    rows, n, step, off, seed = 37, 200, 3, 5, 4242
+    x = torch.ones(rows, n + 8, device=DEV, dtype=dt)[:, :n]
+    y = torch.empty(rows, n, device=DEV, dtype=dt)
+    ctr = torch.full((1,), step, dtype=torch.int64, device=DEV)
+    k.act_2d(x, y, act=k.ACT_RELU, dropout=k.Dropout(p, seed, ctr.data_ptr(), off))
+    torch.cuda.synchronize()
+    keep = O.dropout_keep(seed, O.STREAMS_PER_STEP * step + off, rows, n, p)
+    assert torch.equal(y.cpu() != 0, torch.from_numpy(keep))
+    assert torch.allclose(y[y != 0].float(), torch.full((1,), 1.0 / (1.0 - p), device=DEV).to(dt).float())
+
+
+@pytest.mark.parametrize("M,N,Kd", [(70_000, 256, 512), (70_001, 512, 256), (3_000, 256, 512)])
+def test_gemm_nt_dropout_exact_against_relu(M, N, Kd):
+    """The bf16 dropout forward (pp8p<EPI_FWD_DROP> above 256 tiles, pp8's generic epilogue
+    below) at p = 0.5: scale 2 is exact, so its output is where(keep, 2 * relu output, 0) of
+    the ReLU kernel on the same operands bit for bit, keep = the oracle's dropout_keep, and
+    its ReLU mask is the bits of that output (partial last m-tile at M = 70,001)."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    ctr = torch.full((1,), 7, dtype=torch.int64, device=DEV)
+    R = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, R, k.LLP_BF16, bias=b, act=k.ACT_RELU)
+    D = torch.empty_like(R)
+    mask = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, D, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=mask,
+              dropout=k.Dropout(0.5, 99, ctr.data_ptr(), 2))
+    if M > 65_536:
+        assert "EPI_FWD_DROP" in k.last_gemm_kernel()
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(O.dropout_keep(99, O.STREAMS_PER_STEP * 7 + 2, M, N, 0.5)).to(DEV)
+    exp = torch.where(keep, R.float() * 2.0, torch.zeros((), device=DEV)).to(torch.bfloat16)
+    assert torch.equal(D.view(torch.int16), exp.view(torch.int16))
+    bits = (D.float() > 0).view(M, N // 8, 8).to(torch.uint8)
+    want = (bits << torch.arange(8, device=DEV, dtype=torch.uint8)).sum(-1).to(torch.uint8)
+    assert torch.equal(mask, want)
+
+
+def test_gemm_nt_dropout_16bit_draws():
+    """p = 0.3 (16-bit draws) on the persistent dropout epilogue: the zero pattern is
+    keep & (relu output > 0) exactly, the kept values 1/0.7 x the ReLU output to bf16 rounding."""
+    k = K()
+    M, N, Kd = 70_000, 256, 256
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    ctr = torch.full((1,), 1, dtype=torch.int64, device=DEV)
+    R = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, R, k.LLP_BF16, act=k.ACT_RELU)
+    D = torch.empty_like(R)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, D, k.LLP_BF16, act=k.ACT_RELU,
+              dropout=k.Dropout(0.3, 5, ctr.data_ptr(), 1))
+    assert "EPI_FWD_DROP" in k.last_gemm_kernel()
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(O.dropout_keep(5, O.STREAMS_PER_STEP + 1, M, N, 0.3)).to(DEV)
+    assert torch.equal(D != 0, keep & (R > 0))
+    kept = D != 0
+    assert torch.allclose(D[kept].float(), R[kept].float() / 0.7, rtol=8e-3, atol=0)
+    assert abs(keep.float().mean().item() - 0.7) < 0.005
+
+
 # ------------------------------------------------------------------ GEMM TN (weight grads)
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
-@pytest.mark.parametrize("M,P,Q", [(1000, 64, 48), (5000, 256, 128), (77, 130, 20), (20000, 128, 256)])
+@pytest.mark.parametrize("M,P,Q", [(1000, 64, 48), (5000, 256, 128), (77, 130, 20), (20000, 128, 256),
+                                    (20000, 1024, 136), (20000, 512, 384)])
 def test_gemm_tn(dt, M, P, Q):
+    """Q = 128 / 384: the 256-tile bf16 kernel's waves 4-7 hold only padding in the (last)
+    Q tile and skip their MFMAs; Q = 136 keeps them live for 8 columns."""
     k = K()
     g = torch.Generator().manual_seed(M + P)
     tdt = torch.float32 if dt == "fp32" else torch.bfloat16

@@ -39,6 +39,35 @@ def test_philox_stream_layout():
         assert int(got[i]) == int(blk[i & 3][0])
 
 
+def test_dropout_code_and_keep_layout():
+    """dropout_keep (the device's drop_keep): 8-bit draws when p * 256 is an integer, else
+    16-bit with thr = ceil(p * 65536); element -> (block, word, byte/half) as documented,
+    checked element by element against philox4x32 for both widths; keep rates near 1 - p."""
+    assert O.dropout_code(0.5) == 0x80000000 | 128
+    assert O.dropout_code(0.25) == 0x80000000 | 64
+    assert O.dropout_code(0.3) == math.ceil(float(np.float32(0.3)) * 65536)
+    seed, stream, rows, n = 0xABCDEF12345, 3 * O.STREAMS_PER_STEP + 2, 3, 200
+    for p in (0.5, 0.3):
+        keep = O.dropout_keep(seed, stream, rows, n, p)
+        code = O.dropout_code(p)
+        thr = code & 0x7FFFFFFF
+        ng = (n + 63) // 64
+        for r in range(rows):
+            for c in range(0, n, 7):
+                grp = (r * ng + c // 64) * 4 + ((c >> 2) & 3)
+                if code >> 31:
+                    blk, word, sh, mk = grp, (c >> 4) & 3, 8 * (c & 3), 0xFF
+                else:
+                    blk, word, sh, mk = 2 * grp + ((c >> 5) & 1), ((c >> 4) & 1) * 2 + ((c >> 1) & 1), 16 * (c & 1), 0xFFFF
+                out = O.philox4x32(np.array([blk & 0xFFFFFFFF], np.uint32), np.array([blk >> 32], np.uint32),
+                                   np.array([stream & 0xFFFFFFFF], np.uint32), np.array([stream >> 32], np.uint32),
+                                   seed & 0xFFFFFFFF, seed >> 32)
+                assert bool(keep[r, c]) == (((int(out[word][0]) >> sh) & mk) >= thr)
+        big = O.dropout_keep(seed, stream, 512, 256, p)
+        assert abs(big.mean() - (1 - p)) < 0.01
+        assert np.array_equal(big, O.dropout_keep(seed, stream, 512, 256, p))
+
+
 def test_uniform_and_randint_index_are_exact():
     rng = np.random.default_rng(0)
     x = rng.integers(0, 2 ** 32, 20_000, dtype=np.uint64).astype(np.uint32)

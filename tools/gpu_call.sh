@@ -103,6 +103,14 @@ for RA in "$@"; do
         done
       done
       python tools/agg_ab_table.py $O/agg_ab.jsonl ;;
+    gemm-ab)        # tools/gemm_vs_blaslt.py (GEMM_ARGS) with the default library and each of $AB_LIBS, 2 rounds
+      for i in 1 2; do
+        for L in linkless-link-prediction_amd/libllp_hip.so ${AB_LIBS:-}; do
+          echo "# lib $L round $i" >> $O/gemm_ab.txt
+          LLP_LIB=$L timeout -k 10 240 python tools/gemm_vs_blaslt.py ${GEMM_ARGS:-} >> $O/gemm_ab.txt 2> $O/gemm_ab.err || fail gemm-ab $O/gemm_ab.err
+        done
+      done
+      cat $O/gemm_ab.txt ;;
     emulate8)       # rank 0's shard of the collab step at 8 ranks: bench line and kernel trace
       timeout -k 10 300 python bench.py --steps 20 --warmup 3 --emulate-ranks 8 > $O/emu8.json 2> $O/emu8.err || fail emu8 $O/emu8.err
       cat $O/emu8.json
