@@ -370,6 +370,9 @@ constexpr int EPI_PARTIAL = 6;
 // (drop_keep16, one or two Philox blocks per thread row) applied before the bf16 rounding,
 // and the ReLU mask of the dropped outputs; the values and bits of epilogue_t's dropout
 constexpr int EPI_FWD_DROP = 7;
+// EPI_HEAD_LEAN with dropout before the rounding, as EPI_FWD_DROP (pp8p only; the head dot is
+// over the staged dropped outputs, the lean head's rule)
+constexpr int EPI_HEAD_DROP = 8;
 
 // MASK_LDS (TMv 256, NTHR 512 only): the ReLU-backward bit mask of the tile (256 rows x
 // 32 bytes) is read with ONE 16-byte load per thread into LDS at smem + head_off_u4 + 256
@@ -1028,12 +1031,12 @@ constexpr int PP_STAGE_U4 = 128 * EPI_ROW_U4;          // one 128-row half of th
 template <int MODE>
 __global__ __launch_bounds__(NT2) void gemm_nt_bf16_pp8p(P256 p) {
   static_assert(MODE == EPI_FWD_RELU || MODE == EPI_FWD_NONE || MODE == EPI_BWD_MASK || MODE == EPI_HEAD_LEAN ||
-                    MODE == EPI_FWD_DROP,
+                    MODE == EPI_FWD_DROP || MODE == EPI_HEAD_DROP,
                 "lean modes only");
-  constexpr bool DROP = MODE == EPI_FWD_DROP;
-  constexpr bool RELU = MODE == EPI_FWD_RELU || DROP;
+  constexpr bool DROP = MODE == EPI_FWD_DROP || MODE == EPI_HEAD_DROP;
+  constexpr bool RELU = MODE == EPI_FWD_RELU || MODE == EPI_FWD_DROP;   // (the ReLU bit mask out)
   constexpr bool BWD = MODE == EPI_BWD_MASK;
-  constexpr bool HEAD = MODE == EPI_HEAD_LEAN;
+  constexpr bool HEAD = MODE == EPI_HEAD_LEAN || MODE == EPI_HEAD_DROP;
   constexpr int IMG_U4 = 256 * 8;
   constexpr int TILE_U4 = 2 * IMG_U4;
   constexpr int STG = TILE_U4;                          // staging half: [64 KB, 64 KB + 66 KB)
@@ -1568,7 +1571,18 @@ int llp_gemm_nt_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
       else
         hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_HEAD_RELU>), grid, block, 0, s, p);
       break;
-    default: hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_ANY>), grid, block, 0, s, p);
+    default:
+#ifndef LLP_GEMM_NO_PERSISTENT
+      // ReLU + dropout + fused head (the teacher predictor's hidden layer in training)
+      if (p.drop_p > 0.f && head_w && act == LLP_ACT_RELU && alpha == 1.f && !aux && !mask_in && !mask_out &&
+          N % TN == 0 && !((uintptr_t)head_w & 15) && (!C || (!(ldc & 7) && !((uintptr_t)C & 15))) &&
+          (!bias || !((uintptr_t)bias & 15)) && !A->idx && !B->idx && (K / TK) % 2 == 0 && tiles > 256) {
+        llp::note_kernel("gemm_nt_bf16_pp8p<EPI_HEAD_DROP> (persistent)");
+        hipLaunchKernelGGL((gemm_nt_bf16_pp8p<EPI_HEAD_DROP>), persistent_grid(tiles), block, 0, s, p);
+        break;
+      }
+#endif
+      hipLaunchKernelGGL((gemm_nt_bf16_pp8<EPI_ANY>), grid, block, 0, s, p);
   }
   return (int)hipGetLastError();
 }

@@ -309,7 +309,7 @@ __device__ __forceinline__ void glds16_s(uint32_t voff, const bf16_t* sbase, uin
                : "memory", "m0");
 }
 
-template <int STAG>
+template <int STAG, bool QH = false>
 __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE_T];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -384,11 +384,12 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
     for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
   const int q4 = li >> 2, pp = li & 3;
   const bool do_cs = p.ws_colsum != nullptr && q0 == 0 && wq == 0;
-  // waves 4-7 own the tile's columns q0 + 128 ..: with Q - q0 <= 128 (the first student layer's
-  // weight gradient at F = 128, the teacher's first layer) they hold only padding and skip their
-  // fragment reads and MFMAs, so each SIMD runs one wave's MFMAs (they still stage their DMA
-  // pieces and keep the barrier count)
-  const bool q_live = wq == 0 || q0 + 128 < p.Q;
+  // QH (Q <= 128: the first student layer's weight gradient at F = 128, the teacher's first
+  // layer): waves 4-7 own the tile's columns 128 .. 255, only padding, and skip their fragment
+  // reads and MFMAs, so each SIMD runs one wave's MFMAs (they still stage their DMA pieces and
+  // keep the barrier count).  A compile-time flag: a run-time test in the staggered body cost
+  // every TN launch ~2 % (the lean loop's steady body has no data-dependent branch)
+  constexpr bool q_live = !QH;
   float4_t accb[4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) accb[b] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -466,7 +467,10 @@ __global__ __launch_bounds__(NTT) void gemm_tn_bf16_256c(PTN p) {
       if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
       else if (st + NS - 1 < nsteps) issue(st + NS - 1);
     }
-    if (st > 0 && q_live) { mfma_half(0); mfma_half(1); }
+    if (st > 0 && q_live) {
+      mfma_half(0);
+      mfma_half(1);
+    }
     if (STAG == 2) {
       if (steady) issue_fast(st + NS - 1, (sl + NS - 1) % NS);
       else if (st + NS - 1 < nsteps) issue(st + NS - 1);
@@ -570,8 +574,14 @@ int llp_gemm_tn_bf16_256(const llp_operand* A, const llp_operand* B, int64_t M, 
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
   p.zmajor = 1;
   // the lean loop stages plain operands only; a gathered operand takes the staggered loop
-  if (!A->idx && !B->idx)
-    hipLaunchKernelGGL(gemm_tn_bf16_256c<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+  if (!A->idx && !B->idx && Q <= 128) {
+#ifndef LLP_TN_NO_PAD_SKIP
+    hipLaunchKernelGGL((gemm_tn_bf16_256c<2, true>), dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+#else   // A/B build: waves 4-7 compute their padding columns too
+    hipLaunchKernelGGL((gemm_tn_bf16_256c<2, false>), dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
+#endif
+  } else if (!A->idx && !B->idx)
+    hipLaunchKernelGGL((gemm_tn_bf16_256c<2, false>), dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   else
     hipLaunchKernelGGL(gemm_tn_bf16_256<2>, dim3((unsigned)(tiles * splits)), dim3(NTT), 0, s, p);
   return (int)hipGetLastError();

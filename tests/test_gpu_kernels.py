@@ -1298,6 +1298,38 @@ def test_gemm_nt_persistent_head_bit_identical(M, N, Kd, with_c):
     assert torch.allclose(h1.sum(0), ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item()))
 
 
+@pytest.mark.parametrize("with_c", [True, False])
+def test_gemm_nt_persistent_head_dropout(with_c):
+    """The teacher predictor's hidden layer in training (ReLU + dropout + fused Linear(N,1) head,
+    gemm_nt_bf16_pp8p<EPI_HEAD_DROP>) at p = 0.5: C is where(keep, 2 x the no-dropout head
+    GEMM's C, 0) bit for bit (keep = the oracle's dropout_keep), and the head partials sum to
+    that C times the head weights."""
+    k = K()
+    M, N, Kd = 131_072, 256, 256
+    g = torch.Generator().manual_seed(21)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV) * 0.1
+    hw = torch.randn(N, generator=g).to(DEV)
+    parts = k.head_parts(N)
+    R = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, R, hw, torch.empty(parts, M, device=DEV), bias=b,
+                   act=k.ACT_RELU)
+    ctr = torch.full((1,), 3, dtype=torch.int64, device=DEV)
+    D = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if with_c else None
+    h = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head(k.operand(A), k.operand(W), M, N, Kd, D, hw, h, bias=b, act=k.ACT_RELU,
+                   dropout=k.Dropout(0.5, 17, ctr.data_ptr(), 4))
+    assert "EPI_HEAD_DROP" in k.last_gemm_kernel()
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(O.dropout_keep(17, O.STREAMS_PER_STEP * 3 + 4, M, N, 0.5)).to(DEV)
+    exp = torch.where(keep, R.float() * 2.0, torch.zeros((), device=DEV)).to(torch.bfloat16)
+    if with_c:
+        assert torch.equal(D.view(torch.int16), exp.view(torch.int16))
+    ref = exp.float() @ hw
+    assert torch.allclose(h.sum(0), ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item()))
+
+
 def _mask_bits(m, N):
     sh = torch.arange(8, device=m.device, dtype=torch.int32)
     return ((m.to(torch.int32).unsqueeze(-1) >> sh) & 1).reshape(m.shape[0], N)
