@@ -641,12 +641,12 @@ extern "C" int llp_fullbatch_pairs(int64_t B, int64_t C1, const int32_t* samples
                                    const int32_t* perm, int64_t P, const int32_t* neg, int64_t ld_neg, int64_t n_neg,
                                    const int32_t* neg_count, int64_t neg_offset, int32_t* ia, int32_t* ib,
                                    void* stream) {
-  LLP_CHECK_ARG(ia && ib, "llp_fullbatch_pairs: null output");
   LLP_CHECK_ARG(B == 0 || (samples && C1 >= 2), "llp_fullbatch_pairs: null samples");
   LLP_CHECK_ARG(P == 0 || (pairs && perm), "llp_fullbatch_pairs: null pairs");
   LLP_CHECK_ARG(n_neg == 0 || neg, "llp_fullbatch_pairs: null negatives");
   const int64_t n = B * (C1 > 0 ? C1 - 1 : 0) + P + n_neg;
-  if (n == 0) return LLP_OK;
+  if (n == 0) return LLP_OK;   // an empty batch: nothing to write (the outputs may be empty tensors)
+  LLP_CHECK_ARG(ia && ib, "llp_fullbatch_pairs: null output");
   hipLaunchKernelGGL(fullbatch_pairs_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, B, C1,
                      samples, pairs, perm, P, neg, ld_neg, n_neg, neg_count, neg_offset, ia, ib);
   LLP_LAUNCH_CHECK();

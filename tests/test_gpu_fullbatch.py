@@ -377,3 +377,12 @@ def test_fullbatch_two_streams_bit_identical(dtype):
         for a, b in zip(ref[0], out[key][0]):
             assert torch.equal(a, b), key
         assert torch.equal(ref[1], out[key][1]), key
+
+
+def test_fullbatch_pairs_empty_batch():
+    """An empty batch (no anchors, no pairs, no negatives) writes nothing and is not an
+    error, with empty (possibly null-pointer) output tensors."""
+    K = _K()
+    e = torch.empty(0, dtype=torch.int32, device=DEV)
+    K.fullbatch_pairs(0, 0, None, None, None, 0, None, 0, e, e)
+    torch.cuda.synchronize()
