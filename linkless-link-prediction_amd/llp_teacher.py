@@ -152,6 +152,8 @@ class TeacherEngine(EngineBase):
                 P_, L = self.layers[l - 1], self.layers[l]
                 if L["F"] % 32 == 0 and (2 * P_["F"]) % 64 == 0 and (2 * L["O"]) % 64 == 0:
                     L["M"] = torch.empty(N, L["F"] // 8, dtype=torch.uint8, device=self.dev)
+        # SAGEConv's two weight gradients as one GEMM over [agg(x) | x] (False: two, the A/B baseline)
+        self.fused_wgrad = True
         self._agg0_done = False   # mean aggregate of the input features (first SAGEConv layer) formed
         self.out_dim = self.layers[-1]["O"]
         self.h = torch.empty(N, self.out_dim, dtype=dt, device=self.dev)
@@ -240,17 +242,28 @@ class TeacherEngine(EngineBase):
             # and the stored forward aggregate, so G is not formed there
             if l > 0 or self.updated:
                 K.csr_aggregate(N, O, g.rowptr_t, g.col_t, dOut, g.inv_deg, 1, G[:, :O])
-            wsb = K.gemm_tn_ws_bytes(dc, N, O, F)
-            ws = self._ws("ws_tn", wsb)
             if self.updated:
                 # U = x W_l^T + b is aggregated: dW_l = G^T x, db = colsum(G); dW_r = dOut^T x
+                ws = self._ws("ws_tn", K.gemm_tn_ws_bytes(dc, N, O, F))
                 K.gemm_tn(K.operand(G[:, :O]), K.operand(L["X"]), N, O, F, conv.lin_l.weight.grad, dc, ws,
                           colsum_a=conv.lin_l.bias.grad)
-            else:
-                # dW_l = dOut^T agg(x), db = colsum(dOut); dW_r = dOut^T x
+                K.gemm_tn(K.operand(dOut), K.operand(L["X"]), N, O, F, conv.lin_r.weight.grad, dc, ws)
+            elif not self.fused_wgrad:   # A/B: the two GEMMs of round 4
+                ws = self._ws("ws_tn", K.gemm_tn_ws_bytes(dc, N, O, F))
                 K.gemm_tn(K.operand(dOut), K.operand(L["XA"][:, :F]), N, O, F, conv.lin_l.weight.grad, dc, ws,
                           colsum_a=conv.lin_l.bias.grad)
-            K.gemm_tn(K.operand(dOut), K.operand(L["X"]), N, O, F, conv.lin_r.weight.grad, dc, ws)
+                K.gemm_tn(K.operand(dOut), K.operand(L["X"]), N, O, F, conv.lin_r.weight.grad, dc, ws)
+            else:
+                # dW_l = dOut^T agg(x), db = colsum(dOut); dW_r = dOut^T x: ONE weight-gradient GEMM over
+                # the layer's [agg(x) | x] (XA, the forward's K-concatenated operand), so dOut is read
+                # once and one launch + one slab reduce go (round 5); the [O, 2F] result is split
+                # into the two modules' gradients
+                ws = self._ws("ws_tn", K.gemm_tn_ws_bytes(dc, N, O, 2 * F))
+                dWc = self._buf("dWcat", (O, 2 * F), torch.float32)
+                K.gemm_tn(K.operand(dOut), K.operand(L["XA"]), N, O, 2 * F, dWc, dc, ws,
+                          colsum_a=conv.lin_l.bias.grad)
+                conv.lin_l.weight.grad.copy_(dWc[:, :F])
+                conv.lin_r.weight.grad.copy_(dWc[:, F:])
             if l > 0:
                 # dX = [G | dOut] . [W_l^T | W_r^T]^T, ReLU/dropout mask of layer l-1 in the epilogue,
                 # written straight into layer l-1's output-gradient slot

@@ -75,6 +75,8 @@ def main():
                          "launches each, in the printed order (rocprofv3 --pmc passes), then exit")
     ap.add_argument("--no-agg", action="store_true", help="only the teacher step (kernel traces of it)")
     ap.add_argument("--orders", default="id", help="--agg-only node orders, comma-separated: id, locality")
+    ap.add_argument("--no-fused-wgrad", action="store_true",
+                    help="A/B: SAGEConv's two weight gradients as two GEMMs (TeacherEngine.fused_wgrad = False)")
     opt = ap.parse_args()
     if opt.agg_only:
         return agg_only(opt.iters, tuple(opt.orders.split(",")))
@@ -109,15 +111,17 @@ def main():
     pred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.5).to(dev)
     optim = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=0.005)
     eng = llp_teacher.TeacherEngine(model, pred, data.x.to(dev), data.edge_index, N, optim, dtype=opt.dtype)
+    eng.fused_wgrad = not opt.no_fused_wgrad
     pairs = data.train_pairs.to(torch.int32).to(dev).contiguous()
     P = 64 * 1024
     perm = torch.randperm(pairs.shape[0], device=dev).to(torch.int32)
+    nb = max(1, pairs.shape[0] // P)   # full batches of one epoch, reused past it
     for i in range(2):
-        eng.step(perm[i * P:(i + 1) * P], pairs, dense_negatives=False)
+        eng.step(perm[(i % nb) * P:(i % nb + 1) * P], pairs, dense_negatives=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(opt.steps):
-        eng.step(perm[i * P:(i + 1) * P], pairs, dense_negatives=False)
+        eng.step(perm[(i % nb) * P:(i % nb + 1) * P], pairs, dense_negatives=False)
     torch.cuda.synchronize()
     dt_s = (time.perf_counter() - t0) / opt.steps
     res["teacher_step_ms"] = dt_s * 1e3
