@@ -234,8 +234,9 @@ class EngineBase:
         self.overlap_streams = True
         self._side = None
         # NT GEMM launches of at most this many 256 x 256 tiles run on the 128 x 128 kernel
-        # (llp_set_nt_small_tiles): the physics student's 7,761-row shard at 4 ranks (31 tiles)
-        self.nt_small_tiles = 64
+        # (llp_set_nt_small_tiles).  0: never -- at 64 the physics student's 7,761-row shard at 4
+        # ranks (31 tiles) ran 0.461 -> 0.501 ms per step (profiles/r05_nt_small_tiles_ab.txt)
+        self.nt_small_tiles = 0
         self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
 
     def _init_params(self, all_params, groups, optimizer):
