@@ -146,13 +146,11 @@ def emulated_rank(eng, node_perm, link_perm, pairs, B_full, P_full, n_full, C, R
         for s in range(3):
             step(s)
         ga, gl = (t.clone() for t in sh.batch(node_perm, link_perm, 3 % n_full))
-        g = eng.capture_minibatch(ga, gl, pairs, **sh.kw)
+        g = eng.capture_minibatch(ga, gl, pairs, batches=(node_perm, sh.B, sh.b0, link_perm, sh.P, sh.p0, n_full),
+                                  **sh.kw)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for s in range(steps):
-            an, li = sh.batch(node_perm, link_perm, (4 + s) % n_full)
-            ga.copy_(an)
-            gl.copy_(li)
             g.replay()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t1) / steps * 1e3
@@ -414,8 +412,8 @@ def physics_production_step(dtype):
             "ms_per_step_graph": r1g["ms_per_step"], "rank0_ms_per_step_at_4_ranks_graph": r4g["ms_per_step"],
             "sparse_first_layer": r1["sparse_first_layer"],
             "note": "eager steps with no host sync (the dense negatives' count stays on the device), and the same "
-                    "steps replayed from a hipGraph (capture_fullbatch); rank 0 of 4 runs its slice of the "
-                    "node-sharded student"}
+                    "steps replayed from a hipGraph (capture_fullbatch, which fills its own input batch from the "
+                    "epoch permutations: llp_batch_slices); rank 0 of 4 runs its slice of the node-sharded student"}
 
 
 def main():
@@ -519,10 +517,12 @@ def main():
         mark(f"warmup step {s}")
     graph = None
     if graph_on:
-        # persistent input slots, refilled before each replay (device-to-device copies)
+        # persistent input slots, filled inside the graph with batch j = step_ctr mod n_full of the epoch
+        # permutations (llp_batch_slices): the timed loop is replays only
         g_anchors, g_links = (t.clone() for t in sh.batch(node_perm, link_perm, 0))
+        batches = (node_perm, sh.B, sh.b0, link_perm, sh.P, sh.p0, n_full)
         try:
-            graph = eng.capture_minibatch(g_anchors, g_links, pairs, **sh.kw)
+            graph = eng.capture_minibatch(g_anchors, g_links, pairs, batches=batches, **sh.kw)
             mark("captured")
         except RuntimeError as e:   # keep the run alive: eager launches instead (reported as hipgraph: false)
             print(f"bench.py: hipGraph capture failed ({e}); timing eager steps", file=sys.stderr, flush=True)
@@ -536,9 +536,6 @@ def main():
     t0 = time.perf_counter()
     for s in range(opt.steps):
         if graph is not None:
-            an, li = sh.batch(node_perm, link_perm, (opt.warmup + s) % n_full)
-            g_anchors.copy_(an)
-            g_links.copy_(li)
             graph.replay()
             mark(f"replay {s}")
         else:

@@ -404,6 +404,16 @@ int llp_context_sampler(const int32_t* rowptr, const int32_t* col, int64_t num_n
 int llp_randint_pairs(int64_t num_nodes, int64_t n, int64_t n_total, int64_t offset, uint64_t seed,
                       const int64_t* step_ctr, int64_t stream_offset, int32_t* out, void* stream);
 
+/* The step's batch of two epoch permutations, read on the device so a replayed hipGraph
+ * feeds itself (DataLoader(range(E), P, shuffle=True) / node_perm slices, src/main.py:72-73,
+ * 168-170): out_a[i] = perm_a[j*stride_a + off_a + i] (i < n_a), out_b likewise, with
+ * j = (*step_ctr + ctr_offset) mod n_batches.  len_a / len_b: the permutations' lengths
+ * (every j < n_batches must stay inside them). */
+int llp_batch_slices(const int32_t* perm_a, int64_t stride_a, int64_t off_a, int64_t n_a,
+                     const int32_t* perm_b, int64_t stride_b, int64_t off_b, int64_t n_b,
+                     int64_t n_batches, int64_t len_a, int64_t len_b, const int64_t* step_ctr,
+                     int64_t ctr_offset, int32_t* out_a, int32_t* out_b, void* stream);
+
 /* Per-step index build for the minibatch layout (src/main.py:78,81-95):
  * pos edges = pairs[perm[*step_ctr*P_stride + i]] (i < P), neg edges =
  * neg[2, ld_neg] columns [0, n_neg) (randint: n_neg = P; PyG dense: may be fewer);

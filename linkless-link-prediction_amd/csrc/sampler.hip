@@ -168,6 +168,19 @@ __global__ void minibatch_sample_kernel(MbSample a) {
   }
 }
 
+// The j-th batch of an epoch's permutations, j = (*step_ctr + ctr_offset) mod n_batches
+// (llp_batch_slices): thread i < n_a copies perm_a[j stride_a + off_a + i], thread i < n_b perm_b's.
+__global__ void batch_slices_kernel(const int32_t* __restrict__ pa, int64_t sa, int64_t oa, int64_t na,
+                                    const int32_t* __restrict__ pb, int64_t sb, int64_t ob, int64_t nb,
+                                    int64_t n_batches, const int64_t* __restrict__ step_ctr, int64_t ctr_offset,
+                                    int32_t* __restrict__ out_a, int32_t* __restrict__ out_b) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t j = (*step_ctr + ctr_offset) % n_batches;
+  j = j < 0 ? j + n_batches : j;
+  if (i < na) out_a[i] = pa[j * sa + oa + i];
+  if (i < nb) out_b[i] = pb[j * sb + ob + i];
+}
+
 }  // namespace
 
 extern "C" int llp_minibatch_sample(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
@@ -265,6 +278,26 @@ extern "C" int llp_pair_index_from_samples(int64_t B, int64_t C, const int32_t* 
   if (B * C == 0) return LLP_OK;
   hipLaunchKernelGGL(pair_index_kernel, dim3(ceil_div_u(B * C, 256)), dim3(256), 0, (hipStream_t)stream, B, C,
                      samples, ia, ib);
+  LLP_LAUNCH_CHECK();
+  return LLP_OK;
+}
+
+extern "C" int llp_batch_slices(const int32_t* perm_a, int64_t stride_a, int64_t off_a, int64_t n_a,
+                                const int32_t* perm_b, int64_t stride_b, int64_t off_b, int64_t n_b,
+                                int64_t n_batches, int64_t len_a, int64_t len_b, const int64_t* step_ctr,
+                                int64_t ctr_offset, int32_t* out_a, int32_t* out_b, void* stream) {
+  LLP_CHECK_ARG(n_a >= 0 && n_b >= 0 && n_batches >= 1, "llp_batch_slices: bad sizes");
+  LLP_CHECK_ARG(step_ctr && (n_a == 0 || (perm_a && out_a)) && (n_b == 0 || (perm_b && out_b)),
+                "llp_batch_slices: null pointer");
+  // every batch j < n_batches must lie inside its permutation (len_a / len_b elements)
+  LLP_CHECK_ARG(n_a == 0 || (off_a >= 0 && stride_a >= 0 && (n_batches - 1) * stride_a + off_a + n_a <= len_a),
+                "llp_batch_slices: slice a past its permutation");
+  LLP_CHECK_ARG(n_b == 0 || (off_b >= 0 && stride_b >= 0 && (n_batches - 1) * stride_b + off_b + n_b <= len_b),
+                "llp_batch_slices: slice b past its permutation");
+  const int64_t n = n_a > n_b ? n_a : n_b;
+  if (n == 0) return LLP_OK;
+  hipLaunchKernelGGL(batch_slices_kernel, dim3(ceil_div_u(n, 256)), dim3(256), 0, (hipStream_t)stream, perm_a,
+                     stride_a, off_a, n_a, perm_b, stride_b, off_b, n_b, n_batches, step_ctr, ctr_offset, out_a, out_b);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
 }

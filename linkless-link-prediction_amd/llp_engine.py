@@ -1477,7 +1477,7 @@ class DistillEngine(EngineBase):
             part.copy_(t.view(self.world, *part.shape)[self.rank])
 
     def capture_minibatch(self, anchors, link_ids, pairs, segmented=None, debug_cuts=False, mode="thread_local",
-                          **kw):
+                          batches=None, **kw):
         """Capture one step_minibatch into a hipGraph (torch.cuda.CUDAGraph).
 
         ``anchors`` / ``link_ids`` must be persistent device buffers: refill them
@@ -1489,21 +1489,36 @@ class DistillEngine(EngineBase):
         all-reduces, which run eagerly between them at replay (_SegmentedGraph);
         the returned object has the same ``replay()``.  ``segmented=True`` takes the
         segmented capture on one rank too, ``debug_cuts`` adds a synchronising cut after
-        each stage, ``mode`` is the segments' capture mode (tests, tools/seg_diag.py)."""
-        return self._capture(lambda: self.step_minibatch(anchors, link_ids, pairs, **kw), segmented, debug_cuts,
-                             mode)
+        each stage, ``mode`` is the segments' capture mode (tests, tools/seg_diag.py).
+        ``batches = (node_perm, b_stride, b_offset, link_perm, p_stride, p_offset, n_batches)``: the
+        graph fills ``anchors`` / ``link_ids`` itself with the step's batch of those epoch
+        permutations, j = step_ctr mod n_batches (llp_batch_slices), so a replay needs no host
+        copy; refresh the permutation buffers in place once per epoch."""
+        fill = self._batch_fill(batches, anchors, link_ids)
+        return self._capture(lambda: (fill(), self.step_minibatch(anchors, link_ids, pairs, **kw))[1], segmented,
+                             debug_cuts, mode)
 
-    def capture_fullbatch(self, anchors, link_ids, pairs, segmented=None, mode="thread_local", **kw):
+    def _batch_fill(self, batches, anchors, link_ids):
+        if batches is None:
+            return lambda: None
+        node_perm, b_stride, b_off, link_perm, p_stride, p_off, n_batches = batches
+        return lambda: K.batch_slices(node_perm, b_stride, b_off, anchors, link_perm, p_stride, p_off, link_ids,
+                                      n_batches, self.step_ctr)
+
+    def capture_fullbatch(self, anchors, link_ids, pairs, segmented=None, mode="thread_local", batches=None, **kw):
         """Capture one step_fullbatch (train, src/main.py:167-235) into a hipGraph, as
         capture_minibatch does: persistent ``anchors`` / ``link_ids`` buffers, refilled
-        before each ``replay()``; segments between the collectives at several ranks.
+        before each ``replay()`` or by the graph itself (``batches``, capture_minibatch);
+        segments between the collectives at several ranks.
         The PyG-dense negatives keep their count on the device (step_fullbatch), so
         the step has no host read; KD_LM, whose kernel takes the host count, cannot
         be captured and raises here."""
         if float(self.args.KD_LM) != 0.0 and kw.get("dense_negatives", True) and kw.get("neg") is None:
             raise NotImplementedError("capture_fullbatch: KD_LM reads the dense negatives' count on the host; "
                                       "run the step eagerly")
-        return self._capture(lambda: self.step_fullbatch(anchors, link_ids, pairs, **kw), segmented, False, mode)
+        fill = self._batch_fill(batches, anchors, link_ids)
+        return self._capture(lambda: (fill(), self.step_fullbatch(anchors, link_ids, pairs, **kw))[1], segmented,
+                             False, mode)
 
     def _capture(self, step, segmented, debug_cuts, mode):
         if segmented is None:

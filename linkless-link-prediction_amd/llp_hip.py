@@ -59,6 +59,8 @@ _SIGS = {
     "llp_head_finish": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_gemm_nt_splitk_plan": (c_int, [c_i64, c_i64, c_i64]),
     "llp_set_nt_small_tiles": (c_i64, [c_i64]),
+    "llp_batch_slices": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
+                                 c_i64, c_vp, c_vp, c_vp]),
     "llp_gemm_nt_splitk_ws_bytes": (c_i64, [c_i64, c_i64, c_int]),
     "llp_gemm_nt_splitk": (c_int, [c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_vp,
                                    c_int, c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
@@ -691,6 +693,17 @@ def edge_table_build(edge_keys):
     t = torch.empty(int(L.llp_edge_table_size(n)), dtype=torch.int64, device=edge_keys.device)
     check(L.llp_edge_table_build(ptr(edge_keys), n, t.data_ptr(), t.numel(), stream_ptr()), "llp_edge_table_build")
     return t
+
+
+def batch_slices(perm_a, stride_a, off_a, out_a, perm_b, stride_b, off_b, out_b, n_batches, step_ctr,
+                 ctr_offset=0):
+    """llp_batch_slices: out_a = perm_a[j*stride_a + off_a :][:len(out_a)], out_b likewise, with
+    j = (step_ctr + ctr_offset) mod n_batches read on the device (a hipGraph feeds itself)."""
+    L = lib()
+    check(L.llp_batch_slices(ptr(perm_a), int(stride_a), int(off_a), out_a.numel(), ptr(perm_b), int(stride_b),
+                             int(off_b), out_b.numel(), int(n_batches), perm_a.numel(), perm_b.numel(),
+                             step_ctr.data_ptr(), int(ctr_offset), ptr(out_a), ptr(out_b), stream_ptr()),
+          "llp_batch_slices")
 
 
 def fullbatch_pairs(B, C1, samples, pairs, perm, P, neg, n_neg, ia, ib, neg_count=None, neg_offset=0):

@@ -386,3 +386,57 @@ def test_fullbatch_pairs_empty_batch():
     e = torch.empty(0, dtype=torch.int32, device=DEV)
     K.fullbatch_pairs(0, 0, None, None, None, 0, None, 0, e, e)
     torch.cuda.synchronize()
+
+
+def test_batch_slices_match_host_slicing():
+    """llp_batch_slices: batch j = (step_ctr + offset) mod n_batches of two permutations, read
+    on the device, equals the host slices perm[j*stride + off :][:n]; a slice past its
+    permutation is refused."""
+    K = _K()
+    g = torch.Generator().manual_seed(4)
+    pa = torch.randperm(1000, generator=g).to(torch.int32).to(DEV)
+    pb = torch.randperm(777, generator=g).to(torch.int32).to(DEV)
+    out_a = torch.empty(90, dtype=torch.int32, device=DEV)
+    out_b = torch.empty(64, dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for c in range(0, 23, 3):
+        ctr.fill_(c)
+        K.batch_slices(pa, 100, 7, out_a, pb, 70, 5, out_b, 10, ctr, ctr_offset=2)
+        torch.cuda.synchronize()
+        j = (c + 2) % 10
+        assert torch.equal(out_a, pa[j * 100 + 7: j * 100 + 7 + 90])
+        assert torch.equal(out_b, pb[j * 70 + 5: j * 70 + 5 + 64])
+    with pytest.raises(RuntimeError, match="past its permutation"):
+        K.batch_slices(pa, 100, 20, out_a, pb, 70, 5, out_b, 10, ctr)
+
+
+def test_fullbatch_graph_fills_its_own_batches():
+    """capture_fullbatch(batches=...): the graph fills its input batch from the epoch
+    permutations with llp_batch_slices (j = step_ctr mod n_batches), so replays need no host
+    copies; three replays give the parameters of eager steps on the same host slices, bit for bit."""
+    _K()
+    case = G.load_case("fullbatch_production_small")
+    st = case.steps[0]
+    node_perm = st.node_perm.to(torch.int32).to(DEV)
+    link_perm = st.link_perm.to(torch.int32).to(DEV)
+    B, P = node_perm.numel() // 2, link_perm.numel() // 2
+    out = {}
+    for graph in (False, True):
+        eng, model, pred = _engine(case, "bf16")
+        pairs = case.pos_train_edge.to(torch.int32).to(DEV).contiguous()
+        kw = dict(B_total=B, P_total=P)
+        eng.step_fullbatch(node_perm[:B].clone(), link_perm[:P].clone(), pairs, **kw)   # step 0
+        if graph:
+            a_buf, l_buf = node_perm[:B].clone(), link_perm[:P].clone()
+            g = eng.capture_fullbatch(a_buf, l_buf, pairs, batches=(node_perm, B, 0, link_perm, P, 0, 2), **kw)
+            for _ in range(3):
+                g.replay()
+        else:
+            for s in range(1, 4):
+                j = s % 2
+                eng.step_fullbatch(node_perm[j * B:(j + 1) * B].clone(), link_perm[j * P:(j + 1) * P].clone(), pairs,
+                                   **kw)
+        torch.cuda.synchronize()
+        out[graph] = [p.detach().cpu().clone() for p in list(model.parameters()) + list(pred.parameters())]
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)

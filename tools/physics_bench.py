@@ -55,7 +55,7 @@ def _hb_two_kernel(self, R, tgt, dZ, drow, h, out):
     K.segment_sum_rows(min(R2, N), seg_ptr, seg_rows, dh_rows, out, count=n_u, out_rows=uniq)
 
 
-def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False, sparse_input=True):
+def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False, sparse_input=True, host_slices=False):
     dev = torch.device("cuda", 0)
     a = physics_args()
     td = split[0]                                     # training_data: old nodes, old-old edges
@@ -97,16 +97,20 @@ def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False, s
     if graph:   # the step replayed from a hipGraph (capture_fullbatch), inputs refilled per replay
         g_a = torch.empty(b1 - b0, dtype=torch.int32, device=dev)
         g_l = torch.empty(p1 - p0, dtype=torch.int32, device=dev)
+        # the graph fills its inputs with batch j = step_ctr mod n_full (llp_batch_slices): no host copy
+        # per replay (--host-slices: two device-to-device copies before each replay, the round-4 loop)
+        batches = None if host_slices else (node_perm, B_full, b0, link_perm, P_full, p0, n_full)
         replay = eng.capture_fullbatch(g_a, g_l, pairs, b_offset=b0, p_offset=p0, B_total=B_full, P_total=P_full,
-                                       dense_negatives=True)
+                                       dense_negatives=True, batches=batches)
     torch.cuda.synchronize()
     eng.begin_epoch()
     t0 = time.perf_counter()
     for s in range(steps):
         if replay is not None:
-            j = (warmup + s) % n_full
-            g_a.copy_(node_perm[j * B_full + b0: j * B_full + b1])
-            g_l.copy_(link_perm[j * P_full + p0: j * P_full + p1])
+            if host_slices:
+                j = (warmup + s) % n_full
+                g_a.copy_(node_perm[j * B_full + b0: j * B_full + b1])
+                g_l.copy_(link_perm[j * P_full + p0: j * P_full + p1])
             replay.replay()
         else:
             step(warmup + s)
@@ -118,7 +122,8 @@ def run(dtype, steps, warmup, emulate, split, shard_student=True, graph=False, s
             "emulated_ranks": emulate or None, "fb_shard": eng.emulate_shard is not None, "N_old": N, "F": F, "E_train_directed": E, "anchors_per_step": B_full,
             "contexts_per_anchor": a.rw_step * a.hops * (1 + a.ns_rate), "edges_per_step": P_full,
             "steps_per_epoch": -(-E // P_full), "loss": loss, "hipgraph": replay is not None,
-            "host_issue_ms_per_step": t_issue * 1e3, "sparse_first_layer": eng.xs is not None}
+            "host_issue_ms_per_step": t_issue * 1e3, "sparse_first_layer": eng.xs is not None,
+            "batch_inputs": None if replay is None else ("host copies" if host_slices else "in-graph slices")}
 
 
 def main():
@@ -144,6 +149,9 @@ def main():
     ap.add_argument("--nt-small-tiles", type=int, default=None,
                     help="A/B: DistillEngine.nt_small_tiles (NT launches of <= this many 256-tiles on the 128-tile "
                          "kernel; 0 = always the 256-tile kernel)")
+    ap.add_argument("--host-slices", action="store_true",
+                    help="A/B (--graph): refill the graph's input batch by two copies before each replay instead "
+                         "of the in-graph llp_batch_slices")
     opt = ap.parse_args()
     if opt.nt_small_tiles is not None:
         _init_s = llp_engine.DistillEngine.__init__
@@ -171,7 +179,7 @@ def main():
            "split_s": prep, "runs": []}
     for dt in opt.dtype.split(","):
         out["runs"].append(run(dt, opt.steps, opt.warmup, opt.emulate_ranks, split, not opt.replicated,
-                               opt.graph, not opt.dense_input))
+                               opt.graph, not opt.dense_input, opt.host_slices))
         print(json.dumps(out["runs"][-1]), flush=True)
     print(json.dumps(out), flush=True)
 
