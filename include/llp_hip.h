@@ -99,11 +99,6 @@ int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K,
                 void* C, int64_t ldc, int c_dtype,
                 const float* bias, int act, const void* aux, int64_t ld_aux, int aux_dtype,
                 float alpha, const llp_dropout* dropout, void* stream);
-/* Dispatch knob of llp_gemm_nt (process-wide; returns the previous value): a bf16 launch
- * of at most max_tiles 256 x 256 tiles that writes no ReLU bit mask runs on the 128 x 128
- * kernel instead (four times the workgroups; its epilogue reads a RELU_BWD bit mask).
- * 0 (the default) = never.  The engine sets it around its own steps only. */
-int64_t llp_set_nt_small_tiles(int64_t max_tiles);
 
 /* bf16 GEMM with the LinkPredictor's last Linear(N, 1) fused into the epilogue
  * (src/models.py:143-146): y = act(alpha * A.B^T + bias) (+dropout) is stored to

@@ -65,8 +65,6 @@ struct NTParams {
   int64_t drop_stream;
   const int32_t* m_dev;  // device row count (llp_operand.rows_dev) or NULL
   int64_t ngroups;       // column groups walked one after another (nt_groups): B panel per XCD's L2
-  const uint8_t* mask_in;   // RELU_BWD through a ReLU bit mask (bit c & 7 of byte c >> 3 of the row), or NULL
-  int64_t ld_mask;
 };
 
 struct TNParams {
@@ -337,13 +335,9 @@ __global__ __launch_bounds__(64 * NW, BNT == BN ? 2 : 1) void gemm_nt_kernel(NTP
           // epilogues' sign-bit rule, so every bf16 kernel agrees
           v = p.c_bf16 ? (__float_as_int(v) < 0 ? 0.f : v) : (v < 0.f ? 0.f : v);
         } else if (p.act == LLP_ACT_RELU_BWD) {
-          if (p.mask_in) {
-            v = (p.mask_in[row * p.ld_mask + (col >> 3)] >> (col & 7)) & 1 ? v : 0.f;
-          } else {
-            const float a = p.aux_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p.aux)[row * p.ld_aux + col])
-                                       : reinterpret_cast<const float*>(p.aux)[row * p.ld_aux + col];
-            v = a > 0.f ? v : 0.f;
-          }
+          const float a = p.aux_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p.aux)[row * p.ld_aux + col])
+                                     : reinterpret_cast<const float*>(p.aux)[row * p.ld_aux + col];
+          v = a > 0.f ? v : 0.f;
         }
         if (p.drop_p > 0.f) {
           v = drop_keep(p.drop_thresh, p.drop_seed, dstream, row, col, p.N) ? v * p.drop_scale : 0.f;
@@ -671,14 +665,6 @@ static int64_t nt_groups(int64_t N, int64_t K, int es, int64_t tilesM) {
   return g;
 }
 
-// llp_set_nt_small_tiles: the 256-tile launches of at most this many tiles take the 128 x 128 kernel
-static int64_t g_nt_small_tiles = 0;
-extern "C" int64_t llp_set_nt_small_tiles(int64_t max_tiles) {
-  const int64_t old = g_nt_small_tiles;
-  g_nt_small_tiles = max_tiles < 0 ? 0 : max_tiles;
-  return old;
-}
-
 extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp_operand* A,
                            const llp_operand* B, void* C, int64_t ldc, int c_dtype, const float* bias,
                            int act, const void* aux, int64_t ld_aux, int aux_dtype, float alpha,
@@ -705,8 +691,6 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   p.drop_seed = 0;
   p.drop_ctr = nullptr;
   p.drop_stream = 0;
-  p.mask_in = nullptr;
-  p.ld_mask = 0;
   if (dropout && dropout->p > 0.f) {
     LLP_CHECK_ARG(dropout->p < 1.f && dropout->step_ctr, "llp_gemm_nt: dropout p in (0,1) needs step_ctr");
     p.drop_p = dropout->p;
@@ -719,15 +703,11 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   LLP_CHECK_ARG(tiles < (1ll << 31), "llp_gemm_nt: too many tiles");
   hipStream_t s = (hipStream_t)stream;
-  // Large-tile bf16 kernel (gemm256.hip) whenever the layout allows it -- unless the launch has
-  // at most llp_set_nt_small_tiles(..) 256 x 256 tiles (0: never, the default) and writes no ReLU
-  // bit mask: then the 128 x 128 kernel, four times the workgroups (a 7,761-row shard of the
-  // physics student runs on 31 of 256 CUs in 256 x 256 tiles)
+  // Large-tile bf16 kernel (gemm256.hip) whenever the layout allows it.  (Round 5 measured the
+  // 128 x 128 kernel for launches of <= 64 such tiles -- the physics student's 31-tile rank shard --
+  // and it was slower: DESIGN.md 4.5.)
   auto a16 = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && ((ld * 2) % 16 == 0); };
-  const int64_t tiles256 = ((M + 255) / 256) * ((N + 255) / 256);
-  const bool small = dtype == LLP_BF16 && c_dtype == LLP_BF16 && tiles256 <= g_nt_small_tiles &&
-                     !(mask && act == LLP_ACT_RELU);
-  if (dtype == LLP_BF16 && !small && c_dtype == LLP_BF16 && K > 0 && K % 64 == 0 && N % 8 == 0 && !B->ptr2 &&
+  if (dtype == LLP_BF16 && c_dtype == LLP_BF16 && K > 0 && K % 64 == 0 && N % 8 == 0 && !B->ptr2 &&
       a16(A->ptr, A->ld) && (!A->ptr2 || a16(A->ptr2, A->ld2)) && a16(B->ptr, B->ld) && a16(C, ldc) &&
       (act != LLP_ACT_RELU_BWD || mask || (aux_dtype == LLP_BF16 && a16(aux, ld_aux))) &&
       (!mask || (N % 32 == 0 && ld_aux % 4 == 0 && (uintptr_t)aux % 4 == 0))) {
@@ -739,14 +719,8 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
     if (rc != 0) return llp::set_error(rc, "llp_gemm_nt (256 tile): %s", hipGetErrorString((hipError_t)rc));
     return LLP_OK;
   }
-  LLP_CHECK_ARG(!mask || (small && act == LLP_ACT_RELU_BWD),
-                "llp_gemm_nt: bit-mask aux needs the bf16 256-tile path (bf16 in/out, K %% 64 == 0, "
-                "N %% 32 == 0, 16-byte aligned operands)");
-  if (mask) {   // the small-launch path reads the ReLU bit mask in its epilogue
-    p.mask_in = (const uint8_t*)aux;
-    p.ld_mask = ld_aux;
-    p.aux = nullptr;
-  }
+  LLP_CHECK_ARG(!mask, "llp_gemm_nt: bit-mask aux needs the bf16 256-tile path (bf16 in/out, K %% 64 == 0, "
+                       "N %% 32 == 0, 16-byte aligned operands)");
   const int es = dtype == LLP_BF16 ? 2 : 4;
   const bool vec = aligned_op(A, es, K) && aligned_op(B, es, K);
   p.ngroups = nt_groups(N, K, es, (M + BM - 1) / BM);

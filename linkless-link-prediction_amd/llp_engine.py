@@ -233,10 +233,6 @@ class EngineBase:
         # predictor forward, on a second stream (step_fullbatch); False: one stream
         self.overlap_streams = True
         self._side = None
-        # NT GEMM launches of at most this many 256 x 256 tiles run on the 128 x 128 kernel
-        # (llp_set_nt_small_tiles).  0: never -- at 64 the physics student's 7,761-row shard at 4
-        # ranks (31 tiles) ran 0.461 -> 0.501 ms per step (profiles/r05_nt_small_tiles_ab.txt)
-        self.nt_small_tiles = 0
         self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
 
     def _init_params(self, all_params, groups, optimizer):
@@ -742,10 +738,7 @@ class EngineBase:
             w.reset()
 
     def _guarded(self, step):
-        """Run one step; if it raises (outside a capture), reset the persistent device state.
-        The step's NT GEMMs of at most ``nt_small_tiles`` 256-tiles take the 128-tile kernel
-        (llp_set_nt_small_tiles, restored after the step)."""
-        old = K.set_nt_small_tiles(self.nt_small_tiles)
+        """Run one step; if it raises (outside a capture), reset the persistent device state."""
         try:
             return step()
         except BaseException:
@@ -756,8 +749,6 @@ class EngineBase:
                 except Exception:
                     pass
             raise
-        finally:
-            K.set_nt_small_tiles(old)
 
     # ------------------------------------------------------------------ epoch bookkeeping
     def begin_epoch(self):

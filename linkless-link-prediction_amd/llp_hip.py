@@ -58,7 +58,6 @@ _SIGS = {
                                  c_f32, C.POINTER(Dropout), c_vp, c_vp, c_vp]),
     "llp_head_finish": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_gemm_nt_splitk_plan": (c_int, [c_i64, c_i64, c_i64]),
-    "llp_set_nt_small_tiles": (c_i64, [c_i64]),
     "llp_batch_slices": (c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                                  c_i64, c_vp, c_vp, c_vp]),
     "llp_gemm_nt_splitk_ws_bytes": (c_i64, [c_i64, c_i64, c_int]),
@@ -253,12 +252,6 @@ def gemm_nt(A: Operand, B: Operand, M, N, K, C_out, dtype, bias=None, act=ACT_NO
 
 def head_parts(N):
     return load().llp_gemm_nt_head_parts(N)
-
-
-def set_nt_small_tiles(max_tiles: int) -> int:
-    """llp_set_nt_small_tiles: bf16 NT launches of <= max_tiles 256-tiles (no bit mask written)
-    take the 128 x 128 kernel; returns the previous value (0 = never, the default)."""
-    return load().llp_set_nt_small_tiles(int(max_tiles))
 
 
 def gemm_nt_splitk_plan(M, N, K):

@@ -1298,44 +1298,6 @@ def test_gemm_nt_persistent_head_bit_identical(M, N, Kd, with_c):
     assert torch.allclose(h1.sum(0), ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item()))
 
 
-@pytest.mark.parametrize("M,N,Kd", [(7_761, 256, 256), (7_761, 2_304, 1024), (300, 256, 64)])
-def test_gemm_nt_small_launch_128_tiles_bit_identical(M, N, Kd):
-    """llp_set_nt_small_tiles(64): bf16 launches of <= 64 256-tiles that write no bit mask run
-    on the 128 x 128 kernel (the physics student's rank shard).  Same MFMA k order and the same
-    epilogue rules, so bit-identical to the 256-tile kernel: bias (plain and ReLU), ReLU
-    backward through the bit mask (read in the 128-tile epilogue), a device row count."""
-    k = K()
-    g = torch.Generator().manual_seed(M + N + Kd)
-    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
-    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV, torch.bfloat16)
-    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
-    G = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
-    mask = torch.empty(M, N // 8, device=DEV, dtype=torch.uint8)
-    Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, Y, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=mask)
-    cnt = torch.tensor([M - 37], dtype=torch.int32, device=DEV)
-    outs = {}
-    for small in (0, 64):
-        old = k.set_nt_small_tiles(small)
-        try:
-            o1 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
-            k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, o1, k.LLP_BF16, bias=b)
-            n1 = k.last_gemm_kernel()
-            o2 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
-            k.gemm_nt(k.operand(A, count=cnt), k.operand(W), M, N, Kd, o2, k.LLP_BF16, bias=b, act=k.ACT_RELU)
-            o3 = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)   # masked by Y's ReLU bits
-            k.gemm_nt(k.operand(G), k.operand(W), M, N, Kd, o3, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=mask,
-                      alpha=2.0)
-        finally:
-            k.set_nt_small_tiles(old)
-        assert ("128x128" in n1) == (small > 0 and ((M + 255) // 256) * ((N + 255) // 256) <= 64), n1
-        outs[small] = (o1, o2, o3)
-    torch.cuda.synchronize()
-    for a, c in zip(outs[0], outs[64]):
-        assert torch.equal(a.view(torch.int16), c.view(torch.int16))
-    assert bool((outs[64][1][M - 37:] == 0).all())
-
-
 @pytest.mark.parametrize("with_c", [True, False])
 def test_gemm_nt_persistent_head_dropout(with_c):
     """The teacher predictor's hidden layer in training (ReLU + dropout + fused Linear(N,1) head,

@@ -146,20 +146,10 @@ def main():
                          "teacher after the student / predictor forward instead of beside them")
     ap.add_argument("--hb-two-kernel", action="store_true",
                     help="A/B: the round-3 two-kernel Hadamard backward (profiles/r03_hb_fused_fb_ab.txt)")
-    ap.add_argument("--nt-small-tiles", type=int, default=None,
-                    help="A/B: DistillEngine.nt_small_tiles (NT launches of <= this many 256-tiles on the 128-tile "
-                         "kernel; 0 = always the 256-tile kernel)")
     ap.add_argument("--host-slices", action="store_true",
                     help="A/B (--graph): refill the graph's input batch by two copies before each replay instead "
                          "of the in-graph llp_batch_slices")
     opt = ap.parse_args()
-    if opt.nt_small_tiles is not None:
-        _init_s = llp_engine.DistillEngine.__init__
-
-        def _init_small(self, *a, **kw):
-            _init_s(self, *a, **kw)
-            self.nt_small_tiles = opt.nt_small_tiles
-        llp_engine.DistillEngine.__init__ = _init_small
     if opt.no_edge_table:
         _nsd = llp_engine.K.neg_sample_dense
         llp_engine.K.neg_sample_dense = lambda *a, edge_table=None, **kw: _nsd(*a, **kw)
