@@ -665,6 +665,10 @@ static int64_t nt_groups(int64_t N, int64_t K, int es, int64_t tilesM) {
   return g;
 }
 
+int llp_gemm_nt_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, float* C,
+                        int64_t ldc, const float* bias, int act, const float* aux, int64_t ld_aux, float alpha,
+                        hipStream_t s);
+
 extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp_operand* A,
                            const llp_operand* B, void* C, int64_t ldc, int c_dtype, const float* bias,
                            int act, const void* aux, int64_t ld_aux, int aux_dtype, float alpha,
@@ -730,6 +734,22 @@ extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, true>), grid, dim3(NTHREADS), 0, s, p);
     else hipLaunchKernelGGL((gemm_nt_kernel<bf16_t, false>), grid, dim3(NTHREADS), 0, s, p);
   } else {
+#ifndef LLP_F32_NO_PP8
+    // the persistent 256 x 256 LDS-DMA f32 kernel (gemm256_f32.hip) for plain aligned operands,
+    // N % 256 == 0, K % 64 == 0, more than one wave of tiles, no dropout
+    auto a16f = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && (ld % 4 == 0); };
+    const int64_t tiles256 = ((M + 255) / 256) * (N / 256);
+    if (c_dtype == LLP_F32 && p.drop_p == 0.f && N % 256 == 0 && K > 0 && K % 64 == 0 && tiles256 > 256 &&
+        !A->idx && !A->ptr2 && !B->idx && !B->ptr2 && a16f(A->ptr, A->ld) && a16f(B->ptr, B->ld) && a16f(C, ldc) &&
+        (!bias || (uintptr_t)bias % 16 == 0) &&
+        (act == LLP_ACT_RELU || act == LLP_ACT_NONE ||
+         (act == LLP_ACT_RELU_BWD && aux_dtype == LLP_F32 && a16f(aux, ld_aux)))) {
+      llp::note_kernel("gemm_nt_f32_pp8p (persistent 256x256, LDS-DMA, v_mfma_f32_16x16x4_f32)");
+      const int rc = llp_gemm_nt_f32_256(A, B, M, N, K, (float*)C, ldc, bias, act, (const float*)aux, ld_aux, alpha, s);
+      if (rc != 0) return llp::set_error(rc, "llp_gemm_nt (f32 256 tile): %s", hipGetErrorString((hipError_t)rc));
+      return LLP_OK;
+    }
+#endif
     // eight waves per f32 tile (four per SIMD): 105.3 -> 97.5 ms per fp32 collab step, dominant
     // launch 4.28 -> 3.86 ms (profiles/r04_fp32_8w_ab.jsonl); bf16 keeps four (its 256 path rules)
 #ifdef LLP_F32_NT_WIDE   // A/B build: 128 x 256 f32 tiles on LLP_F32_NT_WIDE (8 or 16) waves

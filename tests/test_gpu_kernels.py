@@ -1169,6 +1169,60 @@ def _nt_sliced(k, A, W, M, N, Kd, dtype_code, slice_rows, **kw):
     return C
 
 
+@pytest.mark.parametrize("mode,M,N,Kd", [("relu", 70_000, 1024, 1024), ("none", 70_001, 512, 256),
+                                          ("bwd", 70_000, 1024, 1024), ("relu", 70_000, 256, 128),
+                                          ("none", 2_000, 9216, 256)])
+def test_gemm_nt_f32_persistent(mode, M, N, Kd):
+    """gemm_nt_f32_pp8p (the bf16 persistent kernel's LDS-DMA pipeline on f32 operands, launched
+    above 256 tiles) against the register-staged 128 x 128 f32 kernel on row slices of <= 256
+    tiles, and against a float64 reference: bias + ReLU (torch's NaN rule), plain, ReLU backward
+    through stored f32 activations with alpha 2; a partial last m-tile, a walk along one m-tile's
+    n-tiles (N = 9216) and a device row count."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N + Kd)
+    A = torch.randn(M, Kd, generator=g).to(DEV)
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    kw = {}
+    if mode == "relu":
+        kw = dict(bias=b, act=k.ACT_RELU)
+    elif mode == "none":
+        kw = dict(bias=b)
+    else:
+        Y = torch.relu(torch.randn(M, N, generator=g)).to(DEV)
+        kw = dict(act=k.ACT_RELU_BWD, aux=Y, alpha=2.0)
+    C1 = torch.empty(M, N, device=DEV)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C1, k.LLP_F32, **kw)
+    assert "f32_pp8p" in k.last_gemm_kernel(), k.last_gemm_kernel()
+    sl = min(64, 256 // (N // 256)) * 256
+    C2 = torch.empty(M, N, device=DEV)
+    aux = kw.pop("aux", None)
+    for s in range(0, M, sl):
+        e = min(M, s + sl)
+        k.gemm_nt(k.operand(A[s:e]), k.operand(W), e - s, N, Kd, C2[s:e], k.LLP_F32,
+                  aux=aux[s:e] if aux is not None else None, **kw)
+    assert "f32_pp8p" not in k.last_gemm_kernel()
+    torch.cuda.synchronize()
+    ref = A.double() @ W.double().t()
+    if mode == "bwd":
+        ref = 2.0 * ref * (aux.double() > 0)
+    else:
+        ref = ref + b.double()
+        if mode == "relu":
+            ref = torch.relu(ref)
+    scale = 1 + ref.abs().max().item()
+    assert (C1.double() - ref).abs().max().item() <= 2e-5 * scale
+    # the same k order per accumulator as the register-staged kernel
+    assert torch.equal(C1, C2)
+    if mode == "relu":   # device row count: rows past it untouched
+        cnt = torch.tensor([M - 300], dtype=torch.int32, device=DEV)
+        C3 = torch.full((M, N), 7.0, device=DEV)
+        k.gemm_nt(k.operand(A, count=cnt), k.operand(W), M, N, Kd, C3, k.LLP_F32, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(C3[:M - 300], C1[:M - 300])
+        assert bool((C3[M - 300:] == 7.0).all())
+
+
 @pytest.mark.parametrize("mode,M,N,Kd", [("relu_mask", 70_000, 1024, 1024), ("relu_mask", 70_000, 1024, 128),
                                           ("none", 70_001, 512, 256), ("bwd_mask", 70_000, 1024, 1024),
                                           ("relu", 70_000, 256, 1024), ("none", 2_000, 9216, 256)])
