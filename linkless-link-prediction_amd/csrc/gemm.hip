@@ -665,6 +665,9 @@ static int64_t nt_groups(int64_t N, int64_t K, int es, int64_t tilesM) {
   return g;
 }
 
+int64_t llp_gemm_tn_f32_256_splits(int64_t M, int64_t P, int64_t Q);
+int llp_gemm_tn_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t P, int64_t Q, float* ws,
+                        float* ws_colsum, int64_t splits, hipStream_t s);
 int llp_gemm_nt_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, float* C,
                         int64_t ldc, const float* bias, int act, const float* aux, int64_t ld_aux, float alpha,
                         hipStream_t s);
@@ -881,6 +884,7 @@ int colsum_rows_dev(int dtype, int64_t M, int64_t N, const void* Y, int64_t ldy,
 static int64_t tn_colsum_region(int dtype, int64_t M, int64_t P) {
   int64_t r = llp_colsum_workspace_bytes(M, P);
   if (dtype == LLP_BF16) r = std::max(r, llp_gemm_tn_256_splits(M, P, 256) * P * (int64_t)sizeof(float));
+  else r = std::max(r, llp_gemm_tn_f32_256_splits(M, P, 256) * P * (int64_t)sizeof(float));
   return r;
 }
 
@@ -892,6 +896,7 @@ static const int32_t* tn_rows_dev(const llp_operand* A, const llp_operand* B) {
 extern "C" int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, int64_t Q) {
   int64_t s = tn_splits(dtype, M, P, Q);
   if (dtype == LLP_BF16) s = std::max(s, llp_gemm_tn_256_splits(M, P, Q));
+  else s = std::max(s, llp_gemm_tn_f32_256_splits(M, P, Q));
   return s * P * Q * (int64_t)sizeof(float) + tn_colsum_region(dtype, M, P);
 }
 
@@ -920,6 +925,21 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     LLP_LAUNCH_CHECK();
     return LLP_OK;
   }
+#ifndef LLP_F32_NO_PP8
+  auto a16f = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && (ld % 4 == 0); };
+  if (dtype == LLP_F32 && P % 4 == 0 && Q % 4 == 0 && !A->idx && !A->ptr2 && !B->idx && !B->ptr2 &&
+      a16f(A->ptr, A->ld) && a16f(B->ptr, B->ld)) {
+    // the f32 256-tile LDS-DMA kernel (gemm256_tn_f32.hip), bias gradient fused
+    const int64_t sp = llp_gemm_tn_f32_256_splits(M, P, Q);
+    float* ws = reinterpret_cast<float*>(workspace);
+    float* wcs = colsum_a ? ws + sp * P * Q : nullptr;
+    const int rc = llp_gemm_tn_f32_256(A, B, M, P, Q, ws, wcs, sp, s);
+    if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (f32 256 tile): %s", hipGetErrorString((hipError_t)rc));
+    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s, wcs, colsum_a ? P : 0, colsum_a);
+    LLP_LAUNCH_CHECK();
+    return LLP_OK;
+  }
+#endif
   const int64_t splits = tn_splits(dtype, M, P, Q);
   if (colsum_a) {
     char* region = reinterpret_cast<char*>(workspace) + splits * P * Q * (int64_t)sizeof(float);

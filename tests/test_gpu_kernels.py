@@ -324,6 +324,30 @@ def test_gemm_tn(dt, M, P, Q):
     assert err <= (1e-4 if dt == "fp32" else 2e-3) * (1 + ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("M,P,Q,with_count", [(30_011, 1024, 1024, False), (4_099, 260, 132, True),
+                                               (225_384, 1024, 128, False)])
+def test_gemm_tn_f32_256(M, P, Q, with_count):
+    """The f32 256-tile TN kernel (gemm256_tn_f32.hip: LDS-DMA ring, ds_read_b32 fragments, the
+    bias gradient as ones-MFMAs) against float64: the weight gradient and the fused column sums,
+    a ragged last stage and P / Q not multiples of 256, a device row count."""
+    k = K()
+    g = torch.Generator().manual_seed(M + P + Q)
+    A = torch.randn(M, P, generator=g).to(DEV)
+    B = torch.randn(M, Q, generator=g).to(DEV)
+    cnt = torch.tensor([M - 77], dtype=torch.int32, device=DEV) if with_count else None
+    Ml = M - 77 if with_count else M
+    out = torch.empty(P, Q, device=DEV)
+    cs = torch.empty(P, device=DEV)
+    ws = torch.empty(k.gemm_tn_ws_bytes(k.LLP_F32, M, P, Q) // 4 + 16, device=DEV)
+    k.gemm_tn(k.operand(A, count=cnt), k.operand(B, count=cnt), M, P, Q, out, k.LLP_F32, ws, colsum_a=cs)
+    torch.cuda.synchronize()
+    ref = A[:Ml].double().t() @ B[:Ml].double()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 1e-4 * (1 + ref.abs().max().item()), err
+    refc = A[:Ml].double().sum(0)
+    assert (cs.double() - refc).abs().max().item() <= 1e-4 * (1 + refc.abs().max().item())
+
+
 def test_gemm_tn_gathered_hadamard_operand():
     k = K()
     g = torch.Generator().manual_seed(3)
