@@ -118,9 +118,13 @@ __global__ __launch_bounds__(NTT) void gemm_tn_f32_256(PTNF p) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = float4_t{0.f, 0.f, 0.f, 0.f};
   const bool do_cs = p.ws_colsum != nullptr && q0 == 0 && wq == 0;
-  float4_t accb[4];
+  // column sums in two levels: the ones-MFMAs accumulate 8 stages (128 rows) in accb_in, which is
+  // then added to accb.  One running sum over a split's ~37k rows (the predictor's bias
+  // gradients, sums that cancel to ~1e-5 of their terms) drifted 100x past the f32 reference's
+  // error in the full-size oracle test; the register-staged path summed 512-row blocks.
+  float4_t accb[4], accb_in[4];
 #pragma unroll
-  for (int b = 0; b < 4; ++b) accb[b] = float4_t{0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < 4; ++b) accb[b] = accb_in[b] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   // per-lane fragment offsets (bytes, slot 0, t = 0): A at (g, 64 wp + 16 ip + li), B at
   // (g, 128 wq + 16 jq + li).  Row 4 t + g has the parity of g, so step t adds 4 KiB and slot s
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(NTT) void gemm_tn_f32_256(PTNF p) {
   auto mfma_t = [&](int buf) {
     if (do_cs) {
 #pragma unroll
-      for (int ip = 0; ip < 4; ++ip) accb[ip] = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, fa[buf][ip], accb[ip], 0, 0, 0);
+      for (int ip = 0; ip < 4; ++ip) accb_in[ip] = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, fa[buf][ip], accb_in[ip], 0, 0, 0);
     }
 #pragma unroll
     for (int jq = 0; jq < 8; ++jq)
@@ -175,6 +179,13 @@ __global__ __launch_bounds__(NTT) void gemm_tn_f32_256(PTNF p) {
       mfma_t(0);
       mfma_t(1);
       __builtin_amdgcn_s_setprio(0);
+      if (do_cs && ((st & 7) == 7 || st + 1 == nsteps)) {
+#pragma unroll
+        for (int ip = 0; ip < 4; ++ip) {
+          accb[ip] += accb_in[ip];
+          accb_in[ip] = float4_t{0.f, 0.f, 0.f, 0.f};
+        }
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
