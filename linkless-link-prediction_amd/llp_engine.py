@@ -19,6 +19,7 @@ transposed copy, refreshed by the Adam kernel.
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 import math
 import os
@@ -232,6 +233,12 @@ class EngineBase:
         # full-batch step: the dense negatives beside the student forward and the frozen teacher beside the
         # predictor forward, on a second stream (step_fullbatch); False: one stream
         self.overlap_streams = True
+        # with overlap_streams (A/B switches, tools/physics_bench.py): the teacher and the node grouping
+        # start right after the pairs when no row-sharded student needs a collective first; the node
+        # grouping of the Hadamard backward runs on the side stream
+        self.early_pair_work = True
+        self.side_grouping = True
+        self.side_wgrad = True   # the full-batch student's small weight-gradient GEMMs beside the data gradients
         self._side = None
         self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
 
@@ -545,14 +552,16 @@ class EngineBase:
                 K.gemm_nt(K.operand(gcur), K.operand(lin.Wt), R2, lin.in_f, lin.out_f, gnext, dc)
         return gnext   # d(loss)/d(h[ia] * h[ib]), the input gradient of the first predictor layer
 
-    def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out):
+    def _hadamard_bwd_nodes(self, R, tgt, dZ, drow, h, out, grouped_in=False):
         """d(loss)/dh of the predictor input h[ia] * h[ib] into ``out`` [N, H] (compute dtype, or f32),
         deterministically: the 2R endpoint rows tgt = [ia | ib] are grouped by node
         (llp_dedup_rows2), and one pass per node (llp_hadamard_bwd_segments in the label-row
         layout, B = C = 0) forms each of its rows' gradient dZ[r] * h[partner] as the row
         kernel would store it and sums them in row order (f32) into its row of ``out``
         (drow: the 'inner' predictor's scalar); other rows are 0.  Bit-identical to
-        llp_hadamard_bwd_blocks + llp_segment_sum_rows without their [2R, H] row buffer."""
+        llp_hadamard_bwd_blocks + llp_segment_sum_rows without their [2R, H] row buffer.
+        grouped_in: the grouping (``_hadamard_group_nodes`` on the same R, tgt, out) already ran,
+        e.g. on the side stream beside the predictor (it needs only the pairs)."""
         N, H = self.N, h.shape[1]
         if not self._grouped_ok(H):
             # rows wider than the grouping kernels take: f32 scatter-add (atomics, so not
@@ -562,6 +571,20 @@ class EngineBase:
             K.hadamard_bwd_scatter(R, H, dZ, tgt[:R], tgt[R:], h, d32, drow=drow)
             out.copy_(d32)
             return
+        if not grouped_in:
+            self._hadamard_group_nodes(R, tgt, out)
+        R2 = 2 * R
+        K.hadamard_bwd_segments(min(R2, N), 0, 0, R, H, self._buf("hb_segp", (R2 + 1,), torch.int32),
+                                self._buf("hb_segr", (R2,), torch.int32), tgt, dZ, h, out, None, drow=drow,
+                                count=self._buf("hb_nu", (1,), torch.int32),
+                                out_rows=self._buf("hb_uniq", (R2,), torch.int32))
+
+    def _hadamard_group_nodes(self, R, tgt, out):
+        """The grouping half of ``_hadamard_bwd_nodes``: the 2R endpoint rows tgt = [ia | ib] by
+        node (llp_dedup_rows2: unique nodes, segments of rows in row order) and the rows of
+        ``out`` that no pair touches zeroed.  Reads only tgt; writes only its own buffers and
+        those rows of ``out``."""
+        N = self.N
         R2 = 2 * R
         uniq = self._buf("hb_uniq", (R2,), torch.int32)
         pos = self._buf("hb_pos", (R2,), torch.int32)
@@ -577,8 +600,6 @@ class EngineBase:
                       zero_rows=out if zfill else None)
         if not zfill:
             out.zero_()
-        K.hadamard_bwd_segments(min(R2, N), 0, 0, R, H, seg_ptr, seg_rows, tgt, dZ, h, out, None, drow=drow,
-                                count=n_u, out_rows=uniq)
 
     def _grouped_ok(self, H):
         """The node-grouped Hadamard-backward kernels (llp_hadamard_bwd_segments,
@@ -697,6 +718,11 @@ class EngineBase:
         # the one-launch Adam reads the step counter; the step-end launch advances it
         K.adam_step(self.descs_dev, self.n_desc, self.max_numel, self.sumsq, 1.0, float(g["lr"]), float(b1),
                     float(b2), float(g["eps"]), self.adam_step, fused=True, n_work=self.n_work_adam)
+
+    def _cu_count(self):
+        if getattr(self, "_cus", None) is None:
+            self._cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        return self._cus
 
     def _side_stream(self):
         """The engine's second HIP stream (created once): forks / joins with the current stream
@@ -1274,17 +1300,55 @@ class DistillEngine(EngineBase):
                               ia_ib[R2:], neg_count=cnt, neg_offset=p_offset)
             return n_neg, n_neg_total, cnt, R2, ia_ib
 
+        # d(loss)/dh: without KD_RM, the pair rows' Hadamard gradients are grouped by node and
+        # summed in row order (deterministic, straight into the compute-dtype buffer); with KD_RM
+        # (which adds at the anchors) they accumulate by f32 scatter-add, then convert
+        grouped = w_rm == 0.0 and self._grouped_ok(H)
+        shard = self._fb_shard(p_drop, grouped)
+        r0, n_rows, n_loc, s_world, s_rank = (0, N, N, 1, 0) if shard is None else shard
+        R_t_of = (lambda R2: R2 if w_lm != 0.0 else BC)
+        t_r = None
+        ev_t = None
+
+        def pair_work(R2, ia_ib, dh_out):
+            """a6 (the frozen teacher on the context pairs, src/main.py:187) and the node grouping of
+            the Hadamard backward: both need only the pairs.  On the side stream the loss waits for
+            the teacher (event ev_t) and the backward for the grouping (the stream's end)."""
+            nonlocal t_r, ev_t
+            R_t = R_t_of(R2)
+            t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
+            self._t_head = None
+            if R_t > 0:
+                self._teacher_forward(R_t, ia_ib[:R_t], ia_ib[R2:R2 + R_t], t_r, defer_head=R_t == BC)
+                if grouped and self.side_grouping:
+                    ev_t = torch.cuda.Event()
+                    ev_t.record(torch.cuda.current_stream(self.dev))
+            if grouped and self.side_grouping:
+                self._hadamard_group_nodes(R2, ia_ib, dh_out)
+            return self._t_head
+
+        def dh_target():   # where the per-node sums go: this rank's f32 rows of all nodes, or dh itself
+            return (self._buf("fb_dhfull", (s_world * n_loc, H), torch.float32)[:N] if shard is not None
+                    else self._buf("gS0", (N, H), dt))
+
         main = torch.cuda.current_stream(self.dev)
+        # without a row-sharded student (no collective before the backward) the teacher and the
+        # grouping follow the pairs on the side stream at once, beside the student forward; with
+        # one, they start after the all-gather (the streams are joined before a collective)
+        early = side is not None and shard is None and self.early_pair_work
+        ev_pairs = None
         if side is not None:
             side.wait_stream(main)               # the samples
             with torch.cuda.stream(side):
                 neg_res = negatives_and_pairs()
+                if early:
+                    ev_pairs = torch.cuda.Event()
+                    ev_pairs.record(side)
+                    t_head_early = pair_work(neg_res[3], neg_res[4], dh_target() if grouped else None)
 
         # ---- a4: student MLP over all nodes (src/main.py:173), queued before the dense negatives'
         # count is read back (one host sync), so the GPU runs it while the host waits; at several ranks each rank
         # runs it on its own slice of the nodes and the slices are all-gathered (_fb_shard)
-        shard = self._fb_shard(p_drop, float(a.KD_RM) == 0.0 and self._grouped_ok(H))
-        r0, n_rows, n_loc, s_world, s_rank = (0, N, N, 1, 0) if shard is None else shard
         x_loc = self.x if shard is None else self.x[r0:r0 + n_rows]
         acts = []
         A = K.operand(x_loc)
@@ -1319,7 +1383,9 @@ class DistillEngine(EngineBase):
                                    count=n_rows)
             acts.append(out)
             A = K.operand(out)
-        if side is not None:
+        if early:
+            main.wait_event(ev_pairs)            # the pairs (the side stream goes on)
+        elif side is not None:
             main.wait_stream(side)               # joined before any collective cut (graph segments)
         else:
             neg_res = negatives_and_pairs()
@@ -1335,22 +1401,28 @@ class DistillEngine(EngineBase):
             self._collective(lambda: self._all_gather_rows(h_full, h_loc, s_world, s_rank))
             h = h_full[:N]
 
-        # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215); it needs
-        # only the pairs, so with the side stream it runs beside the predictor forward
-        R_t = R2 if float(a.KD_LM) != 0.0 else BC
-        t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
-        self._t_head = None
-        if side is not None and R_t > 0:
+        # ---- a6: teacher on the context pairs (+ label pairs for KD_LM, src/main.py:187,215) and the
+        # node grouping: with the side stream beside the student forward (early) or the predictor forward
+        R_t = R_t_of(R2)
+        if early:
+            t_head = t_head_early
+        elif side is not None and (R_t > 0 or (grouped and self.side_grouping)):
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r, defer_head=R_t == BC)
-        t_head = self._t_head
+                t_head = pair_work(R2, ia_ib, dh_target() if grouped else None)
+        else:
+            t_r = self._buf("t_r", (max(R_t, 1),), torch.float32)
+            self._t_head = None
+            t_head = None
 
         # ---- a5: predictor over context + label pairs (src/main.py:186,213)
         logit = self._buf("logit", (R2,), torch.float32)
         A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop, defer_head=True)
         if side is not None and R_t > 0:
-            main.wait_stream(side)
+            if ev_t is not None:
+                main.wait_event(ev_t)            # the teacher (the grouping may still run)
+            else:
+                main.wait_stream(side)
             self._t_head = t_head
         elif R_t > 0:   # (KD_LM reads the label pairs' probabilities: finished here, not in the loss)
             self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r, defer_head=R_t == BC)
@@ -1363,10 +1435,6 @@ class DistillEngine(EngineBase):
                    float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws, neg_count=cnt,
                    neg_offset=p_offset, pos_total=P_total, s_head=self._s_head, t_head=self._t_head,
                    ticket=self.loss_ticket)
-        # d(loss)/dh: without KD_RM, the pair rows' Hadamard gradients are grouped by node and
-        # summed in row order (deterministic, straight into the compute-dtype buffer); with KD_RM
-        # (which adds at the anchors) they accumulate by f32 scatter-add, then convert
-        grouped = w_rm == 0.0 and self._grouped_ok(H)
         if not grouped:   # in fp32 mode dh32 IS the student backward's first gradient buffer
             dh32 = self._buf("gS0" if dt == torch.float32 else "dh32", (N, H), torch.float32)
             dh32.zero_()
@@ -1386,11 +1454,15 @@ class DistillEngine(EngineBase):
         # ---- a10: backward
         dZ0 = self._predictor_backward(dlogit, R2, A0, zacts, p_drop)
         mlp = self.predictor_kind == "mlp"
+        pre = side is not None and grouped and self.side_grouping
+        if side is not None:
+            main.wait_stream(side)               # the node grouping; every side branch joined
         if grouped and shard is not None:
             # every rank's d(h) over all nodes as unrounded f32 per-node sums, summed in f32
             # onto the owners' slices (reduce-scatter), then rounded once to the compute dtype
             dh_full = self._buf("fb_dhfull", (s_world * n_loc, H), torch.float32)
-            self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh_full[:N])
+            self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh_full[:N],
+                                     grouped_in=pre)
             if s_world * n_loc > N:
                 dh_full[N:].zero_()
             if dt == torch.float32:
@@ -1403,7 +1475,8 @@ class DistillEngine(EngineBase):
                 K.convert(dh32, dh)
         elif grouped:
             dh = self._buf("gS0", (N, H), dt)
-            self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh)
+            self._hadamard_bwd_nodes(R2, ia_ib, dZ0 if mlp else None, None if mlp else dlogit, h, dh,
+                                     grouped_in=pre)
         else:
             if mlp:
                 K.hadamard_bwd_scatter(R2, H, dZ0, ia, ib, h, dh32)
@@ -1416,7 +1489,8 @@ class DistillEngine(EngineBase):
                 K.convert(dh32, dh)
         sp = (r0, n_rows) if self.xs is not None and (p_drop == 0.0 or bool(self.stu_norms)) else None
         self._student_backward(dh, n_rows, None, acts, p_drop, x_rows=None if shard is None else x_loc,
-                               norm_count=n_rows, sparse_rows=sp)
+                               norm_count=n_rows, sparse_rows=sp,
+                               side=self._side_stream() if self.overlap_streams and self.side_wgrad else None)
         self._allreduce_and_update()
         K.step_end(self.terms[:1], float(P_total), self.loss_sum, self.step_ctr, adam_step=self.adam_step)
         return n_neg if cnt is None else cnt
@@ -1575,7 +1649,7 @@ class DistillEngine(EngineBase):
         K.head_fwd(out, R, out.shape[1], w, b, prob=t_r)
 
     def _student_backward(self, dh, R1, target, acts, p_drop, count=None, x_rows=None, norm_count=0.0,
-                          norm_sync=False, sparse_rows=None):
+                          norm_sync=False, sparse_rows=None, side=None):
         """count: int32 device row count (unique-node student) or None.  dh lives in
         buffer 'gS0'.  x_rows: x[target] materialised by the forward (else the first
         layer's input is gathered).  norm_count / norm_sync: BatchNorm's batch row count
@@ -1602,12 +1676,22 @@ class DistillEngine(EngineBase):
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
             dW = self._buf("dW_pad", (lin.out_f, lin.k_in), torch.float32) if padded else lin.lin.weight.grad
-            K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc, self._ws("ws_tn", wsb),
-                      colsum_a=lin.lin.bias.grad)
-            if padded:   # the zero-padded input columns' gradient is dropped
-                lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
+            # a data-gradient GEMM of at most half a wave of tiles (the full-batch student at small
+            # shards: 31-122 tiles) leaves most CUs idle: the weight gradient runs beside it on the
+            # side stream (both only read gcur and the activations)
+            par = (side is not None and l > 0 and not self.stu_norms
+                   and -(-R1 // 256) * -(-lin.in_f // 256) <= self._cu_count() // 2)
+            if par:
+                main = torch.cuda.current_stream(self.dev)
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if par else contextlib.nullcontext():
+                K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc, self._ws("ws_tn", wsb),
+                          colsum_a=lin.lin.bias.grad)
+                if padded:   # the zero-padded input columns' gradient is dropped
+                    lin.lin.weight.grad.copy_(dW[:, :lin.in_f])
             if l > 0:    # this layer's gradients are final: all-reduce them under the next layers' GEMMs
-                self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))
+                if not par:
+                    self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))
                 k += 1
                 gnext = self._buf(names[k % 2], (R1, lin.in_f), dt)
                 if self.stu_norms:
@@ -1620,3 +1704,6 @@ class DistillEngine(EngineBase):
                 else:
                     K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
                               act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)
+                if par:   # joined before the bucket's all-reduce reads the weight gradient
+                    main.wait_stream(side)
+                    self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))

@@ -36,7 +36,7 @@ def physics_args():
                                  hidden_channels=256, num_layers=2, link_batch_size=64 * 1024, predictor="mlp")
 
 
-def _hb_two_kernel(self, R, tgt, dZ, drow, h, out):
+def _hb_two_kernel(self, R, tgt, dZ, drow, h, out, grouped_in=False):
     """A/B (--hb-two-kernel): the round-3 Hadamard backward of DistillEngine._hadamard_bwd_nodes,
     the row kernel writing a [2R, H] buffer, then the per-node segment sum."""
     K = llp_engine.K
@@ -146,6 +146,15 @@ def main():
                          "teacher after the student / predictor forward instead of beside them")
     ap.add_argument("--hb-two-kernel", action="store_true",
                     help="A/B: the round-3 two-kernel Hadamard backward (profiles/r03_hb_fused_fb_ab.txt)")
+    ap.add_argument("--late-pairs", action="store_true",
+                    help="A/B (two streams): the frozen teacher and the node grouping start after the student "
+                         "forward (DistillEngine.early_pair_work = False), as with a row-sharded student")
+    ap.add_argument("--main-grouping", action="store_true",
+                    help="A/B (two streams): the Hadamard backward's node grouping on the main stream, before "
+                         "its per-node sums (DistillEngine.side_grouping = False)")
+    ap.add_argument("--main-wgrad", action="store_true",
+                    help="A/B (two streams): the student's small weight-gradient GEMMs on the main stream before "
+                         "the data gradients (DistillEngine.side_wgrad = False)")
     ap.add_argument("--host-slices", action="store_true",
                     help="A/B (--graph): refill the graph's input batch by two copies before each replay instead "
                          "of the in-graph llp_batch_slices")
@@ -155,13 +164,16 @@ def main():
         llp_engine.K.neg_sample_dense = lambda *a, edge_table=None, **kw: _nsd(*a, **kw)
     if opt.hb_two_kernel:
         llp_engine.DistillEngine._hadamard_bwd_nodes = _hb_two_kernel
-    if opt.no_overlap:
+    if opt.no_overlap or opt.late_pairs or opt.main_grouping or opt.main_wgrad or opt.hb_two_kernel:
         _init = llp_engine.DistillEngine.__init__
 
-        def _init_one_stream(self, *a, **kw):
+        def _init_switches(self, *a, **kw):
             _init(self, *a, **kw)
-            self.overlap_streams = False
-        llp_engine.DistillEngine.__init__ = _init_one_stream
+            self.overlap_streams = not opt.no_overlap
+            self.early_pair_work = not opt.late_pairs
+            self.side_grouping = not (opt.main_grouping or opt.hb_two_kernel)
+            self.side_wgrad = not opt.main_wgrad
+        llp_engine.DistillEngine.__init__ = _init_switches
     t0 = time.perf_counter()
     split = llp_split.production_split("coauthor-physics", opt.data_dir, synthetic=True)
     prep = time.perf_counter() - t0
