@@ -223,33 +223,50 @@ __global__ __launch_bounds__(FNT) void gemm_nt_f32_pp8p(PF32 p) {
     const float* __restrict__ aux = p.aux;
     float* __restrict__ C = p.C;
     const float alpha = p.alpha;
+    // column blocks jn = 2 jp, 2 jp + 1 are the two 64-B halves of one 128-B line of each row: the
+    // two stores of a line go out back to back, so L2 merges them into one full-line write
+    // (jn-outer order left them 8 stores apart and counted 1.55x the C bytes in WRITE_SIZE)
 #pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      const int cl = ewn * 64 + jn * 16 + eg * 4;
-      const int64_t col = n0 + cl;
-      const float4_t bv = (!BWD && p.bias) ? *reinterpret_cast<const float4_t*>(blds + cl) : float4_t{0.f, 0.f, 0.f, 0.f};
-      // the ReLU-backward activations of this column quad's 8 rows, loaded together (one wait,
-      // not one round trip per row); rows past M read the last live row and are not stored
-      float4_t av[8];
-      if (BWD) {
+    for (int jp = 0; jp < 2; ++jp) {
+      float4_t bv[2];
 #pragma unroll
-        for (int im = 0; im < 8; ++im) {
-          const int64_t row = min(m0 + ewm * 128 + im * 16 + eli, p.M - 1);
-          av[im] = *reinterpret_cast<const float4_t*>(aux + row * p.ld_aux + col);
+      for (int q = 0; q < 2; ++q)
+        bv[q] = (!BWD && p.bias) ? *reinterpret_cast<const float4_t*>(blds + ewn * 64 + (2 * jp + q) * 16 + eg * 4)
+                                 : float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {
+        // the ReLU-backward activations of these 4 rows x 2 column quads, loaded together (one
+        // wait, not one round trip per row); rows past M read the last live row and are not stored
+        float4_t av[4][2];
+        if (BWD) {
+#pragma unroll
+          for (int iq = 0; iq < 4; ++iq)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int64_t row = min(m0 + ewm * 128 + (4 * ih + iq) * 16 + eli, p.M - 1);
+              const int64_t col = n0 + ewn * 64 + (2 * jp + q) * 16 + eg * 4;
+              av[iq][q] = *reinterpret_cast<const float4_t*>(aux + row * p.ld_aux + col);
+            }
         }
-      }
 #pragma unroll
-      for (int im = 0; im < 8; ++im) {
-        const int64_t row = m0 + ewm * 128 + im * 16 + eli;
-        float4_t v;
+        for (int iq = 0; iq < 4; ++iq) {
+          const int im = 4 * ih + iq;
+          const int64_t row = m0 + ewm * 128 + im * 16 + eli;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = alpha * acc[jn][im][r] + bv[r];
-          if (MODE == F32_RELU) x = x < 0.f ? 0.f : x;   // torch.relu: a NaN stays NaN
-          if (BWD) x = av[im][r] > 0.f ? x : 0.f;
-          v[r] = x;
+          for (int q = 0; q < 2; ++q) {
+            const int jn = 2 * jp + q;
+            const int64_t col = n0 + ewn * 64 + jn * 16 + eg * 4;
+            float4_t v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = alpha * acc[jn][im][r] + bv[q][r];
+              if (MODE == F32_RELU) x = x < 0.f ? 0.f : x;   // torch.relu: a NaN stays NaN
+              if (BWD) x = av[iq][q][r] > 0.f ? x : 0.f;
+              v[r] = x;
+            }
+            if (row < p.M) *reinterpret_cast<float4_t*>(C + row * p.ldc + col) = v;
+          }
         }
-        if (row < p.M) *reinterpret_cast<float4_t*>(C + row * p.ldc + col) = v;
       }
     }
     if (!pf) return;

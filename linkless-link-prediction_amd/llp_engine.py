@@ -238,6 +238,7 @@ class EngineBase:
         # grouping of the Hadamard backward runs on the side stream
         self.early_pair_work = True
         self.side_grouping = True
+        self.side_sampling = True   # the context sampler on the side stream, before the negatives
         self.side_wgrad = True   # the full-batch student's small weight-gradient GEMMs beside the data gradients
         self._side = None
         self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
@@ -1273,14 +1274,16 @@ class DistillEngine(EngineBase):
         p_drop = float(a.dropout)
 
         # ---- samples (src/main.py:180-183)
-        samp = None
-        if use_llp:
+        def sample():
+            if not use_llp:
+                return None
             samp = self._buf("samples", (B, C1), torch.int32)
             if samples is not None:
                 samp.copy_(samples.to(torch.int32))
             else:
                 K.context_sampler(self.rowptr, self.col, N, anchors, B, a.ps_method, rw_step, hops, ns_rate,
                                   self.seed, self.step_ctr, 0, samp, b_offset=b_offset)
+            return samp
         # ---- negatives (src/main.py:205-209) and the pair index.  PyG-dense ones keep their count on
         # the device (label slots past it inert, no host read, so the step is graph-capturable) unless
         # KD_LM, whose kernel takes the host count, needs it.  Without a host read they run on a side
@@ -1290,6 +1293,8 @@ class DistillEngine(EngineBase):
         BC = Bc * C
         side = self._side_stream() if (self.overlap_streams and dense_negatives and neg is None and w_lm == 0.0) \
             else None
+        side_samp = side is not None and self.side_sampling
+        samp = None if side_samp else sample()      # (with the side stream: sampled there, first)
 
         def negatives_and_pairs():
             negb, n_neg, n_neg_total, cnt = self._negatives(P, P_total, p_offset, neg, dense_negatives,
@@ -1338,8 +1343,12 @@ class DistillEngine(EngineBase):
         early = side is not None and shard is None and self.early_pair_work
         ev_pairs = None
         if side is not None:
-            side.wait_stream(main)               # the samples
+            # the samples, the negatives and the pairs need only the step's inputs: on the side
+            # stream from the step's start, while the main stream runs the student forward
+            side.wait_stream(main)
             with torch.cuda.stream(side):
+                if side_samp:
+                    samp = sample()
                 neg_res = negatives_and_pairs()
                 if early:
                     ev_pairs = torch.cuda.Event()
@@ -1670,8 +1679,15 @@ class DistillEngine(EngineBase):
             else:
                 A_in = K.operand(self.x, target, count=count)
             if l == 0 and sparse_rows is not None:
+                if side is not None:   # the bias gradient's column sums beside the sparse weight gradient
+                    main = torch.cuda.current_stream(self.dev)
+                    side.wait_stream(main)
+                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    K.colsum(gcur, R1, lin.out_f, lin.lin.bias.grad,
+                             self._ws("ws_colsum", K.colsum_ws_bytes(R1, lin.out_f)))
                 K.spmm_tn(self.xs, sparse_rows[0], sparse_rows[1], gcur, lin.lin.weight.grad)
-                K.colsum(gcur, R1, lin.out_f, lin.lin.bias.grad, self._ws("ws_colsum", K.colsum_ws_bytes(R1, lin.out_f)))
+                if side is not None:
+                    main.wait_stream(side)
                 continue
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f

@@ -349,8 +349,8 @@ def test_fullbatch_graph_replay_matches_eager(dtype):
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_fullbatch_two_streams_bit_identical(dtype):
-    """DistillEngine.overlap_streams (the default): the dense negatives run beside the student
-    forward, the frozen teacher beside the predictor forward and the node grouping of the Hadamard
+    """DistillEngine.overlap_streams (the default): the context sampler and the dense negatives run
+    beside the student forward, the frozen teacher beside the predictor forward and the node grouping of the Hadamard
     backward beside the predictor and the loss, and the student's small weight-gradient GEMMs beside
     its data-gradient GEMMs, on a second stream.  Two steps
     give the one-stream engine's loss terms and parameters bit for bit, eagerly and from a

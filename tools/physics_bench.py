@@ -152,6 +152,9 @@ def main():
     ap.add_argument("--main-grouping", action="store_true",
                     help="A/B (two streams): the Hadamard backward's node grouping on the main stream, before "
                          "its per-node sums (DistillEngine.side_grouping = False)")
+    ap.add_argument("--main-sampler", action="store_true",
+                    help="A/B (two streams): the context sampler on the main stream before the student forward "
+                         "(DistillEngine.side_sampling = False)")
     ap.add_argument("--main-wgrad", action="store_true",
                     help="A/B (two streams): the student's small weight-gradient GEMMs on the main stream before "
                          "the data gradients (DistillEngine.side_wgrad = False)")
@@ -164,7 +167,7 @@ def main():
         llp_engine.K.neg_sample_dense = lambda *a, edge_table=None, **kw: _nsd(*a, **kw)
     if opt.hb_two_kernel:
         llp_engine.DistillEngine._hadamard_bwd_nodes = _hb_two_kernel
-    if opt.no_overlap or opt.late_pairs or opt.main_grouping or opt.main_wgrad or opt.hb_two_kernel:
+    if opt.no_overlap or opt.late_pairs or opt.main_grouping or opt.main_wgrad or opt.main_sampler or opt.hb_two_kernel:
         _init = llp_engine.DistillEngine.__init__
 
         def _init_switches(self, *a, **kw):
@@ -173,6 +176,7 @@ def main():
             self.early_pair_work = not opt.late_pairs
             self.side_grouping = not (opt.main_grouping or opt.hb_two_kernel)
             self.side_wgrad = not opt.main_wgrad
+            self.side_sampling = not opt.main_sampler
         llp_engine.DistillEngine.__init__ = _init_switches
     t0 = time.perf_counter()
     split = llp_split.production_split("coauthor-physics", opt.data_dir, synthetic=True)
