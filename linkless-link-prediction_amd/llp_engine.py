@@ -241,6 +241,8 @@ class EngineBase:
         self.side_sampling = True   # the context sampler on the side stream, before the negatives
         self.side_wgrad = True   # the full-batch student's small weight-gradient GEMMs beside the data gradients
         self._side = None
+        self._side_open = False   # work forked onto the side stream since its last join
+        self._cut_gen = 0         # segment cuts so far (events from an earlier segment are not waited on)
         self.emulate_pairs = None   # (rank, world): time one rank's owner-decomposed minibatch step
 
     def _init_params(self, all_params, groups, optimizer):
@@ -688,7 +690,12 @@ class EngineBase:
         if self._seg is None:
             fn()
         else:
+            # a segment cannot end with side-stream work unjoined: join it here (the segments
+            # then run it before the collective; the later joins and event waits see it done)
+            if self._side_open:
+                self._join(self._side)
             self._seg.cut(fn)
+            self._cut_gen += 1
 
     def _dbg_cut(self, what):
         """capture_minibatch(debug_cuts=True): one more segment cut here, whose eager step
@@ -724,6 +731,31 @@ class EngineBase:
         if getattr(self, "_cus", None) is None:
             self._cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
         return self._cus
+
+    def _fork(self, side):
+        """The side stream continues from here (stream order of the current stream)."""
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        self._side_open = True
+
+    def _join(self, side):
+        """The current stream waits for everything forked onto the side stream."""
+        if self._side_open:
+            torch.cuda.current_stream(self.dev).wait_stream(side)
+            self._side_open = False
+
+    def _side_event(self, side):
+        """An event at the side stream's current point, waited on by ``_wait_side``."""
+        ev = torch.cuda.Event()
+        ev.record(side)
+        return ev, self._cut_gen
+
+    def _wait_side(self, evg):
+        """The current stream waits for the side stream's work up to the event.  Not needed
+        (and, in a segmented capture, not legal) once the side stream was joined at a
+        collective's segment cut since the event was recorded."""
+        ev, gen = evg
+        if self._side_open and gen == self._cut_gen:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
 
     def _side_stream(self):
         """The engine's second HIP stream (created once): forks / joins with the current stream
@@ -1326,8 +1358,7 @@ class DistillEngine(EngineBase):
             if R_t > 0:
                 self._teacher_forward(R_t, ia_ib[:R_t], ia_ib[R2:R2 + R_t], t_r, defer_head=R_t == BC)
                 if grouped and self.side_grouping:
-                    ev_t = torch.cuda.Event()
-                    ev_t.record(torch.cuda.current_stream(self.dev))
+                    ev_t = self._side_event(side)
             if grouped and self.side_grouping:
                 self._hadamard_group_nodes(R2, ia_ib, dh_out)
             return self._t_head
@@ -1345,14 +1376,13 @@ class DistillEngine(EngineBase):
         if side is not None:
             # the samples, the negatives and the pairs need only the step's inputs: on the side
             # stream from the step's start, while the main stream runs the student forward
-            side.wait_stream(main)
+            self._fork(side)
             with torch.cuda.stream(side):
                 if side_samp:
                     samp = sample()
                 neg_res = negatives_and_pairs()
                 if early:
-                    ev_pairs = torch.cuda.Event()
-                    ev_pairs.record(side)
+                    ev_pairs = self._side_event(side)
                     t_head_early = pair_work(neg_res[3], neg_res[4], dh_target() if grouped else None)
 
         # ---- a4: student MLP over all nodes (src/main.py:173), queued before the dense negatives'
@@ -1393,9 +1423,9 @@ class DistillEngine(EngineBase):
             acts.append(out)
             A = K.operand(out)
         if early:
-            main.wait_event(ev_pairs)            # the pairs (the side stream goes on)
+            self._wait_side(ev_pairs)            # the pairs (the side stream goes on)
         elif side is not None:
-            main.wait_stream(side)               # joined before any collective cut (graph segments)
+            self._join(side)                     # joined before any collective cut (graph segments)
         else:
             neg_res = negatives_and_pairs()
         n_neg, n_neg_total, cnt, R2, ia_ib = neg_res
@@ -1416,7 +1446,7 @@ class DistillEngine(EngineBase):
         if early:
             t_head = t_head_early
         elif side is not None and (R_t > 0 or (grouped and self.side_grouping)):
-            side.wait_stream(main)
+            self._fork(side)
             with torch.cuda.stream(side):
                 t_head = pair_work(R2, ia_ib, dh_target() if grouped else None)
         else:
@@ -1429,9 +1459,9 @@ class DistillEngine(EngineBase):
         A0, zacts = self._predictor_forward(h, ia, ib, R2, logit, p_drop, defer_head=True)
         if side is not None and R_t > 0:
             if ev_t is not None:
-                main.wait_event(ev_t)            # the teacher (the grouping may still run)
+                self._wait_side(ev_t)            # the teacher (the grouping may still run)
             else:
-                main.wait_stream(side)
+                self._join(side)
             self._t_head = t_head
         elif R_t > 0:   # (KD_LM reads the label pairs' probabilities: finished here, not in the loss)
             self._teacher_forward(R_t, ia[:R_t], ib[:R_t], t_r, defer_head=R_t == BC)
@@ -1465,7 +1495,7 @@ class DistillEngine(EngineBase):
         mlp = self.predictor_kind == "mlp"
         pre = side is not None and grouped and self.side_grouping
         if side is not None:
-            main.wait_stream(side)               # the node grouping; every side branch joined
+            self._join(side)                     # the node grouping; every side branch joined
         if grouped and shard is not None:
             # every rank's d(h) over all nodes as unrounded f32 per-node sums, summed in f32
             # onto the owners' slices (reduce-scatter), then rounded once to the compute dtype
@@ -1680,14 +1710,13 @@ class DistillEngine(EngineBase):
                 A_in = K.operand(self.x, target, count=count)
             if l == 0 and sparse_rows is not None:
                 if side is not None:   # the bias gradient's column sums beside the sparse weight gradient
-                    main = torch.cuda.current_stream(self.dev)
-                    side.wait_stream(main)
+                    self._fork(side)
                 with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                     K.colsum(gcur, R1, lin.out_f, lin.lin.bias.grad,
                              self._ws("ws_colsum", K.colsum_ws_bytes(R1, lin.out_f)))
                 K.spmm_tn(self.xs, sparse_rows[0], sparse_rows[1], gcur, lin.lin.weight.grad)
                 if side is not None:
-                    main.wait_stream(side)
+                    self._join(side)
                 continue
             wsb = K.gemm_tn_ws_bytes(dc, R1, lin.out_f, lin.k_in)
             padded = lin.k_in != lin.in_f
@@ -1698,8 +1727,7 @@ class DistillEngine(EngineBase):
             par = (side is not None and l > 0 and not self.stu_norms
                    and -(-R1 // 256) * -(-lin.in_f // 256) <= self._cu_count() // 2)
             if par:
-                main = torch.cuda.current_stream(self.dev)
-                side.wait_stream(main)
+                self._fork(side)
             with torch.cuda.stream(side) if par else contextlib.nullcontext():
                 K.gemm_tn(K.operand(gcur, count=count), A_in, R1, lin.out_f, lin.k_in, dW, dc, self._ws("ws_tn", wsb),
                           colsum_a=lin.lin.bias.grad)
@@ -1721,5 +1749,5 @@ class DistillEngine(EngineBase):
                     K.gemm_nt(K.operand(gcur, count=count), K.operand(lin.Wt), R1, lin.in_f, lin.out_f, gnext, dc,
                               act=K.ACT_RELU_BWD, aux=self._relu_aux(acts[l - 1]), alpha=alpha)
                 if par:   # joined before the bucket's all-reduce reads the weight gradient
-                    main.wait_stream(side)
+                    self._join(side)
                     self._allreduce_bucket(*self._grad_slice(lin.lin.weight, lin.lin.bias))

@@ -190,7 +190,7 @@ def test_two_ranks_segmented_graph_matches_eager(size, world):
         assert np.array_equal(a, b)
 
 
-def _run_fullbatch(rank, world, port, out, shard=True, norm_type="none"):
+def _run_fullbatch(rank, world, port, out, shard=True, norm_type="none", use_graph=False):
     """Two full-batch steps (train(), src/main.py:167-235: the student over all
     nodes, PyG-dense negatives) of this rank's shard: the BASELINE configs[3] path."""
     import sys
@@ -221,9 +221,16 @@ def _run_fullbatch(rank, world, port, out, shard=True, norm_type="none"):
     p0, p1 = rank * P // world, (rank + 1) * P // world
     pr = pairs.to(torch.int32).to(dev).contiguous()
     eng.begin_epoch()
-    for _ in range(2):
-        eng.step_fullbatch(anchors[b0:b1].to(dev), links[p0:p1].to(dev), pr, b_offset=b0, p_offset=p0, B_total=B,
-                           P_total=P, dense_negatives=True)
+    a_dev, l_dev = anchors[b0:b1].to(dev), links[p0:p1].to(dev)
+    kw = dict(b_offset=b0, p_offset=p0, B_total=B, P_total=P, dense_negatives=True)
+    eng.step_fullbatch(a_dev, l_dev, pr, **kw)
+    if use_graph:   # the second step replayed from the (segmented, at world > 1) capture
+        g = eng.capture_fullbatch(a_dev, l_dev, pr, **kw)
+        out["segments"] = (sum(isinstance(it, torch.cuda.CUDAGraph) for it in g.items)
+                           if isinstance(g, llp_engine._SegmentedGraph) else 1)
+        g.replay()
+    else:
+        eng.step_fullbatch(a_dev, l_dev, pr, **kw)
     loss = eng.end_epoch(2 * P)
     torch.cuda.synchronize()
     if rank == 0:
@@ -236,9 +243,9 @@ def _run_fullbatch(rank, world, port, out, shard=True, norm_type="none"):
         dist.destroy_process_group()
 
 
-def _fullbatch_worker(rank, world, port, q, shard, norm_type="none"):
+def _fullbatch_worker(rank, world, port, q, shard, norm_type="none", use_graph=False):
     out = {}
-    _run_fullbatch(rank, world, port, out, shard, norm_type)
+    _run_fullbatch(rank, world, port, out, shard, norm_type, use_graph)
     if rank == 0:
         q.put(out)
 
@@ -253,6 +260,40 @@ def test_two_ranks_fullbatch_equal_one_rank(world):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _fullbatch_compare(world=world)
+
+
+def _fullbatch_ranks(world, shard, use_graph):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fullbatch_worker, args=(r, world, port, q, shard, "none", use_graph))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("shard", [True, False], ids=["sharded_student", "replicated_student"])
+def test_two_ranks_fullbatch_segmented_graph_matches_eager(shard):
+    """capture_fullbatch at 2 ranks: the full-batch step as hipGraph segments cut at its
+    collectives (all-gather / reduce-scatter of the sharded student, the gradient all-reduces),
+    with the side stream's work (samples, negatives, pairs, teacher, node grouping, small
+    weight gradients) forked and joined inside the segments, is bit-identical to eager steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    eager = _fullbatch_ranks(2, shard, False)
+    graph = _fullbatch_ranks(2, shard, True)
+    assert graph["segments"] > 1
+    assert graph["loss"] == eager["loss"], (graph["loss"], eager["loss"])
+    import numpy as np
+    for a, b in zip(graph["grads"], eager["grads"]):
+        assert np.array_equal(a, b)
+    for a, b in zip(graph["params"], eager["params"]):
+        assert np.array_equal(a, b)
 
 
 def test_two_ranks_fullbatch_replicated_student_equal_one_rank():
