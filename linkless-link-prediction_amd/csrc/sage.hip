@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void csr_agg_rows_kernel(int64_t n_rows, const
 // neighbour order, the same arithmetic as csr_agg_rows_kernel: bit-identical outputs.
 constexpr int AGG_CAP = 1024;   // staged col[] entries per workgroup (4 KiB, + 4 KiB of weights)
 #ifndef AGG_UNR
-#define AGG_UNR 8               // neighbour rows in flight per lane
+#define AGG_UNR 4               // neighbour rows in flight per lane (4 / 6 / 8 / 16: profiles/r05_agg_unr_ab.txt)
 #endif
 #ifndef AGG_PIPE_UNR
 #define AGG_PIPE_UNR 12         // the pipelined kernel's neighbour rows in flight per lane (collab degree ~10)
