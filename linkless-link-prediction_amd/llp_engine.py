@@ -1231,18 +1231,15 @@ class DistillEngine(EngineBase):
 
     def _student_forward(self, rows_s, gather_s, n_u, p_drop, R1_total, kernel_events=None):
         """Student MLP over x[gather_s] (src/models.py:45-54), rows_s rows (n_u: device row
-        count of the unique-node student).  bf16: x[gather_s] is gathered once into a plain
-        buffer that the first layer's forward and weight-gradient GEMMs read.  Returns
-        (activations per layer, the gathered x rows or None)."""
+        count of the unique-node student).  x[gather_s] is gathered once into a plain
+        buffer that the first layer's forward and weight-gradient GEMMs read (plain operands
+        take the LDS-DMA kernels, in fp32 too: §4.8).  Returns (activations per layer, the
+        gathered x rows)."""
         dt, dc = self.dtype, self.dc
         acts = []
-        x_rows = None
-        if self.dtype == torch.bfloat16:
-            x_rows = self._buf("Xg", (rows_s, self.x.shape[1]), dt)
-            K.gather_rows(self.x, gather_s, x_rows, count=n_u)
-            A = K.operand(x_rows, count=n_u)
-        else:
-            A = K.operand(self.x, gather_s, count=n_u)
+        x_rows = self._buf("Xg", (rows_s, self.x.shape[1]), dt)
+        K.gather_rows(self.x, gather_s, x_rows, count=n_u)
+        A = K.operand(x_rows, count=n_u)
         for l, lin in enumerate(self.stu):
             last = l == len(self.stu) - 1
             out = self._buf(f"H{l}", (rows_s, lin.out_f), dt)
