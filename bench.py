@@ -413,7 +413,9 @@ def physics_production_step(dtype):
             "sparse_first_layer": r1["sparse_first_layer"],
             "note": "eager steps with no host sync (the dense negatives' count stays on the device), and the same "
                     "steps replayed from a hipGraph (capture_fullbatch, which fills its own input batch from the "
-                    "epoch permutations: llp_batch_slices); rank 0 of 4 runs its slice of the node-sharded student"}
+                    "epoch permutations: llp_batch_slices); two streams (samples, negatives, pairs, the frozen teacher, "
+                    "the Hadamard backward's node grouping and the student's small weight gradients on a side "
+                    "stream, DESIGN.md 4.7); rank 0 of 4 runs its slice of the node-sharded student"}
 
 
 def main():
