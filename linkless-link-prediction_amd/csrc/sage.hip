@@ -214,16 +214,19 @@ constexpr int AGG_CAP = 1024;   // staged col[] entries per workgroup (4 KiB, + 
 #ifndef AGG_WG_PER_CU
 #define AGG_WG_PER_CU 4
 #endif
+#ifndef AGG_WAVES
+#define AGG_WAVES 4             // waves per workgroup of csr_agg_lds_kernel (rows per workgroup: AGG_WAVES * RPW)
+#endif
 
 template <typename T, int NCH, int UNR>
-__global__ __launch_bounds__(256) void csr_agg_lds_kernel(int64_t n_rows, const int32_t* __restrict__ rowptr,
+__global__ __launch_bounds__(64 * AGG_WAVES) void csr_agg_lds_kernel(int64_t n_rows, const int32_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col, const T* __restrict__ x,
                                                           int64_t ldx, const float* __restrict__ inv_deg, int mode,
                                                           const float* __restrict__ bias, T* __restrict__ out,
                                                           int64_t ldo, int accumulate) {
   constexpr int E = V16<T>::E;
   constexpr int RPW = 64 / NCH;
-  constexpr int TR = 4 * RPW;   // rows per workgroup
+  constexpr int TR = AGG_WAVES * RPW;   // rows per workgroup
   __shared__ int32_t s_ptr[TR + 1];
   __shared__ int32_t s_col[AGG_CAP];
   __shared__ float s_w[AGG_CAP];
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(256) void csr_agg_lds_kernel(int64_t n_rows, const 
   const int32_t base = s_ptr[0];
   const int32_t n_e = s_ptr[TR] - base;
   const int32_t n_st = min(n_e, AGG_CAP);
-  for (int32_t i = t; i < n_st; i += 256) {
+  for (int32_t i = t; i < n_st; i += 64 * AGG_WAVES) {
     const int32_t c = col[base + i];
     s_col[i] = c;
     if (mode) s_w[i] = inv_deg[c];
@@ -473,10 +476,15 @@ static int csr_aggregate_launch(int dtype, int64_t n_rows, int64_t F, const int3
       else if (nch == 32) gop(csr_agg_pipe_kernel<TT, 32, AGG_PIPE_UNR>, xx, oo);
       else gop(csr_agg_pipe_kernel<TT, 64, AGG_PIPE_UNR>, xx, oo);
 #else                              // one LDS-staged tile per workgroup (the default)
-      if (nch == 8) go(csr_agg_lds_kernel<TT, 8, AGG_UNR>, xx, oo);
-      else if (nch == 16) go(csr_agg_lds_kernel<TT, 16, AGG_UNR>, xx, oo);
-      else if (nch == 32) go(csr_agg_lds_kernel<TT, 32, AGG_UNR>, xx, oo);
-      else go(csr_agg_lds_kernel<TT, 64, AGG_UNR>, xx, oo);
+      const dim3 gl(ceil_div_u(n_rows, AGG_WAVES * (64 / nch)));
+      auto gol = [&](auto kern, auto* xx2, auto* oo2) {
+        hipLaunchKernelGGL(kern, gl, dim3(64 * AGG_WAVES), 0, s, n_rows, rowptr, col, xx2, ldx, inv_deg, mode, bias,
+                           oo2, ldo, accumulate);
+      };
+      if (nch == 8) gol(csr_agg_lds_kernel<TT, 8, AGG_UNR>, xx, oo);
+      else if (nch == 16) gol(csr_agg_lds_kernel<TT, 16, AGG_UNR>, xx, oo);
+      else if (nch == 32) gol(csr_agg_lds_kernel<TT, 32, AGG_UNR>, xx, oo);
+      else gol(csr_agg_lds_kernel<TT, 64, AGG_UNR>, xx, oo);
 #endif
     };
     if (dtype == LLP_BF16) pick((const bf16_t*)x, (bf16_t*)out);
