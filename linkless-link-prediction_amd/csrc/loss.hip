@@ -331,11 +331,17 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, con
 
 constexpr int HB_ROWS = 512;        // rows per block at large R (see colsum_rows)
 
-// rows per colsum block: HB_ROWS at large R, fewer (>= 64) so that a small R
-// still spreads over >= ~1024 blocks (every CU busy)
+// rows per colsum block: HB_ROWS at large R, fewer (>= COLSUM_MIN_ROWS) so that a small R
+// still spreads over >= ~COLSUM_BLOCKS blocks (every CU busy)
+#ifndef COLSUM_BLOCKS
+#define COLSUM_BLOCKS 1024
+#endif
+#ifndef COLSUM_MIN_ROWS
+#define COLSUM_MIN_ROWS 64
+#endif
 __host__ __device__ inline int64_t colsum_rows(int64_t R) {
-  int64_t hb = (R + 1023) / 1024;
-  hb = hb < 64 ? 64 : (hb > HB_ROWS ? HB_ROWS : hb);
+  int64_t hb = (R + COLSUM_BLOCKS - 1) / COLSUM_BLOCKS;
+  hb = hb < COLSUM_MIN_ROWS ? COLSUM_MIN_ROWS : (hb > HB_ROWS ? HB_ROWS : hb);
   return hb;
 }
 
