@@ -164,6 +164,15 @@ int llp_spmm_rows(int64_t rows, int64_t row0, int64_t H, const int32_t* rowptr, 
 int llp_spmm_tn(int64_t F, int64_t H, const int32_t* colptr, const int32_t* rowidx, const float* val,
                 const int32_t* perm, int64_t n_heavy, const void* dY, int64_t ldy, float* dW, int64_t ldw,
                 int accumulate, void* stream);
+/* The same two operations for Wt / Y / dY of either dtype (LLP_BF16 as above, or LLP_F32: f32
+ * rows in and out, the same order of f32 sums; the fp32 engine's sparse first layer, whose
+ * arithmetic is the reference's own; src/models.py:48).  The ReLU bit mask is bf16-only. */
+int llp_spmm_rows_dt(int dtype, int64_t rows, int64_t row0, int64_t H, const int32_t* rowptr,
+                     const int32_t* colidx, const float* val, const void* Wt, int64_t ldw, const float* bias,
+                     int act, void* Y, int64_t ldy, void* mask_out, int64_t ld_mask, void* stream);
+int llp_spmm_tn_dt(int dtype, int64_t F, int64_t H, const int32_t* colptr, const int32_t* rowidx,
+                   const float* val, const int32_t* perm, int64_t n_heavy, const void* dY, int64_t ldy,
+                   float* dW, int64_t ldw, int accumulate, void* stream);
 /* llp_spmm_tn's schedule: perm = the features by nonzero count, most first (ties by index); the
  * first n_heavy (>= llp_spmm_heavy_nnz() nonzeros) take a workgroup each, split in quarters
  * summed (q0+q1)+(q2+q3); the rest one wave each. */

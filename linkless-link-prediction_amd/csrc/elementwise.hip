@@ -331,6 +331,11 @@ __device__ __forceinline__ void work_item(const llp_tensor_desc* __restrict__ de
   __shared__ uint32_t s_base, s_n;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
+    if (lane == 0) {   // no item matched (a host n_work past the table's items): t_out = -1
+      s_t = -1;
+      s_base = w;
+      s_n = 0;
+    }
     uint32_t base = 0;
     for (int t0 = 0; t0 < n_tensors; t0 += 64) {
       const int t = t0 + lane;
@@ -450,6 +455,11 @@ __global__ __launch_bounds__(256) void grad_sumsq_fused_kernel(const llp_tensor_
               nblk_unused);
     arrival = blockIdx.x;
     total = (uint32_t)n_work;
+    if (t < 0) {   // past the table's items: arrive with nothing (so the last arriver still finalizes)
+      if (llp_arrive_last_tree(ticket, arrival, total))
+        grad_sumsq_finalize_block<true>(descs, n_tensors, max_chunks, partial, n_groups, sumsq);
+      return;
+    }
   } else {
     t = blockIdx.y;
     blk = blockIdx.x;
@@ -617,6 +627,7 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
   if (n_work > 0) {
     int64_t nblk;
     work_item(descs, n_tensors, blockIdx.x, [](const llp_tensor_desc& d) { return adam_blocks(d); }, t, blk0, nblk);
+    if (t < 0) return;     // past the table's items (a stale host n_work): nothing to update
     bstride = nblk;        // one item: the grid-strided loops below run once
   } else {
     t = blockIdx.y;

@@ -215,16 +215,22 @@ __global__ __launch_bounds__(NTT) void gemm_tn_f32_256(PTNF p) {
 
 int llp_cu_count();
 
-// splits of the f32 256-tile TN launch: whole waves of one workgroup per CU, >= 8 stages (128
-// rows) per split, f32 slabs <= 32 MB unless that leaves < 32 stages per split
+// splits of the f32 256-tile TN launch.  Each split's rows are one running f32 sum per output
+// element in the MFMA accumulators, so the split length sets the rounding error: at the collab
+// predictor's 603k rows, 16 splits of ~37.7k rows left its first-layer weight gradient at 2.8x
+// the error of the reference's own fp32 arithmetic (CPU sgemm sums K in blocks of a few hundred)
+// in the full-size oracle test.  Splits of at most TN_F32_ROWS rows, a whole number of waves of
+// one workgroup per CU; the f32 slabs (splits x P x Q) are summed in split order by slab_reduce.
+// At that shape: 160 splits of 3.8k rows, 640 MB of slabs written and read once (~0.25 ms of
+// HBM time against the launch's ~9 ms of MFMA time).
+constexpr int64_t TN_F32_ROWS = 4096;
 int64_t llp_gemm_tn_f32_256_splits(int64_t M, int64_t P, int64_t Q) {
   const int64_t tiles = ((P + TP - 1) / TP) * ((Q + TQ - 1) / TQ);
   const int64_t target = llp_cu_count();
   const int64_t wave = tiles >= target ? 1 : target / tiles;
-  const int64_t s32 = std::min<int64_t>(wave, (M + TKM * 32 - 1) / (TKM * 32));
-  int64_t splits = std::min<int64_t>(wave, (M + TKM * 8 - 1) / (TKM * 8));
-  const int64_t slab = P * Q * (int64_t)sizeof(float);
-  if (splits * slab > (32ll << 20)) splits = std::max<int64_t>(s32, (32ll << 20) / slab);
+  const int64_t need = (M + TN_F32_ROWS - 1) / TN_F32_ROWS;           // splits for <= TN_F32_ROWS rows each
+  int64_t splits = need <= wave ? std::min<int64_t>(wave, (M + TKM * 8 - 1) / (TKM * 8))
+                                : (need + wave - 1) / wave * wave;   // whole waves
   return splits < 1 ? 1 : splits;
 }
 

@@ -307,7 +307,7 @@ class EngineBase:
 
     def _build_descs(self):
         opt = self.optimizer
-        descs = []
+        descs, shapes = [], []
         for p, grp in zip(self.all_params, self.param_groups_of):
             st = opt.state[p]
             shadow, shadow_t, ld, ld_t = self._shadows.get(id(p), (None, None, 0, 0))
@@ -315,14 +315,11 @@ class EngineBase:
             descs.append(K.TensorDesc(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                                       st["exp_avg_sq"].data_ptr(), K.ptr(shadow), K.ptr(shadow_t), p.numel(), rows,
                                       cols, grp, self.dc, ld, ld_t))
+            # the compact grids' item counts from the very tuples the descriptor holds
+            shapes.append((p.numel(), rows, cols, shadow_t is not None))
         self.n_desc = len(descs)
         self.max_numel = max(p.numel() for p in self.all_params)
         # compact grids of the one-launch gradient norm and Adam (llp_grad_sumsq_w / llp_adam_step_w)
-        shapes = []
-        for p in self.all_params:
-            shadow_t = self._shadows.get(id(p), (None, None, 0, 0))[1]
-            rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
-            shapes.append((p.numel(), rows, cols, shadow_t is not None))
         self.n_work_sumsq, self.n_work_adam = K.work_items(shapes)
         self.descs_dev = K.descs_to_device(descs, self.dev)
         self.sumsq = torch.zeros(self.n_groups, dtype=torch.float32, device=self.dev)
@@ -774,19 +771,27 @@ class EngineBase:
         out += [w for w in self.__dict__.get("_neg_wss", {}).values() if w is not None]
         return out
 
-    def check_device_errors(self):
-        """Raise if a single-pass scan of this engine (the dedup compaction, the dense negatives'
-        compaction) timed out in its look-back since the last check: that call's outputs were
-        invalid (in bounds, csrc/llp_common.h).  One host read; end_epoch calls it."""
+    def _device_error_flag(self):
+        """0.0 / 1.0 (float64 device scalar): whether a single-pass scan of this engine (the dedup
+        compaction, the dense negatives' compaction) timed out in its look-back since the last
+        reset.  No host read."""
         words = [w.error_word() for w in self._stateful_workspaces()]
         words = [w for w in words if w is not None]
         if not words:
-            return
-        errs = torch.stack(words).tolist()
-        if any(errs):
+            return torch.zeros((), dtype=torch.float64, device=self.dev)
+        return (torch.stack(words) != 0).any().to(torch.float64)
+
+    def check_device_errors(self, flag=None):
+        """Raise if a single-pass scan timed out since the last check: that call's outputs were
+        invalid (in bounds, csrc/llp_common.h).  ``flag``: the error flag already reduced over
+        the ranks (end_epoch), so that every rank raises and resets together; else this rank's.
+        Parameters updated during the failed steps are NOT rolled back."""
+        bad = float((self._device_error_flag() if flag is None else flag).item()) != 0.0
+        if bad:
             self.reset_device_state()
-            raise RuntimeError("a device look-back scan timed out (dedup / dense-negative compaction); the "
-                               "affected steps are invalid. The engine's persistent device state was reset.")
+            raise RuntimeError("a device look-back scan timed out (dedup / dense-negative compaction) on this or "
+                               "another rank; the affected steps are invalid and the parameters they updated are "
+                               "not rolled back. The engine's persistent device state was reset.")
 
     def reset_device_state(self):
         """Return every piece of persistent device state to zero: the last-arriver ticket
@@ -803,7 +808,10 @@ class EngineBase:
         """Run one step; if it raises (outside a capture), reset the persistent device state."""
         try:
             return step()
-        except BaseException:
+        except Exception:
+            # (not KeyboardInterrupt / SystemExit: a synchronize behind a hung kernel or a stalled
+            # collective would block Ctrl-C; the next step then starts from whatever state is left,
+            # and reset_device_state() is the caller's to run)
             if not torch.cuda.is_current_stream_capturing():
                 try:
                     torch.cuda.synchronize(self.dev)
@@ -819,15 +827,17 @@ class EngineBase:
     def end_epoch(self, total_examples):
         """Returns total_loss / total_examples (src/main.py:141-144); one host sync.  Raises
         if a device scan failed during the epoch (check_device_errors)."""
-        tot = self.loss_sum
+        # the loss sum and the device-error flag in one buffer: with several ranks one all-reduce
+        # carries both, so a scan failure on any rank makes every rank raise (and reset) together
+        # instead of leaving the others to hang in the next epoch's collectives
+        tot = torch.stack([self.loss_sum.view(()), self._device_error_flag()])
         if self.world > 1:
-            tot = tot.clone()
             dist.all_reduce(tot, group=self.group)
-        self.check_device_errors()
+        self.check_device_errors(flag=tot[1])
         steps = int(self.adam_step.item())
         for p in self.all_params:
             self.optimizer.state[p]["step"] = torch.tensor(float(steps))
-        return float(tot.item()) / max(total_examples, 1)
+        return float(tot[0].item()) / max(total_examples, 1)
 
 
 class DistillEngine(EngineBase):
@@ -873,7 +883,8 @@ class DistillEngine(EngineBase):
         # student's first layer gathers rows of its transposed bf16 weight by x's nonzeros
         # (llp_spmm_rows / llp_spmm_tn, csrc/spmm.hip) instead of dense MFMA tiles over zeros
         H0 = stu[0].out_features
-        self.sparse_x = (bool(sparse_input) and self.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[1] >= 256
+        self.sparse_x = (bool(sparse_input) and self.dtype in (torch.bfloat16, torch.float32) and x.dim() == 2
+                         and x.shape[1] >= 256
                          and H0 % 8 == 0 and H0 <= 1024
                          and float(torch.count_nonzero(x)) <= SPARSE_X_MAX_DENSITY * x.numel())
         self.stu = [_Linear(l, self.dtype, need_t=(i > 0 or self.sparse_x), need_c=True) for i, l in enumerate(stu)]
@@ -912,7 +923,7 @@ class DistillEngine(EngineBase):
             self.x[:, :F_in].copy_(x.to(self.dev))
         else:
             self.x = x.to(self.dev).to(self.dtype).contiguous()
-        self.xs = K.SparseRows(x.to(self.dev)) if self.sparse_x else None
+        self.xs = K.SparseRows(x.to(self.dev), round_bf16=self.dtype == torch.bfloat16) if self.sparse_x else None
         self.t_h = t_h.to(self.dev).to(self.dtype).contiguous()
         self._neg_rc = (np.asarray(row), np.asarray(col))
         self._neg_keys = None
@@ -930,6 +941,24 @@ class DistillEngine(EngineBase):
         if self._rows_dev is not None:
             return int(self._rows_dev.item())
         return self._rows_host
+
+    def last_logits(self):
+        """The last single-rank step's predictor outputs, as the reference names them
+        (src/main.py:105-106,126 / 186-187,213): ``s_r`` [B, C] student context-pair probabilities,
+        ``t_r`` [B, C] the frozen teacher's, ``out`` [n_lab] label-pair probabilities, plus the
+        student's pre-sigmoid logits ``s_logit`` / ``out_logit`` (f32 device views of the step's
+        buffers, valid until the next step).  The loss launch finishes every logit from the head
+        partials and writes it back, so these are exactly what the loss terms were computed on."""
+        lay = getattr(self, "_logit_layout", None)
+        if lay is None:
+            raise RuntimeError("last_logits: no single-rank step has run (the owner decomposition keeps each "
+                               "rank's pairs in its own order)")
+        B, C, n_lab = lay
+        logit = self._bufs["logit"][:B * C + n_lab]
+        s_logit, out_logit = logit[:B * C].view(B, C), logit[B * C:]
+        t_r = self._bufs["t_r"][:B * C].view(B, C) if B * C else self._bufs["logit"][:0].view(0, C)
+        return dict(s_r=torch.sigmoid(s_logit), t_r=t_r, out=torch.sigmoid(out_logit), s_logit=s_logit,
+                    out_logit=out_logit)
 
     def _rows_index(self, B, C, P2):
         """Predictor-row -> h-row index for the minibatch layout (static per shape)."""
@@ -1138,6 +1167,8 @@ class DistillEngine(EngineBase):
             K.llp_loss(B, C, logit, t_r, n_lab, P, logit[B * C:], B_total, P_total + n_neg_total, float(a.margin),
                        1.0, float(a.True_label), float(a.LLP_D), float(a.LLP_R), dlogit, dlogit[B * C:], self.terms,
                        ws, s_head=self._s_head, t_head=self._t_head, ticket=self.loss_ticket)
+
+        self._logit_layout = None if owner else (B, C, n_lab)
 
         # ---- a10: backward
         self._dbg_cut("teacher + loss")
@@ -1475,6 +1506,7 @@ class DistillEngine(EngineBase):
                    float(a.LLP_R) if use_llp else 0.0, dlogit, dlogit[BC:], self.terms, ws, neg_count=cnt,
                    neg_offset=p_offset, pos_total=P_total, s_head=self._s_head, t_head=self._t_head,
                    ticket=self.loss_ticket)
+        self._logit_layout = (Bc, C, n_lab)
         if not grouped:   # in fp32 mode dh32 IS the student backward's first gradient buffer
             dh32 = self._buf("gS0" if dt == torch.float32 else "dh32", (N, H), torch.float32)
             dh32.zero_()

@@ -72,6 +72,10 @@ _SIGS = {
                               c_i64, c_vp]),
     "llp_spmm_tn": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
     "llp_spmm_heavy_nnz": (c_int, []),
+    "llp_spmm_rows_dt": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64,
+                                 c_vp, c_i64, c_vp]),
+    "llp_spmm_tn_dt": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int,
+                               c_vp]),
     "llp_head_fwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "llp_head_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_head_bwd": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_vp, c_i64, c_vp, c_vp,
@@ -313,7 +317,7 @@ class SparseRows:
     (csc(r0, n): colptr, rowidx local to the slice, ascending within a column, val).  Built once
     from the dense x with torch (setup plumbing, not the step)."""
 
-    def __init__(self, x):
+    def __init__(self, x, round_bf16=True):
         assert x.dim() == 2
         self.N, self.F = x.shape
         nz = torch.nonzero(x)                                   # row-major order: rows, then columns
@@ -327,7 +331,9 @@ class SparseRows:
         self.colidx = nz[:, 1].to(torch.int32).contiguous()
         # rounded through bf16 as the dense first layer reads x (its bf16 copy): the sparse and the
         # dense path then multiply the same values for non-binary features too
-        v = x[nz[:, 0], nz[:, 1]].to(torch.bfloat16).float().contiguous()
+        # (round_bf16=False: the fp32 engine, whose dense path reads x in f32)
+        v = x[nz[:, 0], nz[:, 1]].float()
+        v = (v.to(torch.bfloat16).float() if round_bf16 else v).contiguous()
         self.val = None if bool((v == 1).all()) else v
         self._csc = {}
 
@@ -353,21 +359,23 @@ class SparseRows:
 
 
 def spmm_rows(xs, rows, row0, Wt, bias, Y, act=ACT_NONE, mask=None):
-    """Y[:rows] = act(x[row0:row0+rows] @ Wt + bias) (llp_spmm_rows); Wt bf16 [F, H]."""
+    """Y[:rows] = act(x[row0:row0+rows] @ Wt + bias) (llp_spmm_rows_dt); Wt [F, H] and Y bf16 or f32
+    (the same dtype)."""
     L = lib()
     H = Wt.shape[1]
-    check(L.llp_spmm_rows(rows, row0, H, xs.rowptr.data_ptr(), xs.colidx.data_ptr(), ptr(xs.val), Wt.data_ptr(),
-                          Wt.stride(0), ptr(bias), act, Y.data_ptr(), Y.stride(0), ptr(mask),
-                          mask.stride(0) if mask is not None else 0, stream_ptr()), "llp_spmm_rows")
+    assert Y.dtype == Wt.dtype
+    check(L.llp_spmm_rows_dt(dtype_code(Wt.dtype), rows, row0, H, xs.rowptr.data_ptr(), xs.colidx.data_ptr(),
+                             ptr(xs.val), Wt.data_ptr(), Wt.stride(0), ptr(bias), act, Y.data_ptr(), Y.stride(0),
+                             ptr(mask), mask.stride(0) if mask is not None else 0, stream_ptr()), "llp_spmm_rows")
 
 
 def spmm_tn(xs, r0, n, dY, dW, accumulate=False):
-    """dW (+)= dY[:n]^T @ x[r0:r0+n] (llp_spmm_tn); dW f32 [H, F] (row stride >= F)."""
+    """dW (+)= dY[:n]^T @ x[r0:r0+n] (llp_spmm_tn_dt); dY bf16 or f32, dW f32 [H, F] (row stride >= F)."""
     L = lib()
     colptr, rowidx, val, perm, n_heavy = xs.csc(r0, n)
-    check(L.llp_spmm_tn(xs.F, dY.shape[1], colptr.data_ptr(), rowidx.data_ptr(), ptr(val), perm.data_ptr(), n_heavy,
-                        dY.data_ptr(), dY.stride(0), dW.data_ptr(), dW.stride(0), int(accumulate), stream_ptr()),
-          "llp_spmm_tn")
+    check(L.llp_spmm_tn_dt(dtype_code(dY.dtype), xs.F, dY.shape[1], colptr.data_ptr(), rowidx.data_ptr(), ptr(val),
+                           perm.data_ptr(), n_heavy, dY.data_ptr(), dY.stride(0), dW.data_ptr(), dW.stride(0),
+                           int(accumulate), stream_ptr()), "llp_spmm_tn")
 
 
 def head_fwd(Z, R, H, w, b, logit=None, prob=None, Z2=None, iz=None, iz2=None):

@@ -166,13 +166,16 @@ def _n_ranks(use_graph, size, world=2):
     return out
 
 
-@pytest.mark.parametrize("size,world", [({}, 2), (dict(N=235_868, n_pairs=400_000, B=4096, P=16384), 2), ({}, 4)],
-                         ids=["small", "collab_nodes", "small_4ranks"])
+@pytest.mark.parametrize("size,world", [({}, 2), (dict(N=235_868, n_pairs=400_000, B=4096, P=16384), 2), ({}, 4),
+                                        (dict(N=235_868, n_pairs=400_000, B=13_110, P=65_536), 8)],
+                         ids=["small", "collab_nodes", "small_4ranks", "collab_batch_8ranks"])
 def test_two_ranks_segmented_graph_matches_eager(size, world):
     """BASELINE configs[4]: the multi-rank step replayed from hipGraph segments (the
     all-reduces run between them) is bit-identical to eager multi-rank steps.  At the
     collab node count the unique-node compaction's scan runs over 116 blocks (the round-2
-    replay fault was there); the 2,000-node case is one block."""
+    replay fault was there); the 2,000-node case is one block.  The 8-rank
+    case is configs[4]'s decomposition at the collab batch (B = 13,110 anchors, P = 65,536
+    edges, the whole batch on every rank, each rank's owned pairs), 8 gloo ranks on one GPU."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     eager = _n_ranks(False, size, world)

@@ -2,15 +2,20 @@
 (src/main.py:147-236) at the coauthor-physics production shape (synthetic
 graph split by the reference's do_production_edge_split: 31,044 old nodes,
 8,415 binary features, 288,498 directed training edges; student 8,415 -> 256
--> 256, C = 20 contexts, 65,536 edges, PyG-dense negatives).  The CPU oracle
-cannot run this size in a test, so the properties checked are size-independent:
+-> 256, C = 20 contexts, 65,536 edges, PyG-dense negatives).
 
+* oracle parity (VERDICT r05 "next" 1b): one fp32 step through the default sparse
+  first layer (llp_spmm_rows_dt / llp_spmm_tn_dt in f32) against the CPU oracle
+  (distill_losses_fullbatch + distill_step, float64 and float32) on the same
+  injected samples and negatives, with the collab test's bars (tests/fullsize_check.py:
+  logits within 1e-4, loss terms, gradients, parameters after clip + Adam).  The
+  oracle runs the whole step in a few seconds at this size;
 * determinism: the same step from the same state is bit-identical in bf16
   (node-grouped Hadamard backward, fixed-order reductions, no atomics);
 * anchor/edge sharding (what each of R ranks computes before the gradient
   all-reduce): the two half-batch shards' gradients sum to the whole batch's;
-* the bf16 step (first layer on zero-padded K = 8,448) tracks the fp32 step
-  on the loss terms and the gradients of the padded first layer and the head."""
+* the bf16 step (sparse first layer on bf16 weight rows) tracks the fp32 step
+  on the loss terms and the gradients of the first layer and the head."""
 import os
 import sys
 import tempfile
@@ -18,6 +23,8 @@ import types
 
 import pytest
 import torch
+
+import fullsize_check as FC
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -119,3 +126,71 @@ def test_physics_fullbatch_bf16_tracks_fp32(physics):
     assert cos(b16.grads[0], f32.grads[0]) > 0.99                 # student layer-0 weight (padded K)
     for i in (-2, -1):                                            # predictor head weight and bias
         assert cos(b16.grads[i], f32.grads[i]) > 0.99, i
+
+
+def test_physics_fullbatch_fp32_step_matches_oracle(physics):
+    """One train() link batch at full physics size, fp32, sparse first layer, against the oracle.
+    State: every student / predictor weight x6.5 and the frozen teacher predictor's x3 (t_h ~ N(0, 1)),
+    so that the student logits spread over (0, 1) without saturating f32 sigmoids (|z| < 15) and
+    both clip coefficients are below 1 (default init: gradient norms ~0.03, coefficient 1)."""
+    import time
+    import llp_engine
+    import models
+    from oracle import llp_oracle as O
+    torch.set_num_threads(16)
+    td, a = physics
+    N, F_ = td.x.size(0), td.x.size(1)
+    E = td.edge_index.size(1)
+    P = a.link_batch_size
+    B = int(N / (E / P))                                  # src/main.py:345-346
+    C = a.rw_step * a.hops * (1 + a.ns_rate)
+    H, L = a.hidden_channels, a.num_layers
+    assert (N, F_, C, H, L) == (31_044, 8_415, 20, 256, 2)
+    g = torch.Generator().manual_seed(7)
+    anchors = torch.randperm(N, generator=g)[:B]
+    samples = torch.cat([anchors.view(B, 1), torch.randint(0, N, (B, C), generator=g)], 1)
+    link = torch.randperm(E, generator=g)[:P]
+    edge = td.edge_index[:, link]
+    neg = torch.randint(0, N, (2, P), generator=g)
+    t_h = torch.randn(N, 256, generator=torch.Generator().manual_seed(2))
+    torch.manual_seed(1)
+    model = models.MLP(L, F_, H, H, 0.0).to(DEV)
+    pred = models.LinkPredictor("mlp", H, H, 1, L, 0.0).to(DEV)
+    tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(DEV)
+    with torch.no_grad():
+        for m, gain in ((model, 6.5), (pred, 6.5), (tpred, 3.0)):
+            for p in m.parameters():
+                if p.dim() == 2:
+                    p.mul_(gain)
+    for p in tpred.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
+    row, col = td.edge_index
+    eng = llp_engine.DistillEngine(model, pred, tpred, td.x.to(DEV), t_h.to(DEV), row.numpy(), col.numpy(), N, a,
+                                   opt, dtype="fp32", seed=11)
+    assert eng.xs is not None                             # the default sparse first layer, in f32
+    params = list(model.parameters()) + list(pred.parameters())
+    params0 = [p.detach().cpu().clone() for p in params]
+    tpar = [p.detach().cpu().clone() for p in tpred.parameters()]
+    pairs = td.edge_index.t().to(torch.int32).to(DEV).contiguous()
+    t0 = time.time()
+    n_neg = eng.step_fullbatch(anchors.to(torch.int32).to(DEV), link.to(torch.int32).to(DEV), pairs,
+                               samples=samples.to(torch.int32).to(DEV), neg=neg.to(torch.int32).to(DEV))
+    torch.cuda.synchronize()
+    assert int(n_neg) == P
+    terms = eng.terms.cpu()
+    lg = {k: v.detach().double().cpu() for k, v in eng.last_logits().items()}
+    grads_gpu = [p.grad.detach().cpu().clone() for p in params]
+    params1 = [p.detach().cpu().clone() for p in params]
+    t1 = time.time()
+    print(f"engine step done; {t1 - t0:.1f} s", flush=True)
+    x = td.x
+
+    def losses(sw, sb, pw, pb, d):
+        tw, tb = [p.to(d) for p in tpar[0::2]], [p.to(d) for p in tpar[1::2]]
+        return O.distill_losses_fullbatch(x.to(d), t_h.to(d), samples, anchors, edge, neg, sw, sb, pw, pb, tw, tb, a)
+
+    o64 = FC.oracle_step(O, losses, params0, L, a.lr, torch.float64)
+    print(f"oracle step (f64) done; {time.time() - t1:.1f} s", flush=True)
+    o32 = FC.oracle_step(O, losses, params0, L, a.lr, torch.float32)
+    FC.check(lg, terms, grads_gpu, params1, params0, o64, o32, a.lr, (B, C), 2 * P)

@@ -50,18 +50,20 @@ def _streams(idx, vals, rows_of, streams):
 @pytest.mark.parametrize("H", [256, 64, 520, 136])
 @pytest.mark.parametrize("values", [False, True])
 @pytest.mark.parametrize("relu", [False, True])
-def test_spmm_rows_bit_exact(H, values, relu):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_spmm_rows_bit_exact(H, values, relu, dtype):
     k = K()
     N, F = 203, 700
     x = _x(N, F, 0.02, values, H + values)
     g = torch.Generator().manual_seed(5)
-    Wt = (torch.randn(F, H, generator=g) * 0.2).to(torch.bfloat16)
+    Wt = (torch.randn(F, H, generator=g) * 0.2).to(dtype)
     bias = torch.randn(H, generator=g) * 0.1
-    xs = k.SparseRows(torch.from_numpy(x).to(DEV))
+    xs = k.SparseRows(torch.from_numpy(x).to(DEV), round_bf16=dtype == torch.bfloat16)
     assert (xs.val is None) == (not values)
     r0, rows = 17, 150
-    Y = torch.full((rows + 3, H), 7.0, dtype=torch.bfloat16, device=DEV)
-    mask = torch.full((rows, H // 8), 0xAB, dtype=torch.uint8, device=DEV) if relu and H % 8 == 0 else None
+    Y = torch.full((rows + 3, H), 7.0, dtype=dtype, device=DEV)
+    bf = dtype == torch.bfloat16
+    mask = torch.full((rows, H // 8), 0xAB, dtype=torch.uint8, device=DEV) if bf and relu and H % 8 == 0 else None
     Wt_d = Wt.to(DEV)
     k.spmm_rows(xs, rows, r0, Wt_d, bias.to(DEV), Y, act=k.ACT_RELU if relu else k.ACT_NONE, mask=mask)
     torch.cuda.synchronize()
@@ -70,10 +72,16 @@ def test_spmm_rows_bit_exact(H, values, relu):
     for r in range(rows):
         cols = np.nonzero(x[r0 + r])[0]
         ref[r] = _streams(cols, x[r0 + r, cols], Wf, 4) + bias.numpy()
+    got = Y[:rows].cpu()
+    if not bf:   # f32 rows: the same sums, no rounding to bf16; ReLU keeps the f32 value
+        if relu:
+            ref = np.where(ref < 0, np.float32(0), ref)
+        assert np.array_equal(got.numpy(), ref)
+        assert torch.equal(Y[rows:].cpu(), torch.full((3, H), 7.0))
+        return
     refb = _bf16_round(ref)
     if relu:
         refb = torch.where(refb.view(torch.int16) < 0, torch.zeros_like(refb), refb)
-    got = Y[:rows].cpu()
     assert torch.equal(got.view(torch.int16), refb.view(torch.int16))
     assert torch.equal(Y[rows:].cpu().float(), torch.full((3, H), 7.0))     # rows past `rows` untouched
     if mask is not None:
@@ -82,17 +90,18 @@ def test_spmm_rows_bit_exact(H, values, relu):
         assert np.array_equal(mask.cpu().numpy(), ref_mask)
 
 
-@pytest.mark.parametrize("H", [256, 128, 1024])
+@pytest.mark.parametrize("H", [256, 128, 1024, 136])
 @pytest.mark.parametrize("values", [False, True])
-def test_spmm_tn_bit_exact(H, values):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_spmm_tn_bit_exact(H, values, dtype):
     k = K()
     N, F = 240, 333
     x = _x(N, F, 0.03, values, 7 * H + values)
     x[:, 5:40:3] = (np.random.default_rng(H).random((N, 12)) < 0.9) * (2.0 if values else 1.0)   # heavy columns
     g = torch.Generator().manual_seed(11)
-    xs = k.SparseRows(torch.from_numpy(x).to(DEV))
+    xs = k.SparseRows(torch.from_numpy(x).to(DEV), round_bf16=dtype == torch.bfloat16)
     r0, n = 30, 180
-    dY = (torch.randn(n, H, generator=g) * 0.3).to(torch.bfloat16)
+    dY = (torch.randn(n, H, generator=g) * 0.3).to(dtype)
     dW = torch.full((H, F + 5), 3.0, device=DEV)[:, :F]     # row stride F + 5
     for accumulate in (False, True):
         k.spmm_tn(xs, r0, n, dY.to(DEV), dW, accumulate=accumulate)
