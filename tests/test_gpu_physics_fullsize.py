@@ -130,9 +130,12 @@ def test_physics_fullbatch_bf16_tracks_fp32(physics):
 
 def test_physics_fullbatch_fp32_step_matches_oracle(physics):
     """One train() link batch at full physics size, fp32, sparse first layer, against the oracle.
-    State: every student / predictor weight x6.5 and the frozen teacher predictor's x3 (t_h ~ N(0, 1)),
-    so that the student logits spread over (0, 1) without saturating f32 sigmoids (|z| < 15) and
-    both clip coefficients are below 1 (default init: gradient norms ~0.03, coefficient 1)."""
+    State: every student / predictor weight x6 and the frozen teacher predictor's x3 (t_h ~ N(0, 1)),
+    so that the student logits spread over (0, 1) without saturating the label logits' f32
+    sigmoids (|z| < 15) and the gradients are ~30x those at default init (norms ~0.8, 92-99 % of
+    every tensor live for the post-Adam check).  The clip coefficient stays 1 here: at x6.5 the
+    norms pass 1 but label logits reach |z| ~ 20, where f32 BCE saturates (tests/fullsize_check.py);
+    the collab test covers coefficients below 1."""
     import time
     import llp_engine
     import models
@@ -158,7 +161,7 @@ def test_physics_fullbatch_fp32_step_matches_oracle(physics):
     pred = models.LinkPredictor("mlp", H, H, 1, L, 0.0).to(DEV)
     tpred = models.LinkPredictor("mlp", 256, 256, 1, 2, 0.0).to(DEV)
     with torch.no_grad():
-        for m, gain in ((model, 6.5), (pred, 6.5), (tpred, 3.0)):
+        for m, gain in ((model, 6.0), (pred, 6.0), (tpred, 3.0)):
             for p in m.parameters():
                 if p.dim() == 2:
                     p.mul_(gain)
@@ -193,4 +196,4 @@ def test_physics_fullbatch_fp32_step_matches_oracle(physics):
     o64 = FC.oracle_step(O, losses, params0, L, a.lr, torch.float64)
     print(f"oracle step (f64) done; {time.time() - t1:.1f} s", flush=True)
     o32 = FC.oracle_step(O, losses, params0, L, a.lr, torch.float32)
-    FC.check(lg, terms, grads_gpu, params1, params0, o64, o32, a.lr, (B, C), 2 * P)
+    FC.check(lg, terms, grads_gpu, params1, params0, o64, o32, a.lr, (B, C), 2 * P, need_clip=False)
