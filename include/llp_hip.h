@@ -111,6 +111,12 @@ int64_t llp_gemm_nt_head_parts(int64_t N);
 int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B,
                      void* C, int64_t ldc, const float* bias, int act, float alpha,
                      const llp_dropout* dropout, const float* head_w, float* head_part, void* stream);
+/* The same for f32 operands (the fp32 path, the reference's arithmetic): C = relu(A.B^T + bias) f32
+ * (stored: the head backward reads it) and head_part[N / 256][M] = the Linear(N,1) head's partial
+ * dots over each 256-column tile, summed in a fixed order (src/models.py:143-146).  Plain 16-B
+ * aligned f32 operands, K % 64 == 0, N % 256 == 0; finish with llp_head_finish (+ bias). */
+int llp_gemm_nt_head_f32(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B, float* C,
+                         int64_t ldc, const float* bias, const float* head_w, float* head_part, void* stream);
 int llp_head_finish(int64_t parts, int64_t M, const float* part, const float* b, float* logit,
                     float* prob, void* stream);
 

@@ -670,7 +670,7 @@ int llp_gemm_tn_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, i
                         float* ws_colsum, int64_t splits, hipStream_t s);
 int llp_gemm_nt_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, float* C,
                         int64_t ldc, const float* bias, int act, const float* aux, int64_t ld_aux, float alpha,
-                        hipStream_t s);
+                        hipStream_t s, const float* head_w = nullptr, float* head_part = nullptr);
 
 extern "C" int llp_gemm_nt(int dtype, int64_t M, int64_t N, int64_t K, const llp_operand* A,
                            const llp_operand* B, void* C, int64_t ldc, int c_dtype, const float* bias,
@@ -859,6 +859,25 @@ extern "C" int llp_gemm_nt_head(int64_t M, int64_t N, int64_t K, const llp_opera
   const int rc = llp_gemm_nt_bf16_256(A, B, M, N, K, C, ldc, bias, act, nullptr, 0, alpha, dp, dth, ds, dseed, dctr,
                                       dstr, head_w, head_part, nullptr, nullptr, 0, (hipStream_t)stream);
   if (rc != 0) return llp::set_error(rc, "llp_gemm_nt_head: %s", hipGetErrorString((hipError_t)rc));
+  return LLP_OK;
+}
+
+// f32 operands: the persistent f32 kernel's F32_HEAD epilogue (gemm256_f32.hip), ReLU + head partials
+// head_part[N / 256][M]; C (the hidden activations the head backward reads) is stored too.
+extern "C" int llp_gemm_nt_head_f32(int64_t M, int64_t N, int64_t K, const llp_operand* A, const llp_operand* B,
+                                    float* C, int64_t ldc, const float* bias, const float* head_w, float* head_part,
+                                    void* stream) {
+  LLP_CHECK_ARG(A && B && C && head_w && (head_part || M == 0), "llp_gemm_nt_head_f32: null pointer");
+  auto a16f = [](const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && (ld % 4 == 0); };
+  LLP_CHECK_ARG(K > 0 && K % 64 == 0 && N % 256 == 0 && !A->idx && !A->ptr2 && !B->idx && !B->ptr2 &&
+                    a16f(A->ptr, A->ld) && a16f(B->ptr, B->ld) && a16f(C, ldc) && (uintptr_t)head_w % 16 == 0 &&
+                    (!bias || (uintptr_t)bias % 16 == 0),
+                "llp_gemm_nt_head_f32: needs plain 16-B aligned f32 operands, K %% 64 == 0, N %% 256 == 0");
+  if (M == 0) return LLP_OK;
+  llp::note_kernel("gemm_nt_f32_pp8p<F32_HEAD> (persistent 256x256, head fused)");
+  const int rc = llp_gemm_nt_f32_256(A, B, M, N, K, C, ldc, bias, LLP_ACT_RELU, nullptr, 0, 1.f, (hipStream_t)stream,
+                                     head_w, head_part);
+  if (rc != 0) return llp::set_error(rc, "llp_gemm_nt_head_f32: %s", hipGetErrorString((hipError_t)rc));
   return LLP_OK;
 }
 

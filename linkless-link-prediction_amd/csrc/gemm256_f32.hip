@@ -28,6 +28,13 @@ constexpr int IMG_U4 = 256 * 8;  // one operand image of a K-tile: 256 rows x 12
 constexpr int TILE_U4 = 2 * IMG_U4;
 
 constexpr int F32_RELU = 1, F32_NONE = 2, F32_BWD = 3;
+// F32_HEAD (round 6): F32_RELU plus LinkPredictor's Linear(N, 1) head (src/models.py:146) in the
+// epilogue: head_part[n0 / 256][m] = sum over the tile's 256 columns of relu(y[m, n]) * head_w[n],
+// in a fixed order (per lane its 4 column blocks x 4 columns, then the 4 lanes of a row by
+// xor-shuffles, then the 4 waves of the row's 64-column quarters through LDS), so deterministic;
+// the logit is bias + the partials in column-tile order (llp_head_finish / the loss launch).
+// Replaces the fp32 step's separate llp_head_fwd pass over the [R2, H] activations.
+constexpr int F32_HEAD = 4;
 
 struct PF32 {
   const float* A; int64_t lda;
@@ -38,6 +45,7 @@ struct PF32 {
   const float* aux; int64_t ld_aux;   // F32_BWD: the layer's stored f32 activations
   float alpha;
   const int32_t* m_dev;               // device row count or NULL
+  const float* head_w; float* head_part; int64_t head_ld;   // F32_HEAD
 };
 
 __device__ __forceinline__ void glds16_s(uint32_t voff, const void* sbase, uint32_t lds_addr_uniform) {
@@ -67,8 +75,11 @@ __device__ __forceinline__ int q64_row(int chunk, int cr) {
 template <int MODE>
 __global__ __launch_bounds__(FNT) void gemm_nt_f32_pp8p(PF32 p) {
   constexpr bool BWD = MODE == F32_BWD;
+  constexpr bool HEAD = MODE == F32_HEAD;
+  constexpr bool RELU = MODE == F32_RELU || HEAD;
   constexpr int BLDS = 2 * TILE_U4;          // the tile's 256 bias floats (1 KB)
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * TILE_U4 + 64];
+  constexpr int HWLDS = BLDS + 64;           // the tile's 256 head weights (1 KB, F32_HEAD)
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * TILE_U4 + 128];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -173,6 +184,7 @@ __global__ __launch_bounds__(FNT) void gemm_nt_f32_pp8p(PF32 p) {
     const bool pf = next_tile(t_next, m1, n1);
     // this tile's bias into LDS by DMA (an ordinary load would drain the DMA ring at its use)
     if (p.bias && wu == 0) glds16(p.bias + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + BLDS)));
+    if (HEAD && wu == 1) glds16(p.head_w + n0 + 4 * lane, __builtin_amdgcn_readfirstlane(lds_u32(smem + HWLDS)));
     barrier();
     if (grp1) barrier();          // waves 4-7: one barrier behind from here on
 #pragma unroll
@@ -223,6 +235,10 @@ __global__ __launch_bounds__(FNT) void gemm_nt_f32_pp8p(PF32 p) {
     const float* __restrict__ aux = p.aux;
     float* __restrict__ C = p.C;
     const float alpha = p.alpha;
+    const float* hwl = reinterpret_cast<const float*>(smem + HWLDS);
+    float hd[8];   // F32_HEAD: this lane's head dot of row block im over its 4 x 4 columns
+#pragma unroll
+    for (int im = 0; im < 8; ++im) hd[im] = 0.f;
     // column blocks jn = 2 jp, 2 jp + 1 are the two 64-B halves of one 128-B line of each row: the
     // two stores of a line go out back to back, so L2 merges them into one full-line write
     // (jn-outer order left them 8 stores apart and counted 1.55x the C bytes in WRITE_SIZE)
@@ -238,6 +254,11 @@ __global__ __launch_bounds__(FNT) void gemm_nt_f32_pp8p(PF32 p) {
         // the ReLU-backward activations of these 4 rows x 2 column quads, loaded together (one
         // wait, not one round trip per row); rows past M read the last live row and are not stored
         float4_t av[4][2];
+        float4_t hw[2];
+        if (HEAD) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) hw[q] = *reinterpret_cast<const float4_t*>(hwl + ewn * 64 + (2 * jp + q) * 16 + eg * 4);
+        }
         if (BWD) {
 #pragma unroll
           for (int iq = 0; iq < 4; ++iq)
@@ -260,18 +281,39 @@ __global__ __launch_bounds__(FNT) void gemm_nt_f32_pp8p(PF32 p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float x = alpha * acc[jn][im][r] + bv[q][r];
-              if (MODE == F32_RELU) x = x < 0.f ? 0.f : x;   // torch.relu: a NaN stays NaN
+              if (RELU) x = x < 0.f ? 0.f : x;   // torch.relu: a NaN stays NaN
               if (BWD) x = av[iq][q][r] > 0.f ? x : 0.f;
               v[r] = x;
+              if (HEAD) hd[im] = fmaf(x, hw[q][r], hd[im]);
             }
             if (row < p.M) *reinterpret_cast<float4_t*>(C + row * p.ldc + col) = v;
           }
         }
       }
     }
+    if (HEAD) {
+      // the 4 lanes of a row (g = 0..3) by xor-shuffles, then the row's 4 wave quarters (ewn) through
+      // LDS in buffer 1 (free: the last K-tile's reads are done, the next tile's K-tile 0 goes to buffer
+      // 0); one thread per row sums them in quarter order
+      float* part = reinterpret_cast<float*>(smem + TILE_U4);
+#pragma unroll
+      for (int im = 0; im < 8; ++im) {
+        float d = hd[im];
+        d += __shfl_xor(d, 16, 64);
+        d += __shfl_xor(d, 32, 64);
+        if (eg == 0) part[(ewm * 128 + im * 16 + eli) * 4 + ewn] = d;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+      if (etid < 256 && m0 + etid < p.M) {
+        const float4_t q4 = *reinterpret_cast<const float4_t*>(part + etid * 4);
+        p.head_part[(n0 / FT) * p.head_ld + m0 + etid] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+      }
+    }
     if (!pf) return;
     t = t_next; m0 = m1; n0 = n1;
-    // the bias image is rewritten by the next tile's DMA: every wave has read it above
+    // the bias / head-weight images (and the head partials in buffer 1) are rewritten by the next
+    // tile's DMA: every wave has read them above
     barrier();
   }
 }
@@ -285,8 +327,9 @@ int llp_cu_count();
 // wave of tiles.  mode: LLP_ACT_RELU / LLP_ACT_NONE / LLP_ACT_RELU_BWD (f32 aux activations).
 int llp_gemm_nt_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, float* C,
                         int64_t ldc, const float* bias, int act, const float* aux, int64_t ld_aux, float alpha,
-                        hipStream_t s) {
+                        hipStream_t s, const float* head_w, float* head_part) {
   PF32 p;
+  p.head_w = head_w; p.head_part = head_part; p.head_ld = M;
   p.A = (const float*)A->ptr; p.lda = A->ld;
   p.B = (const float*)B->ptr; p.ldb = B->ld;
   p.M = M; p.N = N; p.K = K;
@@ -296,7 +339,8 @@ int llp_gemm_nt_f32_256(const llp_operand* A, const llp_operand* B, int64_t M, i
   const int64_t tiles = ((M + FT - 1) / FT + 7) / 8 * 8 * (N / FT);
   const int cus = llp_cu_count();
   const dim3 grid((unsigned)(tiles < cus ? tiles : cus)), block(FNT);
-  if (act == LLP_ACT_RELU) hipLaunchKernelGGL(gemm_nt_f32_pp8p<F32_RELU>, grid, block, 0, s, p);
+  if (head_w) hipLaunchKernelGGL(gemm_nt_f32_pp8p<F32_HEAD>, grid, block, 0, s, p);   // (ReLU + head)
+  else if (act == LLP_ACT_RELU) hipLaunchKernelGGL(gemm_nt_f32_pp8p<F32_RELU>, grid, block, 0, s, p);
   else if (act == LLP_ACT_RELU_BWD) hipLaunchKernelGGL(gemm_nt_f32_pp8p<F32_BWD>, grid, block, 0, s, p);
   else hipLaunchKernelGGL(gemm_nt_f32_pp8p<F32_NONE>, grid, block, 0, s, p);
   return (int)hipGetLastError();

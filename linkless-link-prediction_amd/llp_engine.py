@@ -383,8 +383,12 @@ class EngineBase:
         key = (self.seed ^ 0xD0D0 ^ (int(module) << 40)) & 0xFFFFFFFFFFFFFFFF
         return K.Dropout(float(p), key, self.step_ctr.data_ptr(), 1 + layer)
 
-    def _fusable(self, K_in, N_out):
-        return self.dtype == torch.bfloat16 and K_in % 64 == 0 and N_out % 8 == 0
+    def _fusable(self, K_in, N_out, p_drop=0.0):
+        """The last predictor layer's GEMM can carry the Linear(H,1) head: bf16 (any dropout), or
+        fp32 without dropout on the persistent f32 kernel's shapes (N % 256 == 0)."""
+        if self.dtype == torch.bfloat16:
+            return K_in % 64 == 0 and N_out % 8 == 0
+        return K_in % 64 == 0 and N_out % 256 == 0 and float(p_drop) == 0.0
 
     # ------------------------------------------------------------------ negatives
     def _neg_setup(self):
@@ -490,12 +494,17 @@ class EngineBase:
         for l, lin in enumerate(self.prd):
             out = self._buf(f"Z{l}", (R2, lin.out_f), dt)
             last = l == len(self.prd) - 1
-            if last and self._fusable(lin.in_f, lin.out_f) and (A0 is not A or zin_ok):
+            if last and self._fusable(lin.in_f, lin.out_f, p_drop) and (A0 is not A or zin_ok):
                 # last hidden layer + Linear(H,1) head in one GEMM (partials per 256 columns)
                 parts = K.head_parts(lin.out_f)
                 hpart = self._buf("hpart", (parts, R2), torch.float32)
-                K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out, self.head.weight.data.view(-1),
-                               hpart, bias=lin.b, act=K.ACT_RELU, dropout=self._dropout(p_drop, DROP_PREDICTOR, l))
+                if dt == torch.float32:   # the persistent f32 kernel's head epilogue (no dropout)
+                    K.gemm_nt_head_f32(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out,
+                                       self.head.weight.data.view(-1), hpart, bias=lin.b)
+                else:
+                    K.gemm_nt_head(A, K.operand(lin.Wcomp), R2, lin.out_f, lin.in_f, out,
+                                   self.head.weight.data.view(-1), hpart, bias=lin.b, act=K.ACT_RELU,
+                                   dropout=self._dropout(p_drop, DROP_PREDICTOR, l))
                 if defer_head:
                     self._s_head = K.head_in(hpart, parts, R2, self.head.bias.data)
                 else:
@@ -1694,17 +1703,22 @@ class DistillEngine(EngineBase):
             K.head_fwd(self.t_h, R, self.t_h.shape[1], None, None, prob=t_r, Z2=self.t_h, iz=t_ia, iz2=t_ib)
             return
         Ht = self.t_h.shape[1]
-        if len(self.t_hidden) == 1 and self._fusable(Ht, self.t_hidden[0][0].shape[0]):
-            # t_h[a] * t_h[c] materialised, then hidden layer + head in one GEMM; the
-            # hidden activations are never stored (no backward through the teacher)
+        if len(self.t_hidden) == 1 and self._fusable(Ht, self.t_hidden[0][0].shape[0], self.t_dropout):
+            # t_h[a] * t_h[c] materialised, then hidden layer + head in one GEMM; the bf16
+            # hidden activations are never stored (no backward through the teacher); the f32
+            # kernel's head epilogue stores them (one pass instead of the head's second read)
             tin = self._buf("Tin", (R, Ht), dt)
             K.hadamard_rows(self.t_h, t_ia, self.t_h, t_ib, tin)
             W, b = self.t_hidden[0]
             w2, b2 = self.t_head
             parts = K.head_parts(W.shape[0])
             tpart = self._buf("tpart", (parts, R), torch.float32)
-            K.gemm_nt_head(K.operand(tin), K.operand(W), R, W.shape[0], W.shape[1], None, w2, tpart, bias=b,
-                           act=K.ACT_RELU, dropout=self._dropout(self.t_dropout, DROP_TEACHER_PRED, 0))
+            if dt == torch.float32:
+                K.gemm_nt_head_f32(K.operand(tin), K.operand(W), R, W.shape[0], W.shape[1],
+                                   self._buf("T0", (R, W.shape[0]), dt), w2, tpart, bias=b)
+            else:
+                K.gemm_nt_head(K.operand(tin), K.operand(W), R, W.shape[0], W.shape[1], None, w2, tpart, bias=b,
+                               act=K.ACT_RELU, dropout=self._dropout(self.t_dropout, DROP_TEACHER_PRED, 0))
             if defer_head:
                 self._t_head = K.head_in(tpart, parts, R, b2)
             else:

@@ -72,6 +72,8 @@ _SIGS = {
                               c_i64, c_vp]),
     "llp_spmm_tn": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
     "llp_spmm_heavy_nnz": (c_int, []),
+    "llp_gemm_nt_head_f32": (c_int, [c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_vp,
+                                     c_vp, c_vp, c_vp]),
     "llp_spmm_rows_dt": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64,
                                  c_vp, c_i64, c_vp]),
     "llp_spmm_tn_dt": (c_int, [c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int,
@@ -283,6 +285,13 @@ def gemm_nt_head(A: Operand, B: Operand, M, N, K, C_out, head_w, head_part, bias
     check(L.llp_gemm_nt_head(M, N, K, C.byref(A), C.byref(B), ptr(C_out), C_out.stride(0) if C_out is not None else 0,
                              ptr(bias), act, alpha, C.byref(dropout) if dropout is not None else None, head_w.data_ptr(),
                              head_part.data_ptr(), stream_ptr()), "llp_gemm_nt_head")
+
+
+def gemm_nt_head_f32(A: Operand, B: Operand, M, N, K, C_out, head_w, head_part, bias=None):
+    """f32 GEMM + ReLU with the Linear(N,1) head's per-256-column partials fused (llp_gemm_nt_head_f32)."""
+    L = lib()
+    check(L.llp_gemm_nt_head_f32(M, N, K, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0), ptr(bias),
+                                 head_w.data_ptr(), head_part.data_ptr(), stream_ptr()), "llp_gemm_nt_head_f32")
 
 
 def head_finish(parts, M, head_part, b, logit=None, prob=None):

@@ -171,6 +171,34 @@ def test_gemm_nt_head_lean(M, N, Kd):
     assert torch.allclose(got, ref, rtol=1e-4, atol=1e-4 * (1 + ref.abs().max().item())), (got - ref).abs().max()
 
 
+@pytest.mark.parametrize("M,N,Kd", [(70_000, 256, 256), (20_000, 1024, 1024), (66_000, 512, 128)])
+def test_gemm_nt_head_f32(M, N, Kd):
+    """fp32 fused head (llp_gemm_nt_head_f32, the persistent f32 kernel's F32_HEAD epilogue): C equals
+    the plain ReLU launch bit for bit (the same MFMAs and epilogue values), the head partials summed
+    over the column tiles equal relu(y) @ hw within f32 summation-order tolerance, and repeated
+    launches are bit-identical (a fixed summation order)."""
+    k = K()
+    g = torch.Generator().manual_seed(M + N)
+    A = (torch.randn(M, Kd, generator=g) * 0.5).to(DEV)
+    W = (torch.randn(N, Kd, generator=g) * (1.0 / Kd ** 0.5)).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    hw = torch.randn(N, generator=g).to(DEV)
+    parts = k.head_parts(N)
+    C0 = torch.empty(M, N, device=DEV)
+    k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, C0, k.LLP_F32, bias=b, act=k.ACT_RELU)
+    C1 = torch.empty(M, N, device=DEV)
+    h1 = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head_f32(k.operand(A), k.operand(W), M, N, Kd, C1, hw, h1, bias=b)
+    h2 = torch.empty(parts, M, device=DEV)
+    k.gemm_nt_head_f32(k.operand(A), k.operand(W), M, N, Kd, torch.empty(M, N, device=DEV), hw, h2, bias=b)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C0)
+    assert torch.equal(h1, h2)
+    ref = C0.double() @ hw.double()
+    got = h1.double().sum(0)
+    assert torch.allclose(got, ref, rtol=1e-5, atol=1e-5 * (1 + ref.abs().max().item())), (got - ref).abs().max()
+
+
 def test_gemm_nt_relu_lean_and_generic_agree_with_nan():
     """ReLU forward: full 256 x 256 tiles take the lean epilogue (int16 max on the rounded
     pair), partial tiles the generic one (f32); both follow the sign-bit rule, so the same
