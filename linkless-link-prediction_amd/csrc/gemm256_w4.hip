@@ -99,7 +99,9 @@ __device__ __forceinline__ void w4_sfor(F&& f) {
   w4_sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int MODE>
+// DIAG (diagnostic A/B builds through llp_gemm_nt_w4_probe only; wrong outputs): bit 1 no
+// staging loads in the loop, 2 no staging writes, 4 no barrier, 8 no fragment reads, 16 no epilogue
+template <int MODE, int DIAG = 0>
 __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
   constexpr bool RELU = MODE == W_RELU;
   constexpr bool BWD = MODE == W_BWD;
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
   w4_u32x4 stg[2][16];   // (a native vector type: hipcc keeps HIP_vector_type arrays in scratch)
   auto load_piece = [&](auto SET, auto I) __attribute__((always_inline)) {
     constexpr int set = decltype(SET)::value, i = decltype(I)::value;
+    if constexpr (DIAG & 1) return;
     if constexpr (i < 8) {
       const uint32_t u = (uint32_t)(((ls_m0 + 8 * i) * p.lda + ls_k * WK) * 2);
       stg[set][i] = __builtin_bit_cast(w4_u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(vA + u), 0, 0));
@@ -189,6 +192,7 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
     constexpr int set = decltype(SET)::value, slot = decltype(SLOT)::value, i = decltype(I)::value;
     constexpr int ii = i & 7;
     constexpr uint32_t c = (uint32_t)(ii * 1024 + slot * WSLOT + (i >= 8 ? WB_OFF : 0));
+    if constexpr (DIAG & 2) return;
     *reinterpret_cast<w4_lds_u4*>(sb + woff[ii & 1] + c) = stg[set][i];
   };
   // fragment read offsets (slot 0) per k-step: row (lane % 32) of a 32-row block, logical chunk
@@ -204,6 +208,7 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
   auto read_frag = [&](auto F, auto IDX, auto SLOT, auto KS) __attribute__((always_inline)) {
     constexpr int f = decltype(F)::value, idx = decltype(IDX)::value, slot = decltype(SLOT)::value;
     constexpr int ks = decltype(KS)::value;
+    if constexpr (DIAG & 8) return;
     if constexpr (idx < 4)
       fa[f][idx] = *reinterpret_cast<w4_lds_s8*>(sb + roffA[ks] + (uint32_t)(slot * WSLOT + idx * 4096));
     else
@@ -286,6 +291,9 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
     // states).  Lane (l32, hi) of block (im, jn): row m0 + 128 wm + 32 im + l32, columns
     // n0 + 128 wn + 32 jn + 8 q + 4 hi + (0..3) for q = 0..3 (values 4 q .. 4 q + 3).
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    if constexpr ((DIAG & 16) != 0) {
+      // (the MFMAs are volatile asm: skipping the epilogue deletes none of them)
+    } else {
     // per lane: row m0 + 128 wm + 32 im + l32; columns cb + 8 q + 4 hi + (0..3), cb = n0 + 128 wn + 32 jn
     const int64_t row0 = m0 + 128 * wm + l32;
     const int64_t col0 = n0 + 128 * wn + 4 * hi;
@@ -342,6 +350,7 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
         }
       });
     });
+    }
     int64_t t_next = t_cur + gridDim.x;
     if (!next_tile(t_next, m0, n0)) return;
     t_cur = t_next;
@@ -355,7 +364,7 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
 // ld_mask % 4 == 0).  act: LLP_ACT_RELU (optional mask out), LLP_ACT_NONE, LLP_ACT_RELU_BWD (mask in).
 int llp_gemm_nt_bf16_w4(const llp_operand* A, const llp_operand* B, int64_t M, int64_t N, int64_t K, void* C,
                         int64_t ldc, const float* bias, int act, float alpha, uint8_t* mask_out,
-                        const uint8_t* mask_in, int64_t ld_mask, hipStream_t s) {
+                        const uint8_t* mask_in, int64_t ld_mask, hipStream_t s, int diag = 0) {
   PW4 p;
   p.A = (const bf16_t*)A->ptr; p.lda = A->ld;
   p.B = (const bf16_t*)B->ptr; p.ldb = B->ld;
@@ -367,6 +376,19 @@ int llp_gemm_nt_bf16_w4(const llp_operand* A, const llp_operand* B, int64_t M, i
   const int64_t tiles = ((M + WT - 1) / WT + 7) / 8 * 8 * (N / WT);
   const int cus = llp_cu_count();
   const dim3 grid((unsigned)(tiles < cus ? tiles : cus)), block(WTHR);
+  if (diag) {   // diagnostic builds of the plain mode (llp_gemm_nt_w4_probe)
+    switch (diag) {
+      case 1: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 1>), grid, block, 0, s, p); break;
+      case 2: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 2>), grid, block, 0, s, p); break;
+      case 3: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 3>), grid, block, 0, s, p); break;
+      case 4: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 4>), grid, block, 0, s, p); break;
+      case 8: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 8>), grid, block, 0, s, p); break;
+      case 15: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 15>), grid, block, 0, s, p); break;
+      case 16: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 16>), grid, block, 0, s, p); break;
+      default: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 31>), grid, block, 0, s, p); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (act == LLP_ACT_RELU) hipLaunchKernelGGL(gemm_nt_bf16_w4<W_RELU>, grid, block, 0, s, p);
   else if (act == LLP_ACT_RELU_BWD) hipLaunchKernelGGL(gemm_nt_bf16_w4<W_BWD>, grid, block, 0, s, p);
   else hipLaunchKernelGGL(gemm_nt_bf16_w4<W_NONE>, grid, block, 0, s, p);
@@ -376,7 +398,7 @@ int llp_gemm_nt_bf16_w4(const llp_operand* A, const llp_operand* B, int64_t M, i
 // Diagnostic entry for A/B runs (tools/w4_bench.py): the kernel above on plain device pointers.
 extern "C" int llp_gemm_nt_w4_probe(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N,
                                     int64_t K, void* C, int64_t ldc, const float* bias, int act, float alpha,
-                                    void* mask_out, const void* mask_in, int64_t ld_mask, void* stream) {
+                                    void* mask_out, const void* mask_in, int64_t ld_mask, int diag, void* stream) {
   LLP_CHECK_ARG(A && B && C && N % 256 == 0 && N <= 4096 && K % 128 == 0 && K > 0 && M > 0 && lda % 8 == 0 &&
                     ldb % 8 == 0 && ldc % 8 == 0 && (!mask_out || ld_mask % 4 == 0) &&
                     (act != LLP_ACT_RELU_BWD || (mask_in && ld_mask % 4 == 0)),
@@ -385,7 +407,7 @@ extern "C" int llp_gemm_nt_w4_probe(const void* A, int64_t lda, const void* B, i
   a.ptr = A; a.ld = lda;
   b.ptr = B; b.ld = ldb;
   const int rc = llp_gemm_nt_bf16_w4(&a, &b, M, N, K, C, ldc, bias, act, alpha, (uint8_t*)mask_out,
-                                     (const uint8_t*)mask_in, ld_mask, (hipStream_t)stream);
+                                     (const uint8_t*)mask_in, ld_mask, (hipStream_t)stream, diag);
   if (rc != 0) return llp::set_error(rc, "llp_gemm_nt_w4_probe: %s", hipGetErrorString((hipError_t)rc));
   return LLP_OK;
 }

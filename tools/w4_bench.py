@@ -17,15 +17,15 @@ L = K.lib()
 L.llp_gemm_nt_w4_probe.restype = C.c_int
 L.llp_gemm_nt_w4_probe.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                    C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_float, C.c_void_p, C.c_void_p,
-                                   C.c_int64, C.c_void_p]
+                                   C.c_int64, C.c_int, C.c_void_p]
 dev = torch.device("cuda", 0)
 
 
-def w4(A, W, M, N, Kd, Cout, bias=None, act=K.ACT_RELU, alpha=1.0, mask_out=None, mask_in=None):
+def w4(A, W, M, N, Kd, Cout, bias=None, act=K.ACT_RELU, alpha=1.0, mask_out=None, mask_in=None, diag=0):
     ldm = (mask_out if mask_out is not None else mask_in).stride(0) if (mask_out is not None or mask_in is not None) else 0
     K.check(L.llp_gemm_nt_w4_probe(A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), M, N, Kd, Cout.data_ptr(),
                                    Cout.stride(0), K.ptr(bias), act, alpha, K.ptr(mask_out), K.ptr(mask_in), ldm,
-                                   K.stream_ptr()), "llp_gemm_nt_w4_probe")
+                                   diag, K.stream_ptr()), "llp_gemm_nt_w4_probe")
 
 
 def bits_of(mask, N):
@@ -98,7 +98,9 @@ for M in (225_280, 235_868):
                                                act=K.ACT_RELU, aux=mk)),
                      ("w4", lambda: w4(A, W, M, N, Kd, Cb, bias=b, act=K.ACT_RELU, mask_out=mk)),
                      ("w4_none", lambda: w4(A, W, M, N, Kd, Cb, act=K.ACT_NONE)),
-                     ("w4_bwd", lambda: w4(A, W, M, N, Kd, Cb, act=K.ACT_RELU_BWD, mask_in=mk))):
+                     ("w4_bwd", lambda: w4(A, W, M, N, Kd, Cb, act=K.ACT_RELU_BWD, mask_in=mk)),
+                     *[(f"w4_diag{d}", (lambda d=d: w4(A, W, M, N, Kd, Cb, act=K.ACT_NONE, diag=d)))
+                       for d in (1, 2, 3, 4, 8, 15, 16, 31)]):
         ms = timeit(fn)
         res[name] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
     print(json.dumps(res), flush=True)
