@@ -239,43 +239,39 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
   w4_sfor<8>([&](auto I) __attribute__((always_inline)) { read_frag(C0{}, I, C0{}, C0{}); });
 
   // one K-tile in slot S (compile-time), its k-step-0 fragments in set 0 on entry; leaves the
-  // next K-tile's k-step-0 fragments in set 0, its data in slot 1 - S, K-tile + 3 in flight
+  // next K-tile's k-step-0 fragments in set 0, its data in slot 1 - S, K-tile + 3 in flight.
+  // Flat schedule over the K-tile's 64 MFMAs (J = 16 ks + j; set ks & 1 holds k-step ks):
+  //  * J = 2i (i < 16): ds_write staging piece i of the next K-tile (set 1 - S) into slot 1 - S
+  //    (free since the last barrier); J = 2i + 1: reload that register with piece i of K-tile + 3;
+  //  * even j of k-steps 0-2: one fragment read of k-step ks + 1 (set (ks + 1) & 1), in the order
+  //    the next k-step's MFMAs take them (a0, b0, b1, b2, b3, a1, a2, a3);
+  //  * after MFMA 51 (k-step 3, j = 3): lgkmcnt(0) + barrier (every wave's writes of the next
+  //    K-tile and reads of this one are done), then J = 52..59: the next K-tile's k-step-0 reads.
   auto kiter = [&](auto S_, auto FIRST_) __attribute__((always_inline)) {
     constexpr int S = decltype(S_)::value;
     using NS = std::integral_constant<int, 1 - S>;
-    // k-step 0 (set 0); k-step 1's fragments into set 1
-    w4_sfor<16>([&](auto J) __attribute__((always_inline)) {
-      mfma_j(C0{}, J, FIRST_);
-      if constexpr (!(decltype(J)::value & 1))
-        read_frag(C1{}, std::integral_constant<int, (decltype(J)::value >> 1)>{}, S_, C1{});
-    });
-    // k-step 1 (set 1); k-step 2's fragments into set 0
-    w4_sfor<16>([&](auto J) __attribute__((always_inline)) {
-      mfma_j(C1{}, J, NO{});
-      if constexpr (!(decltype(J)::value & 1))
-        read_frag(C0{}, std::integral_constant<int, (decltype(J)::value >> 1)>{}, S_, std::integral_constant<int, 2>{});
-    });
-    // k-step 2 (set 0); k-step 3's fragments into set 1; the next K-tile (staging set 1 - S)
-    // into slot 1 - S (every wave finished reading that slot before the last barrier)
-    w4_sfor<16>([&](auto J) __attribute__((always_inline)) {
-      mfma_j(C0{}, J, NO{});
-      write_piece(NS{}, NS{}, J);
-      if constexpr (!(decltype(J)::value & 1))
-        read_frag(C1{}, std::integral_constant<int, (decltype(J)::value >> 1)>{}, S_, std::integral_constant<int, 3>{});
-    });
-    // k-step 3 (set 1); K-tile + 3 into staging set 1 - S; after 8 MFMAs every wave's writes of the
-    // next K-tile and reads of this one are done (barrier), then the next K-tile's k-step-0 fragments
-    w4_sfor<8>([&](auto J) __attribute__((always_inline)) {
-      mfma_j(C1{}, J, NO{});
-      load_piece(NS{}, std::integral_constant<int, 2 * decltype(J)::value>{});
-      load_piece(NS{}, std::integral_constant<int, 2 * decltype(J)::value + 1>{});
-    });
-    ls_advance();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    w4_sfor<8>([&](auto J) __attribute__((always_inline)) {
-      mfma_j(C1{}, std::integral_constant<int, decltype(J)::value + 8>{}, NO{});
-      read_frag(C0{}, J, NS{}, C0{});
+    w4_sfor<64>([&](auto J_) __attribute__((always_inline)) {
+      constexpr int J = decltype(J_)::value;
+      constexpr int ks = J / 16, j = J % 16;
+      constexpr int ridx_tab[8] = {0, 4, 5, 6, 7, 1, 2, 3};   // a0 b0 b1 b2 b3 a1 a2 a3
+      if constexpr (ks == 0)
+        mfma_j(C0{}, std::integral_constant<int, j>{}, FIRST_);
+      else
+        mfma_j(std::integral_constant<int, ks & 1>{}, std::integral_constant<int, j>{}, NO{});
+      if constexpr (J < 32) {
+        if constexpr ((J & 1) == 0) write_piece(NS{}, NS{}, std::integral_constant<int, J / 2>{});
+        else load_piece(NS{}, std::integral_constant<int, J / 2>{});
+      }
+      if constexpr (J == 31) ls_advance();
+      if constexpr (ks < 3 && (j & 1) == 0)
+        read_frag(std::integral_constant<int, (ks + 1) & 1>{}, std::integral_constant<int, ridx_tab[j / 2]>{}, S_,
+                  std::integral_constant<int, ks + 1>{});
+      if constexpr (J == 51) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(DIAG & 4)) __builtin_amdgcn_s_barrier();
+      }
+      if constexpr (J >= 52 && J < 60)
+        read_frag(C0{}, std::integral_constant<int, ridx_tab[J - 52]>{}, NS{}, C0{});
     });
   };
 
@@ -385,6 +381,12 @@ int llp_gemm_nt_bf16_w4(const llp_operand* A, const llp_operand* B, int64_t M, i
       case 8: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 8>), grid, block, 0, s, p); break;
       case 15: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 15>), grid, block, 0, s, p); break;
       case 16: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 16>), grid, block, 0, s, p); break;
+      case 17: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 17>), grid, block, 0, s, p); break;
+      case 18: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 18>), grid, block, 0, s, p); break;
+      case 19: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 19>), grid, block, 0, s, p); break;
+      case 20: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 20>), grid, block, 0, s, p); break;
+      case 23: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 23>), grid, block, 0, s, p); break;
+      case 24: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 24>), grid, block, 0, s, p); break;
       default: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 31>), grid, block, 0, s, p); break;
     }
     return (int)hipGetLastError();

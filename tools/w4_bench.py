@@ -84,7 +84,7 @@ ok = all(check(M, N, Kd, i) for i, (M, N, Kd) in enumerate([(256, 256, 128), (10
                                                               (5_000, 256, 1024)]))
 if not ok:
     sys.exit(1)
-for M in (225_280, 235_868):
+for M in (225_280,):
     N = Kd = 1024
     g = torch.Generator(device="cpu").manual_seed(3)
     A = (torch.randn(M, Kd, generator=g) * 0.5).to(torch.bfloat16).to(dev)
@@ -100,7 +100,7 @@ for M in (225_280, 235_868):
                      ("w4_none", lambda: w4(A, W, M, N, Kd, Cb, act=K.ACT_NONE)),
                      ("w4_bwd", lambda: w4(A, W, M, N, Kd, Cb, act=K.ACT_RELU_BWD, mask_in=mk)),
                      *[(f"w4_diag{d}", (lambda d=d: w4(A, W, M, N, Kd, Cb, act=K.ACT_NONE, diag=d)))
-                       for d in (1, 2, 3, 4, 8, 15, 16, 31)]):
+                       for d in (16, 17, 18, 19, 20, 23, 24, 31)]):
         ms = timeit(fn)
         res[name] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
     print(json.dumps(res), flush=True)
