@@ -263,9 +263,14 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
         else load_piece(NS{}, std::integral_constant<int, J / 2>{});
       }
       if constexpr (J == 31) ls_advance();
-      if constexpr (ks < 3 && (j & 1) == 0)
+      if constexpr (DIAG & 32) {   // A/B: the next k-step's reads on MFMAs 0-7 (one per gap)
+        if constexpr (ks < 3 && j < 8)
+          read_frag(std::integral_constant<int, (ks + 1) & 1>{}, std::integral_constant<int, ridx_tab[j]>{}, S_,
+                    std::integral_constant<int, ks + 1>{});
+      } else if constexpr (ks < 3 && (j & 1) == 0) {
         read_frag(std::integral_constant<int, (ks + 1) & 1>{}, std::integral_constant<int, ridx_tab[j / 2]>{}, S_,
                   std::integral_constant<int, ks + 1>{});
+      }
       if constexpr (J == 51) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (!(DIAG & 4)) __builtin_amdgcn_s_barrier();
@@ -387,6 +392,9 @@ int llp_gemm_nt_bf16_w4(const llp_operand* A, const llp_operand* B, int64_t M, i
       case 20: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 20>), grid, block, 0, s, p); break;
       case 23: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 23>), grid, block, 0, s, p); break;
       case 24: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 24>), grid, block, 0, s, p); break;
+      case 48: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 48>), grid, block, 0, s, p); break;
+      case 55: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 55>), grid, block, 0, s, p); break;
+      case 32: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 32>), grid, block, 0, s, p); break;
       default: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 31>), grid, block, 0, s, p); break;
     }
     return (int)hipGetLastError();
