@@ -90,6 +90,12 @@ __device__ __forceinline__ uint32_t w4_relu_pk(uint32_t x) {   // sign-bit ReLU 
 
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1 (every register-array index
 // below must be a constant, or hipcc moves the staging / fragment arrays to scratch)
+__device__ __forceinline__ uint32_t w4_nz_pk(uint32_t x) {   // v_pk_min_u16(x, 1): 1 per nonzero half
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, 1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 template <typename F, int... I>
 __device__ __forceinline__ void w4_sfor_impl(F& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
@@ -241,8 +247,10 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
   // one K-tile in slot S (compile-time), its k-step-0 fragments in set 0 on entry; leaves the
   // next K-tile's k-step-0 fragments in set 0, its data in slot 1 - S, K-tile + 3 in flight.
   // Flat schedule over the K-tile's 64 MFMAs (J = 16 ks + j; set ks & 1 holds k-step ks):
-  //  * J = 2i (i < 16): ds_write staging piece i of the next K-tile (set 1 - S) into slot 1 - S
-  //    (free since the last barrier); J = 2i + 1: reload that register with piece i of K-tile + 3;
+  //  * J = 3i (i < 16): ds_write staging piece i of the next K-tile (set 1 - S) into slot 1 - S
+  //    (free since the last barrier); J = 3i + 1: reload that register with piece i of K-tile + 3
+  //    (spread over k-steps 0-2: writes and reads together at one LDS op per gap saturated the
+  //    LDS queue, SQ_WAIT_INST_LDS 18 % of wave cycles);
   //  * even j of k-steps 0-2: one fragment read of k-step ks + 1 (set (ks + 1) & 1), in the order
   //    the next k-step's MFMAs take them (a0, b0, b1, b2, b3, a1, a2, a3);
   //  * after MFMA 51 (k-step 3, j = 3): lgkmcnt(0) + barrier (every wave's writes of the next
@@ -258,11 +266,11 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
         mfma_j(C0{}, std::integral_constant<int, j>{}, FIRST_);
       else
         mfma_j(std::integral_constant<int, ks & 1>{}, std::integral_constant<int, j>{}, NO{});
-      if constexpr (J < 32) {
-        if constexpr ((J & 1) == 0) write_piece(NS{}, NS{}, std::integral_constant<int, J / 2>{});
-        else load_piece(NS{}, std::integral_constant<int, J / 2>{});
+      if constexpr (J < 48) {   // one staging piece per 3 MFMAs: LDS at <= 0.75 ops per MFMA gap
+        if constexpr (J % 3 == 0) write_piece(NS{}, NS{}, std::integral_constant<int, J / 3>{});
+        else if constexpr (J % 3 == 1) load_piece(NS{}, std::integral_constant<int, J / 3>{});
       }
-      if constexpr (J == 31) ls_advance();
+      if constexpr (J == 46) ls_advance();
       if constexpr (DIAG & 32) {   // A/B: the next k-step's reads on MFMAs 0-7 (one per gap)
         if constexpr (ks < 3 && j < 8)
           read_frag(std::integral_constant<int, (ks + 1) & 1>{}, std::integral_constant<int, ridx_tab[j]>{}, S_,
@@ -341,12 +349,15 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
           if (RELU) {
             lo = w4_relu_pk(lo);
             h2 = w4_relu_pk(h2);
-            const uint32_t nib = ((lo & 0xFFFFu) ? 1u : 0u) | ((lo >> 16) ? 2u : 0u) | ((h2 & 0xFFFFu) ? 4u : 0u) |
-                                 ((h2 >> 16) ? 8u : 0u);
-            mbits[jn] |= nib << (8 * q + 4 * hi);
+            // nonzero flags of the 4 (non-negative) bf16 as bits 0-3: v_pk_min_u16(x, 1) per pair puts
+            // them at bits 0 / 16 and 2 / 18, one fold brings 16 / 18 down to 1 / 3 (pp8p's trick)
+            const uint32_t u = w4_nz_pk(lo) | (w4_nz_pk(h2) << 2);
+            mbits[jn] |= ((u | (u >> 15)) & 0xFu) << (8 * q + 4 * hi);
           }
-          *reinterpret_cast<__attribute__((address_space(3))) w4_u32x2*>(wr + 2 * (32 * jn + 8 * q)) =
-              (w4_u32x2){lo, h2};
+          if constexpr ((DIAG & 128) != 0) asm volatile("" ::"v"(lo), "v"(h2));   // diagnostic: no staging
+          else
+            *reinterpret_cast<__attribute__((address_space(3))) w4_u32x2*>(wr + 2 * (32 * jn + 8 * q)) =
+                (w4_u32x2){lo, h2};
         }
       });
       if (RELU && p.mask_out) {   // the row's 16 mask bytes from lanes l32 and l32 + 32
@@ -363,7 +374,8 @@ __global__ __launch_bounds__(WTHR, 1) void gemm_nt_bf16_w4(PW4 p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const w4_u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) w4_u32x4*>(rd + i * 4 * ES);
-        if (srow0 + 4 * i < M_live) __builtin_nontemporal_store(v, reinterpret_cast<w4_u32x4*>(cst + 4 * i * p.ldc));
+        if constexpr ((DIAG & 64) != 0) asm volatile("" ::"v"(v));   // diagnostic: staged, not stored
+        else if (srow0 + 4 * i < M_live) __builtin_nontemporal_store(v, reinterpret_cast<w4_u32x4*>(cst + 4 * i * p.ldc));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's writes
       __builtin_amdgcn_wave_barrier();
@@ -412,6 +424,8 @@ int llp_gemm_nt_bf16_w4(const llp_operand* A, const llp_operand* B, int64_t M, i
       case 23: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 23>), grid, block, 0, s, p); break;
       case 24: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 24>), grid, block, 0, s, p); break;
       case 48: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 48>), grid, block, 0, s, p); break;
+      case 64: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 64>), grid, block, 0, s, p); break;
+      case 192: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 192>), grid, block, 0, s, p); break;
       case 55: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 55>), grid, block, 0, s, p); break;
       case 32: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 32>), grid, block, 0, s, p); break;
       default: hipLaunchKernelGGL((gemm_nt_bf16_w4<W_NONE, 31>), grid, block, 0, s, p); break;
