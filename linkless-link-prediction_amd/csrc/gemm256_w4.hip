@@ -90,9 +90,9 @@ __device__ __forceinline__ uint32_t w4_relu_pk(uint32_t x) {   // sign-bit ReLU 
 
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1 (every register-array index
 // below must be a constant, or hipcc moves the staging / fragment arrays to scratch)
-__device__ __forceinline__ uint32_t w4_nz_pk(uint32_t x) {   // v_pk_min_u16(x, 1): 1 per nonzero half
-  uint32_t r;
-  asm("v_pk_min_u16 %0, %1, 1" : "=v"(r) : "v"(x));
+__device__ __forceinline__ uint32_t w4_nz_pk(uint32_t x) {   // v_pk_min_u16(x, 0x00010001): 1 per nonzero half
+  uint32_t r;   // (an inline constant 1 would reach the low half only: op_sel_hi takes its upper 16 bits)
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(x), "s"(0x00010001u));
   return r;
 }
 
