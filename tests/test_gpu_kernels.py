@@ -199,6 +199,52 @@ def test_gemm_nt_head_f32(M, N, Kd):
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-5 * (1 + ref.abs().max().item())), (got - ref).abs().max()
 
 
+@pytest.mark.parametrize("M,N,Kd", [(70_001, 1024, 1024), (5_000, 256, 128)])
+def test_gemm_nt_w4_bit_identical(M, N, Kd):
+    """The one-wave-per-SIMD NT kernel (csrc/gemm256_w4.hip, diagnostic entry llp_gemm_nt_w4_probe;
+    DESIGN.md §4.1, measured slower, not dispatched) against the shipped persistent kernel: ReLU +
+    bias + bit mask, plain, and ReLU-mask backward outputs bit-identical (a partial last m-tile
+    included), so its A/B timings compare like for like."""
+    import ctypes as C
+    k = K()
+    L = k.lib()
+    L.llp_gemm_nt_w4_probe.restype = C.c_int
+    L.llp_gemm_nt_w4_probe.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_float, C.c_void_p, C.c_void_p,
+                                       C.c_int64, C.c_int, C.c_void_p]
+    g = torch.Generator().manual_seed(M)
+    A = (torch.randn(M, Kd, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * (1.0 / Kd ** 0.5)).to(DEV, torch.bfloat16)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+
+    def w4(C_, act, bias=None, alpha=1.0, mo=None, mi=None):
+        m = mo if mo is not None else mi
+        k.check(L.llp_gemm_nt_w4_probe(A.data_ptr(), Kd, W.data_ptr(), Kd, M, N, Kd, C_.data_ptr(), N, k.ptr(bias), act,
+                                       alpha, k.ptr(mo), k.ptr(mi), m.stride(0) if m is not None else 0, 0,
+                                       k.stream_ptr()), "llp_gemm_nt_w4_probe")
+
+    outs = {}
+    for name in ("pp8p", "w4"):
+        Cr = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        mr = torch.zeros(M, N // 8, device=DEV, dtype=torch.uint8)
+        Cn = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        Cb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        if name == "pp8p":
+            k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, Cr, k.LLP_BF16, bias=b, act=k.ACT_RELU, aux=mr)
+            k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, Cn, k.LLP_BF16)
+            k.gemm_nt(k.operand(A), k.operand(W), M, N, Kd, Cb, k.LLP_BF16, act=k.ACT_RELU_BWD, aux=mr, alpha=2.0)
+        else:
+            w4(Cr, k.ACT_RELU, bias=b, mo=mr)
+            w4(Cn, k.ACT_NONE)
+            w4(Cb, k.ACT_RELU_BWD, alpha=2.0, mi=outs["pp8p"][1])
+        outs[name] = (Cr, mr, Cn, Cb)
+    torch.cuda.synchronize()
+    for a, c in zip(outs["pp8p"], outs["w4"]):
+        assert torch.equal(a, c)
+    ref = F.relu(A.float() @ W.float().t() + b)
+    assert torch.allclose(outs["w4"][0].float(), ref, rtol=1e-2, atol=1e-2 * (1 + ref.abs().max().item()))
+
+
 def test_gemm_nt_relu_lean_and_generic_agree_with_nan():
     """ReLU forward: full 256 x 256 tiles take the lean epilogue (int16 max on the rounded
     pair), partial tiles the generic one (f32); both follow the sign-bit rule, so the same
