@@ -128,7 +128,8 @@ def test_physics_fullbatch_bf16_tracks_fp32(physics):
         assert cos(b16.grads[i], f32.grads[i]) > 0.99, i
 
 
-def test_physics_fullbatch_fp32_step_matches_oracle(physics):
+@pytest.mark.parametrize("sparse", [True, False], ids=["sparse_first_layer", "dense_first_layer"])
+def test_physics_fullbatch_fp32_step_matches_oracle(physics, sparse):
     """One train() link batch at full physics size, fp32, sparse first layer, against the oracle.
     State: every student / predictor weight x6 and the frozen teacher predictor's x3 (t_h ~ N(0, 1)),
     so that the student logits spread over (0, 1) without saturating the label logits' f32
@@ -170,8 +171,8 @@ def test_physics_fullbatch_fp32_step_matches_oracle(physics):
     opt = torch.optim.Adam(list(model.parameters()) + list(pred.parameters()), lr=a.lr)
     row, col = td.edge_index
     eng = llp_engine.DistillEngine(model, pred, tpred, td.x.to(DEV), t_h.to(DEV), row.numpy(), col.numpy(), N, a,
-                                   opt, dtype="fp32", seed=11)
-    assert eng.xs is not None                             # the default sparse first layer, in f32
+                                   opt, dtype="fp32", seed=11, sparse_input=sparse)
+    assert (eng.xs is not None) == sparse                 # the default: the sparse first layer, in f32
     params = list(model.parameters()) + list(pred.parameters())
     params0 = [p.detach().cpu().clone() for p in params]
     tpar = [p.detach().cpu().clone() for p in tpred.parameters()]
