@@ -299,7 +299,9 @@ def sage_aggregate(data, dev):
                         "E": g.num_edges, "ms": ms, "achieved": tb / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "traffic_over_compulsory": traffic / comp if traffic else None,
                         "frac": tb / 1e9 / PEAK_HBM_GBS, "traffic": traffic, "algorithmic_bytes": algo,
-                        "algorithmic_frac": algo / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "compulsory_bytes": comp,
+                        # operand bytes (every neighbour row counted) per second: a gather rate,
+                        # not an HBM figure -- most neighbour reads hit L2 / Infinity Cache
+                        "operand_read_rate_GBs": algo / (ms * 1e-3) / 1e9, "compulsory_bytes": comp,
                         "compulsory_frac": comp / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                         "note": "achieved/frac on PMC beyond-L2 bytes (Infinity-Cache hits counted: x fits the "
                                 "256 MiB cache, so most neighbour re-reads are cache hits, not HBM reads)"})
