@@ -132,7 +132,11 @@ def check_final_student(name, case, model, pred, lr):
                                      case.stu_final + case.pred_final)):
         d = (p.detach().cpu() - ref).abs()
         if i not in free:
-            assert (d <= 1e-4).float().mean().item() > 0.99, (name, tuple(p.shape), d.max().item())
+            # <= 1 % of the elements beyond 1e-4, and at least one allowed: a 32-element head
+            # weight drifted 1.3e-4 in one element once the teacher's f32 head moved into the
+            # NT epilogue (its logits' summation order changed, ~1e-7, and Adam amplifies it)
+            n_off = int((d > 1e-4).sum().item())
+            assert n_off <= max(1, int(0.01 * d.numel())), (name, tuple(p.shape), n_off, d.max().item())
         assert d.max().item() <= 2 * lr * len(case.steps), (name, tuple(p.shape), d.max().item())
     if case.norm_type == "batch":   # running mean: follows the free biases (momentum x their bound)
         shift = 0.1 * 2 * lr * len(case.steps)
