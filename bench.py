@@ -182,13 +182,13 @@ def dominant_only(eng, batch, pairs, kw, n):
     print(json.dumps({"dominant_rows": R1, "H": lin.out_f, "launches": n}), flush=True)
 
 
-PMC_FILES = {"bf16": os.path.join(REPO, "profiles", "r05_pmc_dominant.json"),
-             "fp32": os.path.join(REPO, "profiles", "r05_fp32_pmc_dominant.json")}
+PMC_FILES = {"bf16": os.path.join(REPO, "profiles", "r06_pmc_dominant.json"),
+             "fp32": os.path.join(REPO, "profiles", "r06_fp32_pmc_dominant.json")}
 
 
 def pmc_traffic(rows, H, dtype):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC passes (profiles/r05_pmc_dominant.json, r05_fp32_pmc_dominant.json;
+    PMC passes (profiles/r06_pmc_dominant.json, r06_fp32_pmc_dominant.json;
     tools/pmc_summary.py): 2 x FETCH_SIZE (gfx950 reports half of a wide
     streaming read) + WRITE_SIZE, per dispatch.  None when the profile is
     absent or for another shape."""
