@@ -329,28 +329,36 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t R, int64_t H, con
   }
 }
 
-constexpr int HB_ROWS = 512;        // rows per block at large R (see colsum_rows)
-
-// rows per colsum block: HB_ROWS at large R, fewer (>= COLSUM_MIN_ROWS) so that a small R
-// still spreads over >= ~COLSUM_BLOCKS blocks (every CU busy)
+// Rows per colsum block (host and device agree: the grid and each block's range derive from
+// R alone).  The vector kernel holds 140 VGPRs, so a CU keeps 3 of its blocks resident (768
+// on the chip): up to 524,288 rows the grid is ~512 blocks (one resident round, no tail round),
+// each a whole number of 64-row batches (LLP_COLSUM_INFLIGHT x rows per pass is 64 at H = 256
+// bf16, 16 at H = 1024, so only the grid's last block runs the row-at-a-time tail); beyond, 512
+// rows per block over several rounds.  Head backward (tools/colsum_probe.py,
+// profiles/r06_colsum_blocks.txt), us, round 5 -> this rule: 603,032 x 1024 508 -> 501,
+// 225,000 x 1024 220 -> 200, 400,000 x 256 108 -> 92, 130,000 x 256 42 -> 31, 100,000 x 256 32 -> 26.
 #ifndef COLSUM_BLOCKS
-#define COLSUM_BLOCKS 1024
+#define COLSUM_BLOCKS 512
 #endif
 #ifndef COLSUM_MIN_ROWS
 #define COLSUM_MIN_ROWS 64
 #endif
 __host__ __device__ inline int64_t colsum_rows(int64_t R) {
   int64_t hb = (R + COLSUM_BLOCKS - 1) / COLSUM_BLOCKS;
-  hb = hb < COLSUM_MIN_ROWS ? COLSUM_MIN_ROWS : (hb > HB_ROWS ? HB_ROWS : hb);
-  return hb;
+  if (hb > 1024) return 512;
+  hb = hb < COLSUM_MIN_ROWS ? COLSUM_MIN_ROWS : hb;
+  return (hb + 63) / 64 * 64;
 }
 
 // Column sums (weighted: sum_r weight[r] * Z[r, n]) with the head backward's dZ
 // write fused in.  Vector form: a row is cpr 16-byte chunks; 256 threads
 // cover rpp = 256 / cpr rows per pass and a block walks HB_ROWS rows; the rpp
 // partial rows are combined in LDS and one slab row [blk][H] is written.
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
+#ifndef LLP_COLSUM_MINB
+#define LLP_COLSUM_MINB 1
+#endif
+template <typename T, bool HAS_W>
+__global__ __launch_bounds__(256, LLP_COLSUM_MINB) void colsum_vec_kernel(int64_t R, int64_t H, const T* __restrict__ Z, int64_t ldz,
                                                          const float* __restrict__ weight,
                                                          const float* __restrict__ w, int relu_mask, float alpha,
                                                          T* __restrict__ dZ, int64_t lddz, float* __restrict__ slab,
@@ -373,8 +381,11 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
   float wv[CH];
 #pragma unroll
   for (int i = 0; i < CH; ++i) wv[i] = (w && active) ? alpha * w[c * CH + i] : alpha;
-  // LLP_COLSUM_INFLIGHT rows in flight per lane: issue the loads, then consume them in order
-  auto consume = [&](int64_t r, const uint4 raw) {
+  // LLP_COLSUM_INFLIGHT rows in flight per lane: issue the loads, then consume them in order.
+  // The rows' weights are loaded BEFORE their chunks: a weight load issued after them (the
+  // round-5 form, weight[r] read inside the row's step) made every row wait for vmcnt(0) --
+  // all chunks in flight and the previous rows' dZ stores -- which serialised the stores.
+  auto consume = [&](int64_t r, const uint4 raw, const float g) {
     float z[CH];
     if constexpr (sizeof(T) == 2) {
       const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -387,7 +398,6 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
       z[0] = __uint_as_float(raw.x); z[1] = __uint_as_float(raw.y);
       z[2] = __uint_as_float(raw.z); z[3] = __uint_as_float(raw.w);
     }
-    const float g = weight ? weight[r] : 1.f;
     accb += g;
 #pragma unroll
     for (int i = 0; i < CH; ++i) acc[i] += g * z[i];
@@ -414,13 +424,19 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t R, int64_t H, c
 #endif
     constexpr int NF = LLP_COLSUM_INFLIGHT;   // rows in flight per lane (16 B each)
     for (; r + (NF - 1) * rpp < r1; r += NF * rpp) {
+      float gw[NF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) gw[j] = HAS_W ? weight[r + j * rpp] : 1.f;
       uint4 raw[NF];
 #pragma unroll
       for (int j = 0; j < NF; ++j) raw[j] = *reinterpret_cast<const uint4*>(Z + (r + j * rpp) * ldz + (int64_t)c * CH);
 #pragma unroll
-      for (int j = 0; j < NF; ++j) consume(r + j * rpp, raw[j]);
+      for (int j = 0; j < NF; ++j) consume(r + j * rpp, raw[j], gw[j]);
     }
-    for (; r < r1; r += rpp) consume(r, *reinterpret_cast<const uint4*>(Z + r * ldz + (int64_t)c * CH));
+    for (; r < r1; r += rpp) {
+      const float g = HAS_W ? weight[r] : 1.f;
+      consume(r, *reinterpret_cast<const uint4*>(Z + r * ldz + (int64_t)c * CH), g);
+    }
   }
   // combine the rpp row-lanes (fixed order -> deterministic)
   if (active)
@@ -614,8 +630,16 @@ extern "C" int llp_head_fwd(int dtype, int64_t R, int64_t H, const void* Z, int6
 
 static int64_t colsum_slabs(int64_t R) { return (R + colsum_rows(R) - 1) / colsum_rows(R); }
 
+// workspace: a bound on colsum_slabs that grows with R (the slab count itself does not: 33,280
+// rows take 260 blocks of 128, 32,768 take 512 of 64), so a workspace sized for the largest R a
+// call site sees fits every smaller one
+static int64_t colsum_slabs_bound(int64_t R) {
+  const int64_t lo = std::min<int64_t>(512, (R + 63) / 64), hi = (R + 511) / 512;
+  return std::max(lo, hi);
+}
+
 extern "C" int64_t llp_head_bwd_workspace_bytes(int64_t R, int64_t H) {
-  return colsum_slabs(R) * (H + 1) * (int64_t)sizeof(float);
+  return colsum_slabs_bound(R) * (H + 1) * (int64_t)sizeof(float);
 }
 extern "C" int64_t llp_colsum_workspace_bytes(int64_t M, int64_t N) { return llp_head_bwd_workspace_bytes(M, N); }
 
@@ -633,17 +657,19 @@ static int colsum_launch(int dtype, int64_t R, int64_t H, const void* Z, int64_t
     const bool vec = (H % ch == 0) && (H / ch <= 256) && ((uintptr_t)Z % 16 == 0) && ((ldz * es) % 16 == 0) &&
                      (!dZ || (((uintptr_t)dZ % 16 == 0) && ((lddz * es) % 16 == 0)));
     if (dtype == LLP_BF16) {
-      if (vec)
-        hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z,
-                           ldz, weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
-      else
+      if (vec) {
+        auto* kern = weight ? colsum_vec_kernel<bf16_t, true> : colsum_vec_kernel<bf16_t, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz, weight, w, relu_mask,
+                           alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
+      } else
         hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const bf16_t*)Z, ldz,
                            weight, w, relu_mask, alpha, (bf16_t*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
     } else {
-      if (vec)
-        hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
-                           weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
-      else
+      if (vec) {
+        auto* kern = weight ? colsum_vec_kernel<float, true> : colsum_vec_kernel<float, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz, weight, w, relu_mask,
+                           alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
+      } else
         hipLaunchKernelGGL(colsum_kernel<float>, dim3((unsigned)ns), dim3(256), 0, s, R, H, (const float*)Z, ldz,
                            weight, w, relu_mask, alpha, (float*)dZ, lddz, slab, db ? slab_b : nullptr, r_dev);
     }
