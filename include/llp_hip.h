@@ -148,6 +148,16 @@ int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q,
                 const llp_operand* A, const llp_operand* B,
                 float* C, int64_t ldc, int accumulate, float* colsum_a,
                 void* workspace, int64_t workspace_bytes, void* stream);
+/* llp_gemm_tn with the output's columns split between two matrices: columns [0, q_split) to C
+ * (row stride ldc), columns [q_split, Q) to C2 (C2 column 0 = column q_split, row stride ldc2).
+ * One weight-gradient GEMM over a K-concatenated operand [agg(x) | x] written straight into a
+ * SAGEConv's lin_l and lin_r gradients (src/sageconv_updated.py:65-81; PyG SAGEConv via
+ * src/models.py:110-119).  0 < q_split < Q; same workspace as llp_gemm_tn. */
+int llp_gemm_tn_split(int dtype, int64_t M, int64_t P, int64_t Q,
+                      const llp_operand* A, const llp_operand* B,
+                      float* C, int64_t ldc, int64_t q_split, float* C2, int64_t ldc2,
+                      int accumulate, float* colsum_a,
+                      void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Sparse-input first Linear (src/models.py:48 on bag-of-words x, e.g. coauthor-physics' 8,415
  * binary keywords at ~0.5 % density; csrc/spmm.hip).  x is held as CSR (rowptr[N+1], colidx,

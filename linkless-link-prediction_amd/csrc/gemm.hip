@@ -518,14 +518,17 @@ __global__ __launch_bounds__(64 * NW, 2) void gemm_tn_kernel(TNParams p) {
   }
 }
 
+// Columns c >= qs go to C2 (column c - qs, row stride ldc2): one weight-gradient GEMM over a
+// K-concatenated operand written straight into two modules' gradients.
 __global__ void slab_reduce_kernel(const float* __restrict__ ws, int64_t splits, int64_t P, int64_t Q,
-                                   float* __restrict__ C, int64_t ldc, int accumulate) {
+                                   float* __restrict__ C, int64_t ldc, int accumulate, int64_t qs,
+                                   float* __restrict__ C2, int64_t ldc2) {
   const int64_t n = P * Q;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
     for (int64_t z = 0; z < splits; ++z) s += ws[z * n + e];
     const int64_t r = e / Q, c = e % Q;
-    float* dst = C + r * ldc + c;
+    float* dst = c < qs ? C + r * ldc + c : C2 + r * ldc2 + (c - qs);
     *dst = accumulate ? *dst + s : s;
   }
 }
@@ -539,6 +542,7 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, int64_t splits,
 constexpr int SR_G = 4, SR_L = 256 / SR_G;
 struct SlabJob {           // C[e4 / Q4][(e4 % Q4) * 4 ..] (+)= sum_z ws[z][e4], e4 < n4
   const float4* ws; int64_t S, n4, Q4; float* C; int64_t ldc;
+  int64_t Q4s; float* C2; int64_t ldc2;   // float4 columns >= Q4s go to C2 (column - Q4s); Q4s = Q4: none
 };
 // One launch can carry two jobs (the weight slabs and the bias-gradient slabs of a TN
 // GEMM): blocks [0, nblk0) take job 0, the rest job 1.
@@ -577,7 +581,8 @@ __global__ __launch_bounds__(256) void slab_reduce_v4_kernel(SlabJob j0, SlabJob
     const float4 v = part[k][lane];
     t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
   }
-  float4* dst = reinterpret_cast<float4*>(j.C + (e4 / j.Q4) * j.ldc + (e4 % j.Q4) * 4);
+  const int64_t row = e4 / j.Q4, q4 = e4 % j.Q4;
+  float4* dst = reinterpret_cast<float4*>(q4 < j.Q4s ? j.C + row * j.ldc + q4 * 4 : j.C2 + row * j.ldc2 + (q4 - j.Q4s) * 4);
   if (accumulate) {
     const float4 o = *dst;
     t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
@@ -588,28 +593,35 @@ __global__ __launch_bounds__(256) void slab_reduce_v4_kernel(SlabJob j0, SlabJob
 // C (+)= sum of the S slabs [S][P][Q] (f32), deterministic; with C2, in the same
 // launch when both take the vector form, also C2 (+)= sum of the S slabs [S][P2] at ws2
 // (a TN GEMM's bias-gradient column sums).
+// C (+)= ... for columns < qs, Cq (row stride ldq) for columns >= qs (qs < 0: Q, no split).
 void slab_reduce(const float* ws, int64_t S, int64_t P, int64_t Q, float* C, int64_t ldc, int accumulate,
-                 hipStream_t s, const float* ws2 = nullptr, int64_t P2 = 0, float* C2 = nullptr) {
+                 hipStream_t s, const float* ws2 = nullptr, int64_t P2 = 0, float* C2 = nullptr, int64_t qs = -1,
+                 float* Cq = nullptr, int64_t ldq = 0) {
   const int64_t n = P * Q;
+  if (qs < 0 || qs >= Q || !Cq) {
+    qs = Q;
+    Cq = C;
+    ldq = ldc;
+  }
   auto vec_ok = [](const float* w, int64_t q, const float* c, int64_t ld) {
     return q % 4 == 0 && ld % 4 == 0 && (uintptr_t)c % 16 == 0 && (uintptr_t)w % 16 == 0;
   };
-  const bool v1 = n > 0 && vec_ok(ws, Q, C, ldc);
+  const bool v1 = n > 0 && vec_ok(ws, Q, C, ldc) && qs % 4 == 0 && vec_ok(ws, Q, Cq, ldq);
   const bool two = C2 && P2 > 0;
   const bool v2 = two && vec_ok(ws2, P2, C2, P2);
   if (v1) {
-    SlabJob j0{reinterpret_cast<const float4*>(ws), S, n / 4, Q / 4, C, ldc};
+    SlabJob j0{reinterpret_cast<const float4*>(ws), S, n / 4, Q / 4, C, ldc, qs / 4, Cq, ldq};
     SlabJob j1 = j0;
     const int64_t nb0 = ceil_div_u(n / 4, SR_L);
     int64_t nb = nb0;
     if (v2) {
-      j1 = SlabJob{reinterpret_cast<const float4*>(ws2), S, P2 / 4, P2 / 4, C2, P2};
+      j1 = SlabJob{reinterpret_cast<const float4*>(ws2), S, P2 / 4, P2 / 4, C2, P2, P2 / 4, C2, P2};
       nb += ceil_div_u(P2 / 4, SR_L);
     }
     hipLaunchKernelGGL(slab_reduce_v4_kernel, dim3((unsigned)nb), dim3(256), 0, s, j0, j1, nb0, accumulate);
   } else if (n > 0) {
     const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, ws, S, P, Q, C, ldc, accumulate);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(nb), dim3(256), 0, s, ws, S, P, Q, C, ldc, accumulate, qs, Cq, ldq);
   }
   if (two && !(v1 && v2)) slab_reduce(ws2, S, (int64_t)1, P2, C2, P2, accumulate, s);
 }
@@ -919,9 +931,9 @@ extern "C" int64_t llp_gemm_tn_workspace_bytes(int dtype, int64_t M, int64_t P, 
   return s * P * Q * (int64_t)sizeof(float) + tn_colsum_region(dtype, M, P);
 }
 
-extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A,
-                           const llp_operand* B, float* C, int64_t ldc, int accumulate, float* colsum_a,
-                           void* workspace, int64_t workspace_bytes, void* stream) {
+static int gemm_tn_impl(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A, const llp_operand* B,
+                        float* C, int64_t ldc, int64_t qs, float* Cq, int64_t ldq, int accumulate, float* colsum_a,
+                        void* workspace, int64_t workspace_bytes, void* stream) {
   LLP_CHECK_ARG(A && B && C, "llp_gemm_tn: null operand");
   LLP_CHECK_ARG(dtype == LLP_F32 || dtype == LLP_BF16, "llp_gemm_tn: bad dtype %d", dtype);
   LLP_CHECK_ARG(!colsum_a || (!A->idx && !A->ptr2), "llp_gemm_tn: colsum_a needs a plain A operand");
@@ -940,7 +952,7 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     const int rc = llp_gemm_tn_bf16_256(A, B, M, P, Q, ws, wcs, sp, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (256 tile): %s", hipGetErrorString((hipError_t)rc));
     // weight slabs and the [sp][P] column-sum slabs in one launch
-    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s, wcs, colsum_a ? P : 0, colsum_a);
+    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s, wcs, colsum_a ? P : 0, colsum_a, qs, Cq, ldq);
     LLP_LAUNCH_CHECK();
     return LLP_OK;
   }
@@ -956,7 +968,7 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     float* wcs = colsum_a ? ws + sp * P * Q : nullptr;
     const int rc = llp_gemm_tn_f32_256(A, B, M, P, Q, ws, wcs, sp, s);
     if (rc != 0) return llp::set_error(rc, "llp_gemm_tn (f32 256 tile): %s", hipGetErrorString((hipError_t)rc));
-    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s, wcs, colsum_a ? P : 0, colsum_a);
+    slab_reduce(ws, sp, P, Q, C, ldc, accumulate, s, wcs, colsum_a ? P : 0, colsum_a, qs, Cq, ldq);
     LLP_LAUNCH_CHECK();
     return LLP_OK;
   }
@@ -994,7 +1006,25 @@ extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp
     else hipLaunchKernelGGL((gemm_tn_kernel<float, false, 8>), g2, dim3(512), 0, s, pp);
   }
   LLP_LAUNCH_CHECK();
-  slab_reduce(reinterpret_cast<const float*>(workspace), splits, P, Q, C, ldc, accumulate, s);
+  slab_reduce(reinterpret_cast<const float*>(workspace), splits, P, Q, C, ldc, accumulate, s, nullptr, 0, nullptr, qs,
+              Cq, ldq);
   LLP_LAUNCH_CHECK();
   return LLP_OK;
+}
+
+extern "C" int llp_gemm_tn(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A,
+                           const llp_operand* B, float* C, int64_t ldc, int accumulate, float* colsum_a,
+                           void* workspace, int64_t workspace_bytes, void* stream) {
+  return gemm_tn_impl(dtype, M, P, Q, A, B, C, ldc, -1, nullptr, 0, accumulate, colsum_a, workspace, workspace_bytes,
+                      stream);
+}
+
+extern "C" int llp_gemm_tn_split(int dtype, int64_t M, int64_t P, int64_t Q, const llp_operand* A,
+                                 const llp_operand* B, float* C, int64_t ldc, int64_t q_split, float* C2,
+                                 int64_t ldc2, int accumulate, float* colsum_a, void* workspace,
+                                 int64_t workspace_bytes, void* stream) {
+  LLP_CHECK_ARG(C2 && q_split > 0 && q_split < Q, "llp_gemm_tn_split: bad split %lld of %lld columns",
+                (long long)q_split, (long long)Q);
+  return gemm_tn_impl(dtype, M, P, Q, A, B, C, ldc, q_split, C2, ldc2, accumulate, colsum_a, workspace,
+                      workspace_bytes, stream);
 }

@@ -66,6 +66,8 @@ _SIGS = {
     "llp_gemm_tn_workspace_bytes": (c_i64, [c_int, c_i64, c_i64, c_i64]),
     "llp_gemm_tn": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64, c_int,
                             c_vp, c_vp, c_i64, c_vp]),
+    "llp_gemm_tn_split": (c_int, [c_int, c_i64, c_i64, c_i64, C.POINTER(Operand), C.POINTER(Operand), c_vp, c_i64,
+                                  c_i64, c_vp, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
     "llp_colsum_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_colsum": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp]),
     "llp_spmm_rows": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_i64, c_vp,
@@ -304,8 +306,16 @@ def gemm_tn_ws_bytes(dtype, M, P, Q):
     return load().llp_gemm_tn_workspace_bytes(dtype, M, P, Q)
 
 
-def gemm_tn(A: Operand, B: Operand, M, P, Q, C_out, dtype, ws, accumulate=False, colsum_a=None):
+def gemm_tn(A: Operand, B: Operand, M, P, Q, C_out, dtype, ws, accumulate=False, colsum_a=None, split=None):
+    """C_out (+)= A^T B (f32).  split=(q, C2): columns [q, Q) go to C2 instead (llp_gemm_tn_split;
+    C_out then holds the first q columns)."""
     L = lib()
+    if split is not None:
+        q, C2 = split
+        check(L.llp_gemm_tn_split(dtype, M, P, Q, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0), q,
+                                  C2.data_ptr(), C2.stride(0), int(accumulate), ptr(colsum_a), ws.data_ptr(),
+                                  ws.numel() * ws.element_size(), stream_ptr()), "llp_gemm_tn_split")
+        return
     check(L.llp_gemm_tn(dtype, M, P, Q, C.byref(A), C.byref(B), C_out.data_ptr(), C_out.stride(0), int(accumulate),
                         ptr(colsum_a), ws.data_ptr(), ws.numel() * ws.element_size(), stream_ptr()), "llp_gemm_tn")
 

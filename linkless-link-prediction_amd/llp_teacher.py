@@ -257,13 +257,11 @@ class TeacherEngine(EngineBase):
                 # dW_l = dOut^T agg(x), db = colsum(dOut); dW_r = dOut^T x: ONE weight-gradient GEMM over
                 # the layer's [agg(x) | x] (XA, the forward's K-concatenated operand), so dOut is read
                 # once and one launch + one slab reduce go (round 5); the [O, 2F] result is split
-                # into the two modules' gradients
+                # into the two modules' gradients by the GEMM's column-split output
+                # (llp_gemm_tn_split, round 6: no [O, 2F] buffer, no two strided copies per layer)
                 ws = self._ws("ws_tn", K.gemm_tn_ws_bytes(dc, N, O, 2 * F))
-                dWc = self._buf("dWcat", (O, 2 * F), torch.float32)
-                K.gemm_tn(K.operand(dOut), K.operand(L["XA"]), N, O, 2 * F, dWc, dc, ws,
-                          colsum_a=conv.lin_l.bias.grad)
-                conv.lin_l.weight.grad.copy_(dWc[:, :F])
-                conv.lin_r.weight.grad.copy_(dWc[:, F:])
+                K.gemm_tn(K.operand(dOut), K.operand(L["XA"]), N, O, 2 * F, conv.lin_l.weight.grad, dc, ws,
+                          colsum_a=conv.lin_l.bias.grad, split=(F, conv.lin_r.weight.grad))
             if l > 0:
                 # dX = [G | dOut] . [W_l^T | W_r^T]^T, ReLU/dropout mask of layer l-1 in the epilogue,
                 # written straight into layer l-1's output-gradient slot

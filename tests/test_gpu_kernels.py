@@ -398,6 +398,33 @@ def test_gemm_tn(dt, M, P, Q):
     assert err <= (1e-4 if dt == "fp32" else 2e-3) * (1 + ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("dt,M,P,Q,qs", [("bf16", 50_003, 256, 512, 256), ("bf16", 9_001, 256, 256, 128),
+                                          ("fp32", 20_011, 256, 512, 256), ("fp32", 7_001, 256, 128, 64),
+                                          ("bf16", 3_001, 100, 90, 30)])
+def test_gemm_tn_split_output(dt, M, P, Q, qs):
+    """llp_gemm_tn_split (the SAGE teacher's one weight-gradient GEMM over [agg(x) | x] written
+    into lin_l's and lin_r's gradients): columns [0, qs) in C, [qs, Q) in C2, bit-identical to
+    the unsplit llp_gemm_tn on every path (bf16 256-tile, f32 256-tile, f32 128-tile (Q <= 128), and the
+    scalar slab reduce at unaligned widths), with the fused bias column sums and accumulate."""
+    k = K()
+    g = torch.Generator().manual_seed(M + Q + qs)
+    tdt = torch.float32 if dt == "fp32" else torch.bfloat16
+    A = torch.randn(M, P, generator=g).to(DEV, tdt)
+    B = torch.randn(M, Q, generator=g).to(DEV, tdt)
+    ws = torch.empty(k.gemm_tn_ws_bytes(k.dtype_code(tdt), M, P, Q) // 4 + 16, device=DEV)
+    full = torch.randn(P, Q, generator=g).to(DEV)
+    cs_full = torch.zeros(P, device=DEV)
+    C1 = full[:, :qs].contiguous()
+    C2 = full[:, qs:].contiguous()
+    cs = torch.zeros(P, device=DEV)
+    k.gemm_tn(k.operand(A), k.operand(B), M, P, Q, full, k.dtype_code(tdt), ws, accumulate=True, colsum_a=cs_full)
+    k.gemm_tn(k.operand(A), k.operand(B), M, P, Q, C1, k.dtype_code(tdt), ws, accumulate=True, colsum_a=cs,
+              split=(qs, C2))
+    torch.cuda.synchronize()
+    assert torch.equal(C1, full[:, :qs]) and torch.equal(C2, full[:, qs:])
+    assert torch.equal(cs, cs_full)
+
+
 @pytest.mark.parametrize("M,P,Q,with_count", [(30_011, 1024, 1024, False), (4_099, 260, 132, True),
                                                (225_384, 1024, 136, False), (225_384, 1024, 128, False)])
 def test_gemm_tn_f32_256(M, P, Q, with_count):
