@@ -276,18 +276,31 @@ __device__ __forceinline__ int64_t shadow_index(const llp_tensor_desc& d, int64_
   return (e / d.cols) * d.shadow_ld + e % d.cols;
 }
 
+// Pointers read from the descriptor table are generic: hipcc then emits FLAT loads and stores,
+// which count on lgkmcnt as well as vmcnt, so every LDS wait (the transposed shadow's tile) also
+// waited for the tensor traffic in flight.  These casts to the global address space make them
+// global_load / global_store (round 6: the physics optimizer's Adam).
+typedef __attribute__((address_space(1))) float g_f32;
+typedef __attribute__((address_space(1))) bf16_t g_bf16;
+typedef __attribute__((address_space(1))) float4_t g_f4;
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x2_t g_u2;
+__device__ __forceinline__ g_f32* gbl(float* p) { return (g_f32*)p; }
+__device__ __forceinline__ const g_f32* gbl(const float* p) { return (const g_f32*)p; }
+
 __device__ __forceinline__ void put_elem(void* base, int64_t i, float v, int dt) {
   if (dt == LLP_BF16)
-    reinterpret_cast<bf16_t*>(base)[i] = f2bf(v);
+    ((g_bf16*)base)[i] = f2bf(v);
   else
-    reinterpret_cast<float*>(base)[i] = v;
+    ((g_f32*)base)[i] = v;
 }
 
 // one thread's share of a chunk's sum of squares: its OPT_CHUNK / 256 loads issued together
 // (a loop that waits on each is latency-bound: 18 us for the 2.3 M-parameter physics student),
 // summed in element order (the order fixes the result; both norm kernels use this)
-__device__ __forceinline__ float chunk_sumsq(const float* __restrict__ grad, int64_t e0, int64_t e1) {
+__device__ __forceinline__ float chunk_sumsq(const float* __restrict__ grad_, int64_t e0, int64_t e1) {
   constexpr int PER = OPT_CHUNK / 256;
+  const g_f32* grad = gbl(grad_);
   float x[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -660,14 +673,18 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
       // every load of the tile issued before the first store (the stores may alias later
       // loads as far as the compiler knows, which kept it to one row's round trip at a time)
       float gv[16], mv[16], vv[16], pv[16];
+      g_f32* const gg = gbl(d.grad);
+      g_f32* const gm = gbl(d.exp_avg);
+      g_f32* const gvv = gbl(d.exp_avg_sq);
+      g_f32* const gp = gbl(d.param);
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int64_t r = r0 + ty + 4 * k, e = r * cols + c;
         const bool ok = r < rows && c < cols;
-        gv[k] = ok ? d.grad[e] : 0.f;
-        mv[k] = ok ? d.exp_avg[e] : 0.f;
-        vv[k] = ok ? d.exp_avg_sq[e] : 0.f;
-        pv[k] = ok ? d.param[e] : 0.f;
+        gv[k] = ok ? gg[e] : 0.f;
+        mv[k] = ok ? gm[e] : 0.f;
+        vv[k] = ok ? gvv[e] : 0.f;
+        pv[k] = ok ? gp[e] : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
@@ -677,11 +694,11 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
         if (r < rows && c < cols) {
           const int64_t e = r * cols + c;
           const float g = gv[k] * coef;
-          if (coef != 1.f) d.grad[e] = g;
+          if (coef != 1.f) gg[e] = g;
           pnew = adam_elem(g, mv[k], vv[k], pv[k], beta1, beta2, eps, bc2s, step_size);
-          d.exp_avg[e] = mv[k];
-          d.exp_avg_sq[e] = vv[k];
-          d.param[e] = pnew;
+          gm[e] = mv[k];
+          gvv[e] = vv[k];
+          gp[e] = pnew;
           if (d.shadow) put_elem(d.shadow, r * lds + c, pnew, d.shadow_dtype);
         }
         tile[i][tx] = pnew;
@@ -701,43 +718,51 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(const llp_tensor_desc* 
                      (d.shadow_ld == 0 || d.shadow_ld == d.cols);
     for (int64_t e0 = blk0 * ADAM_CHUNK; e0 < d.numel; e0 += bstride * ADAM_CHUNK) {
       const int64_t e1 = min(d.numel, e0 + ADAM_CHUNK);
+      g_f32* const gg = gbl(d.grad);
+      g_f32* const gm = gbl(d.exp_avg);
+      g_f32* const gvv = gbl(d.exp_avg_sq);
+      g_f32* const gp = gbl(d.param);
       if (vec) {
         for (int64_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
-          float4 g = *reinterpret_cast<const float4*>(d.grad + e);
+          const float4_t g4 = *(const g_f4*)(gg + e);
+          float4 g = make_float4(g4.x, g4.y, g4.z, g4.w);
           if (coef != 1.f) {
             g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
-            *reinterpret_cast<float4*>(d.grad + e) = g;
+            *(g_f4*)(gg + e) = float4_t{g.x, g.y, g.z, g.w};
           }
-          float4 m = *reinterpret_cast<const float4*>(d.exp_avg + e);
-          float4 v = *reinterpret_cast<const float4*>(d.exp_avg_sq + e);
-          float4 p = *reinterpret_cast<const float4*>(d.param + e);
+          const float4_t m4 = *(const g_f4*)(gm + e);
+          const float4_t v4 = *(const g_f4*)(gvv + e);
+          const float4_t p4 = *(const g_f4*)(gp + e);
+          float4 m = make_float4(m4.x, m4.y, m4.z, m4.w);
+          float4 v = make_float4(v4.x, v4.y, v4.z, v4.w);
+          float4 p = make_float4(p4.x, p4.y, p4.z, p4.w);
           p.x = adam_elem(g.x, m.x, v.x, p.x, beta1, beta2, eps, bc2s, step_size);
           p.y = adam_elem(g.y, m.y, v.y, p.y, beta1, beta2, eps, bc2s, step_size);
           p.z = adam_elem(g.z, m.z, v.z, p.z, beta1, beta2, eps, bc2s, step_size);
           p.w = adam_elem(g.w, m.w, v.w, p.w, beta1, beta2, eps, bc2s, step_size);
-          *reinterpret_cast<float4*>(d.exp_avg + e) = m;
-          *reinterpret_cast<float4*>(d.exp_avg_sq + e) = v;
-          *reinterpret_cast<float4*>(d.param + e) = p;
+          *(g_f4*)(gm + e) = float4_t{m.x, m.y, m.z, m.w};
+          *(g_f4*)(gvv + e) = float4_t{v.x, v.y, v.z, v.w};
+          *(g_f4*)(gp + e) = float4_t{p.x, p.y, p.z, p.w};
           if (d.shadow) {
             if (d.shadow_dtype == LLP_BF16) {
-              uint2 o;
+              u32x2_t o;
               o.x = (uint32_t)f2bf(p.x) | ((uint32_t)f2bf(p.y) << 16);
               o.y = (uint32_t)f2bf(p.z) | ((uint32_t)f2bf(p.w) << 16);
-              *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(d.shadow) + e) = o;
+              *(g_u2*)((g_bf16*)d.shadow + e) = o;
             } else {
-              *reinterpret_cast<float4*>(reinterpret_cast<float*>(d.shadow) + e) = p;
+              *(g_f4*)((g_f32*)d.shadow + e) = float4_t{p.x, p.y, p.z, p.w};
             }
           }
         }
       } else {
         for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-          const float g = d.grad[e] * coef;
-          if (coef != 1.f) d.grad[e] = g;
-          float m = d.exp_avg[e], v = d.exp_avg_sq[e];
-          const float pnew = adam_elem(g, m, v, d.param[e], beta1, beta2, eps, bc2s, step_size);
-          d.exp_avg[e] = m;
-          d.exp_avg_sq[e] = v;
-          d.param[e] = pnew;
+          const float g = gg[e] * coef;
+          if (coef != 1.f) gg[e] = g;
+          float m = gm[e], v = gvv[e];
+          const float pnew = adam_elem(g, m, v, gp[e], beta1, beta2, eps, bc2s, step_size);
+          gm[e] = m;
+          gvv[e] = v;
+          gp[e] = pnew;
           if (d.shadow) put_elem(d.shadow, shadow_index(d, e), pnew, d.shadow_dtype);
         }
       }

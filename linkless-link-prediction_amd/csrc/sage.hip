@@ -254,6 +254,34 @@ __global__ __launch_bounds__(64 * AGG_WAVES) void csr_agg_lds_kernel(int64_t n_r
 #pragma unroll
   for (int i = 0; i < E; ++i) acc[i] = 0.f;
   const T* xc = x + ch * E;
+#ifndef LLP_AGG_NO_LDS_FAST
+  if (n_e <= AGG_CAP) {
+    // every index (and weight) of the workgroup is in LDS (all but hub-holding workgroups): the
+    // mixed form below selects per lane between the LDS slice and col[] / inv_deg in global
+    // memory, which hipcc compiles to divergent branches with a full vmcnt + lgkmcnt wait per
+    // neighbour and FLAT loads for the weights.  Same values, same order: bit-identical.
+    for (int32_t e = beg; e < end; e += UNR) {
+      int32_t j[UNR];
+      float wt[UNR];
+      bool v[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k) {
+        const int32_t q = e + k;
+        v[k] = q < end;
+        const int32_t qq = v[k] ? q : beg;   // an in-range slot (its value unused)
+        j[k] = v[k] ? s_col[qq] : 0;
+        wt[k] = (mode && v[k]) ? s_w[qq] : 1.f;
+      }
+      uint4 r[UNR];
+#pragma unroll
+      for (int k = 0; k < UNR; ++k)
+        r[k] = v[k] ? *reinterpret_cast<const uint4*>(xc + (int64_t)j[k] * ldx) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < UNR; ++k)
+        if (v[k]) V16<T>::add(acc, r[k], wt[k]);
+    }
+  } else
+#endif
   for (int32_t e = beg; e < end; e += UNR) {
     int32_t j[UNR];
     float wt[UNR];
