@@ -703,6 +703,20 @@ int llp_mfma_probe(const void* data, int64_t n_u4, int64_t iters, float* out, do
 /* The same loop on v_mfma_f32_16x16x4_f32 (the fp32 GEMMs' instruction) over n random f32. */
 int llp_mfma_probe_f32(const float* data, int64_t n, int64_t iters, float* out, double* flops, void* stream);
 int64_t llp_mfma_probe_out_floats(void);
+/* Diagnostics of round 6, not used by the engines:
+ * llp_stage_probe: one wave per SIMD issuing v_mfma_f32_32x32x16_bf16 back to back beside `pieces`
+ *   (0 / 4 / 8 / 16 per 32 MFMAs) operand-staging pieces of kind `mode` (0 none, 1 LDS-DMA, 2 global
+ *   load into VGPRs + ds_write, 3 ds_read), reading src (src_u4 16-B chunks, src_u4 / 64 a power of
+ *   two); per-workgroup shader cycles into cycles[], accumulators into out.
+ * llp_gemm_nt_w4_probe: the one-wave-per-SIMD persistent NT GEMM (csrc/gemm256_w4.hip), bf16,
+ *   N % 256 == 0, K % 128 == 0; act 0 plain / 1 ReLU (+ bit mask out) / 3 ReLU backward through
+ *   mask_in; diag selects the diagnostic builds' skips (0: the whole kernel).  Bit-identical to
+ *   llp_gemm_nt where both run. */
+int llp_stage_probe(int mode, int pieces, const void* src, int64_t src_u4, int64_t iters, float* out,
+                    unsigned long long* cycles, void* stream);
+int llp_gemm_nt_w4_probe(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                         void* C, int64_t ldc, const float* bias, int act, float alpha, void* mask_out,
+                         const void* mask_in, int64_t ld_mask, int diag, void* stream);
 
 #ifdef __cplusplus
 }
