@@ -166,6 +166,9 @@ _SIGS = {
     "llp_mfma_probe": (c_int, [c_vp, c_i64, c_i64, c_vp, C.POINTER(c_f64), c_vp]),
     "llp_mfma_probe_out_floats": (c_i64, []),
     "llp_mfma_probe_f32": (c_int, [c_vp, c_i64, c_i64, c_vp, C.POINTER(c_f64), c_vp]),
+    "llp_stage_probe": (c_int, [c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "llp_gemm_nt_w4_probe": (c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_f32,
+                                     c_vp, c_vp, c_i64, c_int, c_vp]),
     "llp_norm_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "llp_norm_colsums": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "llp_norm_fwd": (c_int, [c_int, c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_int, c_vp, c_f64, c_f32,
