@@ -63,15 +63,40 @@ __device__ __forceinline__ void gather_sum(float* acc, const int32_t* __restrict
 #pragma unroll
   for (int i = 0; i < E; ++i) acc[i] = 0.f;
   int32_t k = first + s;
+  const int64_t colc = live ? col : 0;
   for (; k + streams * (U - 1) < last; k += streams * U) {
     uint4 g[U];
     float v[U];
+    int32_t r[U];
+#ifndef LLP_SPMM_INTERLEAVED
+    // all U indices (and values) first, then the U row loads: interleaved per u, each row load
+    // waited for the previous one (the vector-memory counter is in order, and the next index was
+    // issued behind it), so one row was in flight per lane instead of U (round 6)
+    // (no branch between the loads: a dead lane reads its row's column 0 and adds nothing, and
+    // the values' presence is uniform)
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = idx[k + streams * u];
+    if (val) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = val[k + streams * u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) g[u] = *reinterpret_cast<const uint4*>(M + (int64_t)r[u] * ldm + colc);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (live) fma16(acc, g[u], v[u], T());
+    continue;
+#else
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t r = idx[k + streams * u];
+      r[u] = idx[k + streams * u];
       v[u] = val ? val[k + streams * u] : 1.f;
-      g[u] = live ? *reinterpret_cast<const uint4*>(M + r * ldm + col) : make_uint4(0u, 0u, 0u, 0u);
+      g[u] = live ? *reinterpret_cast<const uint4*>(M + (int64_t)r[u] * ldm + col) : make_uint4(0u, 0u, 0u, 0u);
     }
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) fma16(acc, g[u], v[u], T());
   }
