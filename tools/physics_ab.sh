@@ -1,7 +1,9 @@
 #!/bin/bash
 # Same-box A/B of tools/physics_bench.py --graph (bf16) between the default engine and the
-# engine switches in $VAR_ARGS, at 1 rank and rank 0 of 4, 3 interleaved rounds.
+# engine switches in $VAR_ARGS (and/or the library $VAR_LIB, a build_lib.build_variant output),
+# at 1 rank and rank 0 of 4, 3 interleaved rounds.
 #   gpurun -- bash tools/physics_ab.sh OUTTAG "--main-sampler"
+#   gpurun -- 'VAR_LIB=tools/bin/x.so bash tools/physics_ab.sh OUTTAG ""'
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/$1
@@ -12,8 +14,9 @@ for i in 1 2 3; do
   for E in "--emulate-ranks 4" ""; do
     for V in base var; do
       A=$([ $V = var ] && echo "$VAR_ARGS")
-      timeout -k 10 300 $B $E $A > $O/run.tmp 2> $O/run.err || { tail -20 $O/run.err; exit 1; }
-      echo "{\"round\": $i, \"ranks\": \"$E\", \"side\": \"$V\", \"run\": $(head -1 $O/run.tmp)}" >> $O/ab.jsonl
+      L=$([ $V = var ] && [ -n "$VAR_LIB" ] && echo "$VAR_LIB" || echo linkless-link-prediction_amd/libllp_hip.so)
+      LLP_LIB=$L timeout -k 10 300 $B $E $A > $O/run.tmp 2> $O/run.err || { tail -20 $O/run.err; exit 1; }
+      echo "{\"round\": $i, \"ranks\": \"$E\", \"side\": \"$V\", \"run\": $(grep -m1 "^{" $O/run.tmp)}" >> $O/ab.jsonl
     done
   done
 done
